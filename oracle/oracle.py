@@ -1,0 +1,208 @@
+"""CPU oracle for the swarm step -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg may import this
+module.  It is the checker, never the thing measured or shipped: the product path
+(``swarm_amd``) never imports it.
+
+Two restatements of the reference (``agent.py``, see swarm_oracle.c's header for the
+file:line map):
+  * ``liboracle.so`` (swarm_oracle.c, OpenMP) for every size the tests use;
+  * pure-Python loops (``*_py``) for tiny cases, written straight from the handlers.
+Both are pinned against tests/golden/ (generated from the reference's own handlers by
+tools/gen_golden.py) in tests/test_oracle_golden.py.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import struct
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+OPEN, TENTATIVE, LOCKED, ASSIGNED = 0, 1, 2, 3
+FOLLOWER, ELECTION_WAIT, LEADER = 1, 2, 3
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        l, d, i = ctypes.c_long, ctypes.c_double, ctypes.c_int
+        L.orc_elect.restype = l
+        L.orc_elect.argtypes = [l, P, P, P, P, P, l, P]
+        L.orc_utility.restype = None
+        L.orc_utility.argtypes = [l, P, P, P, P, P, P, d, i, P]
+        L.orc_allocate.restype = l
+        L.orc_allocate.argtypes = [l, P, P, P, P, l, P, P, P, d, d, d, i, P, P, P, P, P]
+        L.orc_task_claims.restype = l
+        L.orc_task_claims.argtypes = [l, P, P, P, P, d, d, ctypes.c_int8, d, d, i, P, P, l]
+        L.orc_rgg_csr.restype = l
+        L.orc_rgg_csr.argtypes = [l, P, P, d, P, P]
+        L.orc_num_threads.restype = i
+        L.orc_set_threads.argtypes = [i]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _c(a, dt):
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+def set_threads(n: int):
+    lib().orc_set_threads(int(n))
+
+
+def num_threads() -> int:
+    return int(lib().orc_num_threads())
+
+
+def elect(row_ptr, col, ids, max_rounds=1 << 20):
+    """E2 election to convergence -> (leader int32, state uint8, rounds_exec, changes int64)."""
+    ids = _c(ids, np.int32)
+    n = len(ids)
+    rp = _c(row_ptr, np.int64)
+    cl = _c(col, np.int32)
+    leader = np.empty(n, np.int32)
+    state = np.empty(n, np.uint8)
+    changes = np.zeros(max(1, min(max_rounds, 1 << 20)), np.int64)
+    r = lib().orc_elect(n, _p(rp), _p(cl), _p(ids), _p(leader), _p(state), len(changes), _p(changes))
+    return leader, state, int(r), changes[: max(r, 0)].copy()
+
+
+def utility(ax, ay, caps, tx, ty, treq, use_pow=True, u_scale=100.0):
+    """Elementwise utility of (agent_i, task_i) pairs (agent.py:338-347), fp64."""
+    arrs = [_c(ax, np.float64), _c(ay, np.float64), _c(caps, np.uint32), _c(tx, np.float64),
+            _c(ty, np.float64), _c(treq, np.int8)]
+    out = np.empty(len(arrs[0]), np.float64)
+    lib().orc_utility(len(out), *[_p(a) for a in arrs], u_scale, int(use_pow), _p(out))
+    return out
+
+
+def allocate(ids, ax, ay, caps, tx, ty, treq, winner=None, util=None, claim_thr=20.0,
+             hysteresis=5.0, u_scale=100.0, use_pow=True):
+    """A-H allocation -> dict(winner, util, nclaim, nmsg, won, n_claims, n_conflicts)."""
+    ids = _c(ids, np.int32)
+    n, t = len(ids), len(tx)
+    w = np.full(t, -1, np.int32) if winner is None else _c(winner, np.int32).copy()
+    u = np.zeros(t, np.float64) if util is None else _c(util, np.float64).copy()
+    nclaim = np.zeros(t, np.int64)
+    nmsg = np.zeros(t, np.int64)
+    won = np.zeros(n, np.int32)
+    arrs = [_c(ax, np.float64), _c(ay, np.float64), _c(caps, np.uint32)]
+    tarr = [_c(tx, np.float64), _c(ty, np.float64), _c(treq, np.int8)]
+    total = lib().orc_allocate(n, _p(ids), *[_p(a) for a in arrs], t, *[_p(a) for a in tarr],
+                               claim_thr, hysteresis, u_scale, int(use_pow), _p(w), _p(u),
+                               _p(nclaim), _p(nmsg), _p(won))
+    return dict(winner=w, util=u, nclaim=nclaim, nmsg=nmsg, won=won, n_claims=int(total),
+                n_conflicts=int(nmsg.sum()))
+
+
+def task_claims(ids, ax, ay, caps, tx, ty, treq, claim_thr=20.0, u_scale=100.0, use_pow=True):
+    """Claims on one task in ascending-ID order -> (ids int32, f32 values)."""
+    ids = _c(ids, np.int32)
+    n = len(ids)
+    oid = np.empty(n, np.int32)
+    ox = np.empty(n, np.float32)
+    m = lib().orc_task_claims(n, _p(ids), _p(_c(ax, np.float64)), _p(_c(ay, np.float64)),
+                              _p(_c(caps, np.uint32)), float(tx), float(ty), int(treq), claim_thr,
+                              u_scale, int(use_pow), _p(oid), _p(ox), n)
+    return oid[:m].copy(), ox[:m].copy()
+
+
+def rgg_csr(x, y, radius=1.0):
+    """Radius graph over storage indices (rows ascending) -> (row_ptr int64, col int32)."""
+    x = _c(x, np.float64)
+    y = _c(y, np.float64)
+    n = len(x)
+    rp = np.zeros(n + 1, np.int64)
+    e = lib().orc_rgg_csr(n, _p(x), _p(y), radius, _p(rp), None)
+    col = np.empty(max(e, 1), np.int32)
+    lib().orc_rgg_csr(n, _p(x), _p(y), radius, _p(rp), _p(col))
+    return rp, col[:e].copy()
+
+
+def statuses(ids, winner, nmsg, claimed=None):
+    """Per-agent task status after full TASK_CONFLICT delivery (agent.py:327-336).
+
+    A task with >= 1 conflict message ends ASSIGNED for the final winner and LOCKED for every
+    other agent (the last message names the final winner); with none it stays as the claim
+    phase left it: TENTATIVE where the agent claimed (``claimed[i, k]``), else OPEN."""
+    ids = np.asarray(ids)
+    n, t = len(ids), len(winner)
+    st = np.zeros((n, t), np.uint8)
+    if claimed is not None:
+        st[claimed] = TENTATIVE
+    has = np.asarray(nmsg) > 0
+    st[:, has] = LOCKED
+    win = (ids[:, None] == np.asarray(winner)[None, :]) & has[None, :]
+    st[win] = ASSIGNED
+    return st
+
+
+# ------------------------------------------------------------------ pure-Python restatements
+
+def elect_py(row_ptr, col, ids, max_rounds=100000):
+    """Straight restatement of the E2 rounds (tiny inputs only)."""
+    n = len(ids)
+    leader = [int(i) for i in ids]
+    changes = []
+    for _ in range(max_rounds):
+        snap = list(leader)
+        for v in range(n):
+            for u in col[row_ptr[v]:row_ptr[v + 1]]:
+                if snap[u] > leader[v]:
+                    leader[v] = snap[u]
+        c = sum(1 for v in range(n) if leader[v] != snap[v])
+        changes.append(c)
+        if c == 0:
+            break
+    state = [LEADER if leader[v] == ids[v] else FOLLOWER for v in range(n)]
+    return np.array(leader, np.int32), np.array(state, np.uint8), len(changes), np.array(changes)
+
+
+def utility_py(ax, ay, caps, tx, ty, treq, u_scale=100.0):
+    dist = math.sqrt((ax - tx) ** 2 + (ay - ty) ** 2)
+    has = 0.0 if (treq >= 0 and not (int(caps) >> int(treq)) & 1) else 1.0
+    return (u_scale / (1.0 + dist)) * has
+
+
+def f32(x: float) -> float:
+    return struct.unpack("!f", struct.pack("!f", x))[0]
+
+
+def allocate_py(ids, ax, ay, caps, tx, ty, treq, claim_thr=20.0, hysteresis=5.0):
+    """Straight restatement of claim -> resolve (tiny inputs only)."""
+    order = sorted(range(len(ids)), key=lambda i: int(ids[i]))
+    winner, util, nmsg = [], [], []
+    for k in range(len(tx)):
+        w, u, m = -1, 0.0, 0
+        for i in order:
+            U = utility_py(float(ax[i]), float(ay[i]), caps[i], float(tx[k]), float(ty[k]), int(treq[k]))
+            if U > claim_thr:
+                x = f32(U)
+                if w < 0 or x > u + hysteresis:
+                    w, u, m = int(ids[i]), x, m + 1
+                elif w != int(ids[i]):
+                    m += 1
+        winner.append(w)
+        util.append(u)
+        nmsg.append(m)
+    return np.array(winner, np.int32), np.array(util), np.array(nmsg)

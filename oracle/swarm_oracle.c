@@ -1,0 +1,243 @@
+/*
+ * swarm_oracle.c -- CPU restatement of the reference's per-round swarm step.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the checker: only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg load it.  The product path (libswarm.so) never links or
+ * calls it.
+ *
+ * Parity is pinned: tests/test_oracle_golden.py checks every function below against the
+ * golden vectors that tools/gen_golden.py produced by driving the reference's own handlers.
+ *
+ * Restated reference behaviour (file:line into the reference agent.py):
+ *   orc_elect     _handle_election_acclaim (263-275) / _handle_heartbeat (243-261) under the
+ *                 synchronous round contract E2:
+ *                 leader'[v] = max(leader[v], max_{u in N(v)} leader[u]); state LEADER iff
+ *                 leader == id; stop after the first round with zero changes.
+ *   orc_utility   _calculate_utility (338-347): d = sqrt(pow(dx,2) + pow(dy,2)),
+ *                 U = (100/(1+d)) * has_cap.  `**2` is CPython float_pow -> libm pow(x, 2.0),
+ *                 so this file is compiled with -fno-builtin (gcc would fold pow(x,2) to x*x).
+ *   orc_allocate  _process_tasks (292-302): claim iff U > 20.0 (fp64), payload f32(U) (RNE);
+ *                 _handle_task_claim (304-325) at the single resolver in ascending sender
+ *                 order: first claim wins, later claim wins iff x > u_cur + 5.0 (fp64);
+ *                 every accepted claim and every rejected claim from a non-incumbent emits one
+ *                 TASK_CONFLICT (322, 325).
+ *   orc_rgg_csr   synthetic input builder (not reference code): edge iff dx*dx+dy*dy <= r*r.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define ST_FOLLOWER 1
+#define ST_LEADER 3
+
+int orc_num_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
+void orc_set_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}
+
+/* Election to convergence.  leader[] is the working buffer (in: ignored, out: final).
+ * changes[] receives per-round change counts (capacity max_rounds).  Returns rounds_exec,
+ * or -1 if max_rounds passed without a zero-change round. */
+long orc_elect(long n, const int64_t *row_ptr, const int32_t *col, const int32_t *ids,
+               int32_t *leader, uint8_t *state, long max_rounds, int64_t *changes) {
+    int32_t *next = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+    for (long v = 0; v < n; ++v) leader[v] = ids[v];
+    long rounds = 0, done = 0;
+    while (rounds < max_rounds) {
+        long c = 0;
+#pragma omp parallel for schedule(static) reduction(+ : c)
+        for (long v = 0; v < n; ++v) {
+            int32_t m = leader[v];
+            for (int64_t e = row_ptr[v]; e < row_ptr[v + 1]; ++e) {
+                int32_t s = leader[col[e]];
+                if (s > m) m = s;
+            }
+            next[v] = m;
+            c += (m != leader[v]);
+        }
+        memcpy(leader, next, sizeof(int32_t) * (size_t)n);
+        changes[rounds++] = c;
+        if (c == 0) { done = 1; break; }
+    }
+    for (long v = 0; v < n; ++v) state[v] = (leader[v] == ids[v]) ? ST_LEADER : ST_FOLLOWER;
+    free(next);
+    return done ? rounds : -1;
+}
+
+/* One utility, reference arithmetic (libm pow) or GPU arithmetic (x*x) by `use_pow`. */
+static inline double util_one(double ax, double ay, uint32_t caps, double tx, double ty,
+                              int8_t treq, double u_scale, int use_pow) {
+    double dx = ax - tx, dy = ay - ty;
+    double sx = use_pow ? pow(dx, 2.0) : dx * dx;
+    double sy = use_pow ? pow(dy, 2.0) : dy * dy;
+    double d = sqrt(sx + sy);
+    double has = (treq >= 0 && !((caps >> treq) & 1u)) ? 0.0 : 1.0;
+    return (u_scale / (1.0 + d)) * has;
+}
+
+void orc_utility(long m, const double *ax, const double *ay, const uint32_t *caps,
+                 const double *tx, const double *ty, const int8_t *treq, double u_scale,
+                 int use_pow, double *out) {
+#pragma omp parallel for schedule(static)
+    for (long i = 0; i < m; ++i)
+        out[i] = util_one(ax[i], ay[i], caps[i], tx[i], ty[i], treq[i], u_scale, use_pow);
+}
+
+static int cmp_by_id(const void *a, const void *b, void *ids) {
+    int32_t x = ((const int32_t *)ids)[*(const long *)a], y = ((const int32_t *)ids)[*(const long *)b];
+    return (x > y) - (x < y);
+}
+
+static const int32_t *g_ids;
+static int cmp_by_id_g(const void *a, const void *b) { return cmp_by_id(a, b, (void *)g_ids); }
+
+/* Dense allocation (every agent x every task).  winner[]/util[] are in/out chain state
+ * (winner -1 = no current claim).  Per-task outputs: nclaim[k] claims, nmsg[k] conflict
+ * messages.  won[] (per agent, storage order) counts final wins.  Returns total claims. */
+long orc_allocate(long n, const int32_t *ids, const double *ax, const double *ay,
+                  const uint32_t *caps, long t, const double *tx, const double *ty,
+                  const int8_t *treq, double claim_thr, double hyst, double u_scale, int use_pow,
+                  int32_t *winner, double *util, int64_t *nclaim, int64_t *nmsg, int32_t *won) {
+    long *order = (long *)malloc(sizeof(long) * (size_t)(n > 0 ? n : 1));
+    for (long i = 0; i < n; ++i) order[i] = i;
+    g_ids = ids;
+    qsort(order, (size_t)n, sizeof(long), cmp_by_id_g);
+    long total = 0;
+#pragma omp parallel for schedule(dynamic, 4) reduction(+ : total)
+    for (long k = 0; k < t; ++k) {
+        int32_t w = winner[k];
+        double u = util[k];
+        int has = w >= 0;
+        int64_t cl = 0, ms = 0;
+        for (long j = 0; j < n; ++j) {
+            long i = order[j];
+            double U = util_one(ax[i], ay[i], caps[i], tx[k], ty[k], treq[k], u_scale, use_pow);
+            if (!(U > claim_thr)) continue;
+            ++cl;
+            double x = (double)(float)U;
+            if (!has || x > u + hyst) {
+                w = ids[i]; u = x; has = 1; ++ms;
+            } else if (w != ids[i]) {
+                ++ms;
+            }
+        }
+        winner[k] = w; util[k] = u; nclaim[k] = cl; nmsg[k] = ms; total += cl;
+    }
+    for (long i = 0; i < n; ++i) won[i] = 0;
+    /* won: map winner id -> storage index via the sorted order (binary search) */
+    for (long k = 0; k < t; ++k) {
+        if (winner[k] < 0) continue;
+        long lo = 0, hi = n - 1;
+        while (lo <= hi) {
+            long mid = (lo + hi) / 2;
+            int32_t v = ids[order[mid]];
+            if (v == winner[k]) { won[order[mid]] += 1; break; }
+            if (v < winner[k]) lo = mid + 1; else hi = mid - 1;
+        }
+    }
+    free(order);
+    return total;
+}
+
+/* Claims of one task only, in ascending-ID order (for chain-kernel debugging and the
+ * argmax comparisons in tests).  Returns the number written (<= cap). */
+long orc_task_claims(long n, const int32_t *ids, const double *ax, const double *ay,
+                     const uint32_t *caps, double tx, double ty, int8_t treq, double claim_thr,
+                     double u_scale, int use_pow, int32_t *out_id, float *out_x, long cap) {
+    long *order = (long *)malloc(sizeof(long) * (size_t)(n > 0 ? n : 1));
+    for (long i = 0; i < n; ++i) order[i] = i;
+    g_ids = ids;
+    qsort(order, (size_t)n, sizeof(long), cmp_by_id_g);
+    long m = 0;
+    for (long j = 0; j < n; ++j) {
+        long i = order[j];
+        double U = util_one(ax[i], ay[i], caps[i], tx, ty, treq, u_scale, use_pow);
+        if (U > claim_thr) {
+            if (m < cap) { out_id[m] = ids[i]; out_x[m] = (float)U; }
+            ++m;
+        }
+    }
+    free(order);
+    return m;
+}
+
+/* Radius-r geometric graph, rows sorted ascending.  Two calls: row_ptr only (col == NULL)
+ * to size, then fill.  Cell list with cells of side r. */
+typedef struct { long key; long idx; } kv_t;
+static int cmp_kv(const void *a, const void *b) {
+    const kv_t *x = (const kv_t *)a, *y = (const kv_t *)b;
+    if (x->key != y->key) return (x->key > y->key) - (x->key < y->key);
+    return (x->idx > y->idx) - (x->idx < y->idx);
+}
+static int cmp_i32(const void *a, const void *b) {
+    int32_t x = *(const int32_t *)a, y = *(const int32_t *)b;
+    return (x > y) - (x < y);
+}
+
+long orc_rgg_csr(long n, const double *x, const double *y, double r, int64_t *row_ptr,
+                 int32_t *col) {
+    if (n == 0) { row_ptr[0] = 0; return 0; }
+    double r2 = r * r;
+    long maxcx = 0, maxcy = 0;
+    for (long i = 0; i < n; ++i) {
+        long cx = (long)floor(x[i] / r), cy = (long)floor(y[i] / r);
+        if (cx > maxcx) maxcx = cx;
+        if (cy > maxcy) maxcy = cy;
+    }
+    long ncx = maxcx + 3, ncy = maxcy + 3;
+    kv_t *kv = (kv_t *)malloc(sizeof(kv_t) * (size_t)n);
+    for (long i = 0; i < n; ++i) {
+        long cx = (long)floor(x[i] / r), cy = (long)floor(y[i] / r);
+        kv[i].key = (cy + 1) * ncx + (cx + 1);
+        kv[i].idx = i;
+    }
+    qsort(kv, (size_t)n, sizeof(kv_t), cmp_kv);
+    long ncell = ncx * ncy;
+    long *start = (long *)calloc((size_t)ncell + 1, sizeof(long));
+    for (long i = 0; i < n; ++i) start[kv[i].key + 1]++;
+    for (long c = 0; c < ncell; ++c) start[c + 1] += start[c];
+    int fill = col != NULL;
+    if (!fill) row_ptr[0] = 0;
+#pragma omp parallel for schedule(dynamic, 1024)
+    for (long i = 0; i < n; ++i) {
+        long cx = (long)floor(x[i] / r) + 1, cy = (long)floor(y[i] / r) + 1;
+        long cnt = 0;
+        int64_t base = fill ? row_ptr[i] : 0;
+        for (long oy = -1; oy <= 1; ++oy)
+            for (long ox = -1; ox <= 1; ++ox) {
+                long c = (cy + oy) * ncx + (cx + ox);
+                for (long p = start[c]; p < start[c + 1]; ++p) {
+                    long j = kv[p].idx;
+                    if (j == i) continue;
+                    double dx = x[i] - x[j], dy = y[i] - y[j];
+                    if (dx * dx + dy * dy <= r2) {
+                        if (fill) col[base + cnt] = (int32_t)j;
+                        ++cnt;
+                    }
+                }
+            }
+        if (fill) qsort(col + base, (size_t)cnt, sizeof(int32_t), cmp_i32);
+        else row_ptr[i + 1] = cnt;
+    }
+    if (!fill)
+        for (long i = 0; i < n; ++i) row_ptr[i + 1] += row_ptr[i];
+    free(start);
+    free(kv);
+    return (long)row_ptr[n];
+}
