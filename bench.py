@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Headline benchmark: agent-rounds/sec of the swarm step (election to convergence + one
+10k-task allocation round) at 10M agents on MI355X (BASELINE.json config C3).
+
+A step = one full election (contract E2, all rounds to convergence) + one allocation round,
+over inputs already resident in HBM.  value = agents x rounds_exec x steps / elapsed, summed
+over ranks (weak scaling: every rank owns `--agents` agents).  Rank 0 prints ONE JSON line.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--agents 10000000] [--tasks 10000]
+  multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "distributed-swarm-algorithm_amd"))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--agents", type=int, default=10_000_000)
+    ap.add_argument("--tasks", type=int, default=10_000)
+    ap.add_argument("--deg", type=float, default=16.0)
+    ap.add_argument("--seed", type=int, default=2026)
+    ap.add_argument("--elect-mode", choices=["frontier", "dense"], default="frontier")
+    ap.add_argument("--roofline-rounds", type=int, default=20)
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the oracle timing")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    return ap.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from swarm_amd import _lib, gen
+    from swarm_amd.swarm import Swarm
+
+    dev = torch.device("cuda", local)
+    t0 = time.time()
+    d = gen.swarm_inputs(args.agents, args.seed + 7919 * rank, deg=args.deg, t=args.tasks)
+    sw = Swarm(d["ids"], d["x"], d["y"], d["caps"], device=dev).build_graph(1.0)
+    tpos_x = torch.as_tensor(d["tx"], device=dev)
+    tpos_y = torch.as_tensor(d["ty"], device=dev)
+    treq = torch.as_tensor(d["treq"], device=dev)
+    torch.cuda.synchronize()
+    n, e = sw.n, sw.n_edges
+    log(f"[rank {rank}] setup {time.time() - t0:.1f}s: n={n} E={e} tasks={args.tasks}")
+
+    def step():
+        r = sw.elect(mode=args.elect_mode, max_rounds=1 << 16)
+        a = sw.allocate(tpos_x, tpos_y, treq)
+        return r, a
+
+    for _ in range(args.warmup):
+        r, a = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    rounds_total = 0
+    for _ in range(args.steps):
+        r, a = step()
+        rounds_total += r.rounds_exec
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+
+    agent_rounds = float(n) * rounds_total
+    if world > 1:
+        t = torch.tensor([elapsed, agent_rounds], dtype=torch.float64, device=dev)
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        elapsed, agent_rounds = float(mx[0]), float(t[1])
+
+    # ---- split timing of one step (untimed replay): election vs allocation
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    ev[0].record()
+    r = sw.elect(mode=args.elect_mode, max_rounds=1 << 16)
+    ev[1].record()
+    a = sw.allocate(tpos_x, tpos_y, treq)
+    ev[2].record()
+    torch.cuda.synchronize()
+    t_elect_ms, t_alloc_ms = ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])
+
+    # ---- roofline of the dense election round (the north-star kernel), HIP events on the
+    # stream libswarm launches on (torch's current stream)
+    import ctypes
+    rp, col, lin = sw.row_ptr, sw.col, sw.ids
+    lout = torch.empty_like(lin)
+    changed = torch.zeros(1, dtype=torch.int64, device=dev)
+    L = _lib.lib()
+    for _ in range(3):
+        _lib.check(L.swarm_elect_round(_lib.ctx(), n, _lib.ptr(rp), _lib.ptr(col), _lib.ptr(lin),
+                                       _lib.ptr(lout), _lib.ptr(changed), _lib.stream()))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(args.roofline_rounds):
+        _lib.check(L.swarm_elect_round(_lib.ctx(), n, _lib.ptr(rp), _lib.ptr(col), _lib.ptr(lin),
+                                       _lib.ptr(lout), _lib.ptr(changed), _lib.stream()))
+    e1.record()
+    torch.cuda.synchronize()
+    dense_round_ms = e0.elapsed_time(e1) / args.roofline_rounds
+    bytes_round = 12 * n + 8 * e + 4
+    achieved = bytes_round / (dense_round_ms * 1e-3) / 1e9
+    del ctypes
+
+    out = None
+    if rank == 0:
+        value = agent_rounds / elapsed
+        out = {
+            "metric": "agent-rounds/sec (election+allocation) at 10M agents; % of HBM roofline",
+            "value": value,
+            "unit": "agent-rounds/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32+f64",
+            "data": "synthetic (seeded RGG, SplitMix64)",
+            "config": {"workload": "C3: %d agents/GPU, deg %g RGG, election to convergence + %d-task allocation"
+                       % (n, args.deg, args.tasks),
+                       "agents_per_gpu": n, "edges_per_gpu": e, "tasks": args.tasks,
+                       "elect_mode": args.elect_mode, "alloc_mode": a.stats.get("mode_used"),
+                       "rounds_exec": r.rounds_exec, "parallelism": f"agents sharded x{world}"},
+            "breakdown_ms": {"elect": t_elect_ms, "alloc": t_alloc_ms},
+            "hbm_frac_step": (r.rounds_exec * bytes_round + 24 * n + 36 * args.tasks)
+            / ((t_elect_ms + t_alloc_ms) * 1e-3) / (HBM_PEAK_GBS * 1e9),
+            "roofline": {"kernel": "k_elect_dense (one E2 round)", "bound": "hbm",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "bytes_per_launch": bytes_round, "avg_launch_ms": dense_round_ms},
+            "elect_stats": {"rounds_launched": r.rounds_launched, "active_total": r.active_total,
+                            "edges_total": r.edges_total},
+            "alloc_stats": a.stats,
+        }
+    # ---- CPU baseline: the oracle restatement on the host cores, bounded sample
+    if rank == 0 and args.cpu_baseline:
+        from oracle import oracle
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        oracle.set_threads(threads)
+        rph = rp.cpu().numpy().astype(np.int64)
+        colh = col.cpu().numpy()
+        idsh = sw.ids.cpu().numpy()
+        k = 1
+        t1 = time.perf_counter()
+        oracle.elect(rph, colh, idsh, max_rounds=k)
+        per_round = time.perf_counter() - t1
+        k = max(1, min(200, int(args.cpu_seconds * 0.6 / max(per_round, 1e-6))))
+        t1 = time.perf_counter()
+        oracle.elect(rph, colh, idsh, max_rounds=k)
+        per_round = (time.perf_counter() - t1) / k
+        # allocation: dense reference algorithm over a task sample (probe, then scale)
+        def alloc_sample(ts):
+            t1 = time.perf_counter()
+            oracle.allocate(d["ids"], d["x"], d["y"], d["caps"], d["tx"][:ts], d["ty"][:ts], d["treq"][:ts])
+            return (time.perf_counter() - t1) / ts
+        ts = min(args.tasks, max(threads, 1))
+        per_task = alloc_sample(ts)
+        ts = max(1, min(args.tasks, int(args.cpu_seconds * 0.4 / max(per_task, 1e-9))))
+        per_task = alloc_sample(ts)
+        t_est = per_round * r.rounds_exec + per_task * args.tasks
+        out["cpu_baseline"] = {
+            "value": n * r.rounds_exec / t_est, "unit": "agent-rounds/s", "cores": threads,
+            "kind": "port",
+            "sample": f"C oracle (OpenMP x{threads}): {k} dense E2 rounds on the full {n}-agent graph "
+                      f"({per_round * 1e3:.1f} ms/round) + dense allocation of {ts} tasks "
+                      f"({per_task * 1e3:.2f} ms/task); step time extrapolated to {r.rounds_exec} rounds "
+                      f"+ {args.tasks} tasks = {t_est:.1f} s"}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,559 @@
+// Task allocation round (contract A-H) on gfx950.
+//
+// Replaces, batched over every agent and task:
+//   _process_tasks + _calculate_utility (agent.py:292-302, 338-347): claim iff U > 20.0 (fp64),
+//       claim value x = f32(U) (struct '!If', round-to-nearest-even);
+//   _handle_task_claim (agent.py:304-325) at the resolver, claims in ascending sender ID:
+//       first claim wins, a later one wins iff x > u_cur + 5.0; every accepted claim and every
+//       rejected claim from a non-incumbent emits one TASK_CONFLICT;
+//   _handle_task_conflict (agent.py:327-336): winner ASSIGNED, everyone else LOCKED (derived
+//       from winner / nmsg, never materialised as an N x T matrix).
+//
+// The chain is NOT argmax: with hysteresis h the winner is the end of the "record chain"
+//   c1 = min-ID claim (or min-ID claim with x > u0 + h if the task already had a winner),
+//   c_{k+1} = min-ID claim with ID > id(c_k) and x > x(c_k) + h.
+// Each link is one workgroup-wide min-ID reduction over the task's claims held in LDS; with
+// x in (thr, u_scale] and h = 5 there are at most 17 links.  h = 0 gives argmax with the
+// lowest-ID tie-break (the north star's "wavefront argmin" mode) through the same code.
+//
+// BINNED (exact): U > thr <=> d < Rc = u_scale/thr - 1 (has_cap), so only agents inside a
+// slightly larger radius Rp can claim.  Agents are bucketed in a uniform grid (hipCUB radix
+// sort); one workgroup per task walks the 2-3 grid rows its Rp-disc covers, evaluates U in
+// fp64 (no FMA contraction: matches the reference's separately rounded squares), appends
+// claims to LDS, then walks the chain.  Per task ~pi*Rp^2*density candidates instead of N.
+// DENSE: agents in ascending-ID tiles of 256; each workgroup stages 64 tasks in LDS and
+// records, per (task, tile), the max claim value and claim count; the chain then walks
+// tiles (ballot over tile maxima) and re-evaluates only the one tile a link lands in.
+#include "binning.h"
+
+#include <climits>
+
+namespace swarm {
+namespace {
+
+constexpr int kCap = 2048;  // claims per task kept in LDS (beyond: exact recompute path)
+
+__device__ __forceinline__ double utility(double ax, double ay, uint32_t caps, double tx, double ty,
+                                          int rq, double u_scale) {
+    const double dx = ax - tx, dy = ay - ty;
+    const double d = sqrt(dx * dx + dy * dy);
+    const double has = (rq >= 0 && !((caps >> rq) & 1u)) ? 0.0 : 1.0;
+    return (u_scale / (1.0 + d)) * has;
+}
+
+// Could the reference (libm pow for the squares, <= 2 ulp away) decide or round differently?
+__device__ __forceinline__ bool guard_flag(double U, double thr) {
+    const double band = fmax(fabs(thr), fabs(U)) * 0x1p-49;
+    if (fabs(U - thr) <= band) return true;
+    if (U > thr) {
+        const double e = fabs(U) * 0x1p-50;
+        return float(U - e) != float(U + e);
+    }
+    return false;
+}
+
+__device__ __forceinline__ int block_min_int(int v, int *s_red) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    int m = s_red[0];
+#pragma unroll
+    for (int w = 1; w < kBlock / kWave; ++w) m = min(m, s_red[w]);
+    return m;
+}
+
+__device__ __forceinline__ long long block_sum_ll(long long v, long long *s_red) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    long long m = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / kWave; ++w) m += s_red[w];
+    return m;
+}
+
+struct Params {
+    double thr, h, u_scale, rp2;
+    int32_t *winner;
+    double *util;
+    int32_t *won;
+    const int32_t *id_to_index;
+    int64_t id_span;
+    int64_t *nclaim;
+    int64_t *nmsg;
+    unsigned long long *stats;  // kStatShards x 16 u64: [claims, conflicts, flagged, candidates, overflow]
+};
+
+constexpr int kStatShards = 64;   // each shard on its own 128-B line
+constexpr int kStatStride = 16;
+
+// Per-workgroup totals, flushed once per workgroup into one of 64 shards (a single
+// contended counter costs ~12 ns per arrival: MI355X_MICROARCH.md 'fanin').
+struct BlockStats {
+    unsigned long long claims = 0, msgs = 0, overflow = 0;
+};
+
+__device__ __forceinline__ void flush_stats(const Params &P, unsigned long long claims, unsigned long long msgs,
+                                            unsigned long long flagged, unsigned long long cand,
+                                            unsigned long long overflow) {
+    unsigned long long *sh = P.stats + size_t(blockIdx.x & (kStatShards - 1)) * kStatStride;
+    if (claims) atomicAdd(sh + 0, claims);
+    if (msgs) atomicAdd(sh + 1, msgs);
+    if (flagged) atomicAdd(sh + 2, flagged);
+    if (cand) atomicAdd(sh + 3, cand);
+    if (overflow) atomicAdd(sh + 4, overflow);
+}
+
+__global__ void k_fold_stats(const unsigned long long *__restrict__ sh, unsigned long long *__restrict__ out) {
+    for (int c = 0; c < 5; ++c) {
+        unsigned long long v = sh[size_t(threadIdx.x) * kStatStride + c];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        if (threadIdx.x == 0) out[c] = v;
+    }
+}
+
+// Per-task epilogue shared by both strategies.
+__device__ __forceinline__ void finish_task(const Params &P, int64_t k, int w0, double u0, bool w0_claimed,
+                                            int accepted, int first_id, int cur_id, double cur_u,
+                                            int cur_idx, long long nclaims, BlockStats &bs) {
+    const long long msgs = nclaims - ((w0 >= 0 && w0_claimed && (accepted == 0 || w0 < first_id)) ? 1 : 0);
+    if (accepted > 0) {
+        P.winner[k] = cur_id;
+        P.util[k] = cur_u;
+        if (P.won) atomicAdd(&P.won[cur_idx], 1);
+    } else if (w0 >= 0 && P.won && P.id_to_index && w0 < P.id_span) {
+        const int ix = P.id_to_index[w0];
+        if (ix >= 0) atomicAdd(&P.won[ix], 1);
+    }
+    if (P.nclaim) P.nclaim[k] = nclaims;
+    if (P.nmsg) P.nmsg[k] = msgs;
+    bs.claims += (unsigned long long)nclaims;
+    bs.msgs += (unsigned long long)msgs;
+}
+
+// ------------------------------------------------------------------------------ binned
+__global__ __launch_bounds__(kBlock) void k_alloc_binned(
+    int64_t t_count, const double2 *__restrict__ tpos, const int8_t *__restrict__ treq,
+    const int32_t *__restrict__ ids, const double2 *__restrict__ apos,
+    const uint32_t *__restrict__ caps, const int32_t *__restrict__ sorted_idx,
+    const uint32_t *__restrict__ cell_off, Grid g, double rp, Params P) {
+    __shared__ int s_id[kCap];
+    __shared__ float s_x[kCap];
+    __shared__ int s_ix[kCap];
+    __shared__ int s_n, s_w0c, s_red[kBlock / kWave], s_sel_ix;
+    __shared__ float s_sel_x;
+    __shared__ long long s_red64[kBlock / kWave];
+    long long my_cand = 0, my_flag = 0;
+    BlockStats bs;
+    for (int64_t k = blockIdx.x; k < t_count; k += gridDim.x) {
+        const double2 tp = tpos[k];
+        const int rq = treq[k];
+        const int w0 = P.winner[k];
+        const double u0 = P.util[k];
+        if (threadIdx.x == 0) { s_n = 0; s_w0c = 0; }
+        __syncthreads();
+        // task's Rp-disc in grid coordinates (empty if it misses the agents' bounding box)
+        const bool miss = tp.x + rp < g.xmin || tp.x - rp > g.xmax || tp.y + rp < g.ymin || tp.y - rp > g.ymax;
+        const int64_t x0 = miss ? 1 : cell_coord(tp.x - rp, g.xmin, g.inv_cell, g.ncx);
+        const int64_t x1 = miss ? 0 : cell_coord(tp.x + rp, g.xmin, g.inv_cell, g.ncx);
+        const int64_t y0 = miss ? 1 : cell_coord(tp.y - rp, g.ymin, g.inv_cell, g.ncy);
+        const int64_t y1 = miss ? 0 : cell_coord(tp.y + rp, g.ymin, g.inv_cell, g.ncy);
+        // pass 1: evaluate candidates, keep claims in LDS
+        for (int64_t yy = y0; yy <= y1; ++yy) {
+            const uint32_t a = cell_off[yy * g.ncx + x0], b = cell_off[yy * g.ncx + x1 + 1];
+            for (uint32_t q = a + threadIdx.x; q < b; q += kBlock) {
+                const int32_t i = sorted_idx[q];
+                const double2 p = apos[i];
+                const double dx = p.x - tp.x, dy = p.y - tp.y;
+                if (dx * dx + dy * dy > P.rp2) continue;
+                ++my_cand;
+                const double U = utility(p.x, p.y, caps[i], tp.x, tp.y, rq, P.u_scale);
+                my_flag += guard_flag(U, P.thr);
+                if (U > P.thr) {
+                    const int id = ids[i];
+                    const int slot = atomicAdd(&s_n, 1);
+                    if (slot < kCap) { s_id[slot] = id; s_x[slot] = float(U); s_ix[slot] = i; }
+                    if (id == w0) s_w0c = 1;
+                }
+            }
+        }
+        __syncthreads();
+        const int nclaims = s_n;
+        const bool overflow = nclaims > kCap;
+        // pass 2: the record chain
+        int prev = -1, cur_id = w0, cur_idx = -1, accepted = 0, first_id = -1;
+        bool has = w0 >= 0;
+        double cur_u = u0;
+        for (;;) {
+            int best = INT_MAX, best_ix = -1;
+            float best_x = 0.f;
+            if (!overflow) {
+                for (int j = threadIdx.x; j < nclaims; j += kBlock) {
+                    const int id = s_id[j];
+                    if (id > prev && id < best && (!has || double(s_x[j]) > cur_u + P.h)) {
+                        best = id; best_x = s_x[j]; best_ix = s_ix[j];
+                    }
+                }
+            } else {  // exact recompute over the candidates (rare: > kCap claims on one task)
+                for (int64_t yy = y0; yy <= y1; ++yy) {
+                    const uint32_t a = cell_off[yy * g.ncx + x0], b = cell_off[yy * g.ncx + x1 + 1];
+                    for (uint32_t q = a + threadIdx.x; q < b; q += kBlock) {
+                        const int32_t i = sorted_idx[q];
+                        const double2 p = apos[i];
+                        const double dx = p.x - tp.x, dy = p.y - tp.y;
+                        if (dx * dx + dy * dy > P.rp2) continue;
+                        const double U = utility(p.x, p.y, caps[i], tp.x, tp.y, rq, P.u_scale);
+                        const int id = ids[i];
+                        if (U > P.thr && id > prev && id < best && (!has || double(float(U)) > cur_u + P.h)) {
+                            best = id; best_x = float(U); best_ix = i;
+                        }
+                    }
+                }
+            }
+            const int win = block_min_int(best, s_red);
+            if (win == INT_MAX) break;
+            if (best == win) { s_sel_x = best_x; s_sel_ix = best_ix; }
+            __syncthreads();
+            cur_id = win; cur_u = double(s_sel_x); cur_idx = s_sel_ix; has = true; prev = win;
+            if (++accepted == 1) first_id = win;
+        }
+        if (threadIdx.x == 0) {
+            finish_task(P, k, w0, u0, s_w0c != 0, accepted, first_id, cur_id, cur_u, cur_idx, nclaims, bs);
+            bs.overflow += overflow ? 1 : 0;
+        }
+        __syncthreads();
+    }
+    const long long c = block_sum_ll(my_cand, s_red64);
+    const long long f = block_sum_ll(my_flag, s_red64);
+    if (threadIdx.x == 0) flush_stats(P, bs.claims, bs.msgs, (unsigned long long)f, (unsigned long long)c, bs.overflow);
+}
+
+// ------------------------------------------------------------------------------- dense
+constexpr int kTileA = 256;  // agents per tile (one per thread)
+constexpr int kTileT = 64;   // tasks staged in LDS per workgroup
+
+// Agents in ascending-ID order: order[j] = storage index of the j-th smallest ID.
+// Per (task k, agent tile a): tmax[k * ntiles + a] = max claim value in the tile (or -inf),
+// tcnt likewise the number of claims.
+__global__ __launch_bounds__(kBlock) void k_alloc_dense_tiles(
+    int64_t n, int64_t t_count, const double2 *__restrict__ tpos, const int8_t *__restrict__ treq,
+    const double2 *__restrict__ apos, const uint32_t *__restrict__ caps,
+    const int32_t *__restrict__ order, int64_t ntiles, float *__restrict__ tmax,
+    int *__restrict__ tcnt, Params P) {
+    __shared__ double s_tx[kTileT], s_ty[kTileT];
+    __shared__ int s_rq[kTileT];
+    __shared__ float s_max[kTileT][kBlock / kWave];
+    __shared__ int s_cnt[kTileT][kBlock / kWave];
+    __shared__ long long s_red64[kBlock / kWave];
+    const int64_t ttiles = (t_count + kTileT - 1) / kTileT;
+    long long my_flag = 0;
+    for (int64_t blk = blockIdx.x; blk < ntiles * ttiles; blk += gridDim.x) {
+        const int64_t at = blk % ntiles, tt = blk / ntiles;
+        __syncthreads();
+        if (threadIdx.x < kTileT) {
+            const int64_t k = tt * kTileT + threadIdx.x;
+            const bool ok = k < t_count;
+            s_tx[threadIdx.x] = ok ? tpos[k].x : 0.0;
+            s_ty[threadIdx.x] = ok ? tpos[k].y : 0.0;
+            s_rq[threadIdx.x] = ok ? int(treq[k]) : -1;
+        }
+        __syncthreads();
+        const int64_t j = at * kTileA + threadIdx.x;
+        const bool valid = j < n;
+        double ax = 0, ay = 0;
+        uint32_t c = 0;
+        if (valid) {
+            const int32_t i = order[j];
+            const double2 p = apos[i];
+            ax = p.x; ay = p.y; c = caps[i];
+        }
+        for (int q = 0; q < kTileT; ++q) {
+            float x = -INFINITY;
+            int claim = 0;
+            if (valid) {
+                const double U = utility(ax, ay, c, s_tx[q], s_ty[q], s_rq[q], P.u_scale);
+                my_flag += guard_flag(U, P.thr);
+                if (U > P.thr) { x = float(U); claim = 1; }
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                x = fmaxf(x, __shfl_xor(x, off, 64));
+                claim += __shfl_xor(claim, off, 64);
+            }
+            if ((threadIdx.x & 63) == 0) { s_max[q][threadIdx.x >> 6] = x; s_cnt[q][threadIdx.x >> 6] = claim; }
+        }
+        __syncthreads();
+        if (threadIdx.x < kTileT) {
+            const int64_t k = tt * kTileT + threadIdx.x;
+            if (k < t_count) {
+                float m = s_max[threadIdx.x][0];
+                int cc = s_cnt[threadIdx.x][0];
+                for (int w = 1; w < kBlock / kWave; ++w) { m = fmaxf(m, s_max[threadIdx.x][w]); cc += s_cnt[threadIdx.x][w]; }
+                tmax[k * ntiles + at] = m;
+                tcnt[k * ntiles + at] = cc;
+            }
+        }
+    }
+    const long long f = block_sum_ll(my_flag, s_red64);
+    if (threadIdx.x == 0 && f) flush_stats(P, 0, 0, (unsigned long long)f, 0, 0);
+}
+
+// One wave per task: walk the record chain over the tile summaries.
+__global__ __launch_bounds__(kBlock) void k_alloc_dense_chain(
+    int64_t n, int64_t t_count, const double2 *__restrict__ tpos, const int8_t *__restrict__ treq,
+    const int32_t *__restrict__ ids, const double2 *__restrict__ apos,
+    const uint32_t *__restrict__ caps, const int32_t *__restrict__ order,
+    const uint32_t *__restrict__ sorted_ids, int64_t ntiles, const float *__restrict__ tmax,
+    const int *__restrict__ tcnt, Params P) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> 6;
+    const int64_t nwaves = (int64_t(gridDim.x) * kBlock) >> 6;
+    BlockStats bs;
+    __shared__ unsigned long long s_c[kBlock / kWave], s_m[kBlock / kWave];
+    for (int64_t k = wave; k < t_count; k += nwaves) {
+        const double2 tp = tpos[k];
+        const int rq = treq[k];
+        const int w0 = P.winner[k];
+        const double u0 = P.util[k];
+        const float *mk = tmax + k * ntiles;
+        const int *ck = tcnt + k * ntiles;
+        long long nclaims = 0;
+        for (int64_t a = lane; a < ntiles; a += 64) nclaims += ck[a];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) nclaims += __shfl_xor(nclaims, off, 64);
+        // did the incumbent claim?  (binary search of w0 in the ID-sorted keys)
+        bool w0_claimed = false;
+        if (w0 >= 0 && nclaims > 0) {
+            int64_t lo = 0, hi = n - 1;
+            while (lo <= hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                const uint32_t v = sorted_ids[mid];
+                if (v == uint32_t(w0)) {
+                    const int32_t i = order[mid];
+                    const double2 p = apos[i];
+                    w0_claimed = utility(p.x, p.y, caps[i], tp.x, tp.y, rq, P.u_scale) > P.thr;
+                    break;
+                }
+                if (v < uint32_t(w0)) lo = mid + 1; else hi = mid - 1;
+            }
+        }
+        // chain: position pos (in ID order) of the current winner; -1 before the first link
+        int64_t pos = -1;
+        bool has = w0 >= 0;
+        double cur_u = u0;
+        int cur_id = w0, cur_idx = -1, accepted = 0, first_id = -1;
+        for (;;) {
+            // first tile after pos whose max could host a link
+            const int64_t tstart = (pos + 1) / kTileA;
+            int64_t found_tile = -1;
+            for (int64_t a0 = tstart; a0 < ntiles && found_tile < 0; a0 += 64) {
+                const int64_t a = a0 + lane;
+                const float m = a < ntiles ? mk[a] : -INFINITY;
+                const bool ok = a < ntiles && m != -INFINITY && (!has || double(m) > cur_u + P.h);
+                const unsigned long long b = __ballot(ok);
+                if (b) found_tile = a0 + __ffsll((long long)b) - 1;
+            }
+            if (found_tile < 0) break;
+            // inside the tile: first agent j > pos with a qualifying claim (4 sub-chunks of 64)
+            int64_t hitj = -1;
+            float hitx = 0.f;
+            int hit_ix = -1;
+            for (int64_t j0 = found_tile * kTileA; j0 < (found_tile + 1) * kTileA && hitj < 0; j0 += 64) {
+                const int64_t j = j0 + lane;
+                bool ok = false;
+                float x = 0.f;
+                int32_t i = -1;
+                if (j < n && j > pos) {
+                    i = order[j];
+                    const double2 p = apos[i];
+                    const double U = utility(p.x, p.y, caps[i], tp.x, tp.y, rq, P.u_scale);
+                    x = float(U);
+                    ok = U > P.thr && (!has || double(x) > cur_u + P.h);
+                }
+                const unsigned long long b = __ballot(ok);
+                if (b) {
+                    const int src = __ffsll((long long)b) - 1;
+                    hitj = j0 + src;
+                    hitx = __shfl(x, src, 64);
+                    hit_ix = __shfl(i, src, 64);
+                }
+            }
+            if (hitj < 0) {  // tile max qualified but every qualifying claim sits at or before pos
+                pos = (found_tile + 1) * kTileA - 1;
+                continue;
+            }
+            pos = hitj;
+            cur_idx = hit_ix;
+            cur_id = ids[hit_ix];
+            cur_u = double(hitx);
+            has = true;
+            if (++accepted == 1) first_id = cur_id;
+        }
+        if (lane == 0)
+            finish_task(P, k, w0, u0, w0_claimed, accepted, first_id, cur_id, cur_u, cur_idx, nclaims, bs);
+    }
+    if (lane == 0) { s_c[threadIdx.x >> 6] = bs.claims; s_m[threadIdx.x >> 6] = bs.msgs; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long c = 0, m = 0;
+        for (int w = 0; w < kBlock / kWave; ++w) { c += s_c[w]; m += s_m[w]; }
+        flush_stats(P, c, m, 0, 0, 0);
+    }
+}
+
+// Ascending-ID order of agents (dense mode): radix sort of (id, index).
+__global__ __launch_bounds__(kBlock) void k_iota_ids(const int32_t *__restrict__ ids, int64_t n,
+                                                    uint32_t *__restrict__ keys, int32_t *__restrict__ vals) {
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+        keys[i] = uint32_t(ids[i]);
+        vals[i] = int32_t(i);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_utility(int64_t m, const double2 *__restrict__ apos,
+                                                   const uint32_t *__restrict__ caps,
+                                                   const double2 *__restrict__ tpos,
+                                                   const int8_t *__restrict__ treq, double u_scale,
+                                                   double *__restrict__ out) {
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < m; i += int64_t(gridDim.x) * kBlock) {
+        const double2 a = apos[i], t = tpos[i];
+        out[i] = utility(a.x, a.y, caps[i], t.x, t.y, treq[i], u_scale);
+    }
+}
+
+}  // namespace
+}  // namespace swarm
+
+extern "C" {
+
+int swarm_allocate(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos,
+                   const uint32_t *acaps, int64_t t, const double *tpos, const int8_t *treq,
+                   double claim_thr, double hysteresis, double u_scale, int32_t mode,
+                   int32_t *winner, double *util, int32_t *won, const int32_t *id_to_index,
+                   int64_t id_span, int64_t *nclaim, int64_t *nmsg, swarm_alloc_stats *stats,
+                   void *stream) {
+    using namespace swarm;
+    SW_ARG(ctx != nullptr, "ctx is NULL");
+    SW_ARG(n >= 0 && n < (int64_t(1) << 31), "n out of range");
+    SW_ARG(t >= 0 && t < (int64_t(1) << 31), "t out of range");
+    SW_ARG(std::isfinite(claim_thr) && std::isfinite(hysteresis) && std::isfinite(u_scale),
+           "claim_thr / hysteresis / u_scale must be finite");
+    SW_ARG(mode == SWARM_ALLOC_AUTO || mode == SWARM_ALLOC_BINNED || mode == SWARM_ALLOC_DENSE,
+           "unknown mode");
+    SW_ARG(n == 0 || (ids && apos && acaps), "NULL agent array");
+    SW_ARG(t == 0 || (tpos && treq && winner && util), "NULL task array");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    unsigned long long *dstats;
+    SW_ALLOC(dstats, ctx, S_ASTATS, (size_t(kStatShards) * kStatStride + 8) * 8);
+    SW_HIP(hipMemsetAsync(dstats, 0, size_t(kStatShards) * kStatStride * 8, s));
+    if (won && n) SW_HIP(hipMemsetAsync(won, 0, size_t(n) * 4, s));
+
+    // claim radius: U > thr  <=>  d < u_scale / thr - 1  (thr > 0, u_scale > 0, has_cap)
+    const bool finite_r = claim_thr > 0 && u_scale > 0;
+    const double rc = finite_r ? u_scale / claim_thr - 1.0 : 0.0;
+    int used = mode;
+    if (mode == SWARM_ALLOC_AUTO) used = finite_r ? SWARM_ALLOC_BINNED : SWARM_ALLOC_DENSE;
+    SW_ARG(!(used == SWARM_ALLOC_BINNED && !finite_r),
+           "binned mode needs claim_thr > 0 and u_scale > 0 (finite claim radius)");
+    Params P;
+    P.thr = claim_thr; P.h = hysteresis; P.u_scale = u_scale;
+    P.winner = winner; P.util = util; P.won = won; P.id_to_index = id_to_index;
+    P.id_span = id_span; P.nclaim = nclaim; P.nmsg = nmsg; P.stats = dstats;
+
+    const bool nothing = (n == 0) || (used == SWARM_ALLOC_BINNED && rc <= 0.0);
+    if (t > 0 && nothing) {
+        // no agent can claim: every task keeps its current claim (won credited via id_to_index)
+        const double rp = 0.0;
+        Grid g{0, 0, -1, -1, 1, 1, 1, 1};
+        uint32_t *off;
+        SW_ALLOC(off, ctx, S_CELL_START, 16);
+        SW_HIP(hipMemsetAsync(off, 0, 16, s));
+        P.rp2 = -1.0;
+        hipLaunchKernelGGL(k_alloc_binned, dim3(grid_for(t, 1, 4096)), dim3(kBlock), 0, s, t,
+                           reinterpret_cast<const double2 *>(tpos), treq, ids,
+                           reinterpret_cast<const double2 *>(apos), acaps, (const int32_t *)nullptr,
+                           off, g, rp, P);
+        SW_LAUNCHED();
+    } else if (t > 0 && used == SWARM_ALLOC_BINNED) {
+        const double rp = rc * (1.0 + 1e-9) + 1e-12;
+        P.rp2 = rp * rp;
+        Grid g;
+        int rcode = make_grid(ctx, n, apos, rp, 2 * n + 1024, &g, s);
+        if (rcode) return rcode;
+        int32_t *sorted;
+        uint32_t *off;
+        if ((rcode = bin_agents(ctx, n, apos, g, &sorted, &off, s))) return rcode;
+        hipLaunchKernelGGL(k_alloc_binned, dim3(grid_for(t, 1, 4096)), dim3(kBlock), 0, s, t,
+                           reinterpret_cast<const double2 *>(tpos), treq, ids,
+                           reinterpret_cast<const double2 *>(apos), acaps, sorted, off, g, rp, P);
+        SW_LAUNCHED();
+    } else if (t > 0) {
+        P.rp2 = 0;
+        const int64_t ntiles = (n + kTileA - 1) / kTileA;
+        uint32_t *kin, *kout;
+        int32_t *vin, *order;
+        SW_ALLOC(kin, ctx, S_KEYS_IN, size_t(n) * 4);
+        SW_ALLOC(kout, ctx, S_KEYS_OUT, size_t(n) * 4);
+        SW_ALLOC(vin, ctx, S_VALS_IN, size_t(n) * 4);
+        SW_ALLOC(order, ctx, S_ORDER, size_t(n) * 4);
+        hipLaunchKernelGGL(k_iota_ids, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, ids, n, kin, vin);
+        SW_LAUNCHED();
+        size_t tmp_bytes = 0;
+        SW_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kin, kout, vin, order, int(n), 0, 32, s));
+        void *tmp;
+        SW_ALLOC(tmp, ctx, S_CUB_TMP, tmp_bytes);
+        SW_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, order, int(n), 0, 32, s));
+        float *tmax;
+        int *tcnt;
+        SW_ALLOC(tmax, ctx, S_TILEMAX, size_t(t) * size_t(ntiles) * 4);
+        SW_ALLOC(tcnt, ctx, S_TMP1, size_t(t) * size_t(ntiles) * 4);
+        const int64_t blocks = ntiles * ((t + kTileT - 1) / kTileT);
+        hipLaunchKernelGGL(k_alloc_dense_tiles, dim3(grid_for(blocks, 1, 1u << 20)), dim3(kBlock), 0, s, n, t,
+                           reinterpret_cast<const double2 *>(tpos), treq,
+                           reinterpret_cast<const double2 *>(apos), acaps, order, ntiles, tmax, tcnt, P);
+        SW_LAUNCHED();
+        hipLaunchKernelGGL(k_alloc_dense_chain, dim3(grid_for(t, kBlock / kWave, 1u << 20)), dim3(kBlock), 0, s,
+                           n, t, reinterpret_cast<const double2 *>(tpos), treq, ids,
+                           reinterpret_cast<const double2 *>(apos), acaps, order, kout, ntiles, tmax,
+                           tcnt, P);
+        SW_LAUNCHED();
+    }
+    unsigned long long *hs = static_cast<unsigned long long *>(pinned(ctx, 64));
+    if (!hs) return SWARM_ERR_OOM;
+    unsigned long long *folded = dstats + size_t(kStatShards) * kStatStride;
+    hipLaunchKernelGGL(k_fold_stats, dim3(1), dim3(kWave), 0, s, dstats, folded);
+    SW_LAUNCHED();
+    SW_HIP(hipMemcpyAsync(hs, folded, 40, hipMemcpyDeviceToHost, s));
+    SW_HIP(hipStreamSynchronize(s));
+    if (stats) {
+        stats->n_claims = int64_t(hs[0]);
+        stats->n_conflicts = int64_t(hs[1]);
+        stats->n_flagged = int64_t(hs[2]);
+        stats->n_candidates = used == SWARM_ALLOC_DENSE ? n * t : int64_t(hs[3]);
+        stats->n_overflow = int64_t(hs[4]);
+        stats->mode_used = used;
+    }
+    return SWARM_OK;
+}
+
+int swarm_utility(swarm_ctx *ctx, int64_t m, const double *apos, const uint32_t *acaps,
+                  const double *tpos, const int8_t *treq, double u_scale, double *out, void *stream) {
+    using namespace swarm;
+    SW_ARG(ctx != nullptr, "ctx is NULL");
+    SW_ARG(m >= 0, "m < 0");
+    if (m == 0) return SWARM_OK;
+    SW_ARG(apos && acaps && tpos && treq && out, "NULL array");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(k_utility, dim3(grid_for(m, kBlock, 8192)), dim3(kBlock), 0, s, m,
+                       reinterpret_cast<const double2 *>(apos), acaps,
+                       reinterpret_cast<const double2 *>(tpos), treq, u_scale, out);
+    SW_LAUNCHED();
+    return SWARM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,83 @@
+// Context, scratch ownership and error reporting for libswarm.so.
+#include <cstdarg>
+#include <new>
+
+#include "swarm_common.h"
+
+namespace swarm {
+
+static thread_local char g_err[1024] = "";
+
+void set_error(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+void *scratch(swarm_ctx *ctx, Slot s, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (ctx->cap[s] >= bytes) return ctx->slot[s];
+    if (ctx->slot[s]) {
+        (void)hipFree(ctx->slot[s]);
+        ctx->slot[s] = nullptr;
+        ctx->cap[s] = 0;
+    }
+    size_t want = bytes + bytes / 8;  // headroom against small growth
+    void *p = nullptr;
+    hipError_t e = hipMalloc(&p, want);
+    if (e != hipSuccess) {
+        set_error("scratch slot %d: hipMalloc(%zu) -> %s", int(s), want, hipGetErrorString(e));
+        return nullptr;
+    }
+    ctx->slot[s] = p;
+    ctx->cap[s] = want;
+    return p;
+}
+
+void *pinned(swarm_ctx *ctx, size_t bytes) {
+    if (ctx->host_cap >= bytes) return ctx->host_pinned;
+    if (ctx->host_pinned) (void)hipHostFree(ctx->host_pinned);
+    ctx->host_pinned = nullptr;
+    ctx->host_cap = 0;
+    void *p = nullptr;
+    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        set_error("hipHostMalloc(%zu) -> %s", bytes, hipGetErrorString(e));
+        return nullptr;
+    }
+    ctx->host_pinned = p;
+    ctx->host_cap = bytes;
+    return p;
+}
+
+}  // namespace swarm
+
+extern "C" {
+
+const char *swarm_last_error(void) { return swarm::g_err; }
+
+const char *swarm_version(void) { return "swarm-mi355x 0.1.0 (gfx950)"; }
+
+int swarm_ctx_create(swarm_ctx **out) {
+    SW_ARG(out != nullptr, "out is NULL");
+    swarm_ctx *c = new (std::nothrow) swarm_ctx();
+    if (!c) {
+        swarm::set_error("out of host memory");
+        return SWARM_ERR_OOM;
+    }
+    SW_HIP(hipGetDevice(&c->device));
+    *out = c;
+    return SWARM_OK;
+}
+
+int swarm_ctx_destroy(swarm_ctx *ctx) {
+    if (!ctx) return SWARM_OK;
+    for (int s = 0; s < swarm::S_NUM; ++s)
+        if (ctx->slot[s]) (void)hipFree(ctx->slot[s]);
+    if (ctx->host_pinned) (void)hipHostFree(ctx->host_pinned);
+    delete ctx;
+    return SWARM_OK;
+}
+
+}  // extern "C"

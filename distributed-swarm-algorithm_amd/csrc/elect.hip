@@ -1,0 +1,522 @@
+// Leader election (contract E2) on gfx950.
+//
+// Replaces the per-message handlers _handle_election_acclaim (agent.py:263-275) and
+// _handle_heartbeat (agent.py:243-261) applied by every agent to every neighbour's
+// re-advertised leader, one synchronous round at a time, starting from the state a won
+// _check_election_timeout leaves (agent.py:234-241).  Under E2 both reduce to
+//     leader'[v] = max(leader[v], max_{u in N(v)} leader[u])
+// (verified bit-exact against the handlers; tests/golden/elect_*.npz).
+//
+// Two exact strategies:
+//   DENSE     every round every agent gathers its whole CSR row (Jacobi, double-buffered).
+//             HBM bytes per round = 12N + 8E (+ the gather, mostly served on-die).
+//   FRONTIER  an agent can only change in round t+1 if a neighbour changed in round t, so
+//             round t+1 gathers only those agents.  Same leaders, same per-round change
+//             counts, same rounds_exec -- each agent's row is read O(changes) times instead
+//             of O(rounds) times.  Per round: a 1-byte-per-agent stamp scan, the gathers of
+//             active agents, a block-aggregated append of (agent, new leader), and an apply
+//             pass that writes the new leaders and stamps their neighbours for round t+1.
+//
+// Gather: one wave serves 64 agents at once (lane = agent).  Their rows are concatenated
+// virtually (wave prefix sum of degrees) and swept 64*U edges at a time, lane-contiguous, so
+// col reads coalesce and each lane keeps U independent col loads and then U independent
+// leader gathers in flight; each edge finds its row by a 6-step binary search over the lanes'
+// row offsets and max-combines into a per-wave LDS slot.
+//
+// Counters: every per-round count (changes, active agents, edges) is a 64-way sharded 64-bit
+// counter on its own 128-byte line, added once per workgroup: one contended counter per round
+// costs ~12 ns per arrival (MI355X_MICROARCH.md, 'fanin'), i.e. ~0.8 ms per round at one
+// arrival per wave at 10M agents.  The shards live in a ring of kRing rounds; the host zeroes
+// a batch's slots before launching it and reads them back after.
+#include <climits>
+#include <cstdlib>
+#include <cstring>
+
+#include "swarm_common.h"
+
+namespace swarm {
+namespace {
+
+constexpr int kShards = 64;
+constexpr int kShardStride = 16;                    // u64 per shard: one 128-B line each
+constexpr int kRing = 512;                          // rounds of counter slots
+constexpr int kRoundWords = kShards * kShardStride; // u64 per round per counter
+constexpr int kCounters = 3;                        // changes, active, edges
+constexpr int kChunk = 1024;                        // agents per frontier work unit
+constexpr int kWavesPerBlock = kBlock / kWave;
+
+__device__ __forceinline__ unsigned long long *slot(unsigned long long *ring, int t, int counter, int shard) {
+    return ring + (size_t(t % kRing) * kCounters + counter) * kRoundWords + size_t(shard) * kShardStride;
+}
+
+// Sum of the 64 change shards of round t (every thread of the block gets it).
+__device__ __forceinline__ unsigned long long round_total(unsigned long long *ring, int t,
+                                                          unsigned long long *s_bcast) {
+    if (threadIdx.x < kWave) {
+        unsigned long long v = *slot(ring, t, 0, threadIdx.x);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        if (threadIdx.x == 0) *s_bcast = v;
+    }
+    __syncthreads();
+    return *s_bcast;
+}
+
+__device__ __forceinline__ int wave_excl_scan(int v, int *total) {
+    const int lane = threadIdx.x & 63;
+    int incl = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int u = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += u;
+    }
+    *total = __shfl(incl, 63, 64);
+    return incl - v;
+}
+
+// max over N(v) of lin[], for the 64 agents of this wave (lane = agent; invalid lanes -> INT_MIN).
+// s_acc: this wave's 64-int LDS slot.  *edges += deg (lane-local).
+template <int U, typename Off>
+__device__ __forceinline__ int wave_gather_max(bool valid, int64_t v, const Off *__restrict__ rp,
+                                               const int32_t *__restrict__ col,
+                                               const int32_t *__restrict__ lin, int *s_acc) {
+    const int lane = threadIdx.x & 63;
+    Off b = 0, e = 0;
+    if (valid) {
+        b = rp[v];
+        e = rp[v + 1];
+    }
+    const int d = int(e - b);
+    int D;
+    const int o = wave_excl_scan(d, &D);
+    s_acc[lane] = INT_MIN;
+    __builtin_amdgcn_wave_barrier();
+    for (int f0 = 0; f0 < D; f0 += 64 * U) {
+        int c[U], r[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const int f = f0 + j * 64 + lane;
+            const int fq = f < D ? f : D - 1;
+            int lo = 0;
+#pragma unroll
+            for (int step = 32; step > 0; step >>= 1) {
+                const int cand = lo + step;
+                if (__shfl(o, cand, 64) <= fq) lo = cand;
+            }
+            const Off br = __shfl(b, lo, 64);
+            const int orr = __shfl(o, lo, 64);
+            r[j] = f < D ? lo : -1;
+            c[j] = f < D ? col[br + Off(fq - orr)] : 0;
+        }
+        int val[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) val[j] = r[j] >= 0 ? lin[c[j]] : INT_MIN;  // U gathers in flight
+#pragma unroll
+        for (int j = 0; j < U; ++j)
+            if (r[j] >= 0) atomicMax(&s_acc[r[j]], val[j]);
+    }
+    __builtin_amdgcn_wave_barrier();
+    return s_acc[lane];
+}
+
+// ---------------------------------------------------------------- dense Jacobi round
+// Wave task = 64 consecutive agents.  counters: the ring (round t), or, when single, a plain
+// per-shard array (swarm_elect_round).
+template <int U, typename Off>
+__global__ __launch_bounds__(kBlock) void k_elect_dense(
+    const Off *__restrict__ rp, const int32_t *__restrict__ col, const int32_t *__restrict__ lin,
+    int32_t *__restrict__ lout, int64_t n, unsigned long long *__restrict__ ring, int t, int guard) {
+    __shared__ int s_acc[kWavesPerBlock][64];
+    __shared__ unsigned long long s_bc, s_cnt[kWavesPerBlock];
+    if (guard && t > 1 && round_total(ring, t - 1, &s_bc) == 0) return;  // converged: no-op
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    unsigned long long mine = 0;
+    const int64_t ntask = (n + 63) / 64;
+    for (int64_t task = int64_t(blockIdx.x) * kWavesPerBlock + wid; task < ntask;
+         task += int64_t(gridDim.x) * kWavesPerBlock) {
+        const int64_t v = task * 64 + lane;
+        const bool valid = v < n;
+        const int m = wave_gather_max<U, Off>(valid, v, rp, col, lin, s_acc[wid]);
+        bool up = false;
+        if (valid) {
+            const int own = lin[v];
+            up = m > own;
+            lout[v] = up ? m : own;
+        }
+        mine += __popcll(__ballot(up));
+    }
+    if (lane == 0) s_cnt[wid] = mine;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long s = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) s += s_cnt[w];
+        if (s) atomicAdd(slot(ring, t, 0, blockIdx.x & (kShards - 1)), s);
+    }
+}
+
+// ------------------------------------------------------------- frontier: gather phase
+// Work unit = a chunk of 1024 agents (4 stamps per thread).  Changes of a chunk go to list
+// segment (chunk % 64), reserved by ONE atomic on that segment's counter shard.
+template <int U, typename Off>
+__global__ __launch_bounds__(kBlock) void k_elect_pull(
+    const Off *__restrict__ rp, const int32_t *__restrict__ col, const int32_t *__restrict__ leader,
+    const uint8_t *__restrict__ act, int64_t n, int2 *__restrict__ list, int64_t seg_cap,
+    unsigned long long *__restrict__ ring, int t, int with_stats) {
+    __shared__ int s_list[kChunk];
+    __shared__ int2 s_chg[kChunk];
+    __shared__ int s_acc[kWavesPerBlock][64];
+    __shared__ int s_wave[kWavesPerBlock];
+    __shared__ int s_nchg;
+    __shared__ unsigned long long s_bc, s_base;
+    __shared__ long long s_act[kWavesPerBlock], s_edg[kWavesPerBlock];
+    if (t > 1 && round_total(ring, t - 1, &s_bc) == 0) return;
+    const unsigned stamp4 = unsigned(t & 0xFF) * 0x01010101u;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    long long my_active = 0, my_edges = 0;
+    const int64_t nchunks = (n + kChunk - 1) / kChunk;
+    for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+        const int64_t c0 = chunk * kChunk;
+        // 1. my 4 stamps
+        const int64_t v0 = c0 + int64_t(threadIdx.x) * 4;
+        unsigned mask = 0;
+        if (v0 + 4 <= n) {
+            const unsigned w = *reinterpret_cast<const unsigned *>(act + v0) ^ stamp4;
+            const unsigned z = ~(((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w | 0x7F7F7F7Fu);
+            mask = ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+        } else {
+            for (int j = 0; j < 4 && v0 + j < n; ++j)
+                if (act[v0 + j] == uint8_t(t & 0xFF)) mask |= 1u << j;
+        }
+        // 2. compact this chunk's active agents into LDS
+        const int cnt = __popc(mask);
+        int wtot;
+        const int wexcl = wave_excl_scan(cnt, &wtot);
+        if (lane == 0) s_wave[wid] = wtot;
+        if (threadIdx.x == 0) s_nchg = 0;
+        __syncthreads();
+        int off = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < kWavesPerBlock; ++w) {
+            off += (w < wid) ? s_wave[w] : 0;
+            total += s_wave[w];
+        }
+        int pos = off + wexcl;
+        while (mask) {
+            const int j = __ffs(mask) - 1;
+            mask &= mask - 1;
+            s_list[pos++] = threadIdx.x * 4 + j;
+        }
+        __syncthreads();
+        // 3. 64 active agents per wave task
+        for (int base = wid * 64; base < total; base += kBlock) {
+            const int i = base + lane;
+            const bool valid = i < total;
+            const int64_t v = valid ? c0 + s_list[i] : 0;
+            const int m = wave_gather_max<U, Off>(valid, v, rp, col, leader, s_acc[wid]);
+            if (valid) {
+                const int own = leader[v];
+                if (with_stats) {
+                    my_active += 1;
+                    my_edges += (long long)(rp[v + 1] - rp[v]);
+                }
+                if (m > own) {
+                    const int at = atomicAdd(&s_nchg, 1);  // LDS
+                    s_chg[at] = make_int2(int(v), m);
+                }
+            }
+        }
+        __syncthreads();
+        // 4. one global reservation per chunk, then copy the chunk's changes out
+        const int nchg = s_nchg;
+        if (nchg) {
+            const int seg = int(chunk & (kShards - 1));
+            if (threadIdx.x == 0) s_base = atomicAdd(slot(ring, t, 0, seg), (unsigned long long)nchg);
+            __syncthreads();
+            int2 *dst = list + int64_t(seg) * seg_cap + int64_t(s_base);
+            for (int k = threadIdx.x; k < nchg; k += kBlock) dst[k] = s_chg[k];
+        }
+        __syncthreads();  // LDS reused by the next chunk
+    }
+    if (with_stats) {
+#pragma unroll
+        for (int o2 = 32; o2 > 0; o2 >>= 1) {
+            my_active += __shfl_xor(my_active, o2, 64);
+            my_edges += __shfl_xor(my_edges, o2, 64);
+        }
+        if (lane == 0) { s_act[wid] = my_active; s_edg[wid] = my_edges; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            long long a = 0, ed = 0;
+            for (int w = 0; w < kWavesPerBlock; ++w) { a += s_act[w]; ed += s_edg[w]; }
+            if (a) {
+                atomicAdd(slot(ring, t, 1, blockIdx.x & (kShards - 1)), (unsigned long long)a);
+                atomicAdd(slot(ring, t, 2, blockIdx.x & (kShards - 1)), (unsigned long long)ed);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------- frontier: apply phase
+// grid.y = list segment; G lanes per change stamp the changed agent's neighbours.
+template <int G, typename Off>
+__global__ __launch_bounds__(kBlock) void k_elect_apply(
+    const Off *__restrict__ rp, const int32_t *__restrict__ col, int32_t *__restrict__ leader,
+    uint8_t *__restrict__ act, const int2 *__restrict__ list, int64_t seg_cap,
+    unsigned long long *__restrict__ ring, int t) {
+    const int seg = blockIdx.y;
+    const int64_t cnt = int64_t(*slot(ring, t, 0, seg));
+    if (cnt == 0) return;
+    const int2 *src = list + int64_t(seg) * seg_cap;
+    const uint8_t next = uint8_t((t + 1) & 0xFF);
+    constexpr int GPB = kBlock / G;
+    const int sub = threadIdx.x & (G - 1);
+    for (int64_t base = int64_t(blockIdx.x) * GPB; base < cnt; base += int64_t(gridDim.x) * GPB) {
+        const int64_t i = base + threadIdx.x / G;
+        if (i < cnt) {
+            const int2 e = src[i];
+            if (sub == 0) leader[e.x] = e.y;
+            const Off e1 = rp[e.x + 1];
+            for (Off k = rp[e.x] + sub; k < e1; k += G) act[col[k]] = next;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_state(const int32_t *__restrict__ leader,
+                                                 const int32_t *__restrict__ ids,
+                                                 uint8_t *__restrict__ state, int64_t n) {
+    for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < n;
+         v += int64_t(gridDim.x) * kBlock)
+        state[v] = leader[v] == ids[v] ? SWARM_LEADER : SWARM_FOLLOWER;
+}
+
+// *out += sum of the 64 change shards of ring round t (single-round API).
+__global__ void k_sum_shards(unsigned long long *ring, int t, unsigned long long *out) {
+    unsigned long long v = *slot(ring, t, 0, threadIdx.x);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if (threadIdx.x == 0) *out += v;
+}
+
+// totals[(r - t0) * 3 + c] = sum over shards of counter c of round r, one wave per round.
+__global__ void k_batch_totals(unsigned long long *ring, int t0, unsigned long long *totals) {
+    const int r = t0 + blockIdx.x;
+#pragma unroll
+    for (int c = 0; c < kCounters; ++c) {
+        unsigned long long v = *slot(ring, r, c, threadIdx.x);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        if (threadIdx.x == 0) totals[size_t(blockIdx.x) * kCounters + c] = v;
+    }
+}
+
+int env_int(const char *name, int dflt) {
+    const char *s = getenv(name);
+    return s ? atoi(s) : dflt;
+}
+
+#define SW_DISPATCH_U(U, ...)                                                 \
+    switch (U) {                                                              \
+        case 4: { constexpr int UU = 4; __VA_ARGS__; } break;                 \
+        case 16: { constexpr int UU = 16; __VA_ARGS__; } break;               \
+        default: { constexpr int UU = 8; __VA_ARGS__; } break;                \
+    }
+
+struct Tuning {
+    int U = 8;          // edges in flight per lane (gather)
+    int G = 8;          // lanes per change (apply)
+    int dense_blocks = 4096;
+    Tuning() {
+        U = env_int("SWARM_GATHER_U", 8);
+        G = env_int("SWARM_APPLY_G", 8);
+        if (G != 4 && G != 16) G = 8;
+        dense_blocks = env_int("SWARM_DENSE_BLOCKS", 4096);
+    }
+};
+
+const Tuning &tuning() {
+    static Tuning tu;
+    return tu;
+}
+
+template <typename Off>
+int launch_dense_round(const Off *rp, const int32_t *col, const int32_t *lin, int32_t *lout,
+                       int64_t n, unsigned long long *ring, int t, int guard, hipStream_t s) {
+    const unsigned grid = grid_for((n + 63) / 64, kWavesPerBlock, unsigned(tuning().dense_blocks));
+    SW_DISPATCH_U(tuning().U, hipLaunchKernelGGL((k_elect_dense<UU, Off>), dim3(grid), dim3(kBlock), 0, s,
+                                                 rp, col, lin, lout, n, ring, t, guard));
+    SW_LAUNCHED();
+    return SWARM_OK;
+}
+
+template <typename Off>
+int launch_frontier_round(const Off *rp, const int32_t *col, int32_t *leader, uint8_t *act,
+                          int2 *list, int64_t seg_cap, int64_t n, unsigned long long *ring, int t,
+                          int with_stats, hipStream_t s) {
+    const unsigned gpull = grid_for(n, kChunk, 1u << 20);
+    SW_DISPATCH_U(tuning().U, hipLaunchKernelGGL((k_elect_pull<UU, Off>), dim3(gpull), dim3(kBlock), 0, s,
+                                                 rp, col, leader, act, n, list, seg_cap, ring, t, with_stats));
+    SW_LAUNCHED();
+    const dim3 gapply(grid_for(seg_cap, kBlock / tuning().G, 64), kShards);
+    switch (tuning().G) {
+        case 4: hipLaunchKernelGGL((k_elect_apply<4, Off>), gapply, dim3(kBlock), 0, s, rp, col, leader, act, list, seg_cap, ring, t); break;
+        case 16: hipLaunchKernelGGL((k_elect_apply<16, Off>), gapply, dim3(kBlock), 0, s, rp, col, leader, act, list, seg_cap, ring, t); break;
+        default: hipLaunchKernelGGL((k_elect_apply<8, Off>), gapply, dim3(kBlock), 0, s, rp, col, leader, act, list, seg_cap, ring, t); break;
+    }
+    SW_LAUNCHED();
+    return SWARM_OK;
+}
+
+template <typename Off>
+int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, const int32_t *ids,
+               int32_t *leader, uint8_t *state, int32_t max_rounds, int32_t mode,
+               int32_t *rounds_exec, int64_t *changes_host, swarm_elect_stats *st,
+               void *stream) {
+    SW_ARG(ctx != nullptr, "ctx is NULL");
+    SW_ARG(n >= 0, "n < 0");
+    SW_ARG(n < (int64_t(1) << 31), "n must be < 2^31");
+    SW_ARG(max_rounds >= 1, "max_rounds < 1");
+    SW_ARG(mode == SWARM_ELECT_DENSE || mode == SWARM_ELECT_FRONTIER, "unknown mode");
+    SW_ARG(rounds_exec != nullptr, "rounds_exec is NULL");
+    SW_ARG(n == 0 || (rp && ids && leader && state), "NULL array (col may be NULL only without edges)");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (st) *st = swarm_elect_stats{0, 0, 0};
+    if (n == 0) {  // an empty swarm: round 1 changes nothing
+        *rounds_exec = 1;
+        if (changes_host) changes_host[0] = 0;
+        if (st) st->rounds_launched = 1;
+        return SWARM_OK;
+    }
+    const size_t ring_words = size_t(kRing) * kCounters * kRoundWords;
+    unsigned long long *ring;
+    SW_ALLOC(ring, ctx, S_CHANGES, ring_words * 8);
+    SW_HIP(hipMemcpyAsync(leader, ids, size_t(n) * 4, hipMemcpyDeviceToDevice, s));
+    int32_t *bufs[2] = {leader, nullptr};
+    uint8_t *act = nullptr;
+    int2 *list = nullptr;
+    const int64_t nchunks = (n + kChunk - 1) / kChunk;
+    const int64_t seg_cap = ((nchunks + kShards - 1) / kShards) * kChunk;
+    if (mode == SWARM_ELECT_DENSE) {
+        SW_ALLOC(bufs[1], ctx, S_LEADER_B, size_t(n) * 4);
+    } else {
+        SW_ALLOC(act, ctx, S_ACT, size_t(n) + 16);
+        SW_ALLOC(list, ctx, S_LIST, size_t(seg_cap) * kShards * 8);
+        SW_HIP(hipMemsetAsync(act, 1, size_t(n), s));  // round 1: everybody gathers
+    }
+    const int with_stats = (st != nullptr && mode == SWARM_ELECT_FRONTIER) ? 1 : 0;
+    constexpr int kMaxBatch = 256;
+    const size_t per_round = size_t(kCounters) * kRoundWords;
+    unsigned long long *hbuf = static_cast<unsigned long long *>(pinned(ctx, size_t(kCounters) * 8 * kMaxBatch));
+    if (!hbuf) return SWARM_ERR_OOM;
+    unsigned long long *dtot;
+    SW_ALLOC(dtot, ctx, S_ESTATS, size_t(kCounters) * 8 * kMaxBatch);
+
+    int found = -1, t = 1, batch = 8, launched = 0;
+    int64_t act_sum = 0, edge_sum = 0;
+    auto zero_rounds = [&](int r0, int r1) -> int {  // ring slots of rounds [r0, r1]
+        for (int r = r0; r <= r1;) {
+            const int a = r % kRing;
+            const int len = std::min(r1 - r + 1, kRing - a);
+            SW_HIP(hipMemsetAsync(ring + size_t(a) * per_round, 0, size_t(len) * per_round * 8, s));
+            r += len;
+        }
+        return SWARM_OK;
+    };
+    // slot of round 0 (read by round 1's guard only when t > 1: never) stays untouched
+    while (t <= max_rounds && found < 0) {
+        const int tend = (max_rounds - t + 1 < batch) ? max_rounds : t + batch - 1;
+        int rc = zero_rounds(t, tend);
+        if (rc) return rc;
+        for (int r = t; r <= tend; ++r) {
+            rc = (mode == SWARM_ELECT_DENSE)
+                     ? launch_dense_round<Off>(rp, col, bufs[(r - 1) & 1], bufs[r & 1], n, ring, r, 1, s)
+                     : launch_frontier_round<Off>(rp, col, leader, act, list, seg_cap, n, ring, r,
+                                                  with_stats, s);
+            if (rc) return rc;
+        }
+        launched = tend;
+        // per-round totals of rounds [t, tend], reduced on device, then one small copy
+        hipLaunchKernelGGL(k_batch_totals, dim3(tend - t + 1), dim3(kWave), 0, s, ring, t, dtot);
+        SW_LAUNCHED();
+        SW_HIP(hipMemcpyAsync(hbuf, dtot, size_t(tend - t + 1) * kCounters * 8, hipMemcpyDeviceToHost, s));
+        SW_HIP(hipStreamSynchronize(s));
+        for (int r = t; r <= tend; ++r) {
+            const unsigned long long *rb = hbuf + size_t(r - t) * kCounters;
+            const unsigned long long c = rb[0], a = rb[1], ed = rb[2];
+            if (changes_host) changes_host[r - 1] = int64_t(c);
+            act_sum += int64_t(a);
+            edge_sum += int64_t(ed);
+            if (c == 0) {
+                found = r;
+                break;
+            }
+        }
+        t = tend + 1;
+        batch = batch < kMaxBatch ? batch * 2 : kMaxBatch;
+    }
+    const int last = found > 0 ? found : max_rounds;
+    // dense: after a zero-change round both buffers agree; otherwise the newest is bufs[last&1]
+    if (mode == SWARM_ELECT_DENSE && found < 0 && (last & 1))
+        SW_HIP(hipMemcpyAsync(leader, bufs[1], size_t(n) * 4, hipMemcpyDeviceToDevice, s));
+    hipLaunchKernelGGL(k_state, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s, leader,
+                       ids, state, n);
+    SW_LAUNCHED();
+    *rounds_exec = last;
+    if (st) {
+        st->rounds_launched = launched;
+        if (mode == SWARM_ELECT_DENSE) {
+            Off e = 0;
+            SW_HIP(hipMemcpyAsync(&e, rp + n, sizeof(Off), hipMemcpyDeviceToHost, s));
+            SW_HIP(hipStreamSynchronize(s));
+            st->active_total = n * int64_t(last);
+            st->edges_total = int64_t(e) * int64_t(last);
+        } else {
+            st->active_total = act_sum;
+            st->edges_total = edge_sum;
+        }
+    }
+    return found > 0 ? SWARM_OK : SWARM_NOT_CONVERGED;
+}
+
+}  // namespace
+}  // namespace swarm
+
+extern "C" {
+
+int swarm_elect(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col,
+                const int32_t *ids, int32_t *leader, uint8_t *state, int32_t max_rounds,
+                int32_t mode, int32_t *rounds_exec, int64_t *changes_per_round,
+                swarm_elect_stats *stats, void *stream) {
+    return swarm::elect_impl<int32_t>(ctx, n, row_ptr, col, ids, leader, state, max_rounds, mode,
+                                      rounds_exec, changes_per_round, stats, stream);
+}
+
+int swarm_elect_i64(swarm_ctx *ctx, int64_t n, const int64_t *row_ptr, const int32_t *col,
+                    const int32_t *ids, int32_t *leader, uint8_t *state, int32_t max_rounds,
+                    int32_t mode, int32_t *rounds_exec, int64_t *changes_per_round,
+                    swarm_elect_stats *stats, void *stream) {
+    return swarm::elect_impl<int64_t>(ctx, n, row_ptr, col, ids, leader, state, max_rounds, mode,
+                                      rounds_exec, changes_per_round, stats, stream);
+}
+
+int swarm_elect_round(swarm_ctx *ctx, int64_t n_rows, const int32_t *row_ptr,
+                      const int32_t *col, const int32_t *leader_in, int32_t *leader_out,
+                      int64_t *changed, void *stream) {
+    using namespace swarm;
+    SW_ARG(ctx != nullptr, "ctx is NULL");
+    SW_ARG(n_rows >= 0 && n_rows < (int64_t(1) << 31), "n_rows out of range");
+    SW_ARG(changed != nullptr, "changed is NULL");
+    if (n_rows == 0) return SWARM_OK;
+    SW_ARG(row_ptr && leader_in && leader_out, "NULL array");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    unsigned long long *ring;
+    SW_ALLOC(ring, ctx, S_TMP0, size_t(kCounters) * kRoundWords * 8);
+    SW_HIP(hipMemsetAsync(ring, 0, size_t(kRoundWords) * 8, s));
+    int rc = launch_dense_round<int32_t>(row_ptr, col, leader_in, leader_out, n_rows, ring, 0, 0, s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_sum_shards, dim3(1), dim3(kWave), 0, s, ring, 0,
+                       reinterpret_cast<unsigned long long *>(changed));
+    SW_LAUNCHED();
+    return SWARM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,99 @@
+// Shared host/device plumbing for libswarm.so (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <type_traits>
+
+#include "../../include/swarm.h"
+
+namespace swarm {
+
+constexpr int kBlock = 256;   // threads per workgroup: 4 waves of 64
+constexpr int kWave = 64;
+
+void set_error(const char *fmt, ...);
+
+// Scratch slots owned by a ctx; each grows on demand (never shrinks until destroy).
+enum Slot {
+    S_LEADER_B = 0,   // election: second leader buffer (dense)
+    S_ACT,            // election: per-agent activity stamp (frontier)
+    S_LIST,           // election: changed (agent, value) list (frontier)
+    S_CHANGES,        // election: per-round change counters (device)
+    S_ESTATS,         // election: per-round active/edge counters (device)
+    S_KEYS_IN,        // binning: cell keys
+    S_KEYS_OUT,
+    S_VALS_IN,        // binning: agent indices
+    S_VALS_OUT,
+    S_CELL_START,
+    S_CELL_END,
+    S_CUB_TMP,        // hipcub temporary storage
+    S_BBOX,           // bounding box (device)
+    S_ASTATS,         // allocation counters (device)
+    S_DEG,            // graph builder: degrees
+    S_TILEMAX,        // dense allocation: per (task, agent tile) max claim
+    S_ORDER,          // dense allocation: agents in ascending ID order
+    S_TMP0,
+    S_TMP1,
+    S_NUM
+};
+
+}  // namespace swarm
+
+struct swarm_ctx {
+    int device = 0;
+    void *slot[swarm::S_NUM] = {};
+    size_t cap[swarm::S_NUM] = {};
+    void *host_pinned = nullptr;   // small pinned staging buffer for scalar/array readback
+    size_t host_cap = 0;
+};
+
+namespace swarm {
+
+// Returns a device buffer of at least `bytes` for `s` (nullptr + error on failure).
+void *scratch(swarm_ctx *ctx, Slot s, size_t bytes);
+void *pinned(swarm_ctx *ctx, size_t bytes);
+
+}  // namespace swarm
+
+#define SW_HIP(call)                                                                     \
+    do {                                                                                 \
+        hipError_t e_ = (call);                                                          \
+        if (e_ != hipSuccess) {                                                          \
+            swarm::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #call,                \
+                             hipGetErrorString(e_));                                     \
+            return SWARM_ERR_HIP;                                                        \
+        }                                                                                \
+    } while (0)
+
+#define SW_ARG(cond, msg)                                                                \
+    do {                                                                                 \
+        if (!(cond)) {                                                                   \
+            swarm::set_error("invalid argument: %s", msg);                               \
+            return SWARM_ERR_ARG;                                                        \
+        }                                                                                \
+    } while (0)
+
+#define SW_ALLOC(ptr, ctx, slot, bytes)                                                  \
+    do {                                                                                 \
+        (ptr) = static_cast<std::remove_reference_t<decltype(ptr)>>(swarm::scratch((ctx), (slot), (bytes)));      \
+        if (!(ptr)) return SWARM_ERR_OOM;                                                \
+    } while (0)
+
+// Launch-error check after a kernel launch.
+#define SW_LAUNCHED() SW_HIP(hipGetLastError())
+
+namespace swarm {
+
+// Grid for a grid-stride kernel over `work` items with `per_block` items per block pass.
+inline unsigned grid_for(int64_t work, int64_t per_block, unsigned cap = 8192) {
+    int64_t g = (work + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return static_cast<unsigned>(g);
+}
+
+}  // namespace swarm

@@ -1,0 +1,280 @@
+"""Batched, HBM-resident swarm: the GPU face of the reference's per-round handlers.
+
+One ``Swarm`` holds every agent as structure-of-arrays in device memory (SURVEY §2 "SoA swarm
+state"): ``ids`` int32, ``pos`` float64 (x, y) pairs, ``caps`` uint32 bitmask, the neighbour
+CSR (``row_ptr`` int32, ``col`` int32) and the election outputs ``leader`` int32 / ``state``
+uint8.  Agents are stored in spatial (grid-cell) order by default, so a neighbour gather and a
+task's candidate scan touch nearby memory; ``perm`` maps storage index -> input index.
+
+  elect()     all rounds of contract E2 to convergence  -> swarm_elect (libswarm.so)
+              (SwarmAgent._handle_election_acclaim / _handle_heartbeat, agent.py:243-275)
+  allocate()  one claim/resolve/notify round             -> swarm_allocate
+              (SwarmAgent._process_tasks / _handle_task_claim / _handle_task_conflict /
+               _calculate_utility, agent.py:292-347)
+
+Every compute call goes through the HIP kernels; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _lib
+
+CAP_VOCAB_DEFAULT = ("extinguisher", "sonar", "camera", "gripper")
+STATUS_NAMES = ("OPEN", "TENTATIVE", "LOCKED", "ASSIGNED")
+
+
+def _dev(device):
+    if device is None:
+        if not torch.cuda.is_available():
+            raise RuntimeError("swarm_amd needs a ROCm GPU (torch.cuda.is_available() is False)")
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device(device)
+
+
+def _to(a, dtype, device):
+    if isinstance(a, torch.Tensor):
+        return a.to(device=device, dtype=dtype).contiguous()
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype, device=device)
+
+
+@dataclass
+class ElectResult:
+    rounds_exec: int
+    changes: np.ndarray                 # per-round change counts, rounds 1..rounds_exec
+    leader: torch.Tensor                # int32 [n], storage order
+    state: torch.Tensor                 # uint8 [n], storage order (1 FOLLOWER, 3 LEADER)
+    converged: bool = True
+    rounds_launched: int = 0
+    active_total: int = 0               # agents that gathered, summed over rounds
+    edges_total: int = 0                # neighbour reads, summed over rounds
+
+
+@dataclass
+class AllocResult:
+    winner: torch.Tensor                # int32 [t] (-1 = unclaimed)
+    util: torch.Tensor                  # float64 [t] winning claim value (f32-valued)
+    won: torch.Tensor                   # int32 [n] tasks won per agent (storage order)
+    nclaim: torch.Tensor                # int64 [t] TASK_CLAIMs per task
+    nmsg: torch.Tensor                  # int64 [t] TASK_CONFLICTs per task
+    stats: dict = field(default_factory=dict)
+
+
+class Swarm:
+    """Structure-of-arrays swarm resident on one GPU."""
+
+    def __init__(self, ids, x, y, caps=None, *, layout: str = "spatial", cell: float = 1.0,
+                 device=None):
+        dev = _dev(device)
+        _lib.lib()
+        self.device = dev
+        ids_t = _to(ids, torch.int32, dev)
+        n = ids_t.numel()
+        pos = torch.stack([_to(x, torch.float64, dev), _to(y, torch.float64, dev)], dim=1).contiguous()
+        if caps is None:
+            caps = np.zeros(n, np.uint32)
+        if not isinstance(caps, torch.Tensor):  # uint32 bitmask, carried bit-for-bit as int32
+            caps = np.ascontiguousarray(caps, dtype=np.uint32).view(np.int32)
+        caps_t = _to(caps, torch.int32, dev)
+        self.n = n
+        if layout == "spatial" and n > 1:
+            perm = torch.empty(n, dtype=torch.int32, device=dev)
+            with torch.cuda.device(dev):
+                _lib.check(_lib.lib().swarm_cell_order(_lib.ctx(), n, _lib.ptr(pos, torch.float64),
+                                                       float(cell), _lib.ptr(perm), _lib.stream()))
+            p = perm.long()
+            ids_t, pos, caps_t = ids_t[p].contiguous(), pos[p].contiguous(), caps_t[p].contiguous()
+            self.perm = perm
+        elif layout in ("spatial", "input"):
+            self.perm = torch.arange(n, dtype=torch.int32, device=dev)
+        else:
+            raise ValueError(f"unknown layout {layout!r}")
+        self.layout = layout
+        self.ids, self.pos, self.caps = ids_t, pos, caps_t
+        if n and int(ids_t.min()) < 0:
+            raise ValueError("agent IDs must be non-negative")
+        self.row_ptr = None
+        self.col = None
+        self.leader = torch.empty(n, dtype=torch.int32, device=dev)
+        self.state = torch.full((n,), _lib.FOLLOWER, dtype=torch.uint8, device=dev)
+        self._id_index = None
+
+    # ------------------------------------------------------------------ graph
+    @property
+    def n_edges(self) -> int:
+        return 0 if self.col is None else int(self.col.numel())
+
+    def build_graph(self, radius: float = 1.0):
+        """Radius graph over the current storage order, built on the GPU (swarm_build_rgg)."""
+        n, dev = self.n, self.device
+        L = _lib.lib()
+        row_ptr = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        ne = ctypes.c_int64(0)
+        with torch.cuda.device(dev):
+            _lib.check(L.swarm_build_rgg(_lib.ctx(), n, _lib.ptr(self.pos) if n else None, float(radius),
+                                         _lib.ptr(row_ptr), None, 0, ctypes.byref(ne), _lib.stream()))
+            col = torch.empty(max(ne.value, 1), dtype=torch.int32, device=dev)
+            _lib.check(L.swarm_build_rgg(_lib.ctx(), n, _lib.ptr(self.pos) if n else None, float(radius),
+                                         _lib.ptr(row_ptr), _lib.ptr(col), col.numel(), ctypes.byref(ne),
+                                         _lib.stream()))
+        self.row_ptr, self.col = row_ptr, col[: ne.value]
+        return self
+
+    def set_graph(self, row_ptr, col):
+        """CSR given over INPUT indices (as the caller numbered agents); relabelled to storage."""
+        rp = np.asarray(row_ptr.cpu() if isinstance(row_ptr, torch.Tensor) else row_ptr, np.int64)
+        cl = np.asarray(col.cpu() if isinstance(col, torch.Tensor) else col, np.int64)
+        if rp[-1] >= 2**31:
+            raise ValueError("graph has >= 2^31 edges; shard it (swarm_amd.dist)")
+        perm = self.perm.cpu().numpy().astype(np.int64)
+        if self.layout != "input" and self.n > 1:
+            inv = np.empty(self.n, np.int64)
+            inv[perm] = np.arange(self.n)
+            deg = np.diff(rp)[perm]
+            new_rp = np.zeros(self.n + 1, np.int64)
+            new_rp[1:] = np.cumsum(deg)
+            flat = np.repeat(rp[:-1][perm] - new_rp[:-1], deg) + np.arange(new_rp[-1])
+            cl = inv[cl[flat]]
+            rp = new_rp
+        self.row_ptr = torch.as_tensor(rp.astype(np.int32), device=self.device)
+        self.col = torch.as_tensor(cl.astype(np.int32), device=self.device)
+        return self
+
+    # ------------------------------------------------------------------ election
+    def elect(self, mode: str = "frontier", max_rounds: int = 1 << 20) -> ElectResult:
+        """Contract E2 to convergence on the GPU (swarm_elect)."""
+        if self.row_ptr is None:
+            raise RuntimeError("no neighbour graph: call build_graph() or set_graph()")
+        m = {"dense": _lib.ELECT_DENSE, "frontier": _lib.ELECT_FRONTIER}[mode]
+        n = self.n
+        rounds = ctypes.c_int32(0)
+        cap = int(max_rounds)
+        changes = np.zeros(cap, np.int64)
+        st = _lib.ElectStats()
+        with torch.cuda.device(self.device):
+            rc = _lib.check(_lib.lib().swarm_elect(
+                _lib.ctx(), n, _lib.ptr(self.row_ptr, torch.int32), _lib.ptr(self.col, torch.int32),
+                _lib.ptr(self.ids, torch.int32), _lib.ptr(self.leader, torch.int32),
+                _lib.ptr(self.state, torch.uint8), cap, m, ctypes.byref(rounds),
+                changes.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st), _lib.stream()))
+        r = rounds.value
+        return ElectResult(r, changes[:r].copy(), self.leader, self.state, rc == _lib.OK,
+                           st.rounds_launched, st.active_total, st.edges_total)
+
+    # ------------------------------------------------------------------ allocation
+    def id_index(self) -> torch.Tensor | None:
+        """id -> storage index table (None if IDs are too sparse for a dense table)."""
+        if self._id_index is None and self.n:
+            span = int(self.ids.max()) + 1
+            if span <= 4 * self.n + 1024:
+                t = torch.full((span,), -1, dtype=torch.int32, device=self.device)
+                t[self.ids.long()] = torch.arange(self.n, dtype=torch.int32, device=self.device)
+                self._id_index = t
+        return self._id_index
+
+    def allocate(self, tx, ty, treq, *, winner=None, util=None, claim_thr: float = 20.0,
+                 hysteresis: float = 5.0, u_scale: float = 100.0, mode: str = "auto") -> AllocResult:
+        """One allocation round over t tasks (swarm_allocate).  winner/util = existing claims."""
+        dev = self.device
+        tpos = torch.stack([_to(tx, torch.float64, dev), _to(ty, torch.float64, dev)], 1).contiguous()
+        tq = _to(treq, torch.int8, dev)
+        t = tq.numel()
+        w = (torch.full((t,), -1, dtype=torch.int32, device=dev) if winner is None
+             else _to(winner, torch.int32, dev).clone())
+        u = (torch.zeros(t, dtype=torch.float64, device=dev) if util is None
+             else _to(util, torch.float64, dev).clone())
+        won = torch.zeros(self.n, dtype=torch.int32, device=dev)
+        nclaim = torch.zeros(t, dtype=torch.int64, device=dev)
+        nmsg = torch.zeros(t, dtype=torch.int64, device=dev)
+        idx = self.id_index()
+        st = _lib.AllocStats()
+        m = {"auto": _lib.ALLOC_AUTO, "binned": _lib.ALLOC_BINNED, "dense": _lib.ALLOC_DENSE}[mode]
+        with torch.cuda.device(dev):
+            _lib.check(_lib.lib().swarm_allocate(
+                _lib.ctx(), self.n, _lib.ptr(self.ids), _lib.ptr(self.pos), _lib.ptr(self.caps), t,
+                _lib.ptr(tpos), _lib.ptr(tq), float(claim_thr), float(hysteresis), float(u_scale), m,
+                _lib.ptr(w), _lib.ptr(u), _lib.ptr(won), _lib.ptr(idx),
+                0 if idx is None else idx.numel(), _lib.ptr(nclaim), _lib.ptr(nmsg),
+                ctypes.byref(st), _lib.stream()))
+        stats = {k: getattr(st, k) for k, _ in _lib.AllocStats._fields_}
+        return AllocResult(w, u, won, nclaim, nmsg, stats)
+
+    # ------------------------------------------------------------------ views / bridge
+    def to_input_order(self, storage_tensor) -> np.ndarray:
+        """Host copy of a per-agent tensor re-ordered to the caller's input numbering."""
+        a = storage_tensor.cpu().numpy()
+        out = np.empty_like(a)
+        out[self.perm.cpu().numpy()] = a
+        return out
+
+    @classmethod
+    def from_agents(cls, agents, neighbors=None, cap_vocab=CAP_VOCAB_DEFAULT, device=None, layout="spatial"):
+        """Batch a population of agent.SwarmAgent objects (drop-in bridge).
+
+        neighbors: list of neighbour-index lists (who agent i hears), or None to build the
+        radius-1 graph from positions on the GPU."""
+        vocab = {c: k for k, c in enumerate(cap_vocab)}
+        ids = np.array([a.agent_id for a in agents], np.int32)
+        x = np.array([a.position[0] for a in agents], np.float64)
+        y = np.array([a.position[1] for a in agents], np.float64)
+        caps = np.zeros(len(agents), np.uint32)
+        for i, a in enumerate(agents):
+            for c in a.capabilities:
+                if c not in vocab:
+                    raise ValueError(f"capability {c!r} not in the vocabulary {cap_vocab}")
+                caps[i] |= np.uint32(1 << vocab[c])
+        sw = cls(ids, x, y, caps, device=device, layout=layout)
+        sw.cap_vocab = tuple(cap_vocab)
+        if neighbors is None:
+            sw.build_graph(1.0)
+        else:
+            rp = np.zeros(len(agents) + 1, np.int64)
+            rp[1:] = np.cumsum([len(nb) for nb in neighbors])
+            col = np.array([j for nb in neighbors for j in nb], np.int64)
+            sw.set_graph(rp, col)
+        return sw
+
+    def write_back_election(self, agents, result: ElectResult):
+        """Set leader_id / state on the agent objects as the E2 rounds leave them."""
+        from agent import AgentState  # the drop-in scalar module
+        lead = self.to_input_order(result.leader)
+        st = self.to_input_order(result.state)
+        for i, a in enumerate(agents):
+            a.leader_id = int(lead[i])
+            a.state = AgentState(int(st[i]))
+
+    def tasks_from_dict(self, tasks: dict):
+        """(task_ids, tx, ty, treq) arrays from a reference-style task dict."""
+        vocab = {c: k for k, c in enumerate(getattr(self, "cap_vocab", CAP_VOCAB_DEFAULT))}
+        tid = np.array(list(tasks.keys()), np.int64)
+        tx = np.array([tasks[k]["pos"][0] for k in tid], np.float64)
+        ty = np.array([tasks[k]["pos"][1] for k in tid], np.float64)
+        # a required cap nobody can have still blocks every agent: bit 31 is never set
+        treq = np.array([vocab.get(tasks[k]["required_cap"], 31) if "required_cap" in tasks[k] else -1
+                         for k in tid], np.int8)
+        return tid, tx, ty, treq
+
+    def write_back_allocation(self, agents, task_ids, res: AllocResult, resolver=None):
+        """Statuses every agent holds after full TASK_CONFLICT delivery, and the resolver's
+        task_claims table (agent.py:320)."""
+        winner = res.winner.cpu().numpy()
+        util = res.util.cpu().numpy()
+        nmsg = res.nmsg.cpu().numpy()
+        nclaim = res.nclaim.cpu().numpy()
+        for a in agents:
+            for k, tid in enumerate(task_ids):
+                task = a.tasks.get(int(tid))
+                if task is None:
+                    continue
+                if nmsg[k] > 0:
+                    task["status"] = "ASSIGNED" if a.agent_id == winner[k] else "LOCKED"
+                elif nclaim[k] > 0 and a.agent_id == winner[k]:
+                    task["status"] = "TENTATIVE"  # lone rejected claim of the incumbent
+        if resolver is not None:
+            for k, tid in enumerate(task_ids):
+                if winner[k] >= 0:
+                    resolver.task_claims[int(tid)] = {"winner": int(winner[k]), "utility": float(util[k])}

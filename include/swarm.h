@@ -1,0 +1,165 @@
+/*
+ * swarm.h -- C-ABI of libswarm.so, the MI355X (gfx950) swarm-step library.
+ *
+ * The reference has no FFI: its boundary is the Python module `agent` whose handlers are
+ * called once per message (agent.py:197-214 dispatch).  These entry points replace the
+ * *batched* form of those handlers -- one call runs a whole synchronous round (or all rounds
+ * to convergence) for every agent at once.  Python binds them with ctypes
+ * (distributed-swarm-algorithm_amd/swarm_amd/_lib.py; INTEGRATION.md shows the stub).
+ *
+ * Conventions
+ *   - All array arguments are DEVICE pointers (HBM), borrowed: the library never frees them.
+ *     Positions are interleaved float64 pairs (x0, y0, x1, y1, ...), i.e. agent.py:47
+ *     `self.position` / task['pos'].
+ *   - Agents are addressed by storage index i in [0, n); ids[i] (int32, >= 0, distinct) is
+ *     the protocol ID (agent.py:26 `agent_id`).  The storage order is the caller's choice; the
+ *     batched Python layer stores agents in spatial (grid-cell) order for locality.
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream).  Work is
+ *     stream-ordered; the documented host sync points are the host-pointer outputs
+ *     (rounds_exec, changes_per_round, stats, n_edges).
+ *   - Return 0 (SWARM_OK) on success, > 0 for a soft condition, < 0 on error;
+ *     swarm_last_error() returns the calling thread's last message.
+ *   - Scratch memory is owned by a swarm_ctx (grows on demand, freed by swarm_ctx_destroy).
+ *     A ctx is bound to the device that was current when it was created; one ctx per thread.
+ */
+#ifndef SWARM_H
+#define SWARM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SWARM_OK 0
+#define SWARM_NOT_CONVERGED 1  /* max_rounds reached without a zero-change round */
+#define SWARM_ERR_ARG (-1)     /* invalid argument (sizes, NULL pointers, ranges) */
+#define SWARM_ERR_HIP (-2)     /* HIP runtime error (message has the hipError string) */
+#define SWARM_ERR_OOM (-3)     /* scratch allocation failed */
+#define SWARM_ERR_RANGE (-4)   /* a size exceeds the index type (e.g. >= 2^31 edges) */
+
+/* Agent states as stored in the uint8 state array (agent.py:19-22 AgentState values). */
+#define SWARM_FOLLOWER 1
+#define SWARM_ELECTION_WAIT 2
+#define SWARM_LEADER 3
+
+/* Election execution strategies.  Both are exact: identical leaders, states, rounds_exec
+ * and per-round change counts. */
+#define SWARM_ELECT_DENSE 0    /* every agent gathers every round (Jacobi sweep) */
+#define SWARM_ELECT_FRONTIER 1 /* only neighbours of last round's changed agents gather */
+
+/* Allocation execution strategies (all exact). */
+#define SWARM_ALLOC_AUTO 0
+#define SWARM_ALLOC_BINNED 1   /* cell-list candidates within the claim radius */
+#define SWARM_ALLOC_DENSE 2    /* every agent x every task, ID-ordered tiles */
+
+typedef struct swarm_ctx swarm_ctx;
+
+typedef struct swarm_alloc_stats {
+    int64_t n_claims;        /* TASK_CLAIM messages the round produced (agent.py:302) */
+    int64_t n_conflicts;     /* TASK_CONFLICT messages the resolver emitted (agent.py:322,325) */
+    int64_t n_flagged;       /* claims/decisions inside the libm guard band */
+    int64_t n_candidates;    /* agent x task pairs evaluated exactly in fp64 */
+    int64_t n_overflow;      /* tasks whose claims exceeded the on-chip list (slow exact path) */
+    int64_t mode_used;       /* SWARM_ALLOC_BINNED or SWARM_ALLOC_DENSE */
+} swarm_alloc_stats;
+
+typedef struct swarm_elect_stats {
+    int64_t rounds_launched; /* rounds issued (>= rounds_exec; extra ones are no-ops) */
+    int64_t active_total;    /* agents that gathered, summed over rounds */
+    int64_t edges_total;     /* neighbour reads, summed over rounds */
+} swarm_elect_stats;
+
+const char *swarm_last_error(void);
+const char *swarm_version(void);
+
+int swarm_ctx_create(swarm_ctx **out);
+int swarm_ctx_destroy(swarm_ctx *ctx);
+
+/*
+ * Leader election to convergence (contract E2).
+ * Replaces: SwarmAgent._handle_election_acclaim (agent.py:263-275) and
+ * SwarmAgent._handle_heartbeat (agent.py:243-261) applied by every agent to every
+ * neighbour's re-advertised leader each round, starting from the state
+ * _check_election_timeout leaves after a win (agent.py:234-241: LEADER, leader_id = id).
+ *   round t:  leader[v] <- max(leader[v], max_{u in N(v)} leader[u])   (synchronous)
+ *   stop after the first round with zero changes; rounds_exec counts that round.
+ *   state[v] = SWARM_LEADER iff leader[v] == ids[v], else SWARM_FOLLOWER.
+ * row_ptr/col: CSR of N(v) (who v hears) over storage indices; FRONTIER mode requires it
+ * symmetric.  leader (device, n): output.  changes_per_round (host, capacity max_rounds, may
+ * be NULL): per-round change counts for rounds 1..rounds_exec.  stats (host) may be NULL.
+ * Returns SWARM_NOT_CONVERGED if max_rounds rounds all changed something.
+ */
+int swarm_elect(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col,
+                const int32_t *ids, int32_t *leader, uint8_t *state, int32_t max_rounds,
+                int32_t mode, int32_t *rounds_exec, int64_t *changes_per_round,
+                swarm_elect_stats *stats, void *stream);
+
+/* Same with int64 row offsets (graphs with >= 2^31 edges). */
+int swarm_elect_i64(swarm_ctx *ctx, int64_t n, const int64_t *row_ptr, const int32_t *col,
+                    const int32_t *ids, int32_t *leader, uint8_t *state, int32_t max_rounds,
+                    int32_t mode, int32_t *rounds_exec, int64_t *changes_per_round,
+                    swarm_elect_stats *stats, void *stream);
+
+/* One synchronous E2 round, dense, no convergence loop (building block for sharded runs):
+ * leader_out[v] = max(leader_in[v], max_{u in N(v)} leader_in[u]) for v in [0, n_rows);
+ * leader_in may hold n_rows + ghosts entries (col indexes it).  *changed (device int64) is
+ * incremented by the number of rows whose value rose. */
+int swarm_elect_round(swarm_ctx *ctx, int64_t n_rows, const int32_t *row_ptr,
+                      const int32_t *col, const int32_t *leader_in, int32_t *leader_out,
+                      int64_t *changed, void *stream);
+
+/*
+ * Task allocation round (contract A-H).
+ * Replaces: SwarmAgent._process_tasks + _calculate_utility (agent.py:292-302, 338-347) run by
+ * every agent over every OPEN task, then SwarmAgent._handle_task_claim (agent.py:304-325) at
+ * the resolver for every claim in ascending sender-ID order, then the winner notification
+ * _handle_task_conflict (agent.py:327-336).
+ *   U(a,k) = (u_scale / (1 + sqrt(dx*dx + dy*dy))) * has_cap   (fp64, no FMA contraction)
+ *   claim iff U > claim_thr; claim value x = f32(U) (round to nearest even)
+ *   per task, claims in ascending agent ID: the first claim wins if the task has no current
+ *   winner, otherwise a claim replaces the winner iff x > util + hysteresis (fp64).
+ * apos (n*2 f64), acaps (n u32: bit k = capability k), tpos (t*2 f64), treq (t i8: -1 none).
+ * winner/util (device, t): in = current claim table (-1 = no claim; util fp64), out = final.
+ * won (device, n, may be NULL): out, tasks won per agent.  id_to_index (device, may be NULL,
+ * length id_span): storage index of each ID, used to credit `won` for a pre-existing winner
+ * that keeps its task.  nclaim/nmsg (device, t, may be NULL): claims and TASK_CONFLICT
+ * messages per task.  stats (host, may be NULL).
+ */
+int swarm_allocate(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos,
+                   const uint32_t *acaps, int64_t t, const double *tpos, const int8_t *treq,
+                   double claim_thr, double hysteresis, double u_scale, int32_t mode,
+                   int32_t *winner, double *util, int32_t *won, const int32_t *id_to_index,
+                   int64_t id_span, int64_t *nclaim, int64_t *nmsg, swarm_alloc_stats *stats,
+                   void *stream);
+
+/*
+ * Exact fp64 utility for m (agent, task) pairs (agent.py:338-347), GPU arithmetic.
+ * out (device, m f64).  Used by parity tests and by callers that need costs, not claims.
+ */
+int swarm_utility(swarm_ctx *ctx, int64_t m, const double *apos, const uint32_t *acaps,
+                  const double *tpos, const int8_t *treq, double u_scale, double *out,
+                  void *stream);
+
+/*
+ * Radius graph builder (synthetic/sensor input side of the round):
+ * edge i~j (i != j) iff dx*dx + dy*dy <= radius*radius (fp64).  Rows ascending.
+ * Call with col == NULL to get row_ptr (device, n+1) and *n_edges (host); then again with col
+ * (device, capacity col_capacity) to fill.
+ */
+int swarm_build_rgg(swarm_ctx *ctx, int64_t n, const double *pos, double radius,
+                    int32_t *row_ptr, int32_t *col, int64_t col_capacity, int64_t *n_edges,
+                    void *stream);
+
+/*
+ * Spatial storage order: perm (device, n) such that agents perm[0], perm[1], ... are
+ * grouped by row-major grid cell of side `cell` (stable within a cell).
+ */
+int swarm_cell_order(swarm_ctx *ctx, int64_t n, const double *pos, double cell,
+                     int32_t *perm, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SWARM_H */

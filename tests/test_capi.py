@@ -1,0 +1,53 @@
+"""libswarm.so loads and exports exactly what include/swarm.h declares (no GPU needed)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import PKG, ROOT
+
+HEADER = os.path.join(ROOT, "include", "swarm.h")
+LIB = os.path.join(PKG, "swarm_amd", "libswarm.so")
+
+
+def declared():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(swarm_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_header_declares_the_boundary():
+    names = declared()
+    for must in ("swarm_elect", "swarm_allocate", "swarm_last_error", "swarm_ctx_create"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    assert os.path.exists(LIB), "libswarm.so not built (make -C distributed-swarm-algorithm_amd/csrc)"
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r" T (swarm_[a-z0-9_]+)", out))
+    missing = [n for n in declared() if n not in exported]
+    assert not missing, missing
+    from swarm_amd import _lib
+    assert sorted(_lib.EXPORTS) == declared()
+
+
+def test_library_loads_and_reports_errors_without_gpu():
+    from swarm_amd import _lib
+    L = _lib.load()
+    assert b"gfx950" in L.swarm_version()
+    rc = L.swarm_elect(None, 10, None, None, None, None, None, 1, 0,
+                       ctypes.byref(ctypes.c_int32()), None, None, None)
+    assert rc == _lib.ERR_ARG
+    assert b"ctx is NULL" in L.swarm_last_error()
+    rc = L.swarm_allocate(None, 1, None, None, None, 1, None, None, 20.0, 5.0, 100.0, 0,
+                          None, None, None, None, 0, None, None, None, None)
+    assert rc == _lib.ERR_ARG
+
+
+def test_gpu_code_object_targets_gfx950_only():
+    data = open(LIB, "rb").read()
+    targets = set(re.findall(rb"amdgcn-amd-amdhsa-[-a-z0-9]*?(gfx[0-9a-z]+)", data))
+    assert targets == {b"gfx950"}, targets
