@@ -42,7 +42,8 @@ constexpr int kShardStride = 16;                    // u64 per shard: one 128-B 
 constexpr int kRing = 512;                          // rounds of counter slots
 constexpr int kRoundWords = kShards * kShardStride; // u64 per round per counter
 constexpr int kCounters = 3;                        // changes, active, edges
-constexpr int kChunk = 1024;                        // agents per frontier work unit
+constexpr int kScan = 8;                            // stamps per thread (one 8-B load)
+constexpr int kChunk = kBlock * kScan;              // agents per frontier work unit
 constexpr int kWavesPerBlock = kBlock / kWave;
 
 __device__ __forceinline__ unsigned long long *slot(unsigned long long *ring, int t, int counter, int shard) {
@@ -74,76 +75,88 @@ __device__ __forceinline__ int wave_excl_scan(int v, int *total) {
     return incl - v;
 }
 
-// max over N(v) of lin[], for the 64 agents of this wave (lane = agent; invalid lanes -> INT_MIN).
-// s_acc: this wave's 64-int LDS slot.  *edges += deg (lane-local).
-template <int U, typename Off>
-__device__ __forceinline__ int wave_gather_max(bool valid, int64_t v, const Off *__restrict__ rp,
-                                               const int32_t *__restrict__ col,
-                                               const int32_t *__restrict__ lin, int *s_acc) {
-    const int lane = threadIdx.x & 63;
-    Off b = 0, e = 0;
-    if (valid) {
-        b = rp[v];
-        e = rp[v + 1];
-    }
-    const int d = int(e - b);
-    int D;
-    const int o = wave_excl_scan(d, &D);
-    s_acc[lane] = INT_MIN;
-    __builtin_amdgcn_wave_barrier();
-    for (int f0 = 0; f0 < D; f0 += 64 * U) {
-        int c[U], r[U];
+// 4-bit mask of the bytes of w equal to the byte replicated in b4 (exact, no carry leakage).
+__device__ __forceinline__ unsigned bytes_eq4(unsigned w, unsigned b4) {
+    const unsigned x = w ^ b4;
+    const unsigned z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+    return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+}
+
+// Dense gather.  Wave task = 64 consecutive agents (lane = agent); their rows are one
+// contiguous slice of col.  The slice is staged through LDS in windows of kWin edges with
+// coalesced, unconditional (clamped) loads; then every lane reads its own row's part of the
+// window from LDS and issues kK leader gathers at once (clamped, branch-free: a conditional
+// load would make the compiler wait for it at the join).
+constexpr int kWin = 1024;  // edges per LDS window per wave (4 KiB)
+constexpr int kK = 16;      // gathers in flight per lane
+
+template <typename Off>
+__device__ __forceinline__ int row_max_from_lds(const int *s_col, Off w0, Off lo, Off hi,
+                                                const int32_t *__restrict__ lin, int m) {
+    for (Off k = lo; k < hi; k += kK) {
+        int c[kK];
 #pragma unroll
-        for (int j = 0; j < U; ++j) {
-            const int f = f0 + j * 64 + lane;
-            const int fq = f < D ? f : D - 1;
-            int lo = 0;
-#pragma unroll
-            for (int step = 32; step > 0; step >>= 1) {
-                const int cand = lo + step;
-                if (__shfl(o, cand, 64) <= fq) lo = cand;
-            }
-            const Off br = __shfl(b, lo, 64);
-            const int orr = __shfl(o, lo, 64);
-            r[j] = f < D ? lo : -1;
-            c[j] = f < D ? col[br + Off(fq - orr)] : 0;
+        for (int j = 0; j < kK; ++j) {
+            const Off kk = (k + j < hi) ? k + j : hi - 1;
+            c[j] = s_col[kk - w0];
         }
-        int val[U];
+        int val[kK];
 #pragma unroll
-        for (int j = 0; j < U; ++j) val[j] = r[j] >= 0 ? lin[c[j]] : INT_MIN;  // U gathers in flight
+        for (int j = 0; j < kK; ++j) val[j] = lin[c[j]];
 #pragma unroll
-        for (int j = 0; j < U; ++j)
-            if (r[j] >= 0) atomicMax(&s_acc[r[j]], val[j]);
+        for (int j = 0; j < kK; ++j) m = max(m, val[j]);  // duplicates of the last edge are harmless
     }
-    __builtin_amdgcn_wave_barrier();
-    return s_acc[lane];
+    return m;
 }
 
 // ---------------------------------------------------------------- dense Jacobi round
-// Wave task = 64 consecutive agents.  counters: the ring (round t), or, when single, a plain
-// per-shard array (swarm_elect_round).
-template <int U, typename Off>
+template <typename Off>
 __global__ __launch_bounds__(kBlock) void k_elect_dense(
     const Off *__restrict__ rp, const int32_t *__restrict__ col, const int32_t *__restrict__ lin,
     int32_t *__restrict__ lout, int64_t n, unsigned long long *__restrict__ ring, int t, int guard) {
-    __shared__ int s_acc[kWavesPerBlock][64];
+    __shared__ int s_col[kWavesPerBlock][kWin];
     __shared__ unsigned long long s_bc, s_cnt[kWavesPerBlock];
     if (guard && t > 1 && round_total(ring, t - 1, &s_bc) == 0) return;  // converged: no-op
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int *sc = s_col[wid];
     unsigned long long mine = 0;
     const int64_t ntask = (n + 63) / 64;
-    for (int64_t task = int64_t(blockIdx.x) * kWavesPerBlock + wid; task < ntask;
-         task += int64_t(gridDim.x) * kWavesPerBlock) {
+    const int64_t stride = int64_t(gridDim.x) * kWavesPerBlock;
+    int64_t task = int64_t(blockIdx.x) * kWavesPerBlock + wid;
+    // software pipeline: a task's row bounds are loaded during the previous task.  Lanes past
+    // n get the empty row [rp[n], rp[n]) so lane 0 / lane 63 bound the wave's col slice.
+    auto bounds = [&](int64_t tk, Off &b_, Off &e_) {
+        const int64_t vv = tk * 64 + lane;
+        b_ = rp[vv < n ? vv : n];
+        e_ = rp[vv + 1 < n ? vv + 1 : n];
+    };
+    Off b = 0, e = 0;
+    if (task < ntask) bounds(task, b, e);
+    for (; task < ntask; task += stride) {
         const int64_t v = task * 64 + lane;
         const bool valid = v < n;
-        const int m = wave_gather_max<U, Off>(valid, v, rp, col, lin, s_acc[wid]);
-        bool up = false;
-        if (valid) {
-            const int own = lin[v];
-            up = m > own;
-            lout[v] = up ? m : own;
+        const Off W0 = __shfl(b, 0, 64), W1 = __shfl(e, 63, 64);
+        const int own = lin[valid ? v : n - 1];
+        Off nb = 0, ne = 0;
+        if (task + stride < ntask) bounds(task + stride, nb, ne);  // wave-uniform branch
+        int m = INT_MIN;
+        for (Off w0 = W0; w0 < W1; w0 += kWin) {
+            const Off wend = (W1 - w0 < kWin) ? W1 : w0 + kWin;
+#pragma unroll
+            for (int j = 0; j < kWin / 64; ++j) {
+                const Off k = w0 + j * 64 + lane;
+                sc[j * 64 + lane] = col[k < wend ? k : wend - 1];
+            }
+            __builtin_amdgcn_wave_barrier();
+            const Off lo = b > w0 ? b : w0, hi = e < wend ? e : wend;
+            m = row_max_from_lds<Off>(sc, w0, lo, hi, lin, m);
+            __builtin_amdgcn_wave_barrier();
         }
+        const bool up = valid && m > own;
+        if (valid) lout[v] = up ? m : own;
         mine += __popcll(__ballot(up));
+        b = nb;
+        e = ne;
     }
     if (lane == 0) s_cnt[wid] = mine;
     __syncthreads();
@@ -155,37 +168,40 @@ __global__ __launch_bounds__(kBlock) void k_elect_dense(
 }
 
 // ------------------------------------------------------------- frontier: gather phase
-// Work unit = a chunk of 1024 agents (4 stamps per thread).  Changes of a chunk go to list
-// segment (chunk % 64), reserved by ONE atomic on that segment's counter shard.
-template <int U, typename Off>
+// Work unit = a chunk of kChunk agents (8 stamps per thread, one 8-B load).  Active agents
+// are compacted into LDS; then 2 lanes per agent each issue kK unconditional row loads and
+// kK leader gathers.  Changes of a chunk go to list segment (chunk % 64), reserved by ONE
+// atomic on that segment's counter shard.  tot[t-1] (one word, written by the previous apply)
+// is the convergence guard.
+template <typename Off>
 __global__ __launch_bounds__(kBlock) void k_elect_pull(
     const Off *__restrict__ rp, const int32_t *__restrict__ col, const int32_t *__restrict__ leader,
     const uint8_t *__restrict__ act, int64_t n, int2 *__restrict__ list, int64_t seg_cap,
-    unsigned long long *__restrict__ ring, int t, int with_stats) {
+    unsigned long long *__restrict__ ring, const unsigned long long *__restrict__ tot, int t,
+    int with_stats) {
     __shared__ int s_list[kChunk];
     __shared__ int2 s_chg[kChunk];
-    __shared__ int s_acc[kWavesPerBlock][64];
     __shared__ int s_wave[kWavesPerBlock];
     __shared__ int s_nchg;
-    __shared__ unsigned long long s_bc, s_base;
+    __shared__ unsigned long long s_base;
     __shared__ long long s_act[kWavesPerBlock], s_edg[kWavesPerBlock];
-    if (t > 1 && round_total(ring, t - 1, &s_bc) == 0) return;
-    const unsigned stamp4 = unsigned(t & 0xFF) * 0x01010101u;
+    if (t > 1 && tot[(t - 1) % kRing] == 0) return;
+    const unsigned stamp = unsigned(t & 0xFF);
+    const unsigned stamp4 = stamp * 0x01010101u;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     long long my_active = 0, my_edges = 0;
     const int64_t nchunks = (n + kChunk - 1) / kChunk;
     for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
         const int64_t c0 = chunk * kChunk;
-        // 1. my 4 stamps
-        const int64_t v0 = c0 + int64_t(threadIdx.x) * 4;
+        // 1. my 16 stamps
+        const int64_t v0 = c0 + int64_t(threadIdx.x) * kScan;
         unsigned mask = 0;
-        if (v0 + 4 <= n) {
-            const unsigned w = *reinterpret_cast<const unsigned *>(act + v0) ^ stamp4;
-            const unsigned z = ~(((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w | 0x7F7F7F7Fu);
-            mask = ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+        if (v0 + kScan <= n) {
+            const uint2 w = *reinterpret_cast<const uint2 *>(act + v0);
+            mask = bytes_eq4(w.x, stamp4) | (bytes_eq4(w.y, stamp4) << 4);
         } else {
-            for (int j = 0; j < 4 && v0 + j < n; ++j)
-                if (act[v0 + j] == uint8_t(t & 0xFF)) mask |= 1u << j;
+            for (int j = 0; j < kScan && v0 + j < n; ++j)
+                if (act[v0 + j] == stamp) mask |= 1u << j;
         }
         // 2. compact this chunk's active agents into LDS
         const int cnt = __popc(mask);
@@ -200,24 +216,41 @@ __global__ __launch_bounds__(kBlock) void k_elect_pull(
             off += (w < wid) ? s_wave[w] : 0;
             total += s_wave[w];
         }
+        if (total == 0) {  // block-uniform: nothing active in this chunk
+            __syncthreads();
+            continue;
+        }
         int pos = off + wexcl;
         while (mask) {
             const int j = __ffs(mask) - 1;
             mask &= mask - 1;
-            s_list[pos++] = threadIdx.x * 4 + j;
+            s_list[pos++] = threadIdx.x * kScan + j;
         }
         __syncthreads();
-        // 3. 64 active agents per wave task
-        for (int base = wid * 64; base < total; base += kBlock) {
-            const int i = base + lane;
+        // 3. two lanes per active agent
+        const int half = lane & 1;
+        for (int base = wid * 32; base < total; base += kBlock / 2) {
+            const int i = base + (lane >> 1);
             const bool valid = i < total;
-            const int64_t v = valid ? c0 + s_list[i] : 0;
-            const int m = wave_gather_max<U, Off>(valid, v, rp, col, leader, s_acc[wid]);
-            if (valid) {
-                const int own = leader[v];
+            const int64_t v = c0 + s_list[valid ? i : total - 1];
+            const Off b = rp[v], e = rp[v + 1];
+            int m = INT_MIN;
+            for (Off k = b + half * kK; k < e; k += 2 * kK) {
+                int c[kK];
+#pragma unroll
+                for (int j = 0; j < kK; ++j) c[j] = col[(k + j < e) ? k + j : e - 1];
+                int val[kK];
+#pragma unroll
+                for (int j = 0; j < kK; ++j) val[j] = leader[c[j]];
+#pragma unroll
+                for (int j = 0; j < kK; ++j) m = max(m, val[j]);
+            }
+            m = max(m, __shfl_xor(m, 1, 64));
+            const int own = leader[v];
+            if (valid && half == 0) {
                 if (with_stats) {
                     my_active += 1;
-                    my_edges += (long long)(rp[v + 1] - rp[v]);
+                    my_edges += (long long)(e - b);
                 }
                 if (m > own) {
                     const int at = atomicAdd(&s_nchg, 1);  // LDS
@@ -262,8 +295,14 @@ template <int G, typename Off>
 __global__ __launch_bounds__(kBlock) void k_elect_apply(
     const Off *__restrict__ rp, const int32_t *__restrict__ col, int32_t *__restrict__ leader,
     uint8_t *__restrict__ act, const int2 *__restrict__ list, int64_t seg_cap,
-    unsigned long long *__restrict__ ring, int t) {
+    unsigned long long *__restrict__ ring, unsigned long long *__restrict__ tot, int t) {
     const int seg = blockIdx.y;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < kWave) {  // round total -> guard word
+        unsigned long long v = *slot(ring, t, 0, threadIdx.x);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        if (threadIdx.x == 0) tot[t % kRing] = v;
+    }
     const int64_t cnt = int64_t(*slot(ring, t, 0, seg));
     if (cnt == 0) return;
     const int2 *src = list + int64_t(seg) * seg_cap;
@@ -314,22 +353,13 @@ int env_int(const char *name, int dflt) {
     return s ? atoi(s) : dflt;
 }
 
-#define SW_DISPATCH_U(U, ...)                                                 \
-    switch (U) {                                                              \
-        case 4: { constexpr int UU = 4; __VA_ARGS__; } break;                 \
-        case 16: { constexpr int UU = 16; __VA_ARGS__; } break;               \
-        default: { constexpr int UU = 8; __VA_ARGS__; } break;                \
-    }
-
 struct Tuning {
-    int U = 8;          // edges in flight per lane (gather)
     int G = 8;          // lanes per change (apply)
-    int dense_blocks = 4096;
+    int dense_blocks = 2048;
     Tuning() {
-        U = env_int("SWARM_GATHER_U", 8);
         G = env_int("SWARM_APPLY_G", 8);
         if (G != 4 && G != 16) G = 8;
-        dense_blocks = env_int("SWARM_DENSE_BLOCKS", 4096);
+        dense_blocks = env_int("SWARM_DENSE_BLOCKS", 2048);
     }
 };
 
@@ -342,25 +372,25 @@ template <typename Off>
 int launch_dense_round(const Off *rp, const int32_t *col, const int32_t *lin, int32_t *lout,
                        int64_t n, unsigned long long *ring, int t, int guard, hipStream_t s) {
     const unsigned grid = grid_for((n + 63) / 64, kWavesPerBlock, unsigned(tuning().dense_blocks));
-    SW_DISPATCH_U(tuning().U, hipLaunchKernelGGL((k_elect_dense<UU, Off>), dim3(grid), dim3(kBlock), 0, s,
-                                                 rp, col, lin, lout, n, ring, t, guard));
+    hipLaunchKernelGGL((k_elect_dense<Off>), dim3(grid), dim3(kBlock), 0, s, rp, col, lin, lout, n,
+                       ring, t, guard);
     SW_LAUNCHED();
     return SWARM_OK;
 }
 
 template <typename Off>
 int launch_frontier_round(const Off *rp, const int32_t *col, int32_t *leader, uint8_t *act,
-                          int2 *list, int64_t seg_cap, int64_t n, unsigned long long *ring, int t,
-                          int with_stats, hipStream_t s) {
+                          int2 *list, int64_t seg_cap, int64_t n, unsigned long long *ring,
+                          unsigned long long *tot, int t, int with_stats, hipStream_t s) {
     const unsigned gpull = grid_for(n, kChunk, 1u << 20);
-    SW_DISPATCH_U(tuning().U, hipLaunchKernelGGL((k_elect_pull<UU, Off>), dim3(gpull), dim3(kBlock), 0, s,
-                                                 rp, col, leader, act, n, list, seg_cap, ring, t, with_stats));
+    hipLaunchKernelGGL((k_elect_pull<Off>), dim3(gpull), dim3(kBlock), 0, s, rp, col, leader, act, n,
+                       list, seg_cap, ring, tot, t, with_stats);
     SW_LAUNCHED();
     const dim3 gapply(grid_for(seg_cap, kBlock / tuning().G, 64), kShards);
     switch (tuning().G) {
-        case 4: hipLaunchKernelGGL((k_elect_apply<4, Off>), gapply, dim3(kBlock), 0, s, rp, col, leader, act, list, seg_cap, ring, t); break;
-        case 16: hipLaunchKernelGGL((k_elect_apply<16, Off>), gapply, dim3(kBlock), 0, s, rp, col, leader, act, list, seg_cap, ring, t); break;
-        default: hipLaunchKernelGGL((k_elect_apply<8, Off>), gapply, dim3(kBlock), 0, s, rp, col, leader, act, list, seg_cap, ring, t); break;
+        case 4: hipLaunchKernelGGL((k_elect_apply<4, Off>), gapply, dim3(kBlock), 0, s, rp, col, leader, act, list, seg_cap, ring, tot, t); break;
+        case 16: hipLaunchKernelGGL((k_elect_apply<16, Off>), gapply, dim3(kBlock), 0, s, rp, col, leader, act, list, seg_cap, ring, tot, t); break;
+        default: hipLaunchKernelGGL((k_elect_apply<8, Off>), gapply, dim3(kBlock), 0, s, rp, col, leader, act, list, seg_cap, ring, tot, t); break;
     }
     SW_LAUNCHED();
     return SWARM_OK;
@@ -388,7 +418,8 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     }
     const size_t ring_words = size_t(kRing) * kCounters * kRoundWords;
     unsigned long long *ring;
-    SW_ALLOC(ring, ctx, S_CHANGES, ring_words * 8);
+    SW_ALLOC(ring, ctx, S_CHANGES, (ring_words + kRing) * 8);
+    unsigned long long *tot = ring + ring_words;  // per-round totals (frontier guard words)
     SW_HIP(hipMemcpyAsync(leader, ids, size_t(n) * 4, hipMemcpyDeviceToDevice, s));
     int32_t *bufs[2] = {leader, nullptr};
     uint8_t *act = nullptr;
@@ -429,8 +460,8 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         for (int r = t; r <= tend; ++r) {
             rc = (mode == SWARM_ELECT_DENSE)
                      ? launch_dense_round<Off>(rp, col, bufs[(r - 1) & 1], bufs[r & 1], n, ring, r, 1, s)
-                     : launch_frontier_round<Off>(rp, col, leader, act, list, seg_cap, n, ring, r,
-                                                  with_stats, s);
+                     : launch_frontier_round<Off>(rp, col, leader, act, list, seg_cap, n, ring, tot,
+                                                  r, with_stats, s);
             if (rc) return rc;
         }
         launched = tend;
