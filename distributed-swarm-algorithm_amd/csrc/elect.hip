@@ -31,6 +31,7 @@
 #include <climits>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "swarm_common.h"
 
@@ -117,6 +118,9 @@ __global__ __launch_bounds__(kBlock) void k_elect_dense(
     __shared__ int s_col[kWavesPerBlock][kWin];
     __shared__ unsigned long long s_bc, s_cnt[kWavesPerBlock];
     if (guard && t > 1 && round_total(ring, t - 1, &s_bc) == 0) return;  // converged: no-op
+    if (guard && blockIdx.x == 0)  // recycle the counter slots of round t + kRing/2
+        for (int i = threadIdx.x; i < kCounters * kShards; i += kBlock)
+            *slot(ring, t + kRing / 2, i / kShards, i % kShards) = 0;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     int *sc = s_col[wid];
     unsigned long long mine = 0;
@@ -178,14 +182,14 @@ __global__ __launch_bounds__(kBlock) void k_elect_pull(
     const Off *__restrict__ rp, const int32_t *__restrict__ col, const int32_t *__restrict__ leader,
     const uint8_t *__restrict__ act, int64_t n, int2 *__restrict__ list, int64_t seg_cap,
     unsigned long long *__restrict__ ring, const unsigned long long *__restrict__ tot, int t,
-    int with_stats) {
+    int with_stats, int guard) {
     __shared__ int s_list[kChunk];
     __shared__ int2 s_chg[kChunk];
     __shared__ int s_wave[kWavesPerBlock];
     __shared__ int s_nchg;
     __shared__ unsigned long long s_base;
     __shared__ long long s_act[kWavesPerBlock], s_edg[kWavesPerBlock];
-    if (t > 1 && tot[(t - 1) % kRing] == 0) return;
+    if (guard && t > 1 && tot[(t - 1) % kRing] == 0) return;
     const unsigned stamp = unsigned(t & 0xFF);
     const unsigned stamp4 = stamp * 0x01010101u;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -297,11 +301,17 @@ __global__ __launch_bounds__(kBlock) void k_elect_apply(
     uint8_t *__restrict__ act, const int2 *__restrict__ list, int64_t seg_cap,
     unsigned long long *__restrict__ ring, unsigned long long *__restrict__ tot, int t) {
     const int seg = blockIdx.y;
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < kWave) {  // round total -> guard word
-        unsigned long long v = *slot(ring, t, 0, threadIdx.x);
+    if (blockIdx.x == 0 && blockIdx.y == 0) {
+        if (threadIdx.x < kWave) {  // round total -> guard word
+            unsigned long long v = *slot(ring, t, 0, threadIdx.x);
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-        if (threadIdx.x == 0) tot[t % kRing] = v;
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+            if (threadIdx.x == 0) tot[t % kRing] = v;
+        }
+        // recycle the counter slots of round t + kRing/2 (read back long before: the host
+        // reads every <= kRing/2 rounds)
+        for (int i = threadIdx.x; i < kCounters * kShards; i += kBlock)
+            *slot(ring, t + kRing / 2, i / kShards, i % kShards) = 0;
     }
     const int64_t cnt = int64_t(*slot(ring, t, 0, seg));
     if (cnt == 0) return;
@@ -316,6 +326,32 @@ __global__ __launch_bounds__(kBlock) void k_elect_apply(
             if (sub == 0) leader[e.x] = e.y;
             const Off e1 = rp[e.x + 1];
             for (Off k = rp[e.x] + sub; k < e1; k += G) act[col[k]] = next;
+        }
+    }
+}
+
+// Sharded runs: halo values received for ghost agents [begin, begin + count).  A ghost whose
+// leader rose is written and its local neighbours are stamped for round t + 1 (ghost rows of
+// the local CSR list them).  Ghost changes are their owner's changes: not counted here.
+template <int G, typename Off>
+__global__ __launch_bounds__(kBlock) void k_frontier_ghosts(
+    const Off *__restrict__ rp, const int32_t *__restrict__ col, int32_t *__restrict__ leader,
+    uint8_t *__restrict__ act, int64_t begin, int64_t count, const int32_t *__restrict__ incoming,
+    int t) {
+    const uint8_t next = uint8_t((t + 1) & 0xFF);
+    constexpr int GPB = kBlock / G;
+    const int sub = threadIdx.x & (G - 1);
+    for (int64_t base = int64_t(blockIdx.x) * GPB; base < count; base += int64_t(gridDim.x) * GPB) {
+        const int64_t i = base + threadIdx.x / G;
+        if (i < count) {
+            const int64_t g = begin + i;
+            const int nv = incoming[i];
+            if (nv > leader[g]) {
+                __builtin_amdgcn_wave_barrier();
+                if (sub == 0) leader[g] = nv;
+                const Off e1 = rp[g + 1];
+                for (Off k = rp[g] + sub; k < e1; k += G) act[col[k]] = next;
+            }
         }
     }
 }
@@ -381,11 +417,13 @@ int launch_dense_round(const Off *rp, const int32_t *col, const int32_t *lin, in
 template <typename Off>
 int launch_frontier_round(const Off *rp, const int32_t *col, int32_t *leader, uint8_t *act,
                           int2 *list, int64_t seg_cap, int64_t n, unsigned long long *ring,
-                          unsigned long long *tot, int t, int with_stats, hipStream_t s) {
+                          unsigned long long *tot, int t, int with_stats, hipStream_t s,
+                          hipEvent_t mid = nullptr, int guard = 1) {
     const unsigned gpull = grid_for(n, kChunk, 1u << 20);
     hipLaunchKernelGGL((k_elect_pull<Off>), dim3(gpull), dim3(kBlock), 0, s, rp, col, leader, act, n,
-                       list, seg_cap, ring, tot, t, with_stats);
+                       list, seg_cap, ring, tot, t, with_stats, guard);
     SW_LAUNCHED();
+    if (mid) SW_HIP(hipEventRecord(mid, s));
     const dim3 gapply(grid_for(seg_cap, kBlock / tuning().G, 64), kShards);
     switch (tuning().G) {
         case 4: hipLaunchKernelGGL((k_elect_apply<4, Off>), gapply, dim3(kBlock), 0, s, rp, col, leader, act, list, seg_cap, ring, tot, t); break;
@@ -405,11 +443,13 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     SW_ARG(n >= 0, "n < 0");
     SW_ARG(n < (int64_t(1) << 31), "n must be < 2^31");
     SW_ARG(max_rounds >= 1, "max_rounds < 1");
+    const bool timed = (mode & SWARM_ELECT_TIMED) != 0;
+    mode &= ~SWARM_ELECT_TIMED;
     SW_ARG(mode == SWARM_ELECT_DENSE || mode == SWARM_ELECT_FRONTIER, "unknown mode");
     SW_ARG(rounds_exec != nullptr, "rounds_exec is NULL");
     SW_ARG(n == 0 || (rp && ids && leader && state), "NULL array (col may be NULL only without edges)");
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (st) *st = swarm_elect_stats{0, 0, 0};
+    if (st) *st = swarm_elect_stats{0, 0, 0, 0, 0.0, 0.0, 0};
     if (n == 0) {  // an empty swarm: round 1 changes nothing
         *rounds_exec = 1;
         if (changes_host) changes_host[0] = 0;
@@ -442,27 +482,36 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     SW_ALLOC(dtot, ctx, S_ESTATS, size_t(kCounters) * 8 * kMaxBatch);
 
     int found = -1, t = 1, batch = 8, launched = 0;
-    int64_t act_sum = 0, edge_sum = 0;
-    auto zero_rounds = [&](int r0, int r1) -> int {  // ring slots of rounds [r0, r1]
-        for (int r = r0; r <= r1;) {
-            const int a = r % kRing;
-            const int len = std::min(r1 - r + 1, kRing - a);
-            SW_HIP(hipMemsetAsync(ring + size_t(a) * per_round, 0, size_t(len) * per_round * 8, s));
-            r += len;
-        }
-        return SWARM_OK;
-    };
+    int64_t act_sum = 0, edge_sum = 0, chg_sum = 0;
+    // optional per-kernel timing: events [3r] before gather, [3r+1] between, [3r+2] after apply
+    std::vector<hipEvent_t> ev;
+    double g_ms = 0, a_ms = 0;
+    int64_t timed_rounds = 0;
+    if (timed) {
+        ev.resize(3 * kMaxBatch);
+        for (auto &x : ev) SW_HIP(hipEventCreate(&x));
+    }
+    struct EvFree {
+        std::vector<hipEvent_t> &v;
+        ~EvFree() { for (auto x : v) (void)hipEventDestroy(x); }
+    } ev_free{ev};
+    // every counter slot starts at zero; afterwards each round's kernels recycle the slots of
+    // the round kRing/2 ahead (dense: the batch-totals kernel does it)
+    SW_HIP(hipMemsetAsync(ring, 0, (ring_words + kRing) * 8, s));
+    (void)per_round;
     // slot of round 0 (read by round 1's guard only when t > 1: never) stays untouched
     while (t <= max_rounds && found < 0) {
         const int tend = (max_rounds - t + 1 < batch) ? max_rounds : t + batch - 1;
-        int rc = zero_rounds(t, tend);
-        if (rc) return rc;
+        int rc = 0;
         for (int r = t; r <= tend; ++r) {
+            hipEvent_t *e3 = timed ? &ev[3 * (r - t)] : nullptr;
+            if (e3) SW_HIP(hipEventRecord(e3[0], s));
             rc = (mode == SWARM_ELECT_DENSE)
                      ? launch_dense_round<Off>(rp, col, bufs[(r - 1) & 1], bufs[r & 1], n, ring, r, 1, s)
                      : launch_frontier_round<Off>(rp, col, leader, act, list, seg_cap, n, ring, tot,
-                                                  r, with_stats, s);
+                                                  r, with_stats, s, e3 ? e3[1] : nullptr);
             if (rc) return rc;
+            if (e3) SW_HIP(hipEventRecord(e3[2], s));
         }
         launched = tend;
         // per-round totals of rounds [t, tend], reduced on device, then one small copy
@@ -476,6 +525,20 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
             if (changes_host) changes_host[r - 1] = int64_t(c);
             act_sum += int64_t(a);
             edge_sum += int64_t(ed);
+            chg_sum += int64_t(c);
+            if (timed) {
+                float x = 0, y = 0;
+                hipEvent_t *e3 = &ev[3 * (r - t)];
+                if (mode == SWARM_ELECT_DENSE) {
+                    SW_HIP(hipEventElapsedTime(&x, e3[0], e3[2]));
+                } else {
+                    SW_HIP(hipEventElapsedTime(&x, e3[0], e3[1]));
+                    SW_HIP(hipEventElapsedTime(&y, e3[1], e3[2]));
+                }
+                g_ms += x;
+                a_ms += y;
+                ++timed_rounds;
+            }
             if (c == 0) {
                 found = r;
                 break;
@@ -494,6 +557,10 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     *rounds_exec = last;
     if (st) {
         st->rounds_launched = launched;
+        st->changes_total = chg_sum;
+        st->gather_ms = g_ms;
+        st->apply_ms = a_ms;
+        st->gather_launches = timed_rounds;
         if (mode == SWARM_ELECT_DENSE) {
             Off e = 0;
             SW_HIP(hipMemcpyAsync(&e, rp + n, sizeof(Off), hipMemcpyDeviceToHost, s));
@@ -527,6 +594,85 @@ int swarm_elect_i64(swarm_ctx *ctx, int64_t n, const int64_t *row_ptr, const int
                     swarm_elect_stats *stats, void *stream) {
     return swarm::elect_impl<int64_t>(ctx, n, row_ptr, col, ids, leader, state, max_rounds, mode,
                                       rounds_exec, changes_per_round, stats, stream);
+}
+
+int swarm_frontier_begin(swarm_ctx *ctx, int64_t n_rows, int64_t n_all, const int32_t *init,
+                         int32_t *leader, void *stream) {
+    using namespace swarm;
+    SW_ARG(ctx != nullptr, "ctx is NULL");
+    SW_ARG(n_rows >= 0 && n_all >= n_rows && n_all < (int64_t(1) << 31), "sizes out of range");
+    SW_ARG(n_all == 0 || (init && leader), "NULL array");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const size_t ring_words = size_t(kRing) * kCounters * kRoundWords;
+    unsigned long long *ring;
+    uint8_t *act;
+    int2 *list;
+    const int64_t nchunks = (n_rows + kChunk - 1) / kChunk;
+    const int64_t seg_cap = ((nchunks + kShards - 1) / kShards) * kChunk;
+    SW_ALLOC(ring, ctx, S_CHANGES, (ring_words + kRing) * 8);
+    SW_ALLOC(act, ctx, S_ACT, size_t(n_all) + 16);
+    SW_ALLOC(list, ctx, S_LIST, size_t(seg_cap > 0 ? seg_cap : 1) * kShards * 8);
+    SW_HIP(hipMemsetAsync(ring, 0, (ring_words + kRing) * 8, s));
+    if (n_all) {
+        SW_HIP(hipMemsetAsync(act, 1, size_t(n_all), s));
+        SW_HIP(hipMemcpyAsync(leader, init, size_t(n_all) * 4, hipMemcpyDeviceToDevice, s));
+    }
+    ctx->step_rows = n_rows;
+    ctx->step_all = n_all;
+    return SWARM_OK;
+}
+
+int swarm_frontier_step(swarm_ctx *ctx, int32_t t, const int32_t *row_ptr, const int32_t *col,
+                        int32_t *leader, void *stream) {
+    using namespace swarm;
+    SW_ARG(ctx != nullptr, "ctx is NULL");
+    SW_ARG(t >= 1, "round must be >= 1");
+    SW_ARG(ctx->cap[S_ACT] >= size_t(ctx->step_all), "swarm_frontier_begin first");
+    const int64_t n = ctx->step_rows;
+    if (n == 0) return SWARM_OK;
+    SW_ARG(row_ptr && leader, "NULL array");
+    const int64_t nchunks = (n + kChunk - 1) / kChunk;
+    const int64_t seg_cap = ((nchunks + kShards - 1) / kShards) * kChunk;
+    unsigned long long *ring = static_cast<unsigned long long *>(ctx->slot[S_CHANGES]);
+    unsigned long long *tot = ring + size_t(kRing) * kCounters * kRoundWords;
+    return launch_frontier_round<int32_t>(row_ptr, col, leader, static_cast<uint8_t *>(ctx->slot[S_ACT]),
+                                          static_cast<int2 *>(ctx->slot[S_LIST]), seg_cap, n, ring, tot, t,
+                                          0, static_cast<hipStream_t>(stream), nullptr, /*guard=*/0);
+}
+
+int swarm_frontier_ghosts(swarm_ctx *ctx, int32_t t, int64_t begin, int64_t count,
+                          const int32_t *incoming, const int32_t *row_ptr, const int32_t *col,
+                          int32_t *leader, void *stream) {
+    using namespace swarm;
+    SW_ARG(ctx != nullptr, "ctx is NULL");
+    SW_ARG(begin >= 0 && count >= 0 && begin + count <= ctx->step_all, "ghost range out of bounds");
+    if (count == 0) return SWARM_OK;
+    SW_ARG(incoming && row_ptr && leader, "NULL array");
+    hipLaunchKernelGGL((k_frontier_ghosts<8, int32_t>), dim3(grid_for(count, kBlock / 8, 2048)), dim3(kBlock), 0,
+                       static_cast<hipStream_t>(stream), row_ptr, col, leader,
+                       static_cast<uint8_t *>(ctx->slot[S_ACT]), begin, count, incoming, t);
+    SW_LAUNCHED();
+    return SWARM_OK;
+}
+
+int swarm_frontier_changes(swarm_ctx *ctx, int32_t t0, int32_t t1, int64_t *out, void *stream) {
+    using namespace swarm;
+    SW_ARG(ctx != nullptr && out != nullptr, "NULL argument");
+    SW_ARG(t0 >= 1 && t1 >= t0 && t1 - t0 < kRing / 2, "round range must be 1 <= t0 <= t1 < t0 + 256");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    unsigned long long *ring = static_cast<unsigned long long *>(ctx->slot[S_CHANGES]);
+    SW_ARG(ring != nullptr, "swarm_frontier_begin first");
+    const int nr = t1 - t0 + 1;
+    unsigned long long *dtot;
+    SW_ALLOC(dtot, ctx, S_ESTATS, size_t(kCounters) * 8 * (kRing / 2));
+    hipLaunchKernelGGL(k_batch_totals, dim3(nr), dim3(kWave), 0, s, ring, t0, dtot);
+    SW_LAUNCHED();
+    unsigned long long *h = static_cast<unsigned long long *>(pinned(ctx, size_t(kCounters) * 8 * (kRing / 2)));
+    if (!h) return SWARM_ERR_OOM;
+    SW_HIP(hipMemcpyAsync(h, dtot, size_t(nr) * kCounters * 8, hipMemcpyDeviceToHost, s));
+    SW_HIP(hipStreamSynchronize(s));
+    for (int i = 0; i < nr; ++i) out[i] = int64_t(h[size_t(i) * kCounters]);
+    return SWARM_OK;
 }
 
 int swarm_elect_round(swarm_ctx *ctx, int64_t n_rows, const int32_t *row_ptr,

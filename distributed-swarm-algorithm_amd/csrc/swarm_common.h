@@ -49,6 +49,8 @@ struct swarm_ctx {
     size_t cap[swarm::S_NUM] = {};
     void *host_pinned = nullptr;   // small pinned staging buffer for scalar/array readback
     size_t host_cap = 0;
+    int64_t step_rows = 0;         // frontier stepper: rows gathered / agents (rows + ghosts)
+    int64_t step_all = 0;
 };
 
 namespace swarm {

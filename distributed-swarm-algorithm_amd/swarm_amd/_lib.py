@@ -19,13 +19,14 @@ LIB_PATH = os.path.join(HERE, "libswarm.so")
 OK, NOT_CONVERGED = 0, 1
 ERR_ARG, ERR_HIP, ERR_OOM, ERR_RANGE = -1, -2, -3, -4
 FOLLOWER, ELECTION_WAIT, LEADER = 1, 2, 3
-ELECT_DENSE, ELECT_FRONTIER = 0, 1
+ELECT_DENSE, ELECT_FRONTIER, ELECT_TIMED = 0, 1, 0x100
 ALLOC_AUTO, ALLOC_BINNED, ALLOC_DENSE = 0, 1, 2
 
 # every symbol include/swarm.h declares (tests/test_capi.py checks the two agree)
 EXPORTS = ("swarm_last_error", "swarm_version", "swarm_ctx_create", "swarm_ctx_destroy",
            "swarm_elect", "swarm_elect_i64", "swarm_elect_round", "swarm_allocate",
-           "swarm_utility", "swarm_build_rgg", "swarm_cell_order")
+           "swarm_utility", "swarm_build_rgg", "swarm_cell_order", "swarm_frontier_begin",
+           "swarm_frontier_step", "swarm_frontier_ghosts", "swarm_frontier_changes")
 
 
 class SwarmError(RuntimeError):
@@ -42,7 +43,9 @@ class AllocStats(ctypes.Structure):
 
 class ElectStats(ctypes.Structure):
     _fields_ = [("rounds_launched", ctypes.c_int64), ("active_total", ctypes.c_int64),
-                ("edges_total", ctypes.c_int64)]
+                ("edges_total", ctypes.c_int64), ("changes_total", ctypes.c_int64),
+                ("gather_ms", ctypes.c_double), ("apply_ms", ctypes.c_double),
+                ("gather_launches", ctypes.c_int64)]
 
 
 _lib = None
@@ -74,6 +77,10 @@ def load(path: str = LIB_PATH):
         L.swarm_utility.argtypes = [P, i64, P, P, P, P, d, P, P]
         L.swarm_build_rgg.argtypes = [P, i64, P, d, P, P, i64, ctypes.POINTER(i64), P]
         L.swarm_cell_order.argtypes = [P, i64, P, d, P, P]
+        L.swarm_frontier_begin.argtypes = [P, i64, i64, P, P, P]
+        L.swarm_frontier_step.argtypes = [P, i32, P, P, P, P]
+        L.swarm_frontier_ghosts.argtypes = [P, i32, i64, i64, P, P, P, P, P]
+        L.swarm_frontier_changes.argtypes = [P, i32, i32, P, P]
         for name in EXPORTS:
             if name not in ("swarm_last_error", "swarm_version"):
                 getattr(L, name).restype = ctypes.c_int

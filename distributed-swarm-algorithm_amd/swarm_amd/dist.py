@@ -1,0 +1,263 @@
+"""Multi-GPU swarm step: agents sharded across ranks, one process per GPU.
+
+Partition.  The global square is cut into horizontal strips, one per rank (the agent storage
+order inside a shard is row-major cell order, so a strip is a contiguous ID-free range of the
+spatial order).  Each rank owns the agents inside its strip and keeps read-only *ghost* copies
+of the neighbouring ranks' agents within one radio radius of the shared border.
+
+Election (exact, contract E2).  Rounds run on every rank in lockstep through the frontier
+stepper (include/swarm.h: swarm_frontier_*): round t gathers the owned agents, then the
+owned boundary agents' new leaders go to the neighbour ranks (torch.distributed P2P --
+RCCL over xGMI on GPUs, gloo in the CPU tests) and arrive as ghost updates that activate
+their local neighbours for round t + 1.  Per-round owned change counts are summed over ranks
+with one all-reduce every `check_every` rounds; the first globally zero round ends the run and
+is rounds_exec (rounds after it are no-ops everywhere).  Result: the same leaders, rounds and
+per-round change counts as a single-GPU run on the union graph.
+
+Allocation (exact, contract A-H).  Each rank resolves the tasks inside its strip.  Every
+agent that can claim such a task lies within the claim radius Rp of it, so each rank first
+receives the neighbour ranks' agents within Rp of the border (positions, IDs, capabilities),
+runs swarm_allocate over owned + halo agents, and sends the halo agents' won counts back to
+their owners.  No data-path all-gather; one small all-reduce for the global counters.
+
+Exchanges per election round: 2 x (boundary agents x 4 B) per neighbour; ~20k agents per
+border at 10M agents per GPU, i.e. ~80 KB -- latency-bound, a few microseconds over xGMI.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def _neighbors(rank, world):
+    return (rank - 1 if rank > 0 else None), (rank + 1 if rank < world - 1 else None)
+
+
+class Halo:
+    """Neighbour exchange along the strip chain (rank-1 <-> rank <-> rank+1)."""
+
+    def __init__(self, group=None, device=None):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.lo, self.hi = _neighbors(self.rank, self.world)
+        self.device = device
+
+    def _peer(self, r):
+        return dist.get_global_rank(self.group, r) if self.group is not None else r
+
+    def exchange(self, to_lo, to_hi, n_from_lo, n_from_hi, like):
+        """Send to_lo to rank-1 and to_hi to rank+1; receive n_from_lo / n_from_hi elements."""
+        shape_tail = tuple(like.shape[1:])
+        from_lo = torch.empty((n_from_lo,) + shape_tail, dtype=like.dtype, device=like.device)
+        from_hi = torch.empty((n_from_hi,) + shape_tail, dtype=like.dtype, device=like.device)
+        ops = []
+        if self.lo is not None:
+            if to_lo.numel():
+                ops.append(dist.P2POp(dist.isend, to_lo.contiguous(), self._peer(self.lo), self.group))
+            if n_from_lo:
+                ops.append(dist.P2POp(dist.irecv, from_lo, self._peer(self.lo), self.group))
+        if self.hi is not None:
+            if to_hi.numel():
+                ops.append(dist.P2POp(dist.isend, to_hi.contiguous(), self._peer(self.hi), self.group))
+            if n_from_hi:
+                ops.append(dist.P2POp(dist.irecv, from_hi, self._peer(self.hi), self.group))
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        return from_lo, from_hi
+
+    def all_reduce_sum(self, arr):
+        """Element-wise sum over ranks of a small int64 vector (host array in, host array out)."""
+        t = torch.as_tensor(np.asarray(arr, np.int64), device=self.device)
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t.cpu().numpy()
+
+    def exchange_counts(self, n_to_lo, n_to_hi):
+        t = torch.tensor([n_to_lo], dtype=torch.int64, device=self.device)
+        u = torch.tensor([n_to_hi], dtype=torch.int64, device=self.device)
+        a, b = self.exchange(t if self.lo is not None else t[:0], u if self.hi is not None else u[:0],
+                             1 if self.lo is not None else 0, 1 if self.hi is not None else 0, t)
+        return (int(a.item()) if a.numel() else 0), (int(b.item()) if b.numel() else 0)
+
+
+@dataclass
+class ShardElectResult:
+    rounds_exec: int
+    changes: np.ndarray        # GLOBAL per-round change counts, rounds 1..rounds_exec
+    leader: torch.Tensor       # owned agents (storage order), int32
+    state: torch.Tensor        # owned agents, uint8
+    converged: bool
+
+
+class GpuBackend:
+    """libswarm.so on the rank's GPU (the product path)."""
+
+    def __init__(self, device):
+        from . import _lib
+        self.L = _lib
+        self.device = device
+        _lib.load()
+
+    def cell_order(self, pos):
+        n = pos.shape[0]
+        perm = torch.empty(n, dtype=torch.int32, device=self.device)
+        if n:
+            self.L.check(self.L.lib().swarm_cell_order(self.L.ctx(), n, self.L.ptr(pos), 1.0,
+                                                       self.L.ptr(perm), self.L.stream()))
+        return perm.long()
+
+    def build_graph(self, pos, radius):
+        import ctypes
+        n = pos.shape[0]
+        rp = torch.empty(n + 1, dtype=torch.int32, device=self.device)
+        ne = ctypes.c_int64(0)
+        L = self.L
+        L.check(L.lib().swarm_build_rgg(L.ctx(), n, L.ptr(pos) if n else None, float(radius), L.ptr(rp), None, 0,
+                                        ctypes.byref(ne), L.stream()))
+        col = torch.empty(max(ne.value, 1), dtype=torch.int32, device=self.device)
+        L.check(L.lib().swarm_build_rgg(L.ctx(), n, L.ptr(pos) if n else None, float(radius), L.ptr(rp), L.ptr(col),
+                                        col.numel(), ctypes.byref(ne), L.stream()))
+        return rp, col
+
+    def begin(self, n_rows, init, leader):
+        L = self.L
+        L.check(L.lib().swarm_frontier_begin(L.ctx(), n_rows, init.numel(), L.ptr(init), L.ptr(leader),
+                                             L.stream()))
+
+    def step(self, t, rp, col, leader):
+        L = self.L
+        L.check(L.lib().swarm_frontier_step(L.ctx(), t, L.ptr(rp), L.ptr(col), L.ptr(leader), L.stream()))
+
+    def ghosts(self, t, begin, incoming, rp, col, leader):
+        L = self.L
+        if incoming.numel():
+            L.check(L.lib().swarm_frontier_ghosts(L.ctx(), t, begin, incoming.numel(), L.ptr(incoming),
+                                                  L.ptr(rp), L.ptr(col), L.ptr(leader), L.stream()))
+
+    def changes(self, t0, t1):
+        L = self.L
+        out = np.zeros(t1 - t0 + 1, np.int64)
+        L.check(L.lib().swarm_frontier_changes(L.ctx(), t0, t1, out.ctypes.data_as(__import__("ctypes").c_void_p),
+                                               L.stream()))
+        return out
+
+    def allocate(self, ids, pos, caps, tx, ty, treq, **kw):
+        from .swarm import Swarm
+        s = Swarm.__new__(Swarm)  # a view over already-resident tensors (no reordering)
+        s.device, s.n, s.ids, s.pos, s.caps = self.device, ids.numel(), ids, pos, caps
+        s.perm, s.layout, s._id_index = None, "input", None
+        s.row_ptr = s.col = None
+        return s.allocate(tx, ty, treq, **kw)
+
+
+class ShardedSwarm:
+    """This rank's shard of a strip-partitioned swarm (see module docstring)."""
+
+    def __init__(self, ids, x, y, caps, strip, *, radius: float = 1.0, group=None, device=None,
+                 backend=None, halo=None):
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.backend = backend if backend is not None else GpuBackend(self.device)
+        self.halo = halo if halo is not None else Halo(group, self.device)
+        self.radius = float(radius)
+        self.strip = (float(strip[0]), float(strip[1]))
+        if self.halo.world > 1 and self.strip[1] - self.strip[0] <= self.radius:
+            raise ValueError("strips must be taller than the radio radius")
+        dev = self.device
+        pos = torch.stack([torch.as_tensor(np.ascontiguousarray(x), dtype=torch.float64),
+                           torch.as_tensor(np.ascontiguousarray(y), dtype=torch.float64)], 1).to(dev)
+        ids_t = torch.as_tensor(np.ascontiguousarray(ids, dtype=np.int32)).to(dev)
+        caps_np = np.ascontiguousarray(caps if caps is not None else np.zeros(len(ids), np.uint32),
+                                       dtype=np.uint32).view(np.int32)
+        caps_t = torch.as_tensor(caps_np).to(dev)
+        perm = self.backend.cell_order(pos) if pos.shape[0] > 1 else torch.arange(pos.shape[0], device=dev)
+        self.pos, self.ids, self.caps = pos[perm].contiguous(), ids_t[perm].contiguous(), caps_t[perm].contiguous()
+        self.perm = perm
+        self.n_own = int(self.ids.numel())
+        # ghosts: neighbour ranks' agents within one radius of the shared borders
+        self.send_lo, self.send_hi = self._border(self.radius)
+        n_lo, n_hi = self.halo.exchange_counts(self.send_lo.numel(), self.send_hi.numel())
+        gp_lo, gp_hi = self.halo.exchange(self.pos[self.send_lo], self.pos[self.send_hi], n_lo, n_hi, self.pos)
+        gi_lo, gi_hi = self.halo.exchange(self.ids[self.send_lo], self.ids[self.send_hi], n_lo, n_hi, self.ids)
+        self.n_glo, self.n_ghi = n_lo, n_hi
+        self.all_pos = torch.cat([self.pos, gp_lo, gp_hi]).contiguous()
+        self.all_ids = torch.cat([self.ids, gi_lo, gi_hi]).contiguous()
+        self.row_ptr, self.col = self.backend.build_graph(self.all_pos, self.radius)
+        self.leader = torch.empty(self.all_ids.numel(), dtype=torch.int32, device=dev)
+
+    def _border(self, width):
+        y = self.pos[:, 1]
+        lo = torch.nonzero(y <= self.strip[0] + width + 1e-9).flatten() if self.halo.lo is not None \
+            else torch.zeros(0, dtype=torch.long, device=self.device)
+        hi = torch.nonzero(y >= self.strip[1] - width - 1e-9).flatten() if self.halo.hi is not None \
+            else torch.zeros(0, dtype=torch.long, device=self.device)
+        return lo, hi
+
+    # ------------------------------------------------------------------ election
+    def elect(self, max_rounds: int = 1 << 16, check_every: int = 64) -> ShardElectResult:
+        be, h = self.backend, self.halo
+        rp, col, lead = self.row_ptr, self.col, self.leader
+        be.begin(self.n_own, self.all_ids, lead)
+        g_lo, g_hi = self.n_own, self.n_own + self.n_glo
+        changes = []
+        t, found = 1, -1
+        check_every = max(1, min(int(check_every), 256))
+        while t <= max_rounds and found < 0:
+            tend = min(max_rounds, t + check_every - 1)
+            for r in range(t, tend + 1):
+                be.step(r, rp, col, lead)
+                in_lo, in_hi = h.exchange(lead[self.send_lo], lead[self.send_hi], self.n_glo, self.n_ghi, lead)
+                be.ghosts(r, g_lo, in_lo, rp, col, lead)
+                be.ghosts(r, g_hi, in_hi, rp, col, lead)
+            glob = h.all_reduce_sum(be.changes(t, tend))
+            for i, c in enumerate(glob):
+                changes.append(int(c))
+                if c == 0:
+                    found = t + i
+                    break
+            t = tend + 1
+        rounds = found if found > 0 else max_rounds
+        own = lead[: self.n_own]
+        state = torch.where(own == self.ids, 3, 1).to(torch.uint8)
+        return ShardElectResult(rounds, np.array(changes[:rounds], np.int64), own, state, found > 0)
+
+    # ------------------------------------------------------------------ allocation
+    def allocate(self, tx, ty, treq, *, claim_thr: float = 20.0, hysteresis: float = 5.0,
+                 u_scale: float = 100.0, mode: str = "auto"):
+        """Resolve this rank's tasks (inside its strip) exactly; returns (AllocResult over the
+        owned tasks, won counts of the owned agents in storage order, global stats)."""
+        h = self.halo
+        rp_claim = (u_scale / claim_thr - 1.0) * (1 + 1e-9) + 1e-12 if claim_thr > 0 and u_scale > 0 else math.inf
+        if math.isinf(rp_claim) and h.world > 1:
+            raise ValueError("sharded allocation needs a finite claim radius (claim_thr > 0)")
+        if h.world > 1 and self.strip[1] - self.strip[0] <= rp_claim:
+            raise ValueError("strips must be taller than the claim radius")
+        s_lo, s_hi = self._border(rp_claim if h.world > 1 else 0.0)
+        n_lo, n_hi = h.exchange_counts(s_lo.numel(), s_hi.numel())
+        hp = h.exchange(self.pos[s_lo], self.pos[s_hi], n_lo, n_hi, self.pos)
+        hi_ = h.exchange(self.ids[s_lo], self.ids[s_hi], n_lo, n_hi, self.ids)
+        hc = h.exchange(self.caps[s_lo], self.caps[s_hi], n_lo, n_hi, self.caps)
+        ids = torch.cat([self.ids, hi_[0], hi_[1]]).contiguous()
+        pos = torch.cat([self.pos, hp[0], hp[1]]).contiguous()
+        caps = torch.cat([self.caps, hc[0], hc[1]]).contiguous()
+        res = self.backend.allocate(ids, pos, caps, tx, ty, treq, claim_thr=claim_thr,
+                                    hysteresis=hysteresis, u_scale=u_scale, mode=mode)
+        won_all = res.won
+        # halo agents' wins go back to their owners (reverse of the halo exchange)
+        w_lo = won_all[self.n_own:self.n_own + n_lo]
+        w_hi = won_all[self.n_own + n_lo:]
+        back_lo, back_hi = h.exchange(w_lo, w_hi, s_lo.numel(), s_hi.numel(), won_all)
+        won = won_all[: self.n_own].clone()
+        if back_lo.numel():
+            won.index_add_(0, s_lo, back_lo)
+        if back_hi.numel():
+            won.index_add_(0, s_hi, back_hi)
+        keys = ("n_claims", "n_conflicts", "n_flagged", "n_candidates", "n_overflow")
+        st = h.all_reduce_sum([res.stats[k] for k in keys])
+        gstats = dict(zip(keys, (int(v) for v in st)))
+        return res, won, gstats

@@ -62,6 +62,55 @@ def random_ids(n: int, seed: int) -> np.ndarray:
     return np.argsort(stream(seed, TAG_ID, n), kind="stable").astype(np.int32)
 
 
+def feistel_ids(index: np.ndarray, total: int, seed: int, rounds: int = 4) -> np.ndarray:
+    """Seeded pseudo-random bijection of [0, total) evaluated at `index` (int64 array):
+    a balanced Feistel network on the next even power of two, with cycle walking.  Lets every
+    shard draw globally unique random IDs without materialising a global permutation."""
+    bits = max(2, int(total - 1).bit_length())
+    bits += bits & 1
+    half = bits // 2
+    mask = np.uint64((1 << half) - 1)
+    keys = [_mix(np.array([(seed * 0x2545F4914F6CDD1D + 977 * (k + 1)) & 0xFFFFFFFFFFFFFFFF],
+                          dtype=np.uint64))[0] for k in range(rounds)]
+
+    def perm(v):
+        lo = v & mask
+        hi = (v >> np.uint64(half)) & mask
+        with np.errstate(over="ignore"):
+            for k in keys:
+                f = _mix(lo ^ k) & mask
+                lo, hi = hi ^ f, lo
+        return (hi << np.uint64(half)) | lo
+
+    v = np.asarray(index, dtype=np.uint64).copy()
+    out = perm(v)
+    bad = out >= np.uint64(total)
+    while bad.any():  # cycle walking: stays inside [0, total), still a bijection
+        out[bad] = perm(out[bad])
+        bad = out >= np.uint64(total)
+    return out.astype(np.int64)
+
+
+def shard_inputs(n_per: int, seed: int, world: int, rank: int, deg: float = 16.0, t: int = 0):
+    """Rank `rank`'s part of a world-wide synthetic swarm of n_per*world agents: uniform
+    positions inside the rank's horizontal strip of the global square, IDs from a global
+    seeded bijection (unique across ranks), tasks inside the strip."""
+    total = n_per * world
+    side = side_length(total, deg)
+    h = side / world
+    sseed = seed * 1000003 + rank
+    x = uniform(sseed, TAG_X, n_per) * side
+    y = rank * h + uniform(sseed, TAG_Y, n_per) * h
+    gidx = np.arange(n_per, dtype=np.int64) + np.int64(rank) * n_per
+    ids = feistel_ids(gidx, total, seed).astype(np.int32)
+    out = dict(n=n_per, total=total, seed=seed, deg=deg, side=side, strip=(rank * h, (rank + 1) * h),
+               x=x, y=y, ids=ids, caps=capabilities(n_per, sseed))
+    if t:
+        tx, ty, treq = tasks(t, sseed, side)
+        out["tx"], out["ty"], out["treq"] = tx, rank * h + ty / side * h, treq
+    return out
+
+
 def capabilities(n: int, seed: int, ncaps: int = 4, p: float = 0.5) -> np.ndarray:
     """uint32 bitmask, each of ``ncaps`` bits set independently with probability p."""
     out = np.zeros(n, dtype=np.uint32)

@@ -145,11 +145,11 @@ class Swarm:
         return self
 
     # ------------------------------------------------------------------ election
-    def elect(self, mode: str = "frontier", max_rounds: int = 1 << 20) -> ElectResult:
-        """Contract E2 to convergence on the GPU (swarm_elect)."""
+    def elect(self, mode: str = "frontier", max_rounds: int = 1 << 16, timed: bool = False) -> ElectResult:
+        """Contract E2 to convergence on the GPU (swarm_elect).  timed: per-kernel HIP events."""
         if self.row_ptr is None:
             raise RuntimeError("no neighbour graph: call build_graph() or set_graph()")
-        m = {"dense": _lib.ELECT_DENSE, "frontier": _lib.ELECT_FRONTIER}[mode]
+        m = {"dense": _lib.ELECT_DENSE, "frontier": _lib.ELECT_FRONTIER}[mode] | (_lib.ELECT_TIMED if timed else 0)
         n = self.n
         rounds = ctypes.c_int32(0)
         cap = int(max_rounds)
@@ -162,8 +162,11 @@ class Swarm:
                 _lib.ptr(self.state, torch.uint8), cap, m, ctypes.byref(rounds),
                 changes.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st), _lib.stream()))
         r = rounds.value
-        return ElectResult(r, changes[:r].copy(), self.leader, self.state, rc == _lib.OK,
-                           st.rounds_launched, st.active_total, st.edges_total)
+        res = ElectResult(r, changes[:r].copy(), self.leader, self.state, rc == _lib.OK,
+                          st.rounds_launched, st.active_total, st.edges_total)
+        res.changes_total = st.changes_total
+        res.gather_ms, res.apply_ms, res.timed_launches = st.gather_ms, st.apply_ms, st.gather_launches
+        return res
 
     # ------------------------------------------------------------------ allocation
     def id_index(self) -> torch.Tensor | None:

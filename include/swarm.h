@@ -47,6 +47,7 @@ extern "C" {
  * and per-round change counts. */
 #define SWARM_ELECT_DENSE 0    /* every agent gathers every round (Jacobi sweep) */
 #define SWARM_ELECT_FRONTIER 1 /* only neighbours of last round's changed agents gather */
+#define SWARM_ELECT_TIMED 0x100 /* OR into mode: time every kernel with HIP events (stats) */
 
 /* Allocation execution strategies (all exact). */
 #define SWARM_ALLOC_AUTO 0
@@ -68,6 +69,10 @@ typedef struct swarm_elect_stats {
     int64_t rounds_launched; /* rounds issued (>= rounds_exec; extra ones are no-ops) */
     int64_t active_total;    /* agents that gathered, summed over rounds */
     int64_t edges_total;     /* neighbour reads, summed over rounds */
+    int64_t changes_total;   /* leader changes, summed over rounds */
+    double gather_ms;        /* SWARM_ELECT_TIMED: summed device time of the gather kernel */
+    double apply_ms;         /* SWARM_ELECT_TIMED: summed device time of the apply kernel */
+    int64_t gather_launches; /* launches behind gather_ms / apply_ms (rounds 1..rounds_exec) */
 } swarm_elect_stats;
 
 const char *swarm_last_error(void);
@@ -108,6 +113,30 @@ int swarm_elect_i64(swarm_ctx *ctx, int64_t n, const int64_t *row_ptr, const int
 int swarm_elect_round(swarm_ctx *ctx, int64_t n_rows, const int32_t *row_ptr,
                       const int32_t *col, const int32_t *leader_in, int32_t *leader_out,
                       int64_t *changed, void *stream);
+
+/*
+ * Frontier stepper for sharded (multi-GPU) elections: the same exact rounds as
+ * swarm_elect(FRONTIER) but driven one round at a time, so a caller can exchange halo values
+ * between rounds (swarm_amd/dist.py does it over RCCL).  Local storage = n_rows owned agents
+ * followed by ghosts (copies of other shards' boundary agents), n_all in total; the CSR has
+ * n_all rows (ghost rows list their local neighbours) and col indexes [0, n_all).
+ *   begin:   leader[0:n_all] = init; every agent active for round 1.
+ *   step:    round t over the owned rows (no convergence guard: a shard with no local change
+ *            can still receive ghost changes).  Owned changes are counted per round.
+ *   ghosts:  after the halo exchange of round t, incoming[i] is the round-t leader of ghost
+ *            begin+i; rises are written and their neighbours activated for round t+1.
+ *   changes: per-round owned change counts of rounds t0..t1 (t1 - t0 < 256); host sync.
+ *            Read at least every 256 rounds (counter slots are recycled).
+ * One stepper per ctx; swarm_elect() on the same ctx resets it.
+ */
+int swarm_frontier_begin(swarm_ctx *ctx, int64_t n_rows, int64_t n_all, const int32_t *init,
+                         int32_t *leader, void *stream);
+int swarm_frontier_step(swarm_ctx *ctx, int32_t t, const int32_t *row_ptr, const int32_t *col,
+                        int32_t *leader, void *stream);
+int swarm_frontier_ghosts(swarm_ctx *ctx, int32_t t, int64_t begin, int64_t count,
+                          const int32_t *incoming, const int32_t *row_ptr, const int32_t *col,
+                          int32_t *leader, void *stream);
+int swarm_frontier_changes(swarm_ctx *ctx, int32_t t0, int32_t t1, int64_t *out, void *stream);
 
 /*
  * Task allocation round (contract A-H).

@@ -1,0 +1,100 @@
+"""Sharded (multi-rank) swarm step on CPU: world_size 2 and 3 over gloo, numpy stepper double.
+
+Checks that strip partitioning + ghost halos + per-round halo exchange + batched global change
+counts reproduce, exactly, the single-graph election of the union swarm (leaders per agent ID,
+rounds_exec, per-round change counts), and that the halo-based sharded allocation reproduces
+the single-resolver allocation (winners, claim values, won per agent)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import PKG, ROOT
+
+N_PER, SEED, T_PER = 1500, 5, 60
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_q, n_per, deg, check_every):
+    import sys
+    for p in (PKG, ROOT, os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from shard_doubles import NumpyBackend
+        from swarm_amd import gen
+        from swarm_amd.dist import ShardedSwarm
+        d = gen.shard_inputs(n_per, SEED, world, rank, deg=deg, t=T_PER)
+        sh = ShardedSwarm(d["ids"], d["x"], d["y"], d["caps"], d["strip"], device="cpu", backend=NumpyBackend())
+        r = sh.elect(check_every=check_every)
+        res, won, gst = sh.allocate(d["tx"], d["ty"], d["treq"])
+        out_q.put(dict(rank=rank, rounds=r.rounds_exec, changes=r.changes, ids=sh.ids.numpy(),
+                       leader=r.leader.numpy(), state=r.state.numpy(), winner=res.winner.numpy(),
+                       util=res.util.numpy(), won=won.numpy(), gstats=gst,
+                       n_ghost=(sh.n_glo, sh.n_ghi)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world, n_per=N_PER, deg=16.0, check_every=7):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, n_per, deg, check_every)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return sorted(outs, key=lambda o: o["rank"])
+
+
+def _union(world, n_per=N_PER, deg=16.0):
+    from swarm_amd import gen
+    ds = [gen.shard_inputs(n_per, SEED, world, r, deg=deg, t=T_PER) for r in range(world)]
+    cat = lambda k: np.concatenate([d[k] for d in ds])  # noqa: E731
+    return ds, cat
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_election_and_allocation_match_single_graph(world, oracle_mod):
+    outs = _run(world)
+    ds, cat = _union(world)
+    x, y, ids, caps = cat("x"), cat("y"), cat("ids"), cat("caps")
+    rp, col = oracle_mod.rgg_csr(x, y, 1.0)
+    lead, state, rounds, changes = oracle_mod.elect(rp, col, ids)
+    want = dict(zip(ids.tolist(), lead.tolist()))
+    for o in outs:
+        assert o["rounds"] == rounds
+        np.testing.assert_array_equal(o["changes"], changes)
+        got = dict(zip(o["ids"].tolist(), o["leader"].tolist()))
+        assert all(got[k] == want[k] for k in got)
+        assert ((o["state"] == 3) == (o["leader"] == o["ids"])).all()
+        assert sum(o["n_ghost"]) > 0
+    assert sum(len(o["ids"]) for o in outs) == len(ids)
+    # allocation: every rank resolves its own tasks; the union resolver must agree
+    wa = oracle_mod.allocate(ids, x, y, caps, cat("tx"), cat("ty"), cat("treq"))
+    np.testing.assert_array_equal(np.concatenate([o["winner"] for o in outs]), wa["winner"])
+    np.testing.assert_array_equal(np.concatenate([o["util"] for o in outs]), wa["util"])
+    won_want = dict(zip(ids.tolist(), wa["won"].tolist()))
+    for o in outs:
+        assert all(won_want[int(i)] == int(w) for i, w in zip(o["ids"], o["won"]))
+        assert o["gstats"]["n_claims"] == wa["n_claims"]
+        assert o["gstats"]["n_conflicts"] == wa["n_conflicts"]
+
+
+def test_shard_ids_are_a_global_permutation():
+    from swarm_amd import gen
+    ids = np.concatenate([gen.shard_inputs(777, 3, 5, r)["ids"] for r in range(5)])
+    assert (np.sort(ids) == np.arange(777 * 5)).all()

@@ -284,3 +284,64 @@ def test_dropin_bridge_round_trip(sw, oracle_mod):
     for a in agents:
         assert a.state in (agent.AgentState.LEADER, agent.AgentState.FOLLOWER)
         assert (a.state == agent.AgentState.LEADER) == (a.leader_id == a.agent_id)
+
+
+def test_sharded_stepper_two_shards_on_one_gpu(sw, oracle_mod):
+    """The frontier stepper + ghost kernels through ShardedSwarm: two shards driven by two
+    threads on cuda:0 with an in-process halo; union-graph oracle as the reference."""
+    import threading
+    from shard_doubles import ThreadHalo
+    from swarm_amd import gen
+    from swarm_amd.dist import ShardedSwarm
+    world, n_per = 2, 40000
+    hub = ThreadHalo(world)
+    outs, errs = {}, []
+
+    def run(rank):
+        try:
+            torch.cuda.set_device(0)
+            d = gen.shard_inputs(n_per, 9, world, rank, t=400)
+            sh = ShardedSwarm(d["ids"], d["x"], d["y"], d["caps"], d["strip"], device="cuda:0",
+                              halo=hub.member(rank))
+            r = sh.elect(check_every=32)
+            res, won, gst = sh.allocate(d["tx"], d["ty"], d["treq"])
+            torch.cuda.synchronize()
+            outs[rank] = dict(r=r, ids=sh.ids.cpu().numpy(), leader=r.leader.cpu().numpy(),
+                              winner=res.winner.cpu().numpy(), won=won.cpu().numpy(), gst=gst)
+        except Exception as e:  # surfaced below
+            errs.append(e)
+            hub.barrier.abort()
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errs, errs
+    ds = [gen.shard_inputs(n_per, 9, world, k, t=400) for k in range(world)]
+    cat = lambda k: np.concatenate([d[k] for d in ds])  # noqa: E731
+    x, y, ids = cat("x"), cat("y"), cat("ids")
+    rp, col = oracle_mod.rgg_csr(x, y, 1.0)
+    lead, _, rounds, changes = oracle_mod.elect(rp, col, ids)
+    want = dict(zip(ids.tolist(), lead.tolist()))
+    for k in range(world):
+        o = outs[k]
+        assert o["r"].rounds_exec == rounds
+        np.testing.assert_array_equal(o["r"].changes, changes)
+        assert all(want[int(i)] == int(v) for i, v in zip(o["ids"], o["leader"]))
+    wa = oracle_mod.allocate(ids, x, y, cat("caps"), cat("tx"), cat("ty"), cat("treq"))
+    np.testing.assert_array_equal(np.concatenate([outs[k]["winner"] for k in range(world)]), wa["winner"])
+    won_want = dict(zip(ids.tolist(), wa["won"].tolist()))
+    for k in range(world):
+        assert all(won_want[int(i)] == int(w) for i, w in zip(outs[k]["ids"], outs[k]["won"]))
+
+
+def test_elect_timed_stats(sw, oracle_mod):
+    g = load_golden("elect_n10000")
+    s = _swarm(sw, g, "spatial").set_graph(g["row_ptr"], g["col"])
+    r = s.elect(mode="frontier", timed=True)
+    assert r.rounds_exec == int(g["rounds_exec"])
+    assert r.changes_total == int(g["changes"].sum())
+    assert r.timed_launches == r.rounds_exec and r.gather_ms > 0 and r.apply_ms > 0
+    r2 = s.elect(mode="dense", timed=True)
+    assert r2.rounds_exec == int(g["rounds_exec"]) and r2.gather_ms > 0
