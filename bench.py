@@ -120,11 +120,11 @@ def main():
     rt = sw.elect(mode=args.elect_mode, max_rounds=1 << 16, timed=True)
     launches = max(rt.timed_launches, 1)
     if args.elect_mode == "frontier":
-        # k_elect_pull algorithmic bytes: 1 stamp byte per agent per launch; per active agent
-        # its two row offsets + own leader (12 B); per gathered edge col + neighbour leader (8 B);
-        # per change one (agent, leader) list entry (8 B)
-        pull_bytes = launches * n + 12 * rt.active_total + 8 * rt.edges_total + 8 * rt.changes_total
-        dom = {"kernel": "k_elect_pull (frontier gather, one E2 round)", "bytes_per_launch": pull_bytes / launches,
+        # k_frontier_round algorithmic bytes (lower bound): 1 stamp byte per agent per launch; per
+        # active agent its two row offsets + own leader + new leader (16 B); per gathered edge
+        # col + neighbour leader (8 B); per change its self-stamp (1 B; neighbour stamps uncounted)
+        pull_bytes = launches * n + 16 * rt.active_total + 8 * rt.edges_total + rt.changes_total
+        dom = {"kernel": "k_frontier_round (fused frontier E2 round)", "bytes_per_launch": pull_bytes / launches,
                "avg_launch_ms": rt.gather_ms / launches, "launches": launches,
                "apply_avg_launch_ms": rt.apply_ms / launches,
                "share_of_elect": rt.gather_ms / max(rt.gather_ms + rt.apply_ms, 1e-9)}

@@ -91,21 +91,21 @@ __device__ __forceinline__ unsigned bytes_eq4(unsigned w, unsigned b4) {
 constexpr int kWin = 1024;  // edges per LDS window per wave (4 KiB)
 constexpr int kK = 16;      // gathers in flight per lane
 
-template <typename Off>
+template <typename Off, int K = kK>
 __device__ __forceinline__ int row_max_from_lds(const int *s_col, Off w0, Off lo, Off hi,
                                                 const int32_t *__restrict__ lin, int m) {
-    for (Off k = lo; k < hi; k += kK) {
-        int c[kK];
+    for (Off k = lo; k < hi; k += K) {
+        int c[K];
 #pragma unroll
-        for (int j = 0; j < kK; ++j) {
+        for (int j = 0; j < K; ++j) {
             const Off kk = (k + j < hi) ? k + j : hi - 1;
             c[j] = s_col[kk - w0];
         }
-        int val[kK];
+        int val[K];
 #pragma unroll
-        for (int j = 0; j < kK; ++j) val[j] = lin[c[j]];
+        for (int j = 0; j < K; ++j) val[j] = lin[c[j]];
 #pragma unroll
-        for (int j = 0; j < kK; ++j) m = max(m, val[j]);  // duplicates of the last edge are harmless
+        for (int j = 0; j < K; ++j) m = max(m, val[j]);  // duplicates of the last edge are harmless
     }
     return m;
 }
@@ -171,48 +171,69 @@ __global__ __launch_bounds__(kBlock) void k_elect_dense(
     }
 }
 
-// ------------------------------------------------------------- frontier: gather phase
-// Work unit = a chunk of kChunk agents (8 stamps per thread, one 8-B load).  Active agents
-// are compacted into LDS; then 2 lanes per agent each issue kK unconditional row loads and
-// kK leader gathers.  Changes of a chunk go to list segment (chunk % 64), reserved by ONE
-// atomic on that segment's counter shard.  tot[t-1] (one word, written by the previous apply)
-// is the convergence guard.
+// ------------------------------------------------------------- frontier: fused round
+// One kernel per round.  Buffers alternate by round parity:
+//   leaders  Lr = L[(t-1)&1] (state after round t-1, read), Lw = L[t&1] (written)
+//   stamps   act[t&1] (agents active in round t carry t&255), act[(t+1)&1] (written)
+// Invariant: before round t, Lw holds the state after round t-2.  An agent that changes in a
+// round stamps its neighbours AND itself for the next round, so every agent that changed in
+// round t-1 is active in round t; every active agent writes its round-t value to Lw.  Agents
+// that changed in neither round t-1 nor t already hold the right value in Lw.  Hence Lw is the
+// state after round t, with no fold, no change list and no global atomic on the critical path.
+// A chunk's workgroup finds its active agents (8 stamp bytes per lane) and gathers them from
+// Lr: per-agent rows (2 lanes x kK loads) for a sparse chunk, coalesced LDS windows over all
+// of the chunk's agents for a dense one.  Counters are fire-and-forget shard adds.
+constexpr int kDenseChunk = kChunk / 2;  // active agents above which a chunk gathers densely
+constexpr int kG = 4;                    // sparse chunk: lanes per active agent
+constexpr int kKs = 8;                   // sparse chunk: loads in flight per lane
+constexpr int kKd = 8;                   // dense chunk: gathers in flight per lane
+
 template <typename Off>
-__global__ __launch_bounds__(kBlock) void k_elect_pull(
-    const Off *__restrict__ rp, const int32_t *__restrict__ col, const int32_t *__restrict__ leader,
-    const uint8_t *__restrict__ act, int64_t n, int2 *__restrict__ list, int64_t seg_cap,
-    unsigned long long *__restrict__ ring, const unsigned long long *__restrict__ tot, int t,
-    int with_stats, int guard) {
-    __shared__ int s_list[kChunk];
-    __shared__ int2 s_chg[kChunk];
+__global__ __launch_bounds__(kBlock) void k_frontier_round(
+    const Off *__restrict__ rp, const int32_t *__restrict__ col, const int32_t *__restrict__ Lr,
+    int32_t *__restrict__ Lw, const uint8_t *__restrict__ act_r, uint8_t *__restrict__ act_w,
+    int64_t n, unsigned long long *__restrict__ ring, unsigned long long *__restrict__ tot, int t,
+    int with_stats, int guard, int dense_at) {
+    __shared__ union {
+        int list[kChunk];
+        int col[kWavesPerBlock][kWin];
+    } u;
     __shared__ int s_wave[kWavesPerBlock];
-    __shared__ int s_nchg;
-    __shared__ unsigned long long s_base;
-    __shared__ long long s_act[kWavesPerBlock], s_edg[kWavesPerBlock];
-    if (guard && t > 1 && tot[(t - 1) % kRing] == 0) return;
+    __shared__ long long s_red[3][kWavesPerBlock];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (blockIdx.x == 0) {  // bookkeeping: total of round t-1 (guard word), recycle slots
+        if (t > 1 && threadIdx.x < kWave) {
+            unsigned long long v = *slot(ring, t - 1, 0, threadIdx.x);
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+            if (threadIdx.x == 0) tot[(t - 1) % kRing] = v;
+        }
+        for (int i = threadIdx.x; i < kCounters * kShards; i += kBlock)
+            *slot(ring, t + kRing / 2, i / kShards, i % kShards) = 0;
+    }
+    // single-GPU runs: round t-2 changed nothing => round t-1 had no active agent => neither t
+    if (guard && t > 2 && tot[(t - 2) % kRing] == 0) return;
     const unsigned stamp = unsigned(t & 0xFF);
     const unsigned stamp4 = stamp * 0x01010101u;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    long long my_active = 0, my_edges = 0;
+    const uint8_t next = uint8_t((t + 1) & 0xFF);
+    long long my_active = 0, my_edges = 0, my_chg = 0;
     const int64_t nchunks = (n + kChunk - 1) / kChunk;
     for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
         const int64_t c0 = chunk * kChunk;
-        // 1. my 16 stamps
+        // 1. my 8 stamps -> the chunk's active agents
         const int64_t v0 = c0 + int64_t(threadIdx.x) * kScan;
         unsigned mask = 0;
         if (v0 + kScan <= n) {
-            const uint2 w = *reinterpret_cast<const uint2 *>(act + v0);
+            const uint2 w = *reinterpret_cast<const uint2 *>(act_r + v0);
             mask = bytes_eq4(w.x, stamp4) | (bytes_eq4(w.y, stamp4) << 4);
         } else {
             for (int j = 0; j < kScan && v0 + j < n; ++j)
-                if (act[v0 + j] == stamp) mask |= 1u << j;
+                if (act_r[v0 + j] == stamp) mask |= 1u << j;
         }
-        // 2. compact this chunk's active agents into LDS
         const int cnt = __popc(mask);
         int wtot;
         const int wexcl = wave_excl_scan(cnt, &wtot);
         if (lane == 0) s_wave[wid] = wtot;
-        if (threadIdx.x == 0) s_nchg = 0;
         __syncthreads();
         int off = 0, total = 0;
 #pragma unroll
@@ -220,125 +241,123 @@ __global__ __launch_bounds__(kBlock) void k_elect_pull(
             off += (w < wid) ? s_wave[w] : 0;
             total += s_wave[w];
         }
-        if (total == 0) {  // block-uniform: nothing active in this chunk
-            __syncthreads();
-            continue;
-        }
-        int pos = off + wexcl;
-        while (mask) {
-            const int j = __ffs(mask) - 1;
-            mask &= mask - 1;
-            s_list[pos++] = threadIdx.x * kScan + j;
-        }
-        __syncthreads();
-        // 3. two lanes per active agent
-        const int half = lane & 1;
-        for (int base = wid * 32; base < total; base += kBlock / 2) {
-            const int i = base + (lane >> 1);
-            const bool valid = i < total;
-            const int64_t v = c0 + s_list[valid ? i : total - 1];
-            const Off b = rp[v], e = rp[v + 1];
-            int m = INT_MIN;
-            for (Off k = b + half * kK; k < e; k += 2 * kK) {
-                int c[kK];
+        if (total > dense_at) {
+            // 2a. dense chunk: every agent of the chunk, 64 per wave task, coalesced windows
+            const int64_t cend = (c0 + kChunk < n) ? c0 + kChunk : n;
+            int *sc = u.col[wid];
+            for (int64_t tb = c0 + int64_t(wid) * 64; tb < cend; tb += kBlock) {
+                const int64_t v = tb + lane;
+                const bool valid = v < cend;
+                const Off b = rp[valid ? v : cend], e = rp[(v + 1 < cend) ? v + 1 : cend];
+                const Off W0 = __shfl(b, 0, 64), W1 = __shfl(e, 63, 64);
+                const int own = Lr[valid ? v : cend - 1];
+                int m = own;
+                for (Off w0 = W0; w0 < W1; w0 += kWin) {
+                    const Off wend = (W1 - w0 < kWin) ? W1 : w0 + kWin;
 #pragma unroll
-                for (int j = 0; j < kK; ++j) c[j] = col[(k + j < e) ? k + j : e - 1];
-                int val[kK];
-#pragma unroll
-                for (int j = 0; j < kK; ++j) val[j] = leader[c[j]];
-#pragma unroll
-                for (int j = 0; j < kK; ++j) m = max(m, val[j]);
-            }
-            m = max(m, __shfl_xor(m, 1, 64));
-            const int own = leader[v];
-            if (valid && half == 0) {
-                if (with_stats) {
+                    for (int j = 0; j < kWin / 64; ++j) {
+                        const Off k = w0 + j * 64 + lane;
+                        sc[j * 64 + lane] = col[k < wend ? k : wend - 1];
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    const Off lo = b > w0 ? b : w0, hi = e < wend ? e : wend;
+                    m = row_max_from_lds<Off, kKd>(sc, w0, lo, hi, Lr, m);
+                    __builtin_amdgcn_wave_barrier();
+                }
+                const bool up = valid && m > own;
+                if (valid) Lw[v] = m;
+                if (up) {
+                    act_w[v] = next;
+                    if (W1 - W0 <= kWin) {  // the wave's whole slice is still in LDS
+                        for (Off k = b; k < e; ++k) act_w[sc[k - W0]] = next;
+                    } else {
+                        for (Off k = b; k < e; ++k) act_w[col[k]] = next;
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                my_chg += __popcll(__ballot(up));
+                if (with_stats && valid) {
                     my_active += 1;
                     my_edges += (long long)(e - b);
                 }
-                if (m > own) {
-                    const int at = atomicAdd(&s_nchg, 1);  // LDS
-                    s_chg[at] = make_int2(int(v), m);
+            }
+        } else if (total > 0) {
+            // 2b. sparse chunk: compacted active agents, kG lanes per agent, kKs loads per lane
+            int pos = off + wexcl;
+            while (mask) {
+                const int j = __ffs(mask) - 1;
+                mask &= mask - 1;
+                u.list[pos++] = threadIdx.x * kScan + j;
+            }
+            __syncthreads();
+            const int sub = lane & (kG - 1);
+            for (int base = wid * (64 / kG); base < total; base += kBlock / kG) {
+                const int i = base + lane / kG;
+                const bool valid = i < total;
+                const int64_t v = c0 + u.list[valid ? i : total - 1];
+                const Off b = rp[v], e = rp[v + 1];
+                const int own = Lr[v];
+                int m = own;
+                int c[kKs];
+                for (Off k = b + sub * kKs; k < e; k += kG * kKs) {
+#pragma unroll
+                    for (int j = 0; j < kKs; ++j) c[j] = col[(k + j < e) ? k + j : e - 1];
+                    int val[kKs];
+#pragma unroll
+                    for (int j = 0; j < kKs; ++j) val[j] = Lr[c[j]];
+#pragma unroll
+                    for (int j = 0; j < kKs; ++j) m = max(m, val[j]);
+                }
+#pragma unroll
+                for (int o2 = 1; o2 < kG; o2 <<= 1) m = max(m, __shfl_xor(m, o2, 64));
+                const bool up = valid && m > own;
+                if (valid && sub == 0) Lw[v] = m;
+                if (up) {
+                    if (sub == 0) act_w[v] = next;
+                    if (e - b <= kG * kKs) {  // one pass per lane: c[] still holds this lane's edges
+#pragma unroll
+                        for (int j = 0; j < kKs; ++j)
+                            if (b + sub * kKs + j < e) act_w[c[j]] = next;
+                    } else {
+                        for (Off k = b + sub; k < e; k += kG) act_w[col[k]] = next;
+                    }
+                }
+                my_chg += __popcll(__ballot(up && sub == 0));
+                if (with_stats && valid && sub == 0) {
+                    my_active += 1;
+                    my_edges += (long long)(e - b);
                 }
             }
         }
-        __syncthreads();
-        // 4. one global reservation per chunk, then copy the chunk's changes out
-        const int nchg = s_nchg;
-        if (nchg) {
-            const int seg = int(chunk & (kShards - 1));
-            if (threadIdx.x == 0) s_base = atomicAdd(slot(ring, t, 0, seg), (unsigned long long)nchg);
-            __syncthreads();
-            int2 *dst = list + int64_t(seg) * seg_cap + int64_t(s_base);
-            for (int k = threadIdx.x; k < nchg; k += kBlock) dst[k] = s_chg[k];
-        }
-        __syncthreads();  // LDS reused by the next chunk
+        __syncthreads();  // LDS (s_wave, u) reused by the next chunk
     }
-    if (with_stats) {
+    // per-workgroup totals -> one shard add per counter
+    if (lane == 0) s_red[0][wid] = my_chg;  // my_chg is wave-uniform (ballot counts)
 #pragma unroll
-        for (int o2 = 32; o2 > 0; o2 >>= 1) {
-            my_active += __shfl_xor(my_active, o2, 64);
-            my_edges += __shfl_xor(my_edges, o2, 64);
-        }
-        if (lane == 0) { s_act[wid] = my_active; s_edg[wid] = my_edges; }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            long long a = 0, ed = 0;
-            for (int w = 0; w < kWavesPerBlock; ++w) { a += s_act[w]; ed += s_edg[w]; }
-            if (a) {
-                atomicAdd(slot(ring, t, 1, blockIdx.x & (kShards - 1)), (unsigned long long)a);
-                atomicAdd(slot(ring, t, 2, blockIdx.x & (kShards - 1)), (unsigned long long)ed);
-            }
-        }
+    for (int o2 = 32; o2 > 0; o2 >>= 1) {
+        my_active += __shfl_xor(my_active, o2, 64);
+        my_edges += __shfl_xor(my_edges, o2, 64);
+    }
+    if (lane == 0) { s_red[1][wid] = my_active; s_red[2][wid] = my_edges; }
+    __syncthreads();
+    if (threadIdx.x < kCounters) {
+        long long a = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) a += s_red[threadIdx.x][w];
+        if (a) atomicAdd(slot(ring, t, threadIdx.x, blockIdx.x & (kShards - 1)), (unsigned long long)a);
     }
 }
 
-// ------------------------------------------------------------- frontier: apply phase
-// grid.y = list segment; G lanes per change stamp the changed agent's neighbours.
-template <int G, typename Off>
-__global__ __launch_bounds__(kBlock) void k_elect_apply(
-    const Off *__restrict__ rp, const int32_t *__restrict__ col, int32_t *__restrict__ leader,
-    uint8_t *__restrict__ act, const int2 *__restrict__ list, int64_t seg_cap,
-    unsigned long long *__restrict__ ring, unsigned long long *__restrict__ tot, int t) {
-    const int seg = blockIdx.y;
-    if (blockIdx.x == 0 && blockIdx.y == 0) {
-        if (threadIdx.x < kWave) {  // round total -> guard word
-            unsigned long long v = *slot(ring, t, 0, threadIdx.x);
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-            if (threadIdx.x == 0) tot[t % kRing] = v;
-        }
-        // recycle the counter slots of round t + kRing/2 (read back long before: the host
-        // reads every <= kRing/2 rounds)
-        for (int i = threadIdx.x; i < kCounters * kShards; i += kBlock)
-            *slot(ring, t + kRing / 2, i / kShards, i % kShards) = 0;
-    }
-    const int64_t cnt = int64_t(*slot(ring, t, 0, seg));
-    if (cnt == 0) return;
-    const int2 *src = list + int64_t(seg) * seg_cap;
-    const uint8_t next = uint8_t((t + 1) & 0xFF);
-    constexpr int GPB = kBlock / G;
-    const int sub = threadIdx.x & (G - 1);
-    for (int64_t base = int64_t(blockIdx.x) * GPB; base < cnt; base += int64_t(gridDim.x) * GPB) {
-        const int64_t i = base + threadIdx.x / G;
-        if (i < cnt) {
-            const int2 e = src[i];
-            if (sub == 0) leader[e.x] = e.y;
-            const Off e1 = rp[e.x + 1];
-            for (Off k = rp[e.x] + sub; k < e1; k += G) act[col[k]] = next;
-        }
-    }
-}
-
-// Sharded runs: halo values received for ghost agents [begin, begin + count).  A ghost whose
-// leader rose is written and its local neighbours are stamped for round t + 1 (ghost rows of
-// the local CSR list them).  Ghost changes are their owner's changes: not counted here.
+// Sharded runs: halo values received for ghost agents [begin, begin + count) after round t.
+// A ghost whose leader rose is written to BOTH leader buffers (ghosts are never gathered, so
+// either buffer may serve round t+1 and t+2) and its local neighbours are stamped for round
+// t+1 (ghost rows of the local CSR list them).  Ghost changes are counted by their owner.
 template <int G, typename Off>
 __global__ __launch_bounds__(kBlock) void k_frontier_ghosts(
-    const Off *__restrict__ rp, const int32_t *__restrict__ col, int32_t *__restrict__ leader,
-    uint8_t *__restrict__ act, int64_t begin, int64_t count, const int32_t *__restrict__ incoming,
-    int t) {
+    const Off *__restrict__ rp, const int32_t *__restrict__ col, int32_t *__restrict__ L0,
+    int32_t *__restrict__ L1, uint8_t *__restrict__ act_w, int64_t begin, int64_t count,
+    const int32_t *__restrict__ incoming, int t) {
     const uint8_t next = uint8_t((t + 1) & 0xFF);
+    int32_t *Lcur = (t & 1) ? L1 : L0;
     constexpr int GPB = kBlock / G;
     const int sub = threadIdx.x & (G - 1);
     for (int64_t base = int64_t(blockIdx.x) * GPB; base < count; base += int64_t(gridDim.x) * GPB) {
@@ -346,11 +365,13 @@ __global__ __launch_bounds__(kBlock) void k_frontier_ghosts(
         if (i < count) {
             const int64_t g = begin + i;
             const int nv = incoming[i];
-            if (nv > leader[g]) {
-                __builtin_amdgcn_wave_barrier();
-                if (sub == 0) leader[g] = nv;
+            if (nv > Lcur[g]) {
+                if (sub == 0) {
+                    L0[g] = nv;
+                    L1[g] = nv;
+                }
                 const Off e1 = rp[g + 1];
-                for (Off k = rp[g] + sub; k < e1; k += G) act[col[k]] = next;
+                for (Off k = rp[g] + sub; k < e1; k += G) act_w[col[k]] = next;
             }
         }
     }
@@ -390,12 +411,11 @@ int env_int(const char *name, int dflt) {
 }
 
 struct Tuning {
-    int G = 8;          // lanes per change (apply)
-    int dense_blocks = 2048;
+    int dense_blocks = 2048;     // grid cap of the dense round kernel
+    int dense_at = kDenseChunk;  // frontier: active agents per chunk above which it gathers densely
     Tuning() {
-        G = env_int("SWARM_APPLY_G", 8);
-        if (G != 4 && G != 16) G = 8;
         dense_blocks = env_int("SWARM_DENSE_BLOCKS", 2048);
+        dense_at = env_int("SWARM_DENSE_CHUNK", kDenseChunk);
     }
 };
 
@@ -414,22 +434,41 @@ int launch_dense_round(const Off *rp, const int32_t *col, const int32_t *lin, in
     return SWARM_OK;
 }
 
+// Frontier state: two leader buffers and two stamp arrays (round parity), counter ring.
+struct Frontier {
+    int32_t *L[2];
+    uint8_t *act[2];
+    unsigned long long *ring, *tot;
+    int64_t n_rows;
+};
+
+int frontier_alloc(swarm_ctx *ctx, int64_t n_rows, int64_t n_all, int32_t *L0, int32_t *L1, Frontier *f,
+                   hipStream_t s) {
+    const size_t na = size_t(n_all) + 16;
+    uint8_t *act;
+    SW_ALLOC(act, ctx, S_ACT, 2 * na);
+    const size_t ring_words = size_t(kRing) * kCounters * kRoundWords;
+    SW_ALLOC(f->ring, ctx, S_CHANGES, (ring_words + kRing) * 8);
+    f->tot = f->ring + ring_words;
+    f->L[0] = L0;
+    f->L[1] = L1;
+    f->act[0] = act;
+    f->act[1] = act + na;
+    f->n_rows = n_rows;
+    SW_HIP(hipMemsetAsync(f->ring, 0, (ring_words + kRing) * 8, s));
+    SW_HIP(hipMemsetAsync(act, 0, 2 * na, s));
+    if (n_all) SW_HIP(hipMemsetAsync(f->act[1], 1, size_t(n_all), s));  // round 1 reads act[1]: all active
+    return SWARM_OK;
+}
+
 template <typename Off>
-int launch_frontier_round(const Off *rp, const int32_t *col, int32_t *leader, uint8_t *act,
-                          int2 *list, int64_t seg_cap, int64_t n, unsigned long long *ring,
-                          unsigned long long *tot, int t, int with_stats, hipStream_t s,
-                          hipEvent_t mid = nullptr, int guard = 1) {
-    const unsigned gpull = grid_for(n, kChunk, 1u << 20);
-    hipLaunchKernelGGL((k_elect_pull<Off>), dim3(gpull), dim3(kBlock), 0, s, rp, col, leader, act, n,
-                       list, seg_cap, ring, tot, t, with_stats, guard);
-    SW_LAUNCHED();
-    if (mid) SW_HIP(hipEventRecord(mid, s));
-    const dim3 gapply(grid_for(seg_cap, kBlock / tuning().G, 64), kShards);
-    switch (tuning().G) {
-        case 4: hipLaunchKernelGGL((k_elect_apply<4, Off>), gapply, dim3(kBlock), 0, s, rp, col, leader, act, list, seg_cap, ring, tot, t); break;
-        case 16: hipLaunchKernelGGL((k_elect_apply<16, Off>), gapply, dim3(kBlock), 0, s, rp, col, leader, act, list, seg_cap, ring, tot, t); break;
-        default: hipLaunchKernelGGL((k_elect_apply<8, Off>), gapply, dim3(kBlock), 0, s, rp, col, leader, act, list, seg_cap, ring, tot, t); break;
-    }
+int launch_frontier_round(const Off *rp, const int32_t *col, const Frontier &f, int t, int with_stats,
+                          int guard, hipStream_t s) {
+    const int64_t nchunks = (f.n_rows + kChunk - 1) / kChunk;
+    const unsigned grid = grid_for(nchunks > 0 ? nchunks : 1, 1, 1u << 20);
+    const int r = t & 1, p = r ^ 1;
+    hipLaunchKernelGGL((k_frontier_round<Off>), dim3(grid), dim3(kBlock), 0, s, rp, col, f.L[p], f.L[r],
+                       f.act[r], f.act[p], f.n_rows, f.ring, f.tot, t, with_stats, guard, tuning().dense_at);
     SW_LAUNCHED();
     return SWARM_OK;
 }
@@ -456,22 +495,19 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         if (st) st->rounds_launched = 1;
         return SWARM_OK;
     }
-    const size_t ring_words = size_t(kRing) * kCounters * kRoundWords;
-    unsigned long long *ring;
-    SW_ALLOC(ring, ctx, S_CHANGES, (ring_words + kRing) * 8);
-    unsigned long long *tot = ring + ring_words;  // per-round totals (frontier guard words)
-    SW_HIP(hipMemcpyAsync(leader, ids, size_t(n) * 4, hipMemcpyDeviceToDevice, s));
     int32_t *bufs[2] = {leader, nullptr};
-    uint8_t *act = nullptr;
-    int2 *list = nullptr;
-    const int64_t nchunks = (n + kChunk - 1) / kChunk;
-    const int64_t seg_cap = ((nchunks + kShards - 1) / kShards) * kChunk;
-    if (mode == SWARM_ELECT_DENSE) {
-        SW_ALLOC(bufs[1], ctx, S_LEADER_B, size_t(n) * 4);
+    SW_ALLOC(bufs[1], ctx, S_LEADER_B, size_t(n) * 4);
+    SW_HIP(hipMemcpyAsync(leader, ids, size_t(n) * 4, hipMemcpyDeviceToDevice, s));
+    Frontier f{};
+    unsigned long long *ring;
+    const size_t ring_words = size_t(kRing) * kCounters * kRoundWords;
+    if (mode == SWARM_ELECT_FRONTIER) {
+        SW_HIP(hipMemcpyAsync(bufs[1], ids, size_t(n) * 4, hipMemcpyDeviceToDevice, s));
+        int rc0 = frontier_alloc(ctx, n, n, bufs[0], bufs[1], &f, s);
+        if (rc0) return rc0;
+        ring = f.ring;
     } else {
-        SW_ALLOC(act, ctx, S_ACT, size_t(n) + 16);
-        SW_ALLOC(list, ctx, S_LIST, size_t(seg_cap) * kShards * 8);
-        SW_HIP(hipMemsetAsync(act, 1, size_t(n), s));  // round 1: everybody gathers
+        SW_ALLOC(ring, ctx, S_CHANGES, (ring_words + kRing) * 8);
     }
     const int with_stats = (st != nullptr && mode == SWARM_ELECT_FRONTIER) ? 1 : 0;
     constexpr int kMaxBatch = 256;
@@ -495,9 +531,9 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         std::vector<hipEvent_t> &v;
         ~EvFree() { for (auto x : v) (void)hipEventDestroy(x); }
     } ev_free{ev};
-    // every counter slot starts at zero; afterwards each round's kernels recycle the slots of
-    // the round kRing/2 ahead (dense: the batch-totals kernel does it)
-    SW_HIP(hipMemsetAsync(ring, 0, (ring_words + kRing) * 8, s));
+    // every counter slot starts at zero; afterwards each round's kernel recycles the slots of
+    // the round kRing/2 ahead
+    if (mode == SWARM_ELECT_DENSE) SW_HIP(hipMemsetAsync(ring, 0, (ring_words + kRing) * 8, s));
     (void)per_round;
     // slot of round 0 (read by round 1's guard only when t > 1: never) stays untouched
     while (t <= max_rounds && found < 0) {
@@ -508,8 +544,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
             if (e3) SW_HIP(hipEventRecord(e3[0], s));
             rc = (mode == SWARM_ELECT_DENSE)
                      ? launch_dense_round<Off>(rp, col, bufs[(r - 1) & 1], bufs[r & 1], n, ring, r, 1, s)
-                     : launch_frontier_round<Off>(rp, col, leader, act, list, seg_cap, n, ring, tot,
-                                                  r, with_stats, s, e3 ? e3[1] : nullptr);
+                     : launch_frontier_round<Off>(rp, col, f, r, with_stats, /*guard=*/1, s);
             if (rc) return rc;
             if (e3) SW_HIP(hipEventRecord(e3[2], s));
         }
@@ -529,12 +564,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
             if (timed) {
                 float x = 0, y = 0;
                 hipEvent_t *e3 = &ev[3 * (r - t)];
-                if (mode == SWARM_ELECT_DENSE) {
-                    SW_HIP(hipEventElapsedTime(&x, e3[0], e3[2]));
-                } else {
-                    SW_HIP(hipEventElapsedTime(&x, e3[0], e3[1]));
-                    SW_HIP(hipEventElapsedTime(&y, e3[1], e3[2]));
-                }
+                SW_HIP(hipEventElapsedTime(&x, e3[0], e3[2]));  // one kernel per round
                 g_ms += x;
                 a_ms += y;
                 ++timed_rounds;
@@ -548,8 +578,9 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         batch = batch < kMaxBatch ? batch * 2 : kMaxBatch;
     }
     const int last = found > 0 ? found : max_rounds;
-    // dense: after a zero-change round both buffers agree; otherwise the newest is bufs[last&1]
-    if (mode == SWARM_ELECT_DENSE && found < 0 && (last & 1))
+    // after a zero-change round both buffers hold the final state (dense and frontier alike);
+    // otherwise the newest is bufs[last & 1]
+    if (found < 0 && (last & 1))
         SW_HIP(hipMemcpyAsync(leader, bufs[1], size_t(n) * 4, hipMemcpyDeviceToDevice, s));
     hipLaunchKernelGGL(k_state, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s, leader,
                        ids, state, n);
@@ -597,60 +628,65 @@ int swarm_elect_i64(swarm_ctx *ctx, int64_t n, const int64_t *row_ptr, const int
 }
 
 int swarm_frontier_begin(swarm_ctx *ctx, int64_t n_rows, int64_t n_all, const int32_t *init,
-                         int32_t *leader, void *stream) {
+                         int32_t *leader0, int32_t *leader1, void *stream) {
     using namespace swarm;
     SW_ARG(ctx != nullptr, "ctx is NULL");
     SW_ARG(n_rows >= 0 && n_all >= n_rows && n_all < (int64_t(1) << 31), "sizes out of range");
-    SW_ARG(n_all == 0 || (init && leader), "NULL array");
+    SW_ARG(n_all == 0 || (init && leader0 && leader1), "NULL array");
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const size_t ring_words = size_t(kRing) * kCounters * kRoundWords;
-    unsigned long long *ring;
-    uint8_t *act;
-    int2 *list;
-    const int64_t nchunks = (n_rows + kChunk - 1) / kChunk;
-    const int64_t seg_cap = ((nchunks + kShards - 1) / kShards) * kChunk;
-    SW_ALLOC(ring, ctx, S_CHANGES, (ring_words + kRing) * 8);
-    SW_ALLOC(act, ctx, S_ACT, size_t(n_all) + 16);
-    SW_ALLOC(list, ctx, S_LIST, size_t(seg_cap > 0 ? seg_cap : 1) * kShards * 8);
-    SW_HIP(hipMemsetAsync(ring, 0, (ring_words + kRing) * 8, s));
+    Frontier f{};
+    int rc = frontier_alloc(ctx, n_rows, n_all, leader0, leader1, &f, s);
+    if (rc) return rc;
     if (n_all) {
-        SW_HIP(hipMemsetAsync(act, 1, size_t(n_all), s));
-        SW_HIP(hipMemcpyAsync(leader, init, size_t(n_all) * 4, hipMemcpyDeviceToDevice, s));
+        SW_HIP(hipMemcpyAsync(leader0, init, size_t(n_all) * 4, hipMemcpyDeviceToDevice, s));
+        SW_HIP(hipMemcpyAsync(leader1, init, size_t(n_all) * 4, hipMemcpyDeviceToDevice, s));
     }
     ctx->step_rows = n_rows;
     ctx->step_all = n_all;
     return SWARM_OK;
 }
 
+static int stepper_state(swarm_ctx *ctx, int32_t *leader0, int32_t *leader1, swarm::Frontier *f) {
+    using namespace swarm;
+    SW_ARG(ctx->slot[S_ACT] != nullptr && ctx->slot[S_CHANGES] != nullptr, "swarm_frontier_begin first");
+    const size_t na = size_t(ctx->step_all) + 16;
+    f->L[0] = leader0;
+    f->L[1] = leader1;
+    f->act[0] = static_cast<uint8_t *>(ctx->slot[S_ACT]);
+    f->act[1] = f->act[0] + na;
+    f->ring = static_cast<unsigned long long *>(ctx->slot[S_CHANGES]);
+    f->tot = f->ring + size_t(kRing) * kCounters * kRoundWords;
+    f->n_rows = ctx->step_rows;
+    return SWARM_OK;
+}
+
 int swarm_frontier_step(swarm_ctx *ctx, int32_t t, const int32_t *row_ptr, const int32_t *col,
-                        int32_t *leader, void *stream) {
+                        int32_t *leader0, int32_t *leader1, void *stream) {
     using namespace swarm;
     SW_ARG(ctx != nullptr, "ctx is NULL");
     SW_ARG(t >= 1, "round must be >= 1");
-    SW_ARG(ctx->cap[S_ACT] >= size_t(ctx->step_all), "swarm_frontier_begin first");
-    const int64_t n = ctx->step_rows;
-    if (n == 0) return SWARM_OK;
-    SW_ARG(row_ptr && leader, "NULL array");
-    const int64_t nchunks = (n + kChunk - 1) / kChunk;
-    const int64_t seg_cap = ((nchunks + kShards - 1) / kShards) * kChunk;
-    unsigned long long *ring = static_cast<unsigned long long *>(ctx->slot[S_CHANGES]);
-    unsigned long long *tot = ring + size_t(kRing) * kCounters * kRoundWords;
-    return launch_frontier_round<int32_t>(row_ptr, col, leader, static_cast<uint8_t *>(ctx->slot[S_ACT]),
-                                          static_cast<int2 *>(ctx->slot[S_LIST]), seg_cap, n, ring, tot, t,
-                                          0, static_cast<hipStream_t>(stream), nullptr, /*guard=*/0);
+    if (ctx->step_rows == 0) return SWARM_OK;
+    SW_ARG(row_ptr && leader0 && leader1, "NULL array");
+    Frontier f{};
+    int rc = stepper_state(ctx, leader0, leader1, &f);
+    if (rc) return rc;
+    return launch_frontier_round<int32_t>(row_ptr, col, f, t, 0, /*guard=*/0, static_cast<hipStream_t>(stream));
 }
 
 int swarm_frontier_ghosts(swarm_ctx *ctx, int32_t t, int64_t begin, int64_t count,
                           const int32_t *incoming, const int32_t *row_ptr, const int32_t *col,
-                          int32_t *leader, void *stream) {
+                          int32_t *leader0, int32_t *leader1, void *stream) {
     using namespace swarm;
     SW_ARG(ctx != nullptr, "ctx is NULL");
     SW_ARG(begin >= 0 && count >= 0 && begin + count <= ctx->step_all, "ghost range out of bounds");
     if (count == 0) return SWARM_OK;
-    SW_ARG(incoming && row_ptr && leader, "NULL array");
+    SW_ARG(incoming && row_ptr && leader0 && leader1, "NULL array");
+    Frontier f{};
+    int rc = stepper_state(ctx, leader0, leader1, &f);
+    if (rc) return rc;
     hipLaunchKernelGGL((k_frontier_ghosts<8, int32_t>), dim3(grid_for(count, kBlock / 8, 2048)), dim3(kBlock), 0,
-                       static_cast<hipStream_t>(stream), row_ptr, col, leader,
-                       static_cast<uint8_t *>(ctx->slot[S_ACT]), begin, count, incoming, t);
+                       static_cast<hipStream_t>(stream), row_ptr, col, leader0, leader1,
+                       f.act[(t + 1) & 1], begin, count, incoming, t);
     SW_LAUNCHED();
     return SWARM_OK;
 }

@@ -77,9 +77,9 @@ def load(path: str = LIB_PATH):
         L.swarm_utility.argtypes = [P, i64, P, P, P, P, d, P, P]
         L.swarm_build_rgg.argtypes = [P, i64, P, d, P, P, i64, ctypes.POINTER(i64), P]
         L.swarm_cell_order.argtypes = [P, i64, P, d, P, P]
-        L.swarm_frontier_begin.argtypes = [P, i64, i64, P, P, P]
-        L.swarm_frontier_step.argtypes = [P, i32, P, P, P, P]
-        L.swarm_frontier_ghosts.argtypes = [P, i32, i64, i64, P, P, P, P, P]
+        L.swarm_frontier_begin.argtypes = [P, i64, i64, P, P, P, P]
+        L.swarm_frontier_step.argtypes = [P, i32, P, P, P, P, P]
+        L.swarm_frontier_ghosts.argtypes = [P, i32, i64, i64, P, P, P, P, P, P]
         L.swarm_frontier_changes.argtypes = [P, i32, i32, P, P]
         for name in EXPORTS:
             if name not in ("swarm_last_error", "swarm_version"):

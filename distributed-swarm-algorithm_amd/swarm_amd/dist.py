@@ -125,20 +125,22 @@ class GpuBackend:
                                         col.numel(), ctypes.byref(ne), L.stream()))
         return rp, col
 
-    def begin(self, n_rows, init, leader):
+    def begin(self, n_rows, init, leaders):
         L = self.L
-        L.check(L.lib().swarm_frontier_begin(L.ctx(), n_rows, init.numel(), L.ptr(init), L.ptr(leader),
-                                             L.stream()))
+        L.check(L.lib().swarm_frontier_begin(L.ctx(), n_rows, init.numel(), L.ptr(init), L.ptr(leaders[0]),
+                                             L.ptr(leaders[1]), L.stream()))
 
-    def step(self, t, rp, col, leader):
+    def step(self, t, rp, col, leaders):
         L = self.L
-        L.check(L.lib().swarm_frontier_step(L.ctx(), t, L.ptr(rp), L.ptr(col), L.ptr(leader), L.stream()))
+        L.check(L.lib().swarm_frontier_step(L.ctx(), t, L.ptr(rp), L.ptr(col), L.ptr(leaders[0]),
+                                            L.ptr(leaders[1]), L.stream()))
 
-    def ghosts(self, t, begin, incoming, rp, col, leader):
+    def ghosts(self, t, begin, incoming, rp, col, leaders):
         L = self.L
         if incoming.numel():
             L.check(L.lib().swarm_frontier_ghosts(L.ctx(), t, begin, incoming.numel(), L.ptr(incoming),
-                                                  L.ptr(rp), L.ptr(col), L.ptr(leader), L.stream()))
+                                                  L.ptr(rp), L.ptr(col), L.ptr(leaders[0]), L.ptr(leaders[1]),
+                                                  L.stream()))
 
     def changes(self, t0, t1):
         L = self.L
@@ -188,7 +190,8 @@ class ShardedSwarm:
         self.all_pos = torch.cat([self.pos, gp_lo, gp_hi]).contiguous()
         self.all_ids = torch.cat([self.ids, gi_lo, gi_hi]).contiguous()
         self.row_ptr, self.col = self.backend.build_graph(self.all_pos, self.radius)
-        self.leader = torch.empty(self.all_ids.numel(), dtype=torch.int32, device=dev)
+        self.leaders = (torch.empty(self.all_ids.numel(), dtype=torch.int32, device=dev),
+                        torch.empty(self.all_ids.numel(), dtype=torch.int32, device=dev))
 
     def _border(self, width):
         y = self.pos[:, 1]
@@ -201,7 +204,7 @@ class ShardedSwarm:
     # ------------------------------------------------------------------ election
     def elect(self, max_rounds: int = 1 << 16, check_every: int = 64) -> ShardElectResult:
         be, h = self.backend, self.halo
-        rp, col, lead = self.row_ptr, self.col, self.leader
+        rp, col, lead = self.row_ptr, self.col, self.leaders
         be.begin(self.n_own, self.all_ids, lead)
         g_lo, g_hi = self.n_own, self.n_own + self.n_glo
         changes = []
@@ -211,7 +214,8 @@ class ShardedSwarm:
             tend = min(max_rounds, t + check_every - 1)
             for r in range(t, tend + 1):
                 be.step(r, rp, col, lead)
-                in_lo, in_hi = h.exchange(lead[self.send_lo], lead[self.send_hi], self.n_glo, self.n_ghi, lead)
+                cur = lead[r & 1]  # state after round r
+                in_lo, in_hi = h.exchange(cur[self.send_lo], cur[self.send_hi], self.n_glo, self.n_ghi, cur)
                 be.ghosts(r, g_lo, in_lo, rp, col, lead)
                 be.ghosts(r, g_hi, in_hi, rp, col, lead)
             glob = h.all_reduce_sum(be.changes(t, tend))
@@ -222,7 +226,7 @@ class ShardedSwarm:
                     break
             t = tend + 1
         rounds = found if found > 0 else max_rounds
-        own = lead[: self.n_own]
+        own = lead[rounds & 1][: self.n_own]
         state = torch.where(own == self.ids, 3, 1).to(torch.uint8)
         return ShardElectResult(rounds, np.array(changes[:rounds], np.int64), own, state, found > 0)
 

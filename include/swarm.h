@@ -120,22 +120,26 @@ int swarm_elect_round(swarm_ctx *ctx, int64_t n_rows, const int32_t *row_ptr,
  * between rounds (swarm_amd/dist.py does it over RCCL).  Local storage = n_rows owned agents
  * followed by ghosts (copies of other shards' boundary agents), n_all in total; the CSR has
  * n_all rows (ghost rows list their local neighbours) and col indexes [0, n_all).
- *   begin:   leader[0:n_all] = init; every agent active for round 1.
+ * Leaders are double-buffered by round parity: round t reads leader[(t-1)&1] and writes
+ * leader[t&1], so after round t the current state is leader[t&1] (leader0 / leader1, both
+ * n_all, owned by the caller).
+ *   begin:   leader0 = leader1 = init; every agent active for round 1.
  *   step:    round t over the owned rows (no convergence guard: a shard with no local change
  *            can still receive ghost changes).  Owned changes are counted per round.
  *   ghosts:  after the halo exchange of round t, incoming[i] is the round-t leader of ghost
- *            begin+i; rises are written and their neighbours activated for round t+1.
+ *            begin+i; rises are written to both buffers and their neighbours activated for
+ *            round t+1.
  *   changes: per-round owned change counts of rounds t0..t1 (t1 - t0 < 256); host sync.
  *            Read at least every 256 rounds (counter slots are recycled).
  * One stepper per ctx; swarm_elect() on the same ctx resets it.
  */
 int swarm_frontier_begin(swarm_ctx *ctx, int64_t n_rows, int64_t n_all, const int32_t *init,
-                         int32_t *leader, void *stream);
+                         int32_t *leader0, int32_t *leader1, void *stream);
 int swarm_frontier_step(swarm_ctx *ctx, int32_t t, const int32_t *row_ptr, const int32_t *col,
-                        int32_t *leader, void *stream);
+                        int32_t *leader0, int32_t *leader1, void *stream);
 int swarm_frontier_ghosts(swarm_ctx *ctx, int32_t t, int64_t begin, int64_t count,
                           const int32_t *incoming, const int32_t *row_ptr, const int32_t *col,
-                          int32_t *leader, void *stream);
+                          int32_t *leader0, int32_t *leader1, void *stream);
 int swarm_frontier_changes(swarm_ctx *ctx, int32_t t0, int32_t t1, int64_t *out, void *stream);
 
 /*

@@ -28,35 +28,38 @@ class NumpyBackend:
         rp, col = oracle.rgg_csr(p[:, 0], p[:, 1], radius)
         return torch.as_tensor(rp), torch.as_tensor(col)
 
-    def begin(self, n_rows, init, leader):
-        leader.copy_(init)
+    # leaders: two buffers, round t reads [(t-1)&1] and writes [t&1] (swarm_frontier_* contract)
+    def begin(self, n_rows, init, leaders):
+        leaders[0].copy_(init)
+        leaders[1].copy_(init)
         self.n_rows = n_rows
         self.act = np.ones(init.numel(), np.int64)
         self.counts = {}
 
-    def step(self, t, rp, col, leader):
-        L = leader.numpy()
+    def step(self, t, rp, col, leaders):
+        Lr, Lw = leaders[(t - 1) & 1].numpy(), leaders[t & 1].numpy()
         rp_, col_ = rp.numpy(), col.numpy()
-        snap = L.copy()
+        Lw[: self.n_rows] = Lr[: self.n_rows]
         act = np.nonzero(self.act[: self.n_rows] == t)[0]
         changed = []
         for v in act:
             nb = col_[rp_[v]:rp_[v + 1]]
-            m = snap[nb].max() if len(nb) else snap[v]
-            if m > snap[v]:
+            m = Lr[nb].max() if len(nb) else Lr[v]
+            if m > Lr[v]:
                 changed.append((v, m))
         for v, m in changed:
-            L[v] = m
+            Lw[v] = m
             self.act[col_[rp_[v]:rp_[v + 1]]] = t + 1
         self.counts[t] = len(changed)
 
-    def ghosts(self, t, begin, incoming, rp, col, leader):
-        L = leader.numpy()
+    def ghosts(self, t, begin, incoming, rp, col, leaders):
+        cur = leaders[t & 1].numpy()
         rp_, col_ = rp.numpy(), col.numpy()
         for i, nv in enumerate(incoming.numpy()):
             g = begin + i
-            if nv > L[g]:
-                L[g] = nv
+            if nv > cur[g]:
+                leaders[0].numpy()[g] = nv
+                leaders[1].numpy()[g] = nv
                 self.act[col_[rp_[g]:rp_[g + 1]]] = t + 1
 
     def changes(self, t0, t1):
