@@ -54,9 +54,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # SWARM_DIST_BACKEND=gloo: rehearse N ranks on fewer GPUs (halo staged through the host);
+    # the default and the measured configuration is nccl (RCCL over xGMI), one GPU per rank
+    backend = os.environ.get("SWARM_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     from swarm_amd import _lib, gen
     from swarm_amd.swarm import Swarm
@@ -273,7 +281,7 @@ def sharded(args, rank, world, dev):
     dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t[0])
     total_agents = args.agents * world

@@ -607,6 +607,34 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
 }
 
 }  // namespace
+
+// Internal entry points for comm.hip (the RCCL round loop): one stepper round, and the device
+// per-round totals [changes, active, edges] of rounds t0..t1 into dtot.
+int frontier_round_stepper(swarm_ctx *ctx, int t, const int32_t *rp, const int32_t *col, int32_t *L0,
+                           int32_t *L1, hipStream_t s, uint8_t **act_next) {
+    Frontier f{};
+    SW_ARG(ctx->slot[S_ACT] != nullptr && ctx->slot[S_CHANGES] != nullptr, "swarm_frontier_begin first");
+    const size_t na = size_t(ctx->step_all) + 16;
+    f.L[0] = L0;
+    f.L[1] = L1;
+    f.act[0] = static_cast<uint8_t *>(ctx->slot[S_ACT]);
+    f.act[1] = f.act[0] + na;
+    f.ring = static_cast<unsigned long long *>(ctx->slot[S_CHANGES]);
+    f.tot = f.ring + size_t(kRing) * kCounters * kRoundWords;
+    f.n_rows = ctx->step_rows;
+    *act_next = f.act[(t + 1) & 1];
+    if (f.n_rows == 0) return SWARM_OK;
+    return launch_frontier_round<int32_t>(rp, col, f, t, 0, /*guard=*/0, s);
+}
+
+int frontier_round_totals(swarm_ctx *ctx, int t0, int t1, unsigned long long *dtot, hipStream_t s) {
+    SW_ARG(t1 >= t0 && t1 - t0 < kRing / 2, "round range");
+    unsigned long long *ring = static_cast<unsigned long long *>(ctx->slot[S_CHANGES]);
+    hipLaunchKernelGGL(k_batch_totals, dim3(t1 - t0 + 1), dim3(kWave), 0, s, ring, t0, dtot);
+    SW_LAUNCHED();
+    return SWARM_OK;
+}
+
 }  // namespace swarm
 
 extern "C" {

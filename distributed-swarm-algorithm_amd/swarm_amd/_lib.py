@@ -26,7 +26,9 @@ ALLOC_AUTO, ALLOC_BINNED, ALLOC_DENSE = 0, 1, 2
 EXPORTS = ("swarm_last_error", "swarm_version", "swarm_ctx_create", "swarm_ctx_destroy",
            "swarm_elect", "swarm_elect_i64", "swarm_elect_round", "swarm_allocate",
            "swarm_utility", "swarm_build_rgg", "swarm_cell_order", "swarm_frontier_begin",
-           "swarm_frontier_step", "swarm_frontier_ghosts", "swarm_frontier_changes")
+           "swarm_frontier_step", "swarm_frontier_ghosts", "swarm_frontier_changes",
+           "swarm_comm_available", "swarm_comm_unique_id", "swarm_comm_create", "swarm_comm_destroy",
+           "swarm_elect_sharded")
 
 
 class SwarmError(RuntimeError):
@@ -46,6 +48,15 @@ class ElectStats(ctypes.Structure):
                 ("edges_total", ctypes.c_int64), ("changes_total", ctypes.c_int64),
                 ("gather_ms", ctypes.c_double), ("apply_ms", ctypes.c_double),
                 ("gather_launches", ctypes.c_int64)]
+
+
+class Shard(ctypes.Structure):
+    _fields_ = [("n_rows", ctypes.c_int64), ("n_all", ctypes.c_int64), ("row_ptr", ctypes.c_void_p),
+                ("col", ctypes.c_void_p), ("init", ctypes.c_void_p), ("send_lo", ctypes.c_void_p),
+                ("n_send_lo", ctypes.c_int64), ("send_hi", ctypes.c_void_p), ("n_send_hi", ctypes.c_int64),
+                ("ghost_lo_begin", ctypes.c_int64), ("n_ghost_lo", ctypes.c_int64),
+                ("ghost_hi_begin", ctypes.c_int64), ("n_ghost_hi", ctypes.c_int64),
+                ("peer_lo", ctypes.c_int32), ("peer_hi", ctypes.c_int32)]
 
 
 _lib = None
@@ -81,6 +92,11 @@ def load(path: str = LIB_PATH):
         L.swarm_frontier_step.argtypes = [P, i32, P, P, P, P, P]
         L.swarm_frontier_ghosts.argtypes = [P, i32, i64, i64, P, P, P, P, P, P]
         L.swarm_frontier_changes.argtypes = [P, i32, i32, P, P]
+        L.swarm_comm_available.argtypes = []
+        L.swarm_comm_unique_id.argtypes = [P]
+        L.swarm_comm_create.argtypes = [ctypes.POINTER(P), ctypes.c_int, ctypes.c_int, P]
+        L.swarm_comm_destroy.argtypes = [P]
+        L.swarm_elect_sharded.argtypes = [P, P, ctypes.POINTER(Shard), P, P, i32, ctypes.POINTER(i32), P, P]
         for name in EXPORTS:
             if name not in ("swarm_last_error", "swarm_version"):
                 getattr(L, name).restype = ctypes.c_int

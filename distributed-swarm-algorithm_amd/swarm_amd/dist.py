@@ -46,12 +46,20 @@ class Halo:
         self.world = dist.get_world_size(group)
         self.lo, self.hi = _neighbors(self.rank, self.world)
         self.device = device
+        # gloo cannot move device tensors: stage through host memory (tests / 1-GPU rehearsal)
+        self.host_staged = dist.get_backend(group) == "gloo"
 
     def _peer(self, r):
         return dist.get_global_rank(self.group, r) if self.group is not None else r
 
     def exchange(self, to_lo, to_hi, n_from_lo, n_from_hi, like):
         """Send to_lo to rank-1 and to_hi to rank+1; receive n_from_lo / n_from_hi elements."""
+        if self.host_staged and like.is_cuda:
+            a, b = self._exchange(to_lo.cpu(), to_hi.cpu(), n_from_lo, n_from_hi, like.cpu()[:0])
+            return a.to(like.device), b.to(like.device)
+        return self._exchange(to_lo, to_hi, n_from_lo, n_from_hi, like)
+
+    def _exchange(self, to_lo, to_hi, n_from_lo, n_from_hi, like):
         shape_tail = tuple(like.shape[1:])
         from_lo = torch.empty((n_from_lo,) + shape_tail, dtype=like.dtype, device=like.device)
         from_hi = torch.empty((n_from_hi,) + shape_tail, dtype=like.dtype, device=like.device)
@@ -73,14 +81,15 @@ class Halo:
 
     def all_reduce_sum(self, arr):
         """Element-wise sum over ranks of a small int64 vector (host array in, host array out)."""
-        t = torch.as_tensor(np.asarray(arr, np.int64), device=self.device)
+        t = torch.as_tensor(np.asarray(arr, np.int64), device="cpu" if self.host_staged else self.device)
         if self.world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
         return t.cpu().numpy()
 
     def exchange_counts(self, n_to_lo, n_to_hi):
-        t = torch.tensor([n_to_lo], dtype=torch.int64, device=self.device)
-        u = torch.tensor([n_to_hi], dtype=torch.int64, device=self.device)
+        dev = "cpu" if self.host_staged else self.device
+        t = torch.tensor([n_to_lo], dtype=torch.int64, device=dev)
+        u = torch.tensor([n_to_hi], dtype=torch.int64, device=dev)
         a, b = self.exchange(t if self.lo is not None else t[:0], u if self.hi is not None else u[:0],
                              1 if self.lo is not None else 0, 1 if self.hi is not None else 0, t)
         return (int(a.item()) if a.numel() else 0), (int(b.item()) if b.numel() else 0)
@@ -141,6 +150,46 @@ class GpuBackend:
             L.check(L.lib().swarm_frontier_ghosts(L.ctx(), t, begin, incoming.numel(), L.ptr(incoming),
                                                   L.ptr(rp), L.ptr(col), L.ptr(leaders[0]), L.ptr(leaders[1]),
                                                   L.stream()))
+
+    # ---- native sharded loop (RCCL on the device stream; see csrc/comm.hip)
+    def native_comm(self, halo):
+        """A libswarm RCCL communicator over the halo's group (None if unavailable)."""
+        import ctypes
+        import os
+        L = self.L
+        if os.environ.get("SWARM_NATIVE_HALO", "1") == "0" or halo.host_staged or halo.world < 2:
+            return None
+        if not L.lib().swarm_comm_available():
+            return None
+        uid = torch.zeros(128, dtype=torch.uint8, device=self.device)
+        if halo.rank == 0:
+            buf = (ctypes.c_uint8 * 128)()
+            L.check(L.lib().swarm_comm_unique_id(ctypes.cast(buf, ctypes.c_void_p)))
+            uid.copy_(torch.frombuffer(bytearray(buf), dtype=torch.uint8))
+        dist.broadcast(uid, src=halo._peer(0), group=halo.group)
+        raw = (ctypes.c_uint8 * 128)(*uid.cpu().tolist())
+        comm = ctypes.c_void_p()
+        L.check(L.lib().swarm_comm_create(ctypes.byref(comm), halo.world, halo.rank,
+                                          ctypes.cast(raw, ctypes.c_void_p)))
+        return comm
+
+    def elect_sharded(self, comm, sh, max_rounds):
+        import ctypes
+        L = self.L
+        z = ctypes.c_void_p(0)
+        desc = L.Shard(sh.n_own, sh.all_ids.numel(), L.ptr(sh.row_ptr), L.ptr(sh.col) if sh.col.numel() else z,
+                       L.ptr(sh.all_ids), L.ptr(sh.send_lo) if sh.send_lo.numel() else z, sh.send_lo.numel(),
+                       L.ptr(sh.send_hi) if sh.send_hi.numel() else z, sh.send_hi.numel(),
+                       sh.n_own, sh.n_glo, sh.n_own + sh.n_glo, sh.n_ghi,
+                       sh.halo.lo if sh.halo.lo is not None else -1,
+                       sh.halo.hi if sh.halo.hi is not None else -1)
+        rounds = ctypes.c_int32(0)
+        changes = np.zeros(max_rounds, np.int64)
+        rc = L.check(L.lib().swarm_elect_sharded(L.ctx(), comm, ctypes.byref(desc), L.ptr(sh.leaders[0]),
+                                                 L.ptr(sh.leaders[1]), max_rounds, ctypes.byref(rounds),
+                                                 changes.ctypes.data_as(ctypes.c_void_p), L.stream()))
+        r = rounds.value
+        return r, changes[:r].copy(), rc == L.OK
 
     def changes(self, t0, t1):
         L = self.L
@@ -204,6 +253,14 @@ class ShardedSwarm:
     # ------------------------------------------------------------------ election
     def elect(self, max_rounds: int = 1 << 16, check_every: int = 64) -> ShardElectResult:
         be, h = self.backend, self.halo
+        if getattr(self, "_native", "unset") == "unset":
+            self._native = be.native_comm(h) if hasattr(be, "native_comm") else None
+        if self._native is not None:
+            rounds, changes, conv = be.elect_sharded(self._native, self, max_rounds)
+            own = self.leaders[rounds & 1][: self.n_own]
+            self._check_ghosts(self.leaders[rounds & 1])
+            state = torch.where(own == self.ids, 3, 1).to(torch.uint8)
+            return ShardElectResult(rounds, changes, own, state, conv)
         rp, col, lead = self.row_ptr, self.col, self.leaders
         be.begin(self.n_own, self.all_ids, lead)
         g_lo, g_hi = self.n_own, self.n_own + self.n_glo
@@ -229,6 +286,15 @@ class ShardedSwarm:
         own = lead[rounds & 1][: self.n_own]
         state = torch.where(own == self.ids, 3, 1).to(torch.uint8)
         return ShardElectResult(rounds, np.array(changes[:rounds], np.int64), own, state, found > 0)
+
+    def _check_ghosts(self, cur):
+        """Every ghost must hold its owner's final leader (cheap end-to-end halo check)."""
+        h = self.halo
+        in_lo, in_hi = h.exchange(cur[self.send_lo], cur[self.send_hi], self.n_glo, self.n_ghi, cur)
+        g_lo = cur[self.n_own:self.n_own + self.n_glo]
+        g_hi = cur[self.n_own + self.n_glo:self.n_own + self.n_glo + self.n_ghi]
+        if not (torch.equal(in_lo, g_lo) and torch.equal(in_hi, g_hi)):
+            raise RuntimeError("sharded election: ghost leaders disagree with their owners")
 
     # ------------------------------------------------------------------ allocation
     def allocate(self, tx, ty, treq, *, claim_thr: float = 20.0, hysteresis: float = 5.0,

@@ -143,6 +143,45 @@ int swarm_frontier_ghosts(swarm_ctx *ctx, int32_t t, int64_t begin, int64_t coun
 int swarm_frontier_changes(swarm_ctx *ctx, int32_t t0, int32_t t1, int64_t *out, void *stream);
 
 /*
+ * Multi-GPU election: the sharded round loop on the device stream.  Each round:
+ * the frontier round over the owned rows, the owned boundary agents' leaders packed and sent
+ * to the neighbour shards with RCCL point-to-point calls (ncclSend/ncclRecv in one group), the
+ * received ghost leaders applied (swarm_frontier_ghosts semantics); every batch of rounds one
+ * ncclAllReduce(sum) of the per-round owned change counts decides convergence.  Same results
+ * as swarm_elect(FRONTIER) on the union graph.  RCCL is taken from the process at run time
+ * (the instance torch loaded); swarm_comm_available() says whether it was found.
+ */
+typedef struct swarm_comm swarm_comm;
+
+typedef struct swarm_shard {
+    int64_t n_rows;          /* owned agents (rows gathered), stored first */
+    int64_t n_all;           /* owned + ghost agents */
+    const int32_t *row_ptr;  /* CSR over all n_all rows (ghost rows list their local neighbours) */
+    const int32_t *col;
+    const int32_t *init;     /* initial leaders = IDs of all n_all agents */
+    const int64_t *send_lo;  /* owned agents the lower neighbour keeps as ghosts (device idx) */
+    int64_t n_send_lo;
+    const int64_t *send_hi;  /* owned agents the upper neighbour keeps as ghosts */
+    int64_t n_send_hi;
+    int64_t ghost_lo_begin;  /* ghosts received from the lower neighbour: [begin, begin + n) */
+    int64_t n_ghost_lo;
+    int64_t ghost_hi_begin;  /* ghosts received from the upper neighbour */
+    int64_t n_ghost_hi;
+    int32_t peer_lo;         /* RCCL rank of the lower / upper neighbour, -1 = none */
+    int32_t peer_hi;
+} swarm_shard;
+
+int swarm_comm_available(void);
+int swarm_comm_unique_id(void *out128);
+int swarm_comm_create(swarm_comm **out, int nranks, int rank, const void *id128);
+int swarm_comm_destroy(swarm_comm *comm);
+/* leader0 / leader1: n_all each; after rounds_exec rounds the state is leader[rounds_exec&1].
+ * changes_per_round (host, capacity max_rounds): GLOBAL per-round change counts. */
+int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *shard,
+                        int32_t *leader0, int32_t *leader1, int32_t max_rounds,
+                        int32_t *rounds_exec, int64_t *changes_per_round, void *stream);
+
+/*
  * Task allocation round (contract A-H).
  * Replaces: SwarmAgent._process_tasks + _calculate_utility (agent.py:292-302, 338-347) run by
  * every agent over every OPEN task, then SwarmAgent._handle_task_claim (agent.py:304-325) at

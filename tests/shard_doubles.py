@@ -99,6 +99,7 @@ class ThreadHalo:
         class Member:
             group = None
             world = hub.world
+            host_staged = True  # no RCCL communicator behind an in-process halo
 
             def __init__(self):
                 self.rank = rank

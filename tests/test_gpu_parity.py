@@ -345,3 +345,38 @@ def test_elect_timed_stats(sw, oracle_mod):
     assert r.timed_launches == r.rounds_exec and r.gather_ms > 0 and r.apply_ms >= 0
     r2 = s.elect(mode="dense", timed=True)
     assert r2.rounds_exec == int(g["rounds_exec"]) and r2.gather_ms > 0
+
+
+def test_native_sharded_loop_single_rank_rccl(sw, oracle_mod):
+    """swarm_elect_sharded (the RCCL round loop) on a 1-rank communicator: same rounds, changes
+    and leaders as the single-GPU frontier election (no halos; exercises the loop, the batched
+    RCCL all-reduce and the convergence test)."""
+    import ctypes
+    from swarm_amd import _lib as L
+    from swarm_amd import gen
+    if not L.lib().swarm_comm_available():
+        pytest.skip("RCCL not resolvable in this process")
+    d = gen.swarm_inputs(120000, 77)
+    s = sw.Swarm(d["ids"], d["x"], d["y"], device="cuda").build_graph(1.0)
+    want = s.elect(mode="frontier")
+    uid = (ctypes.c_uint8 * 128)()
+    L.check(L.lib().swarm_comm_unique_id(ctypes.cast(uid, ctypes.c_void_p)))
+    comm = ctypes.c_void_p()
+    L.check(L.lib().swarm_comm_create(ctypes.byref(comm), 1, 0, ctypes.cast(uid, ctypes.c_void_p)))
+    try:
+        n = s.n
+        l0 = torch.empty(n, dtype=torch.int32, device="cuda")
+        l1 = torch.empty(n, dtype=torch.int32, device="cuda")
+        z = ctypes.c_void_p(0)
+        desc = L.Shard(n, n, L.ptr(s.row_ptr), L.ptr(s.col), L.ptr(s.ids), z, 0, z, 0, n, 0, n, 0, -1, -1)
+        rounds = ctypes.c_int32(0)
+        ch = np.zeros(1 << 12, np.int64)
+        L.check(L.lib().swarm_elect_sharded(L.ctx(), comm, ctypes.byref(desc), L.ptr(l0), L.ptr(l1), len(ch),
+                                            ctypes.byref(rounds), ch.ctypes.data_as(ctypes.c_void_p), L.stream()))
+        r = rounds.value
+        assert r == want.rounds_exec
+        np.testing.assert_array_equal(ch[:r], want.changes)
+        final = (l1 if r & 1 else l0).cpu().numpy()
+        np.testing.assert_array_equal(final, want.leader.cpu().numpy())
+    finally:
+        L.lib().swarm_comm_destroy(comm)
