@@ -180,23 +180,22 @@ __global__ __launch_bounds__(kBlock) void k_elect_dense(
 // round t-1 is active in round t; every active agent writes its round-t value to Lw.  Agents
 // that changed in neither round t-1 nor t already hold the right value in Lw.  Hence Lw is the
 // state after round t, with no fold, no change list and no global atomic on the critical path.
-// A chunk's workgroup finds its active agents (8 stamp bytes per lane) and gathers them from
-// Lr: per-agent rows (2 lanes x kK loads) for a sparse chunk, coalesced LDS windows over all
-// of the chunk's agents for a dense one.  Counters are fire-and-forget shard adds.
-constexpr int kDenseChunk = kChunk / 2;  // active agents above which a chunk gathers densely
+// A chunk's workgroup finds its active agents (8 stamp bytes per lane), compacts them in LDS and
+// gathers them from Lr, kG lanes per agent with kKs loads in flight per lane.  (A dense variant
+// that staged whole chunks through LDS windows measured no faster even on the first, nearly
+// all-active rounds, and its registers cost occupancy: 62 VGPRs now = 8 waves per SIMD.)
+// Counters are fire-and-forget shard adds.
 constexpr int kG = 4;                    // sparse chunk: lanes per active agent
 constexpr int kKs = 8;                   // sparse chunk: loads in flight per lane
-constexpr int kKd = 8;                   // dense chunk: gathers in flight per lane
 
 template <typename Off>
-__global__ __launch_bounds__(kBlock) void k_frontier_round(
+__global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_frontier_round(
     const Off *__restrict__ rp, const int32_t *__restrict__ col, const int32_t *__restrict__ Lr,
     int32_t *__restrict__ Lw, const uint8_t *__restrict__ act_r, uint8_t *__restrict__ act_w,
     int64_t n, unsigned long long *__restrict__ ring, unsigned long long *__restrict__ tot, int t,
-    int with_stats, int guard, int dense_at) {
-    __shared__ union {
+    int with_stats, int guard) {
+    __shared__ struct {
         int list[kChunk];
-        int col[kWavesPerBlock][kWin];
     } u;
     __shared__ int s_wave[kWavesPerBlock];
     __shared__ long long s_red[3][kWavesPerBlock];
@@ -241,48 +240,8 @@ __global__ __launch_bounds__(kBlock) void k_frontier_round(
             off += (w < wid) ? s_wave[w] : 0;
             total += s_wave[w];
         }
-        if (total > dense_at) {
-            // 2a. dense chunk: every agent of the chunk, 64 per wave task, coalesced windows
-            const int64_t cend = (c0 + kChunk < n) ? c0 + kChunk : n;
-            int *sc = u.col[wid];
-            for (int64_t tb = c0 + int64_t(wid) * 64; tb < cend; tb += kBlock) {
-                const int64_t v = tb + lane;
-                const bool valid = v < cend;
-                const Off b = rp[valid ? v : cend], e = rp[(v + 1 < cend) ? v + 1 : cend];
-                const Off W0 = __shfl(b, 0, 64), W1 = __shfl(e, 63, 64);
-                const int own = Lr[valid ? v : cend - 1];
-                int m = own;
-                for (Off w0 = W0; w0 < W1; w0 += kWin) {
-                    const Off wend = (W1 - w0 < kWin) ? W1 : w0 + kWin;
-#pragma unroll
-                    for (int j = 0; j < kWin / 64; ++j) {
-                        const Off k = w0 + j * 64 + lane;
-                        sc[j * 64 + lane] = col[k < wend ? k : wend - 1];
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    const Off lo = b > w0 ? b : w0, hi = e < wend ? e : wend;
-                    m = row_max_from_lds<Off, kKd>(sc, w0, lo, hi, Lr, m);
-                    __builtin_amdgcn_wave_barrier();
-                }
-                const bool up = valid && m > own;
-                if (valid) Lw[v] = m;
-                if (up) {
-                    act_w[v] = next;
-                    if (W1 - W0 <= kWin) {  // the wave's whole slice is still in LDS
-                        for (Off k = b; k < e; ++k) act_w[sc[k - W0]] = next;
-                    } else {
-                        for (Off k = b; k < e; ++k) act_w[col[k]] = next;
-                    }
-                }
-                __builtin_amdgcn_wave_barrier();
-                my_chg += __popcll(__ballot(up));
-                if (with_stats && valid) {
-                    my_active += 1;
-                    my_edges += (long long)(e - b);
-                }
-            }
-        } else if (total > 0) {
-            // 2b. sparse chunk: compacted active agents, kG lanes per agent, kKs loads per lane
+        if (total > 0) {
+            // 2. compacted active agents, kG lanes per agent, kKs loads per lane
             int pos = off + wexcl;
             while (mask) {
                 const int j = __ffs(mask) - 1;
@@ -412,11 +371,7 @@ int env_int(const char *name, int dflt) {
 
 struct Tuning {
     int dense_blocks = 2048;     // grid cap of the dense round kernel
-    int dense_at = kDenseChunk;  // frontier: active agents per chunk above which it gathers densely
-    Tuning() {
-        dense_blocks = env_int("SWARM_DENSE_BLOCKS", 2048);
-        dense_at = env_int("SWARM_DENSE_CHUNK", kDenseChunk);
-    }
+    Tuning() { dense_blocks = env_int("SWARM_DENSE_BLOCKS", 2048); }
 };
 
 const Tuning &tuning() {
@@ -468,7 +423,7 @@ int launch_frontier_round(const Off *rp, const int32_t *col, const Frontier &f, 
     const unsigned grid = grid_for(nchunks > 0 ? nchunks : 1, 1, 1u << 20);
     const int r = t & 1, p = r ^ 1;
     hipLaunchKernelGGL((k_frontier_round<Off>), dim3(grid), dim3(kBlock), 0, s, rp, col, f.L[p], f.L[r],
-                       f.act[r], f.act[p], f.n_rows, f.ring, f.tot, t, with_stats, guard, tuning().dense_at);
+                       f.act[r], f.act[p], f.n_rows, f.ring, f.tot, t, with_stats, guard);
     SW_LAUNCHED();
     return SWARM_OK;
 }
