@@ -128,14 +128,14 @@ def main():
     rt = sw.elect(mode=args.elect_mode, max_rounds=1 << 16, timed=True)
     launches = max(rt.timed_launches, 1)
     if args.elect_mode == "frontier":
-        # k_frontier_round algorithmic bytes (lower bound): 1 stamp byte per agent per launch; per
-        # active agent its two row offsets + own leader + new leader (16 B); per gathered edge
-        # col + neighbour leader (8 B); per change its self-stamp (1 B; neighbour stamps uncounted)
-        pull_bytes = launches * n + 16 * rt.active_total + 8 * rt.edges_total + rt.changes_total
-        dom = {"kernel": "k_frontier_round (fused frontier E2 round)", "bytes_per_launch": pull_bytes / launches,
+        # k_frontier_round algorithmic bytes, summed by libswarm from the per-round counters
+        # (DESIGN.md §4): dense rounds 12N + 8E + 4; sparse rounds N (stamps) + 16/marked agent
+        # + 8/edge
+        dom = {"kernel": "k_frontier_round (E2 round: dense sweep / marked-agent sparse gather)",
+               "bytes_per_launch": rt.bytes_total / launches,
                "avg_launch_ms": rt.gather_ms / launches, "launches": launches,
-               "apply_avg_launch_ms": rt.apply_ms / launches,
-               "share_of_elect": rt.gather_ms / max(rt.gather_ms + rt.apply_ms, 1e-9)}
+               "dense_rounds": rt.dense_rounds, "sparse_rounds": launches - rt.dense_rounds,
+               "edges_total": rt.edges_total}
     else:
         dom = None
 
@@ -201,7 +201,8 @@ def main():
                                      "bytes_per_launch": bytes_round, "avg_launch_ms": dense_round_ms,
                                      "agent_rounds_per_s": n / (dense_round_ms * 1e-3)},
             "elect_stats": {"rounds_launched": r.rounds_launched, "active_total": r.active_total,
-                            "edges_total": r.edges_total, "changes_total": rt.changes_total},
+                            "edges_total": r.edges_total,
+                            "dense_rounds": r.dense_rounds, "changes_total": rt.changes_total},
             "alloc_stats": a.stats,
         }
     # ---- CPU baseline: the oracle restatement on the host cores, bounded sample

@@ -84,40 +84,16 @@ __global__ __launch_bounds__(kBlock) void k_pack(const int32_t *__restrict__ L, 
     }
 }
 
-// ghost rises (both borders in one launch): write both buffers, stamp local neighbours for t+1
-__global__ __launch_bounds__(kBlock) void k_ghosts2(const int32_t *__restrict__ rp, const int32_t *__restrict__ col,
-                                                   int32_t *__restrict__ L0, int32_t *__restrict__ L1,
-                                                   uint8_t *__restrict__ act_w, int64_t b_lo, int64_t n_lo,
-                                                   const int32_t *__restrict__ in_lo, int64_t b_hi, int64_t n_hi,
-                                                   const int32_t *__restrict__ in_hi, int t) {
-    const uint8_t next = uint8_t((t + 1) & 0xFF);
-    int32_t *Lcur = (t & 1) ? L1 : L0;
-    constexpr int G = 8;
-    const int sub = threadIdx.x & (G - 1);
-    const int64_t total = n_lo + n_hi;
-    for (int64_t base = int64_t(blockIdx.x) * (kBlock / G); base < total; base += int64_t(gridDim.x) * (kBlock / G)) {
-        const int64_t i = base + threadIdx.x / G;
-        if (i < total) {
-            const int64_t g = i < n_lo ? b_lo + i : b_hi + (i - n_lo);
-            const int nv = i < n_lo ? in_lo[i] : in_hi[i - n_lo];
-            if (nv > Lcur[g]) {
-                if (sub == 0) {
-                    L0[g] = nv;
-                    L1[g] = nv;
-                }
-                for (int32_t k = rp[g] + sub; k < rp[g + 1]; k += G) act_w[col[k]] = next;
-            }
-        }
-    }
-}
-
 }  // namespace
 }  // namespace swarm
 
 // the frontier round launcher lives in elect.hip
 namespace swarm {
 int frontier_round_stepper(swarm_ctx *ctx, int t, const int32_t *rp, const int32_t *col, int32_t *L0,
-                           int32_t *L1, hipStream_t s, uint8_t **act_next);
+                           int32_t *L1, int64_t last_changes, hipStream_t s);
+int frontier_ghosts_both(swarm_ctx *ctx, int t, const int32_t *rp, const int32_t *col, int64_t b_lo, int64_t n_lo,
+                         const int32_t *in_lo, int64_t b_hi, int64_t n_hi, const int32_t *in_hi, int32_t *L0,
+                         int32_t *L1, hipStream_t s);
 int frontier_round_totals(swarm_ctx *ctx, int t0, int t1, unsigned long long *dtot, hipStream_t s);
 }  // namespace swarm
 
@@ -189,16 +165,18 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sh,
     int32_t *s_lo = bufs, *s_hi = s_lo + sh->n_send_lo, *r_lo = s_hi + sh->n_send_hi, *r_hi = r_lo + sh->n_ghost_lo;
     constexpr int kMaxBatch = 256;
     unsigned long long *dtot;
-    SW_ALLOC(dtot, ctx, S_ESTATS, size_t(3) * 8 * kMaxBatch);
-    unsigned long long *h = static_cast<unsigned long long *>(pinned(ctx, size_t(3) * 8 * kMaxBatch));
+    constexpr int kC = kElectCounters;
+    SW_ALLOC(dtot, ctx, S_ESTATS, size_t(kC) * 8 * kMaxBatch);
+    unsigned long long *h = static_cast<unsigned long long *>(pinned(ctx, size_t(kC) * 8 * kMaxBatch));
     if (!h) return SWARM_ERR_OOM;
     const Rccl &R = rccl();
     int found = -1, t = 1, batch = 8;
+    int64_t last_changes = -1;  // newest global change count read (picks the sparse kernel)
     while (t <= max_rounds && found < 0) {
         const int tend = std::min(max_rounds, t + batch - 1);
         for (int r = t; r <= tend; ++r) {
-            uint8_t *act_next = nullptr;
-            if ((rc = frontier_round_stepper(ctx, r, sh->row_ptr, sh->col, leader0, leader1, s, &act_next))) return rc;
+            if ((rc = frontier_round_stepper(ctx, r, sh->row_ptr, sh->col, leader0, leader1, last_changes, s)))
+                return rc;
             int32_t *Lcur = (r & 1) ? leader1 : leader0;
             const int64_t ns = sh->n_send_lo + sh->n_send_hi;
             if (ns) {
@@ -216,22 +194,19 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sh,
                 if (sh->n_ghost_hi) SW_NCCL(R.recv(r_hi, size_t(sh->n_ghost_hi), ncclInt32, sh->peer_hi, comm->comm, s));
             }
             SW_NCCL(R.groupEnd());
-            const int64_t ng = sh->n_ghost_lo + sh->n_ghost_hi;
-            if (ng) {
-                hipLaunchKernelGGL(k_ghosts2, dim3(grid_for(ng, kBlock / 8, 1024)), dim3(kBlock), 0, s, sh->row_ptr,
-                                   sh->col, leader0, leader1, act_next, sh->ghost_lo_begin, sh->n_ghost_lo, r_lo,
-                                   sh->ghost_hi_begin, sh->n_ghost_hi, r_hi, r);
-                SW_LAUNCHED();
-            }
+            if ((rc = frontier_ghosts_both(ctx, r, sh->row_ptr, sh->col, sh->ghost_lo_begin, sh->n_ghost_lo, r_lo,
+                                           sh->ghost_hi_begin, sh->n_ghost_hi, r_hi, leader0, leader1, s)))
+                return rc;
         }
         const int nr = tend - t + 1;
         if ((rc = frontier_round_totals(ctx, t, tend, dtot, s))) return rc;
-        SW_NCCL(R.allReduce(dtot, dtot, size_t(nr) * 3, ncclUint64, ncclSum, comm->comm, s));
-        SW_HIP(hipMemcpyAsync(h, dtot, size_t(nr) * 3 * 8, hipMemcpyDeviceToHost, s));
+        SW_NCCL(R.allReduce(dtot, dtot, size_t(nr) * kC, ncclUint64, ncclSum, comm->comm, s));
+        SW_HIP(hipMemcpyAsync(h, dtot, size_t(nr) * kC * 8, hipMemcpyDeviceToHost, s));
         SW_HIP(hipStreamSynchronize(s));
         for (int r = t; r <= tend; ++r) {
-            const unsigned long long c = h[size_t(r - t) * 3];
+            const unsigned long long c = h[size_t(r - t) * kC];  // C_CHG: owned changes
             if (changes_host) changes_host[r - 1] = int64_t(c);
+            last_changes = int64_t(c);
             if (c == 0) {
                 found = r;
                 break;

@@ -9,26 +9,37 @@
 //
 // Two exact strategies:
 //   DENSE     every round every agent gathers its whole CSR row (Jacobi, double-buffered).
-//             HBM bytes per round = 12N + 8E (+ the gather, mostly served on-die).
-//   FRONTIER  an agent can only change in round t+1 if a neighbour changed in round t, so
-//             round t+1 gathers only those agents.  Same leaders, same per-round change
-//             counts, same rounds_exec -- each agent's row is read O(changes) times instead
-//             of O(rounds) times.  Per round: a 1-byte-per-agent stamp scan, the gathers of
-//             active agents, a block-aggregated append of (agent, new leader), and an apply
-//             pass that writes the new leaders and stamps their neighbours for round t+1.
+//   FRONTIER  an agent can only change in round t+1 if a neighbour changed in round t (its own
+//             value already dominates every unchanged neighbour), so after a few dense rounds
+//             only the agents MARKED by the previous round's risers gather.  Same leaders, same
+//             per-round change counts, same rounds_exec; each agent's row is read O(changes)
+//             times instead of O(rounds) times.
 //
-// Gather: one wave serves 64 agents at once (lane = agent).  Their rows are concatenated
-// virtually (wave prefix sum of degrees) and swept 64*U edges at a time, lane-contiguous, so
-// col reads coalesce and each lane keeps U independent col loads and then U independent
-// leader gathers in flight; each edge finds its row by a 6-step binary search over the lanes'
-// row offsets and max-combines into a per-wave LDS slot.
+// One kernel per round, picked by the host per round from the last change counts it has read
+// (every batch of rounds):
+//   k_elect_dense<MARK=false>  the first dense_rounds-1 rounds (nearly every agent changes)
+//   k_elect_dense<MARK=true>   the last dense round: also marks the risers' neighbourhoods
+//   k_sparse_block             2048-agent chunk per workgroup: stamps -> LDS list -> gather
+//   k_sparse_wave              late rounds (few marks): 512-agent chunks per wave, grid =
+//                              resident waves, next chunk's stamps loaded ahead, no barriers
+// Marks are plain byte stores, no atomics: stamp act[v] = t+1 (mod 256), double-buffered by
+// round parity and consumed (zeroed) by the sparse round that reads them.  Leaders alternate by
+// parity: round t reads L[(t-1)&1] and writes L[t&1], which still holds the state after t-2; it
+// differs from the state after t-1 only on round t-1's risers, all marked (self-mark), so all
+// rewrite their entry.
 //
-// Counters: every per-round count (changes, active agents, edges) is a 64-way sharded 64-bit
-// counter on its own 128-byte line, added once per workgroup: one contended counter per round
-// costs ~12 ns per arrival (MI355X_MICROARCH.md, 'fanin'), i.e. ~0.8 ms per round at one
-// arrival per wave at 10M agents.  The shards live in a ring of kRing rounds; the host zeroes
-// a batch's slots before launching it and reads them back after.
+// Counters: every per-round count (changes, marked agents, edges, ghost rises) is a 64-way
+// sharded 64-bit counter on its own 128-byte line, added once per workgroup: one contended
+// counter per round costs ~12 ns per arrival (MI355X_MICROARCH.md, 'fanin').  The shards live
+// in a ring of kRing rounds; block 0 of round t recycles the slots of round t + kRing/2 and
+// publishes the total changes of round t-1 (tot[]), which sparse rounds use as their guard.
+//
+// Measured and rejected: a push variant (risers atomicMax their value into the
+// neighbours: scattered device-scope atomics run at ~20 G/s), dense and sparse paths fused in
+// one kernel (register pressure: 6 instead of 8 waves per SIMD, +10 %), one lane per marked
+// agent or 16 lanes per agent over 1024-agent units (+40 % / +130 %).
 #include <climits>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -42,9 +53,8 @@ constexpr int kShards = 64;
 constexpr int kShardStride = 16;                    // u64 per shard: one 128-B line each
 constexpr int kRing = 512;                          // rounds of counter slots
 constexpr int kRoundWords = kShards * kShardStride; // u64 per round per counter
-constexpr int kCounters = 3;                        // changes, active, edges
-constexpr int kScan = 8;                            // stamps per thread (one 8-B load)
-constexpr int kChunk = kBlock * kScan;              // agents per frontier work unit
+constexpr int kCounters = kElectCounters;
+constexpr int C_CHG = 0, C_ACT = 1, C_EDGE = 2, C_GHOST = 3;
 constexpr int kWavesPerBlock = kBlock / kWave;
 
 __device__ __forceinline__ unsigned long long *slot(unsigned long long *ring, int t, int counter, int shard) {
@@ -55,7 +65,7 @@ __device__ __forceinline__ unsigned long long *slot(unsigned long long *ring, in
 __device__ __forceinline__ unsigned long long round_total(unsigned long long *ring, int t,
                                                           unsigned long long *s_bcast) {
     if (threadIdx.x < kWave) {
-        unsigned long long v = *slot(ring, t, 0, threadIdx.x);
+        unsigned long long v = *slot(ring, t, C_CHG, threadIdx.x);
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
         if (threadIdx.x == 0) *s_bcast = v;
@@ -64,23 +74,55 @@ __device__ __forceinline__ unsigned long long round_total(unsigned long long *ri
     return *s_bcast;
 }
 
-__device__ __forceinline__ int wave_excl_scan(int v, int *total) {
-    const int lane = threadIdx.x & 63;
-    int incl = v;
+// Block 0 of round t: publish the total changes of round t-1 and recycle round t + kRing/2.
+__device__ __forceinline__ void bookkeeping(unsigned long long *ring, unsigned long long *tot, int t) {
+    if (blockIdx.x != 0) return;
+    if (tot && t > 1 && threadIdx.x < kWave) {
+        unsigned long long v = *slot(ring, t - 1, C_CHG, threadIdx.x);
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int u = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += u;
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        if (threadIdx.x == 0) tot[(t - 1) % kRing] = v;
     }
-    *total = __shfl(incl, 63, 64);
-    return incl - v;
+    for (int i = threadIdx.x; i < kCounters * kShards; i += kBlock)
+        *slot(ring, t + kRing / 2, i / kShards, i % kShards) = 0;
 }
+
+#ifdef SWARM_PHASES  // debug build only: per-wave phase timestamps of the last launched round
+__device__ unsigned long long g_phase[8192 * 8];
+#define PHASE(k)                                                                         \
+    do {                                                                                 \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                      \
+        const int64_t wg_ = int64_t(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6);   \
+        if ((threadIdx.x & 63) == 0 && wg_ < 8192) g_phase[wg_ * 8 + (k)] = wall_clock64(); \
+    } while (0)
+#else
+#define PHASE(k) do {} while (0)
+#endif
 
 // 4-bit mask of the bytes of w equal to the byte replicated in b4 (exact, no carry leakage).
 __device__ __forceinline__ unsigned bytes_eq4(unsigned w, unsigned b4) {
     const unsigned x = w ^ b4;
     const unsigned z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
     return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+}
+
+constexpr int kKm = 8;  // marking re-walks: col loads in flight per lane
+
+// Mark col[k] for k = k0, k0 + step, ... < e with kKm loads in flight per batch.
+template <typename Off>
+__device__ __forceinline__ void mark_row(uint8_t *aw, const int32_t *__restrict__ col, Off k0, Off e, Off step,
+                                         uint8_t s) {
+    for (Off k = k0; k < e; k += step * kKm) {
+        int c[kKm];
+#pragma unroll
+        for (int j = 0; j < kKm; ++j) {
+            const Off kk = k + step * j;
+            c[j] = col[kk < e ? kk : e - 1];
+        }
+#pragma unroll
+        for (int j = 0; j < kKm; ++j)
+            if (k + step * j < e) aw[c[j]] = s;
+    }
 }
 
 // Dense gather.  Wave task = 64 consecutive agents (lane = agent); their rows are one
@@ -111,17 +153,19 @@ __device__ __forceinline__ int row_max_from_lds(const int *s_col, Off w0, Off lo
 }
 
 // ---------------------------------------------------------------- dense Jacobi round
-template <typename Off>
+// MARK: also stamp every riser and its neighbours for round t+1 (act_w = t+1), so that round
+// t+1 can run sparse.
+template <typename Off, bool MARK>
 __global__ __launch_bounds__(kBlock) void k_elect_dense(
     const Off *__restrict__ rp, const int32_t *__restrict__ col, const int32_t *__restrict__ lin,
-    int32_t *__restrict__ lout, int64_t n, unsigned long long *__restrict__ ring, int t, int guard) {
+    int32_t *__restrict__ lout, int64_t n, unsigned long long *__restrict__ ring,
+    unsigned long long *__restrict__ tot, uint8_t *__restrict__ act_w, int t, int guard) {
     __shared__ int s_col[kWavesPerBlock][kWin];
     __shared__ unsigned long long s_bc, s_cnt[kWavesPerBlock];
     if (guard && t > 1 && round_total(ring, t - 1, &s_bc) == 0) return;  // converged: no-op
-    if (guard && blockIdx.x == 0)  // recycle the counter slots of round t + kRing/2
-        for (int i = threadIdx.x; i < kCounters * kShards; i += kBlock)
-            *slot(ring, t + kRing / 2, i / kShards, i % kShards) = 0;
+    if (guard || tot) bookkeeping(ring, tot, t);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint8_t sw = uint8_t((t + 1) & 0xFF);
     int *sc = s_col[wid];
     unsigned long long mine = 0;
     const int64_t ntask = (n + 63) / 64;
@@ -159,6 +203,10 @@ __global__ __launch_bounds__(kBlock) void k_elect_dense(
         const bool up = valid && m > own;
         if (valid) lout[v] = up ? m : own;
         mine += __popcll(__ballot(up));
+        if (MARK && up) {
+            act_w[v] = sw;
+            mark_row<Off>(act_w, col, b, e, Off(1), sw);
+        }
         b = nb;
         e = ne;
     }
@@ -167,72 +215,140 @@ __global__ __launch_bounds__(kBlock) void k_elect_dense(
     if (threadIdx.x == 0) {
         unsigned long long s = 0;
         for (int w = 0; w < kWavesPerBlock; ++w) s += s_cnt[w];
-        if (s) atomicAdd(slot(ring, t, 0, blockIdx.x & (kShards - 1)), s);
+        if (s) atomicAdd(slot(ring, t, C_CHG, blockIdx.x & (kShards - 1)), s);
     }
 }
 
-// ------------------------------------------------------------- frontier: fused round
-// One kernel per round.  Buffers alternate by round parity:
-//   leaders  Lr = L[(t-1)&1] (state after round t-1, read), Lw = L[t&1] (written)
-//   stamps   act[t&1] (agents active in round t carry t&255), act[(t+1)&1] (written)
-// Invariant: before round t, Lw holds the state after round t-2.  An agent that changes in a
-// round stamps its neighbours AND itself for the next round, so every agent that changed in
-// round t-1 is active in round t; every active agent writes its round-t value to Lw.  Agents
-// that changed in neither round t-1 nor t already hold the right value in Lw.  Hence Lw is the
-// state after round t, with no fold, no change list and no global atomic on the critical path.
-// A chunk's workgroup finds its active agents (8 stamp bytes per lane), compacts them in LDS and
-// gathers them from Lr, kG lanes per agent with kKs loads in flight per lane.  (A dense variant
-// that staged whole chunks through LDS windows measured no faster even on the first, nearly
-// all-active rounds, and its registers cost occupancy: 62 VGPRs now = 8 waves per SIMD.)
-// Counters are fire-and-forget shard adds.
-constexpr int kG = 4;                    // sparse chunk: lanes per active agent
-constexpr int kKs = 8;                   // sparse chunk: loads in flight per lane
+// ------------------------------------------------------------------ sparse rounds
+constexpr int kScan = 8;                 // stamps per thread (one 8-B load)
+constexpr int kChunk = kBlock * kScan;   // k_sparse_block: agents per workgroup work unit
+constexpr int kWChunk = kWave * kScan;   // k_sparse_wave: agents per wave work unit
+constexpr int kG = 4;                    // lanes per marked agent
+constexpr int kKs = 8;                   // loads in flight per lane
 
+struct Frontier {
+    int32_t *L[2];
+    uint8_t *act[2];         // stamps, act_bytes(n_all) each (padded past n_all)
+    unsigned long long *ring, *tot;
+    int64_t n_rows, n_all;
+};
+
+// Gather of the marked agents listed (chunk-relative) in lst[0, total), kG lanes per agent,
+// `first`/`step` select this wave's share; risers mark themselves and their neighbours.
 template <typename Off>
-__global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_frontier_round(
-    const Off *__restrict__ rp, const int32_t *__restrict__ col, const int32_t *__restrict__ Lr,
-    int32_t *__restrict__ Lw, const uint8_t *__restrict__ act_r, uint8_t *__restrict__ act_w,
-    int64_t n, unsigned long long *__restrict__ ring, unsigned long long *__restrict__ tot, int t,
-    int with_stats, int guard) {
-    __shared__ struct {
-        int list[kChunk];
-    } u;
+__device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, const int32_t *__restrict__ col,
+                                              const int32_t *__restrict__ P, int32_t *__restrict__ Q,
+                                              uint8_t *__restrict__ aw, uint8_t sw, int64_t c0, const int *lst,
+                                              int total, int first, int step, long long &my_chg,
+                                              long long &my_act, long long &my_edges) {
+    const int lane = threadIdx.x & 63, sub = lane & (kG - 1);
+    for (int base = first; base < total; base += step) {
+        const int i = base + lane / kG;
+        const bool valid = i < total;
+        const int64_t v = c0 + lst[valid ? i : total - 1];
+        const Off b = rp[v], e = rp[v + 1];
+        const int own = P[v];
+        int m = own;
+        int c[kKs];
+        for (Off k = b + sub * kKs; k < e; k += kG * kKs) {
+#pragma unroll
+            for (int j = 0; j < kKs; ++j) c[j] = col[(k + j < e) ? k + j : e - 1];
+            int val[kKs];
+#pragma unroll
+            for (int j = 0; j < kKs; ++j) val[j] = P[c[j]];
+#pragma unroll
+            for (int j = 0; j < kKs; ++j) m = max(m, val[j]);
+        }
+#pragma unroll
+        for (int o2 = 1; o2 < kG; o2 <<= 1) m = max(m, __shfl_xor(m, o2, 64));
+        const bool up = valid && m > own;
+        if (valid && sub == 0) Q[v] = m;
+        if (up) {
+            if (sub == 0) aw[v] = sw;
+            if (e - b <= kG * kKs) {  // one pass per lane: c[] still holds this lane's edges
+#pragma unroll
+                for (int j = 0; j < kKs; ++j)
+                    if (b + sub * kKs + j < e) aw[c[j]] = sw;
+            } else {
+                mark_row<Off>(aw, col, b + sub, e, Off(kG), sw);
+            }
+        }
+        my_chg += __popcll(__ballot(up && sub == 0));
+        if (valid && sub == 0) {
+            my_act += 1;
+            my_edges += (long long)(e - b);
+        }
+    }
+}
+
+// Marked lanes of 8 stamps, consuming them (this parity is next written in round t+1, marks
+// for t+2; a stamp left behind would match again 256 rounds later: a spurious gather).
+__device__ __forceinline__ unsigned take_stamps(uint8_t *ar, int64_t v0, int64_t n, uint2 wv, unsigned stamp4) {
+    unsigned mask = bytes_eq4(wv.x, stamp4) | (bytes_eq4(wv.y, stamp4) << 4);
+    if (v0 + kScan > n) mask &= (v0 >= n) ? 0u : ((1u << (n - v0)) - 1u);
+    if (wv.x | wv.y) *reinterpret_cast<uint2 *>(ar + v0) = make_uint2(0u, 0u);
+    return mask;
+}
+
+__device__ __forceinline__ void flush_counts(unsigned long long *ring, int t, long long my_chg, long long my_act,
+                                             long long my_edges, long long (*s_red)[kWavesPerBlock]) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int o2 = 32; o2 > 0; o2 >>= 1) {
+        my_act += __shfl_xor(my_act, o2, 64);
+        my_edges += __shfl_xor(my_edges, o2, 64);
+    }
+    if (lane == 0) {
+        s_red[0][wid] = my_chg;  // wave-uniform (ballot counts)
+        s_red[1][wid] = my_act;
+        s_red[2][wid] = my_edges;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        long long a = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) a += s_red[threadIdx.x][w];
+        if (a) atomicAdd(slot(ring, t, threadIdx.x, blockIdx.x & (kShards - 1)), (unsigned long long)a);
+    }
+}
+
+// One workgroup per 2048-agent chunk: 8 stamps per thread, the chunk's marked agents compacted
+// in LDS and gathered by the whole workgroup.
+template <typename Off>
+__global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_block(
+    const Off *__restrict__ rp, const int32_t *__restrict__ col, Frontier f, int t, int guard) {
+    __shared__ int s_list[kChunk];
     __shared__ int s_wave[kWavesPerBlock];
     __shared__ long long s_red[3][kWavesPerBlock];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (blockIdx.x == 0) {  // bookkeeping: total of round t-1 (guard word), recycle slots
-        if (t > 1 && threadIdx.x < kWave) {
-            unsigned long long v = *slot(ring, t - 1, 0, threadIdx.x);
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-            if (threadIdx.x == 0) tot[(t - 1) % kRing] = v;
-        }
-        for (int i = threadIdx.x; i < kCounters * kShards; i += kBlock)
-            *slot(ring, t + kRing / 2, i / kShards, i % kShards) = 0;
-    }
-    // single-GPU runs: round t-2 changed nothing => round t-1 had no active agent => neither t
-    if (guard && t > 2 && tot[(t - 2) % kRing] == 0) return;
-    const unsigned stamp = unsigned(t & 0xFF);
-    const unsigned stamp4 = stamp * 0x01010101u;
-    const uint8_t next = uint8_t((t + 1) & 0xFF);
-    long long my_active = 0, my_edges = 0, my_chg = 0;
+    bookkeeping(f.ring, f.tot, t);
+    // single-GPU runs: round t-2 changed nothing => round t-1 had no marked agent => neither t
+    if (guard && t > 2 && f.tot[(t - 2) % kRing] == 0) return;
+    const int32_t *__restrict__ P = f.L[(t - 1) & 1];
+    int32_t *__restrict__ Q = f.L[t & 1];
+    uint8_t *ar = f.act[t & 1], *aw = f.act[(t + 1) & 1];
+    const unsigned stamp4 = unsigned(t & 0xFF) * 0x01010101u;
+    const uint8_t sw = uint8_t((t + 1) & 0xFF);
+    const int64_t n = f.n_rows;
+    long long my_chg = 0, my_act = 0, my_edges = 0;
     const int64_t nchunks = (n + kChunk - 1) / kChunk;
-    for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+    const int64_t G = gridDim.x;
+    uint2 nxt = make_uint2(0u, 0u);  // stamps are padded past n_all; the next chunk's are loaded ahead
+    if (int64_t(blockIdx.x) < nchunks)
+        nxt = *reinterpret_cast<const uint2 *>(ar + int64_t(blockIdx.x) * kChunk + int64_t(threadIdx.x) * kScan);
+    for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += G) {
         const int64_t c0 = chunk * kChunk;
-        // 1. my 8 stamps -> the chunk's active agents
         const int64_t v0 = c0 + int64_t(threadIdx.x) * kScan;
-        unsigned mask = 0;
-        if (v0 + kScan <= n) {
-            const uint2 w = *reinterpret_cast<const uint2 *>(act_r + v0);
-            mask = bytes_eq4(w.x, stamp4) | (bytes_eq4(w.y, stamp4) << 4);
-        } else {
-            for (int j = 0; j < kScan && v0 + j < n; ++j)
-                if (act_r[v0 + j] == stamp) mask |= 1u << j;
-        }
+        const uint2 wv = nxt;
+        if (chunk + G < nchunks) nxt = *reinterpret_cast<const uint2 *>(ar + v0 + G * kChunk);
+        unsigned mask = take_stamps(ar, v0, n, wv, stamp4);
         const int cnt = __popc(mask);
-        int wtot;
-        const int wexcl = wave_excl_scan(cnt, &wtot);
-        if (lane == 0) s_wave[wid] = wtot;
+        int incl = cnt;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int x = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += x;
+        }
+        if (lane == 63) s_wave[wid] = incl;
         __syncthreads();
         int off = 0, total = 0;
 #pragma unroll
@@ -241,99 +357,115 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_frontier_r
             total += s_wave[w];
         }
         if (total > 0) {
-            // 2. compacted active agents, kG lanes per agent, kKs loads per lane
-            int pos = off + wexcl;
+            int pos = off + incl - cnt;
             while (mask) {
                 const int j = __ffs(mask) - 1;
                 mask &= mask - 1;
-                u.list[pos++] = threadIdx.x * kScan + j;
+                s_list[pos++] = threadIdx.x * kScan + j;
             }
             __syncthreads();
-            const int sub = lane & (kG - 1);
-            for (int base = wid * (64 / kG); base < total; base += kBlock / kG) {
-                const int i = base + lane / kG;
-                const bool valid = i < total;
-                const int64_t v = c0 + u.list[valid ? i : total - 1];
-                const Off b = rp[v], e = rp[v + 1];
-                const int own = Lr[v];
-                int m = own;
-                int c[kKs];
-                for (Off k = b + sub * kKs; k < e; k += kG * kKs) {
-#pragma unroll
-                    for (int j = 0; j < kKs; ++j) c[j] = col[(k + j < e) ? k + j : e - 1];
-                    int val[kKs];
-#pragma unroll
-                    for (int j = 0; j < kKs; ++j) val[j] = Lr[c[j]];
-#pragma unroll
-                    for (int j = 0; j < kKs; ++j) m = max(m, val[j]);
-                }
-#pragma unroll
-                for (int o2 = 1; o2 < kG; o2 <<= 1) m = max(m, __shfl_xor(m, o2, 64));
-                const bool up = valid && m > own;
-                if (valid && sub == 0) Lw[v] = m;
-                if (up) {
-                    if (sub == 0) act_w[v] = next;
-                    if (e - b <= kG * kKs) {  // one pass per lane: c[] still holds this lane's edges
-#pragma unroll
-                        for (int j = 0; j < kKs; ++j)
-                            if (b + sub * kKs + j < e) act_w[c[j]] = next;
-                    } else {
-                        for (Off k = b + sub; k < e; k += kG) act_w[col[k]] = next;
-                    }
-                }
-                my_chg += __popcll(__ballot(up && sub == 0));
-                if (with_stats && valid && sub == 0) {
-                    my_active += 1;
-                    my_edges += (long long)(e - b);
-                }
-            }
+            gather_listed<Off>(rp, col, P, Q, aw, sw, c0, s_list, total, wid * (64 / kG), kBlock / kG, my_chg,
+                               my_act, my_edges);
         }
-        __syncthreads();  // LDS (s_wave, u) reused by the next chunk
+        __syncthreads();  // LDS (s_wave, s_list) reused by the next chunk
     }
-    // per-workgroup totals -> one shard add per counter
-    if (lane == 0) s_red[0][wid] = my_chg;  // my_chg is wave-uniform (ballot counts)
-#pragma unroll
-    for (int o2 = 32; o2 > 0; o2 >>= 1) {
-        my_active += __shfl_xor(my_active, o2, 64);
-        my_edges += __shfl_xor(my_edges, o2, 64);
-    }
-    if (lane == 0) { s_red[1][wid] = my_active; s_red[2][wid] = my_edges; }
-    __syncthreads();
-    if (threadIdx.x < kCounters) {
-        long long a = 0;
-        for (int w = 0; w < kWavesPerBlock; ++w) a += s_red[threadIdx.x][w];
-        if (a) atomicAdd(slot(ring, t, threadIdx.x, blockIdx.x & (kShards - 1)), (unsigned long long)a);
-    }
+    flush_counts(f.ring, t, my_chg, my_act, my_edges, s_red);
 }
 
-// Sharded runs: halo values received for ghost agents [begin, begin + count) after round t.
-// A ghost whose leader rose is written to BOTH leader buffers (ghosts are never gathered, so
-// either buffer may serve round t+1 and t+2) and its local neighbours are stamped for round
-// t+1 (ghost rows of the local CSR list them).  Ghost changes are counted by their owner.
-template <int G, typename Off>
-__global__ __launch_bounds__(kBlock) void k_frontier_ghosts(
-    const Off *__restrict__ rp, const int32_t *__restrict__ col, int32_t *__restrict__ L0,
-    int32_t *__restrict__ L1, uint8_t *__restrict__ act_w, int64_t begin, int64_t count,
-    const int32_t *__restrict__ incoming, int t) {
-    const uint8_t next = uint8_t((t + 1) & 0xFF);
-    int32_t *Lcur = (t & 1) ? L1 : L0;
-    constexpr int GPB = kBlock / G;
+// Late rounds: 512-agent chunks dealt to waves (grid-stride over exactly the resident waves),
+// the next chunk's stamps loaded ahead; each wave compacts and gathers its own chunk's marked
+// agents, with no workgroup barrier until the final counter flush.
+template <typename Off>
+__global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_wave(
+    const Off *__restrict__ rp, const int32_t *__restrict__ col, Frontier f, int t, int guard) {
+    __shared__ int s_list[kWavesPerBlock][kWChunk];
+    __shared__ long long s_red[3][kWavesPerBlock];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    bookkeeping(f.ring, f.tot, t);
+    if (guard && t > 2 && f.tot[(t - 2) % kRing] == 0) return;
+    PHASE(0);
+    const int32_t *__restrict__ P = f.L[(t - 1) & 1];
+    int32_t *__restrict__ Q = f.L[t & 1];
+    uint8_t *ar = f.act[t & 1], *aw = f.act[(t + 1) & 1];
+    const unsigned stamp4 = unsigned(t & 0xFF) * 0x01010101u;
+    const uint8_t sw = uint8_t((t + 1) & 0xFF);
+    const int64_t n = f.n_rows;
+    long long my_chg = 0, my_act = 0, my_edges = 0;
+    const int64_t nwc = (n + kWChunk - 1) / kWChunk;
+    const int64_t W = int64_t(gridDim.x) * kWavesPerBlock;
+    int *lst = s_list[wid];
+    int64_t wc = int64_t(blockIdx.x) * kWavesPerBlock + wid;
+    uint2 nxt = make_uint2(0u, 0u);  // stamps are padded past n_all
+    if (wc < nwc) nxt = *reinterpret_cast<const uint2 *>(ar + wc * kWChunk + int64_t(lane) * kScan);
+    for (; wc < nwc; wc += W) {
+        const int64_t c0 = wc * kWChunk;
+        const int64_t v0 = c0 + int64_t(lane) * kScan;
+        const uint2 wv = nxt;
+        if (wc + W < nwc) nxt = *reinterpret_cast<const uint2 *>(ar + v0 + W * kWChunk);
+        unsigned mask = take_stamps(ar, v0, n, wv, stamp4);
+        const int cnt = __popc(mask);
+        int incl = cnt;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int x = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += x;
+        }
+        const int total = __shfl(incl, 63, 64);
+        if (total == 0) continue;  // wave-uniform
+        int pos = incl - cnt;
+        while (mask) {
+            const int j = __ffs(mask) - 1;
+            mask &= mask - 1;
+            lst[pos++] = lane * kScan + j;
+        }
+        __builtin_amdgcn_wave_barrier();
+        gather_listed<Off>(rp, col, P, Q, aw, sw, c0, lst, total, 0, 64 / kG, my_chg, my_act, my_edges);
+        __builtin_amdgcn_wave_barrier();  // lst reused by the next chunk
+        PHASE(1);
+    }
+    PHASE(2);
+    flush_counts(f.ring, t, my_chg, my_act, my_edges, s_red);
+    PHASE(3);
+}
+
+// Sharded runs: halo values for ghosts [b_lo, b_lo + n_lo) and [b_hi, b_hi + n_hi) after round
+// t.  A ghost whose leader rose is written to BOTH leader buffers (ghosts are never gathered)
+// and its local neighbours are marked for round t+1 (ghost rows of the local CSR list them).
+// Rises are counted in C_GHOST; the owner counts them as changes.
+template <typename Off>
+__global__ __launch_bounds__(kBlock) void k_frontier_ghosts(const Off *__restrict__ rp, const int32_t *__restrict__ col,
+                                                            Frontier f, int64_t b_lo, int64_t n_lo,
+                                                            const int32_t *__restrict__ in_lo, int64_t b_hi,
+                                                            int64_t n_hi, const int32_t *__restrict__ in_hi, int t) {
+    constexpr int G = 8;
+    const uint8_t sw = uint8_t((t + 1) & 0xFF);
+    uint8_t *aw = f.act[(t + 1) & 1];
+    const int32_t *Lcur = f.L[t & 1];
     const int sub = threadIdx.x & (G - 1);
-    for (int64_t base = int64_t(blockIdx.x) * GPB; base < count; base += int64_t(gridDim.x) * GPB) {
+    const int64_t total = n_lo + n_hi;
+    long long rises = 0;
+    for (int64_t base = int64_t(blockIdx.x) * (kBlock / G); base < total; base += int64_t(gridDim.x) * (kBlock / G)) {
         const int64_t i = base + threadIdx.x / G;
-        if (i < count) {
-            const int64_t g = begin + i;
-            const int nv = incoming[i];
+        if (i < total) {
+            const int64_t g = i < n_lo ? b_lo + i : b_hi + (i - n_lo);
+            const int nv = i < n_lo ? in_lo[i] : in_hi[i - n_lo];
             if (nv > Lcur[g]) {
                 if (sub == 0) {
-                    L0[g] = nv;
-                    L1[g] = nv;
+                    f.L[0][g] = nv;
+                    f.L[1][g] = nv;
+                    ++rises;
                 }
-                const Off e1 = rp[g + 1];
-                for (Off k = rp[g] + sub; k < e1; k += G) act_w[col[k]] = next;
+                for (Off k = rp[g] + sub; k < rp[g + 1]; k += G) {
+                    const int32_t c = col[k];
+                    if (c < f.n_rows) aw[c] = sw;
+                }
             }
         }
     }
+#pragma unroll
+    for (int o2 = 32; o2 > 0; o2 >>= 1) rises += __shfl_xor(rises, o2, 64);
+    if ((threadIdx.x & 63) == 0 && rises)
+        atomicAdd(slot(f.ring, t, C_GHOST, blockIdx.x & (kShards - 1)), (unsigned long long)rises);
 }
 
 __global__ __launch_bounds__(kBlock) void k_state(const int32_t *__restrict__ leader,
@@ -346,13 +478,13 @@ __global__ __launch_bounds__(kBlock) void k_state(const int32_t *__restrict__ le
 
 // *out += sum of the 64 change shards of ring round t (single-round API).
 __global__ void k_sum_shards(unsigned long long *ring, int t, unsigned long long *out) {
-    unsigned long long v = *slot(ring, t, 0, threadIdx.x);
+    unsigned long long v = *slot(ring, t, C_CHG, threadIdx.x);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     if (threadIdx.x == 0) *out += v;
 }
 
-// totals[(r - t0) * 3 + c] = sum over shards of counter c of round r, one wave per round.
+// totals[(r - t0) * kCounters + c] = sum over shards of counter c of round r, one wave per round.
 __global__ void k_batch_totals(unsigned long long *ring, int t0, unsigned long long *totals) {
     const int r = t0 + blockIdx.x;
 #pragma unroll
@@ -370,8 +502,19 @@ int env_int(const char *name, int dflt) {
 }
 
 struct Tuning {
-    int dense_blocks = 2048;     // grid cap of the dense round kernel
-    Tuning() { dense_blocks = env_int("SWARM_DENSE_BLOCKS", 2048); }
+    int dense_blocks = 2048;  // grid cap of the dense round kernel
+    int dense_rounds = 8;     // frontier: rounds 1..dense_rounds run dense (the last one marks)
+    int wave_div = 0;         // frontier: k_sparse_wave once last known changes * wave_div <= n
+                              // (0 = never: measured slower than k_sparse_block at 10M agents)
+    int sparse_blocks = 2048; // grid cap of k_sparse_block (8 resident workgroups per CU)
+    Tuning() {
+        dense_blocks = env_int("SWARM_DENSE_BLOCKS", 2048);
+        dense_rounds = env_int("SWARM_DENSE_ROUNDS", 8);
+        wave_div = env_int("SWARM_WAVE_DIV", 0);
+        sparse_blocks = env_int("SWARM_SPARSE_BLOCKS", 2048);
+        if (dense_blocks < 1) dense_blocks = 1;
+        if (dense_rounds < 0) dense_rounds = 0;
+    }
 };
 
 const Tuning &tuning() {
@@ -379,53 +522,115 @@ const Tuning &tuning() {
     return tu;
 }
 
+size_t ring_bytes() { return size_t(kRing) * kCounters * kRoundWords * 8 + size_t(kRing) * 8; }
+
+size_t act_bytes(int64_t n_all) {  // one parity, padded to whole chunks (+1 of slack)
+    return size_t((n_all + 2 * kChunk - 1) / kChunk) * kChunk;
+}
+
 template <typename Off>
-int launch_dense_round(const Off *rp, const int32_t *col, const int32_t *lin, int32_t *lout,
-                       int64_t n, unsigned long long *ring, int t, int guard, hipStream_t s) {
+int launch_dense_round(const Off *rp, const int32_t *col, const int32_t *lin, int32_t *lout, int64_t n,
+                       unsigned long long *ring, unsigned long long *tot, uint8_t *act_w, int t, int guard,
+                       hipStream_t s) {
     const unsigned grid = grid_for((n + 63) / 64, kWavesPerBlock, unsigned(tuning().dense_blocks));
-    hipLaunchKernelGGL((k_elect_dense<Off>), dim3(grid), dim3(kBlock), 0, s, rp, col, lin, lout, n,
-                       ring, t, guard);
+    if (act_w)
+        hipLaunchKernelGGL((k_elect_dense<Off, true>), dim3(grid), dim3(kBlock), 0, s, rp, col, lin, lout, n, ring,
+                           tot, act_w, t, guard);
+    else
+        hipLaunchKernelGGL((k_elect_dense<Off, false>), dim3(grid), dim3(kBlock), 0, s, rp, col, lin, lout, n, ring,
+                           tot, act_w, t, guard);
     SW_LAUNCHED();
     return SWARM_OK;
 }
 
-// Frontier state: two leader buffers and two stamp arrays (round parity), counter ring.
-struct Frontier {
-    int32_t *L[2];
-    uint8_t *act[2];
-    unsigned long long *ring, *tot;
-    int64_t n_rows;
-};
+// Workgroups of k_sparse_wave<Off> resident at once (its waves must all run together).
+template <typename Off>
+unsigned resident_blocks() {
+    static unsigned cached = 0;
+    if (!cached) {
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sparse_wave<Off>, kBlock, 0) != hipSuccess ||
+            cus <= 0 || per_cu <= 0)
+            return 2048u;
+        cached = unsigned(cus) * unsigned(per_cu);
+    }
+    return cached;
+}
 
-int frontier_alloc(swarm_ctx *ctx, int64_t n_rows, int64_t n_all, int32_t *L0, int32_t *L1, Frontier *f,
-                   hipStream_t s) {
-    const size_t na = size_t(n_all) + 16;
-    uint8_t *act;
-    SW_ALLOC(act, ctx, S_ACT, 2 * na);
-    const size_t ring_words = size_t(kRing) * kCounters * kRoundWords;
-    SW_ALLOC(f->ring, ctx, S_CHANGES, (ring_words + kRing) * 8);
-    f->tot = f->ring + ring_words;
+// Frontier view of the ctx slots for n_rows owned agents of n_all.
+int frontier_bind(swarm_ctx *ctx, int32_t *L0, int32_t *L1, Frontier *f) {
+    SW_ARG(ctx->slot[S_ACT] != nullptr && ctx->slot[S_CHANGES] != nullptr, "swarm_frontier_begin first");
+    f->n_rows = ctx->step_rows;
+    f->n_all = ctx->step_all;
     f->L[0] = L0;
     f->L[1] = L1;
-    f->act[0] = act;
-    f->act[1] = act + na;
-    f->n_rows = n_rows;
-    SW_HIP(hipMemsetAsync(f->ring, 0, (ring_words + kRing) * 8, s));
-    SW_HIP(hipMemsetAsync(act, 0, 2 * na, s));
-    if (n_all) SW_HIP(hipMemsetAsync(f->act[1], 1, size_t(n_all), s));  // round 1 reads act[1]: all active
+    uint8_t *a = static_cast<uint8_t *>(ctx->slot[S_ACT]);
+    f->act[0] = a;
+    f->act[1] = a + act_bytes(f->n_all);
+    f->ring = static_cast<unsigned long long *>(ctx->slot[S_CHANGES]);
+    f->tot = f->ring + size_t(kRing) * kCounters * kRoundWords;
     return SWARM_OK;
 }
 
+// Scratch for a frontier run: stamps of both parities, the counter ring (all zeroed).  With no
+// dense round, round 1 reads act[1]: every agent marked.
+int frontier_alloc(swarm_ctx *ctx, int64_t n_rows, int64_t n_all, int32_t *L0, int32_t *L1, Frontier *f,
+                   hipStream_t s) {
+    const size_t sb = 2 * act_bytes(n_all);
+    void *p;
+    SW_ALLOC(p, ctx, S_ACT, sb);
+    SW_ALLOC(p, ctx, S_CHANGES, ring_bytes());
+    (void)p;
+    ctx->step_rows = n_rows;
+    ctx->step_all = n_all;
+    int rc = frontier_bind(ctx, L0, L1, f);
+    if (rc) return rc;
+    SW_HIP(hipMemsetAsync(f->ring, 0, ring_bytes(), s));
+    SW_HIP(hipMemsetAsync(f->act[0], 0, sb, s));
+    if (tuning().dense_rounds == 0 && n_all) SW_HIP(hipMemsetAsync(f->act[1], 1, size_t(n_all), s));
+    return SWARM_OK;
+}
+
+enum RoundKind { RK_DENSE = 0, RK_DENSE_MARK = 1, RK_SPARSE_BLOCK = 2, RK_SPARSE_WAVE = 3 };
+
+// Kind of frontier round t given the last change count the host has read (-1: unknown).
+RoundKind plan_round(int t, int64_t n, int64_t last_changes) {
+    const int R = tuning().dense_rounds;
+    if (t < R) return RK_DENSE;
+    if (t == R) return RK_DENSE_MARK;
+    if (tuning().wave_div > 0 && last_changes >= 0 && last_changes * int64_t(tuning().wave_div) <= n)
+        return RK_SPARSE_WAVE;
+    return RK_SPARSE_BLOCK;
+}
+
 template <typename Off>
-int launch_frontier_round(const Off *rp, const int32_t *col, const Frontier &f, int t, int with_stats,
-                          int guard, hipStream_t s) {
-    const int64_t nchunks = (f.n_rows + kChunk - 1) / kChunk;
-    const unsigned grid = grid_for(nchunks > 0 ? nchunks : 1, 1, 1u << 20);
-    const int r = t & 1, p = r ^ 1;
-    hipLaunchKernelGGL((k_frontier_round<Off>), dim3(grid), dim3(kBlock), 0, s, rp, col, f.L[p], f.L[r],
-                       f.act[r], f.act[p], f.n_rows, f.ring, f.tot, t, with_stats, guard);
+int launch_frontier_round(const Off *rp, const int32_t *col, const Frontier &f, int t, RoundKind k, int guard,
+                          hipStream_t s) {
+    if (k == RK_DENSE || k == RK_DENSE_MARK)
+        return launch_dense_round<Off>(rp, col, f.L[(t - 1) & 1], f.L[t & 1], f.n_rows, f.ring, f.tot,
+                                       k == RK_DENSE_MARK ? f.act[(t + 1) & 1] : nullptr, t, guard, s);
+    if (k == RK_SPARSE_WAVE) {
+        const unsigned grid = grid_for((f.n_rows + kWChunk - 1) / kWChunk, kWavesPerBlock, resident_blocks<Off>());
+        hipLaunchKernelGGL((k_sparse_wave<Off>), dim3(grid), dim3(kBlock), 0, s, rp, col, f, t, guard);
+    } else {
+        const int64_t nchunks = (f.n_rows + kChunk - 1) / kChunk;
+        const unsigned cap = tuning().sparse_blocks > 0 ? unsigned(tuning().sparse_blocks) : (1u << 20);
+        hipLaunchKernelGGL((k_sparse_block<Off>), dim3(grid_for(nchunks, 1, cap)), dim3(kBlock), 0, s, rp, col, f, t,
+                           guard);
+    }
     SW_LAUNCHED();
     return SWARM_OK;
+}
+
+// Algorithmic HBM bytes of one round:
+//   dense   12 n + 8 E + 4: row offsets, own leader, leader write, col, gathered leader
+//   sparse  n (stamps) + 16 per marked agent (row offsets, own leader, leader write) + 8 per
+//           edge (col, neighbour leader); marks (1 B per riser and neighbour) not counted
+double round_bytes(bool dense, int64_t n, int64_t e, int64_t active, int64_t edges) {
+    if (dense) return 12.0 * n + 8.0 * e + 4.0;
+    return double(n) + 16.0 * active + 8.0 * edges;
 }
 
 template <typename Off>
@@ -443,65 +648,76 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     SW_ARG(rounds_exec != nullptr, "rounds_exec is NULL");
     SW_ARG(n == 0 || (rp && ids && leader && state), "NULL array (col may be NULL only without edges)");
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (st) *st = swarm_elect_stats{0, 0, 0, 0, 0.0, 0.0, 0};
+    if (st) *st = swarm_elect_stats{};
     if (n == 0) {  // an empty swarm: round 1 changes nothing
         *rounds_exec = 1;
         if (changes_host) changes_host[0] = 0;
         if (st) st->rounds_launched = 1;
         return SWARM_OK;
     }
+    Off e_total = 0;
+    SW_HIP(hipMemcpyAsync(&e_total, rp + n, sizeof(Off), hipMemcpyDeviceToHost, s));
+    SW_HIP(hipStreamSynchronize(s));
+    SW_ARG(e_total == 0 || col != nullptr, "col is NULL but the graph has edges");
     int32_t *bufs[2] = {leader, nullptr};
     SW_ALLOC(bufs[1], ctx, S_LEADER_B, size_t(n) * 4);
     SW_HIP(hipMemcpyAsync(leader, ids, size_t(n) * 4, hipMemcpyDeviceToDevice, s));
     Frontier f{};
     unsigned long long *ring;
-    const size_t ring_words = size_t(kRing) * kCounters * kRoundWords;
     if (mode == SWARM_ELECT_FRONTIER) {
         SW_HIP(hipMemcpyAsync(bufs[1], ids, size_t(n) * 4, hipMemcpyDeviceToDevice, s));
         int rc0 = frontier_alloc(ctx, n, n, bufs[0], bufs[1], &f, s);
         if (rc0) return rc0;
         ring = f.ring;
     } else {
-        SW_ALLOC(ring, ctx, S_CHANGES, (ring_words + kRing) * 8);
+        SW_ALLOC(ring, ctx, S_CHANGES, ring_bytes());
+        SW_HIP(hipMemsetAsync(ring, 0, ring_bytes(), s));
+        ctx->step_rows = ctx->step_all = 0;  // the stepper state is gone
     }
-    const int with_stats = (st != nullptr && mode == SWARM_ELECT_FRONTIER) ? 1 : 0;
     constexpr int kMaxBatch = 256;
-    const size_t per_round = size_t(kCounters) * kRoundWords;
     unsigned long long *hbuf = static_cast<unsigned long long *>(pinned(ctx, size_t(kCounters) * 8 * kMaxBatch));
     if (!hbuf) return SWARM_ERR_OOM;
     unsigned long long *dtot;
     SW_ALLOC(dtot, ctx, S_ESTATS, size_t(kCounters) * 8 * kMaxBatch);
 
     int found = -1, t = 1, batch = 8, launched = 0;
-    int64_t act_sum = 0, edge_sum = 0, chg_sum = 0;
-    // optional per-kernel timing: events [3r] before gather, [3r+1] between, [3r+2] after apply
+    int64_t act_sum = 0, edge_sum = 0, chg_sum = 0, dense_rounds = 0, last_changes = -1;
+    double bytes = 0.0;
+    std::vector<RoundKind> kinds(kMaxBatch);
+    // optional per-round timing: events before and after every round kernel
     std::vector<hipEvent_t> ev;
-    double g_ms = 0, a_ms = 0;
+    double k_ms = 0;
     int64_t timed_rounds = 0;
     if (timed) {
-        ev.resize(3 * kMaxBatch);
+        ev.resize(2 * kMaxBatch);
         for (auto &x : ev) SW_HIP(hipEventCreate(&x));
     }
     struct EvFree {
         std::vector<hipEvent_t> &v;
         ~EvFree() { for (auto x : v) (void)hipEventDestroy(x); }
     } ev_free{ev};
-    // every counter slot starts at zero; afterwards each round's kernel recycles the slots of
-    // the round kRing/2 ahead
-    if (mode == SWARM_ELECT_DENSE) SW_HIP(hipMemsetAsync(ring, 0, (ring_words + kRing) * 8, s));
-    (void)per_round;
-    // slot of round 0 (read by round 1's guard only when t > 1: never) stays untouched
+    FILE *rlog = nullptr;  // SWARM_ROUND_LOG=path: one line per round (tuning aid)
+    if (const char *pth = getenv("SWARM_ROUND_LOG")) rlog = fopen(pth, "w");
+    struct LogClose {
+        FILE *&f;
+        ~LogClose() { if (f) fclose(f); }
+    } log_close{rlog};
     while (t <= max_rounds && found < 0) {
         const int tend = (max_rounds - t + 1 < batch) ? max_rounds : t + batch - 1;
         int rc = 0;
         for (int r = t; r <= tend; ++r) {
-            hipEvent_t *e3 = timed ? &ev[3 * (r - t)] : nullptr;
-            if (e3) SW_HIP(hipEventRecord(e3[0], s));
-            rc = (mode == SWARM_ELECT_DENSE)
-                     ? launch_dense_round<Off>(rp, col, bufs[(r - 1) & 1], bufs[r & 1], n, ring, r, 1, s)
-                     : launch_frontier_round<Off>(rp, col, f, r, with_stats, /*guard=*/1, s);
+            hipEvent_t *e2 = timed ? &ev[2 * (r - t)] : nullptr;
+            if (e2) SW_HIP(hipEventRecord(e2[0], s));
+            if (mode == SWARM_ELECT_DENSE) {
+                kinds[r - t] = RK_DENSE;
+                rc = launch_dense_round<Off>(rp, col, bufs[(r - 1) & 1], bufs[r & 1], n, ring, nullptr, nullptr, r,
+                                             1, s);
+            } else {
+                kinds[r - t] = plan_round(r, n, last_changes);
+                rc = launch_frontier_round<Off>(rp, col, f, r, kinds[r - t], 1, s);
+            }
             if (rc) return rc;
-            if (e3) SW_HIP(hipEventRecord(e3[2], s));
+            if (e2) SW_HIP(hipEventRecord(e2[1], s));
         }
         launched = tend;
         // per-round totals of rounds [t, tend], reduced on device, then one small copy
@@ -511,19 +727,26 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         SW_HIP(hipStreamSynchronize(s));
         for (int r = t; r <= tend; ++r) {
             const unsigned long long *rb = hbuf + size_t(r - t) * kCounters;
-            const unsigned long long c = rb[0], a = rb[1], ed = rb[2];
-            if (changes_host) changes_host[r - 1] = int64_t(c);
-            act_sum += int64_t(a);
-            edge_sum += int64_t(ed);
-            chg_sum += int64_t(c);
+            const int64_t c = int64_t(rb[C_CHG]);
+            const bool dn = kinds[r - t] == RK_DENSE || kinds[r - t] == RK_DENSE_MARK;
+            if (changes_host) changes_host[r - 1] = c;
+            const int64_t act = dn ? n : int64_t(rb[C_ACT]);
+            const int64_t ed = dn ? int64_t(e_total) : int64_t(rb[C_EDGE]);
+            act_sum += act;
+            edge_sum += ed;
+            chg_sum += c;
+            dense_rounds += dn ? 1 : 0;
+            bytes += round_bytes(dn, n, int64_t(e_total), act, ed);
+            last_changes = c;
+            float x = 0;
             if (timed) {
-                float x = 0, y = 0;
-                hipEvent_t *e3 = &ev[3 * (r - t)];
-                SW_HIP(hipEventElapsedTime(&x, e3[0], e3[2]));  // one kernel per round
-                g_ms += x;
-                a_ms += y;
+                SW_HIP(hipEventElapsedTime(&x, ev[2 * (r - t)], ev[2 * (r - t) + 1]));
+                k_ms += x;
                 ++timed_rounds;
             }
+            if (rlog)
+                fprintf(rlog, "%d %lld %lld %lld %d %.2f\n", r, (long long)c, (long long)act, (long long)ed,
+                        int(kinds[r - t]), x * 1e3);
             if (c == 0) {
                 found = r;
                 break;
@@ -544,42 +767,44 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     if (st) {
         st->rounds_launched = launched;
         st->changes_total = chg_sum;
-        st->gather_ms = g_ms;
-        st->apply_ms = a_ms;
+        st->gather_ms = k_ms;
+        st->apply_ms = 0.0;
         st->gather_launches = timed_rounds;
-        if (mode == SWARM_ELECT_DENSE) {
-            Off e = 0;
-            SW_HIP(hipMemcpyAsync(&e, rp + n, sizeof(Off), hipMemcpyDeviceToHost, s));
-            SW_HIP(hipStreamSynchronize(s));
-            st->active_total = n * int64_t(last);
-            st->edges_total = int64_t(e) * int64_t(last);
-        } else {
-            st->active_total = act_sum;
-            st->edges_total = edge_sum;
-        }
+        st->active_total = act_sum;
+        st->edges_total = edge_sum;
+        st->dense_rounds = dense_rounds;
+        st->bytes_total = bytes;
     }
     return found > 0 ? SWARM_OK : SWARM_NOT_CONVERGED;
 }
 
 }  // namespace
 
-// Internal entry points for comm.hip (the RCCL round loop): one stepper round, and the device
-// per-round totals [changes, active, edges] of rounds t0..t1 into dtot.
+// Internal entry points for comm.hip (the RCCL round loop): one stepper round (last_changes =
+// the newest global change count the caller has read, -1 if none), the ghost update of both
+// borders, and the device per-round totals (kCounters each) of rounds t0..t1.
 int frontier_round_stepper(swarm_ctx *ctx, int t, const int32_t *rp, const int32_t *col, int32_t *L0,
-                           int32_t *L1, hipStream_t s, uint8_t **act_next) {
+                           int32_t *L1, int64_t last_changes, hipStream_t s) {
     Frontier f{};
-    SW_ARG(ctx->slot[S_ACT] != nullptr && ctx->slot[S_CHANGES] != nullptr, "swarm_frontier_begin first");
-    const size_t na = size_t(ctx->step_all) + 16;
-    f.L[0] = L0;
-    f.L[1] = L1;
-    f.act[0] = static_cast<uint8_t *>(ctx->slot[S_ACT]);
-    f.act[1] = f.act[0] + na;
-    f.ring = static_cast<unsigned long long *>(ctx->slot[S_CHANGES]);
-    f.tot = f.ring + size_t(kRing) * kCounters * kRoundWords;
-    f.n_rows = ctx->step_rows;
-    *act_next = f.act[(t + 1) & 1];
+    int rc = frontier_bind(ctx, L0, L1, &f);
+    if (rc) return rc;
     if (f.n_rows == 0) return SWARM_OK;
-    return launch_frontier_round<int32_t>(rp, col, f, t, 0, /*guard=*/0, s);
+    return launch_frontier_round<int32_t>(rp, col, f, t, plan_round(t, f.n_rows, last_changes), /*guard=*/0, s);
+}
+
+int frontier_ghosts_both(swarm_ctx *ctx, int t, const int32_t *rp, const int32_t *col, int64_t b_lo, int64_t n_lo,
+                         const int32_t *in_lo, int64_t b_hi, int64_t n_hi, const int32_t *in_hi, int32_t *L0,
+                         int32_t *L1, hipStream_t s) {
+    Frontier f{};
+    int rc = frontier_bind(ctx, L0, L1, &f);
+    if (rc) return rc;
+    SW_ARG(b_lo >= f.n_rows && b_lo + n_lo <= f.n_all && b_hi >= f.n_rows && b_hi + n_hi <= f.n_all,
+           "ghost ranges must lie in [n_rows, n_all)");
+    if (n_lo + n_hi == 0) return SWARM_OK;
+    hipLaunchKernelGGL((k_frontier_ghosts<int32_t>), dim3(grid_for(n_lo + n_hi, kBlock / 8, 1024)), dim3(kBlock), 0,
+                       s, rp, col, f, b_lo, n_lo, in_lo, b_hi, n_hi, in_hi, t);
+    SW_LAUNCHED();
+    return SWARM_OK;
 }
 
 int frontier_round_totals(swarm_ctx *ctx, int t0, int t1, unsigned long long *dtot, hipStream_t s) {
@@ -624,22 +849,6 @@ int swarm_frontier_begin(swarm_ctx *ctx, int64_t n_rows, int64_t n_all, const in
         SW_HIP(hipMemcpyAsync(leader0, init, size_t(n_all) * 4, hipMemcpyDeviceToDevice, s));
         SW_HIP(hipMemcpyAsync(leader1, init, size_t(n_all) * 4, hipMemcpyDeviceToDevice, s));
     }
-    ctx->step_rows = n_rows;
-    ctx->step_all = n_all;
-    return SWARM_OK;
-}
-
-static int stepper_state(swarm_ctx *ctx, int32_t *leader0, int32_t *leader1, swarm::Frontier *f) {
-    using namespace swarm;
-    SW_ARG(ctx->slot[S_ACT] != nullptr && ctx->slot[S_CHANGES] != nullptr, "swarm_frontier_begin first");
-    const size_t na = size_t(ctx->step_all) + 16;
-    f->L[0] = leader0;
-    f->L[1] = leader1;
-    f->act[0] = static_cast<uint8_t *>(ctx->slot[S_ACT]);
-    f->act[1] = f->act[0] + na;
-    f->ring = static_cast<unsigned long long *>(ctx->slot[S_CHANGES]);
-    f->tot = f->ring + size_t(kRing) * kCounters * kRoundWords;
-    f->n_rows = ctx->step_rows;
     return SWARM_OK;
 }
 
@@ -650,10 +859,7 @@ int swarm_frontier_step(swarm_ctx *ctx, int32_t t, const int32_t *row_ptr, const
     SW_ARG(t >= 1, "round must be >= 1");
     if (ctx->step_rows == 0) return SWARM_OK;
     SW_ARG(row_ptr && leader0 && leader1, "NULL array");
-    Frontier f{};
-    int rc = stepper_state(ctx, leader0, leader1, &f);
-    if (rc) return rc;
-    return launch_frontier_round<int32_t>(row_ptr, col, f, t, 0, /*guard=*/0, static_cast<hipStream_t>(stream));
+    return frontier_round_stepper(ctx, t, row_ptr, col, leader0, leader1, -1, static_cast<hipStream_t>(stream));
 }
 
 int swarm_frontier_ghosts(swarm_ctx *ctx, int32_t t, int64_t begin, int64_t count,
@@ -664,15 +870,17 @@ int swarm_frontier_ghosts(swarm_ctx *ctx, int32_t t, int64_t begin, int64_t coun
     SW_ARG(begin >= 0 && count >= 0 && begin + count <= ctx->step_all, "ghost range out of bounds");
     if (count == 0) return SWARM_OK;
     SW_ARG(incoming && row_ptr && leader0 && leader1, "NULL array");
-    Frontier f{};
-    int rc = stepper_state(ctx, leader0, leader1, &f);
-    if (rc) return rc;
-    hipLaunchKernelGGL((k_frontier_ghosts<8, int32_t>), dim3(grid_for(count, kBlock / 8, 2048)), dim3(kBlock), 0,
-                       static_cast<hipStream_t>(stream), row_ptr, col, leader0, leader1,
-                       f.act[(t + 1) & 1], begin, count, incoming, t);
-    SW_LAUNCHED();
+    return frontier_ghosts_both(ctx, t, row_ptr, col, begin, count, incoming, ctx->step_all, 0, nullptr, leader0,
+                                leader1, static_cast<hipStream_t>(stream));
+}
+
+#ifdef SWARM_PHASES
+int swarm_debug_phases(unsigned long long *out, int count) {
+    SW_HIP(hipDeviceSynchronize());
+    SW_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(swarm::g_phase), size_t(count) * 8));
     return SWARM_OK;
 }
+#endif
 
 int swarm_frontier_changes(swarm_ctx *ctx, int32_t t0, int32_t t1, int64_t *out, void *stream) {
     using namespace swarm;
@@ -690,7 +898,7 @@ int swarm_frontier_changes(swarm_ctx *ctx, int32_t t0, int32_t t1, int64_t *out,
     if (!h) return SWARM_ERR_OOM;
     SW_HIP(hipMemcpyAsync(h, dtot, size_t(nr) * kCounters * 8, hipMemcpyDeviceToHost, s));
     SW_HIP(hipStreamSynchronize(s));
-    for (int i = 0; i < nr; ++i) out[i] = int64_t(h[size_t(i) * kCounters]);
+    for (int i = 0; i < nr; ++i) out[i] = int64_t(h[size_t(i) * kCounters + C_CHG]);
     return SWARM_OK;
 }
 
@@ -707,7 +915,7 @@ int swarm_elect_round(swarm_ctx *ctx, int64_t n_rows, const int32_t *row_ptr,
     unsigned long long *ring;
     SW_ALLOC(ring, ctx, S_TMP0, size_t(kCounters) * kRoundWords * 8);
     SW_HIP(hipMemsetAsync(ring, 0, size_t(kRoundWords) * 8, s));
-    int rc = launch_dense_round<int32_t>(row_ptr, col, leader_in, leader_out, n_rows, ring, 0, 0, s);
+    int rc = launch_dense_round<int32_t>(row_ptr, col, leader_in, leader_out, n_rows, ring, nullptr, nullptr, 0, 0, s);
     if (rc) return rc;
     hipLaunchKernelGGL(k_sum_shards, dim3(1), dim3(kWave), 0, s, ring, 0,
                        reinterpret_cast<unsigned long long *>(changed));

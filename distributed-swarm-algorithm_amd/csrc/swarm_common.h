@@ -14,14 +14,15 @@ namespace swarm {
 
 constexpr int kBlock = 256;   // threads per workgroup: 4 waves of 64
 constexpr int kWave = 64;
+constexpr int kElectCounters = 4;  // per-round election counters (elect.hip C_CHG..C_GHOST)
 
 void set_error(const char *fmt, ...);
 
 // Scratch slots owned by a ctx; each grows on demand (never shrinks until destroy).
 enum Slot {
     S_LEADER_B = 0,   // election: second leader buffer (dense)
-    S_ACT,            // election: per-agent activity stamp (frontier)
-    S_LIST,           // election: changed (agent, value) list (frontier)
+    S_ACT,            // election: per-agent append stamp (frontier)
+    S_LIST,           // election: change lists, both round parities (frontier)
     S_CHANGES,        // election: per-round change counters (device)
     S_ESTATS,         // election: per-round active/edge counters (device)
     S_KEYS_IN,        // binning: cell keys
@@ -49,7 +50,7 @@ struct swarm_ctx {
     size_t cap[swarm::S_NUM] = {};
     void *host_pinned = nullptr;   // small pinned staging buffer for scalar/array readback
     size_t host_cap = 0;
-    int64_t step_rows = 0;         // frontier stepper: rows gathered / agents (rows + ghosts)
+    int64_t step_rows = 0;         // frontier stepper: owned rows / agents (rows + ghosts)
     int64_t step_all = 0;
 };
 

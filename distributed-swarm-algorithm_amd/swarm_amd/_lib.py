@@ -47,7 +47,8 @@ class ElectStats(ctypes.Structure):
     _fields_ = [("rounds_launched", ctypes.c_int64), ("active_total", ctypes.c_int64),
                 ("edges_total", ctypes.c_int64), ("changes_total", ctypes.c_int64),
                 ("gather_ms", ctypes.c_double), ("apply_ms", ctypes.c_double),
-                ("gather_launches", ctypes.c_int64)]
+                ("gather_launches", ctypes.c_int64), ("dense_rounds", ctypes.c_int64),
+                ("bytes_total", ctypes.c_double)]
 
 
 class Shard(ctypes.Structure):

@@ -50,8 +50,10 @@ class ElectResult:
     state: torch.Tensor                 # uint8 [n], storage order (1 FOLLOWER, 3 LEADER)
     converged: bool = True
     rounds_launched: int = 0
-    active_total: int = 0               # agents that gathered, summed over rounds
-    edges_total: int = 0                # neighbour reads, summed over rounds
+    active_total: int = 0               # agents gathered (dense: all, sparse: marked), summed over rounds
+    edges_total: int = 0                # CSR edges visited, summed over rounds
+    dense_rounds: int = 0               # rounds run as a full dense sweep
+    bytes_total: float = 0.0            # algorithmic HBM bytes of rounds 1..rounds_exec
 
 
 @dataclass
@@ -163,7 +165,8 @@ class Swarm:
                 changes.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st), _lib.stream()))
         r = rounds.value
         res = ElectResult(r, changes[:r].copy(), self.leader, self.state, rc == _lib.OK,
-                          st.rounds_launched, st.active_total, st.edges_total)
+                          st.rounds_launched, st.active_total, st.edges_total, st.dense_rounds,
+                          st.bytes_total)
         res.changes_total = st.changes_total
         res.gather_ms, res.apply_ms, res.timed_launches = st.gather_ms, st.apply_ms, st.gather_launches
         return res

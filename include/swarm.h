@@ -46,7 +46,8 @@ extern "C" {
 /* Election execution strategies.  Both are exact: identical leaders, states, rounds_exec
  * and per-round change counts. */
 #define SWARM_ELECT_DENSE 0    /* every agent gathers every round (Jacobi sweep) */
-#define SWARM_ELECT_FRONTIER 1 /* only neighbours of last round's changed agents gather */
+#define SWARM_ELECT_FRONTIER 1 /* dense sweeps while many agents change, then only the agents
+                                  marked by last round's risers gather (sparse rounds) */
 #define SWARM_ELECT_TIMED 0x100 /* OR into mode: time every kernel with HIP events (stats) */
 
 /* Allocation execution strategies (all exact). */
@@ -67,12 +68,14 @@ typedef struct swarm_alloc_stats {
 
 typedef struct swarm_elect_stats {
     int64_t rounds_launched; /* rounds issued (>= rounds_exec; extra ones are no-ops) */
-    int64_t active_total;    /* agents that gathered, summed over rounds */
-    int64_t edges_total;     /* neighbour reads, summed over rounds */
+    int64_t active_total;    /* agents gathered (DENSE: all; SPARSE: marked), rounds 1..rounds_exec */
+    int64_t edges_total;     /* CSR edges visited, summed over rounds 1..rounds_exec */
     int64_t changes_total;   /* leader changes, summed over rounds */
-    double gather_ms;        /* SWARM_ELECT_TIMED: summed device time of the gather kernel */
-    double apply_ms;         /* SWARM_ELECT_TIMED: summed device time of the apply kernel */
-    int64_t gather_launches; /* launches behind gather_ms / apply_ms (rounds 1..rounds_exec) */
+    double gather_ms;        /* SWARM_ELECT_TIMED: summed device time of the round kernels */
+    double apply_ms;         /* always 0 (one kernel per round); kept for layout stability */
+    int64_t gather_launches; /* launches behind gather_ms (rounds 1..rounds_exec) */
+    int64_t dense_rounds;    /* rounds executed as a full DENSE sweep */
+    double bytes_total;      /* algorithmic HBM bytes of rounds 1..rounds_exec */
 } swarm_elect_stats;
 
 const char *swarm_last_error(void);
@@ -123,11 +126,12 @@ int swarm_elect_round(swarm_ctx *ctx, int64_t n_rows, const int32_t *row_ptr,
  * Leaders are double-buffered by round parity: round t reads leader[(t-1)&1] and writes
  * leader[t&1], so after round t the current state is leader[t&1] (leader0 / leader1, both
  * n_all, owned by the caller).
- *   begin:   leader0 = leader1 = init; every agent active for round 1.
- *   step:    round t over the owned rows (no convergence guard: a shard with no local change
+ *   begin:   leader0 = leader1 = init; round 1 is a full dense sweep.
+ *   step:    round t over the owned rows (dense or sparse, decided on the device from round
+ *            t-1's changes + ghost rises; no convergence guard: a shard with no local change
  *            can still receive ghost changes).  Owned changes are counted per round.
  *   ghosts:  after the halo exchange of round t, incoming[i] is the round-t leader of ghost
- *            begin+i; rises are written to both buffers and their neighbours activated for
+ *            begin+i; rises are written to both buffers and their local neighbours marked for
  *            round t+1.
  *   changes: per-round owned change counts of rounds t0..t1 (t1 - t0 < 256); host sync.
  *            Read at least every 256 rounds (counter slots are recycled).
