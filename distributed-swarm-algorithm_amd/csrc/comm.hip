@@ -90,7 +90,7 @@ __global__ __launch_bounds__(kBlock) void k_pack(const int32_t *__restrict__ L, 
 // the frontier round launcher lives in elect.hip
 namespace swarm {
 int frontier_round_stepper(swarm_ctx *ctx, int t, const int32_t *rp, const int32_t *col, int32_t *L0,
-                           int32_t *L1, int64_t last_changes, hipStream_t s);
+                           int32_t *L1, hipStream_t s);
 int frontier_ghosts_both(swarm_ctx *ctx, int t, const int32_t *rp, const int32_t *col, int64_t b_lo, int64_t n_lo,
                          const int32_t *in_lo, int64_t b_hi, int64_t n_hi, const int32_t *in_hi, int32_t *L0,
                          int32_t *L1, hipStream_t s);
@@ -171,12 +171,10 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sh,
     if (!h) return SWARM_ERR_OOM;
     const Rccl &R = rccl();
     int found = -1, t = 1, batch = 8;
-    int64_t last_changes = -1;  // newest global change count read (picks the sparse kernel)
     while (t <= max_rounds && found < 0) {
         const int tend = std::min(max_rounds, t + batch - 1);
         for (int r = t; r <= tend; ++r) {
-            if ((rc = frontier_round_stepper(ctx, r, sh->row_ptr, sh->col, leader0, leader1, last_changes, s)))
-                return rc;
+            if ((rc = frontier_round_stepper(ctx, r, sh->row_ptr, sh->col, leader0, leader1, s))) return rc;
             int32_t *Lcur = (r & 1) ? leader1 : leader0;
             const int64_t ns = sh->n_send_lo + sh->n_send_hi;
             if (ns) {
@@ -206,7 +204,6 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sh,
         for (int r = t; r <= tend; ++r) {
             const unsigned long long c = h[size_t(r - t) * kC];  // C_CHG: owned changes
             if (changes_host) changes_host[r - 1] = int64_t(c);
-            last_changes = int64_t(c);
             if (c == 0) {
                 found = r;
                 break;

@@ -19,9 +19,9 @@
 // (every batch of rounds):
 //   k_elect_dense<MARK=false>  the first dense_rounds-1 rounds (nearly every agent changes)
 //   k_elect_dense<MARK=true>   the last dense round: also marks the risers' neighbourhoods
-//   k_sparse_block             2048-agent chunk per workgroup: stamps -> LDS list -> gather
-//   k_sparse_wave              late rounds (few marks): 512-agent chunks per wave, grid =
-//                              resident waves, next chunk's stamps loaded ahead, no barriers
+//   k_sparse_block             2048-agent chunk per workgroup (grid = resident workgroups,
+//                              next chunk's stamps loaded ahead): stamps -> LDS list -> gather,
+//                              4 lanes per marked agent with interleaved edges
 // Marks are plain byte stores, no atomics: stamp act[v] = t+1 (mod 256), double-buffered by
 // round parity and consumed (zeroed) by the sparse round that reads them.  Leaders alternate by
 // parity: round t reads L[(t-1)&1] and writes L[t&1], which still holds the state after t-2; it
@@ -36,8 +36,9 @@
 //
 // Measured and rejected: a push variant (risers atomicMax their value into the
 // neighbours: scattered device-scope atomics run at ~20 G/s), dense and sparse paths fused in
-// one kernel (register pressure: 6 instead of 8 waves per SIMD, +10 %), one lane per marked
-// agent or 16 lanes per agent over 1024-agent units (+40 % / +130 %).
+// one kernel (register pressure: 6 instead of 8 waves per SIMD, +10 %), per-wave chunks with no
+// workgroup barrier (+6..30 %), 1 / 8 / 16 lanes per marked agent (+33..65 %), contiguous
+// instead of interleaved edge slices per lane (+14 %).
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
@@ -222,7 +223,6 @@ __global__ __launch_bounds__(kBlock) void k_elect_dense(
 // ------------------------------------------------------------------ sparse rounds
 constexpr int kScan = 8;                 // stamps per thread (one 8-B load)
 constexpr int kChunk = kBlock * kScan;   // k_sparse_block: agents per workgroup work unit
-constexpr int kWChunk = kWave * kScan;   // k_sparse_wave: agents per wave work unit
 constexpr int kG = 4;                    // lanes per marked agent
 constexpr int kKs = 8;                   // loads in flight per lane
 
@@ -233,44 +233,46 @@ struct Frontier {
     int64_t n_rows, n_all;
 };
 
-// Gather of the marked agents listed (chunk-relative) in lst[0, total), kG lanes per agent,
-// `first`/`step` select this wave's share; risers mark themselves and their neighbours.
-template <typename Off>
+// Gather of the marked agents listed (chunk-relative) in lst[0, total), G lanes per agent,
+// `first`/`step` select this wave's share; risers mark themselves and their neighbours.  Lane
+// `sub` of an agent takes edges b + sub + G*j (interleaved: one load instruction covers G
+// consecutive edges of every agent it serves, so each touches one cache line per agent).
+template <typename Off, int G, int K>
 __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, const int32_t *__restrict__ col,
                                               const int32_t *__restrict__ P, int32_t *__restrict__ Q,
                                               uint8_t *__restrict__ aw, uint8_t sw, int64_t c0, const int *lst,
                                               int total, int first, int step, long long &my_chg,
                                               long long &my_act, long long &my_edges) {
-    const int lane = threadIdx.x & 63, sub = lane & (kG - 1);
+    const int lane = threadIdx.x & 63, sub = lane & (G - 1);
     for (int base = first; base < total; base += step) {
-        const int i = base + lane / kG;
+        const int i = base + lane / G;
         const bool valid = i < total;
         const int64_t v = c0 + lst[valid ? i : total - 1];
         const Off b = rp[v], e = rp[v + 1];
         const int own = P[v];
         int m = own;
-        int c[kKs];
-        for (Off k = b + sub * kKs; k < e; k += kG * kKs) {
+        int c[K];
+        for (Off k = b + sub; k < e; k += G * K) {
 #pragma unroll
-            for (int j = 0; j < kKs; ++j) c[j] = col[(k + j < e) ? k + j : e - 1];
-            int val[kKs];
+            for (int j = 0; j < K; ++j) c[j] = col[(k + G * j < e) ? k + G * j : e - 1];
+            int val[K];
 #pragma unroll
-            for (int j = 0; j < kKs; ++j) val[j] = P[c[j]];
+            for (int j = 0; j < K; ++j) val[j] = P[c[j]];
 #pragma unroll
-            for (int j = 0; j < kKs; ++j) m = max(m, val[j]);
+            for (int j = 0; j < K; ++j) m = max(m, val[j]);
         }
 #pragma unroll
-        for (int o2 = 1; o2 < kG; o2 <<= 1) m = max(m, __shfl_xor(m, o2, 64));
+        for (int o2 = 1; o2 < G; o2 <<= 1) m = max(m, __shfl_xor(m, o2, 64));
         const bool up = valid && m > own;
         if (valid && sub == 0) Q[v] = m;
         if (up) {
             if (sub == 0) aw[v] = sw;
-            if (e - b <= kG * kKs) {  // one pass per lane: c[] still holds this lane's edges
+            if (e - b <= G * K) {  // one pass: c[] still holds this lane's edges
 #pragma unroll
-                for (int j = 0; j < kKs; ++j)
-                    if (b + sub * kKs + j < e) aw[c[j]] = sw;
+                for (int j = 0; j < K; ++j)
+                    if (b + sub + G * j < e) aw[c[j]] = sw;
             } else {
-                mark_row<Off>(aw, col, b + sub, e, Off(kG), sw);
+                mark_row<Off>(aw, col, b + sub, e, Off(G), sw);
             }
         }
         my_chg += __popcll(__ballot(up && sub == 0));
@@ -313,7 +315,7 @@ __device__ __forceinline__ void flush_counts(unsigned long long *ring, int t, lo
 
 // One workgroup per 2048-agent chunk: 8 stamps per thread, the chunk's marked agents compacted
 // in LDS and gathered by the whole workgroup.
-template <typename Off>
+template <typename Off, int G = kG, int K = kKs>
 __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_block(
     const Off *__restrict__ rp, const int32_t *__restrict__ col, Frontier f, int t, int guard) {
     __shared__ int s_list[kChunk];
@@ -331,15 +333,15 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
     const int64_t n = f.n_rows;
     long long my_chg = 0, my_act = 0, my_edges = 0;
     const int64_t nchunks = (n + kChunk - 1) / kChunk;
-    const int64_t G = gridDim.x;
+    const int64_t NG = gridDim.x;
     uint2 nxt = make_uint2(0u, 0u);  // stamps are padded past n_all; the next chunk's are loaded ahead
     if (int64_t(blockIdx.x) < nchunks)
         nxt = *reinterpret_cast<const uint2 *>(ar + int64_t(blockIdx.x) * kChunk + int64_t(threadIdx.x) * kScan);
-    for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += G) {
+    for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += NG) {
         const int64_t c0 = chunk * kChunk;
         const int64_t v0 = c0 + int64_t(threadIdx.x) * kScan;
         const uint2 wv = nxt;
-        if (chunk + G < nchunks) nxt = *reinterpret_cast<const uint2 *>(ar + v0 + G * kChunk);
+        if (chunk + NG < nchunks) nxt = *reinterpret_cast<const uint2 *>(ar + v0 + NG * kChunk);
         unsigned mask = take_stamps(ar, v0, n, wv, stamp4);
         const int cnt = __popc(mask);
         int incl = cnt;
@@ -364,68 +366,12 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
                 s_list[pos++] = threadIdx.x * kScan + j;
             }
             __syncthreads();
-            gather_listed<Off>(rp, col, P, Q, aw, sw, c0, s_list, total, wid * (64 / kG), kBlock / kG, my_chg,
-                               my_act, my_edges);
+            gather_listed<Off, G, K>(rp, col, P, Q, aw, sw, c0, s_list, total, wid * (64 / G), kBlock / G, my_chg,
+                                     my_act, my_edges);
         }
         __syncthreads();  // LDS (s_wave, s_list) reused by the next chunk
     }
     flush_counts(f.ring, t, my_chg, my_act, my_edges, s_red);
-}
-
-// Late rounds: 512-agent chunks dealt to waves (grid-stride over exactly the resident waves),
-// the next chunk's stamps loaded ahead; each wave compacts and gathers its own chunk's marked
-// agents, with no workgroup barrier until the final counter flush.
-template <typename Off>
-__global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_wave(
-    const Off *__restrict__ rp, const int32_t *__restrict__ col, Frontier f, int t, int guard) {
-    __shared__ int s_list[kWavesPerBlock][kWChunk];
-    __shared__ long long s_red[3][kWavesPerBlock];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    bookkeeping(f.ring, f.tot, t);
-    if (guard && t > 2 && f.tot[(t - 2) % kRing] == 0) return;
-    PHASE(0);
-    const int32_t *__restrict__ P = f.L[(t - 1) & 1];
-    int32_t *__restrict__ Q = f.L[t & 1];
-    uint8_t *ar = f.act[t & 1], *aw = f.act[(t + 1) & 1];
-    const unsigned stamp4 = unsigned(t & 0xFF) * 0x01010101u;
-    const uint8_t sw = uint8_t((t + 1) & 0xFF);
-    const int64_t n = f.n_rows;
-    long long my_chg = 0, my_act = 0, my_edges = 0;
-    const int64_t nwc = (n + kWChunk - 1) / kWChunk;
-    const int64_t W = int64_t(gridDim.x) * kWavesPerBlock;
-    int *lst = s_list[wid];
-    int64_t wc = int64_t(blockIdx.x) * kWavesPerBlock + wid;
-    uint2 nxt = make_uint2(0u, 0u);  // stamps are padded past n_all
-    if (wc < nwc) nxt = *reinterpret_cast<const uint2 *>(ar + wc * kWChunk + int64_t(lane) * kScan);
-    for (; wc < nwc; wc += W) {
-        const int64_t c0 = wc * kWChunk;
-        const int64_t v0 = c0 + int64_t(lane) * kScan;
-        const uint2 wv = nxt;
-        if (wc + W < nwc) nxt = *reinterpret_cast<const uint2 *>(ar + v0 + W * kWChunk);
-        unsigned mask = take_stamps(ar, v0, n, wv, stamp4);
-        const int cnt = __popc(mask);
-        int incl = cnt;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int x = __shfl_up(incl, off, 64);
-            if (lane >= off) incl += x;
-        }
-        const int total = __shfl(incl, 63, 64);
-        if (total == 0) continue;  // wave-uniform
-        int pos = incl - cnt;
-        while (mask) {
-            const int j = __ffs(mask) - 1;
-            mask &= mask - 1;
-            lst[pos++] = lane * kScan + j;
-        }
-        __builtin_amdgcn_wave_barrier();
-        gather_listed<Off>(rp, col, P, Q, aw, sw, c0, lst, total, 0, 64 / kG, my_chg, my_act, my_edges);
-        __builtin_amdgcn_wave_barrier();  // lst reused by the next chunk
-        PHASE(1);
-    }
-    PHASE(2);
-    flush_counts(f.ring, t, my_chg, my_act, my_edges, s_red);
-    PHASE(3);
 }
 
 // Sharded runs: halo values for ghosts [b_lo, b_lo + n_lo) and [b_hi, b_hi + n_hi) after round
@@ -504,16 +450,14 @@ int env_int(const char *name, int dflt) {
 struct Tuning {
     int dense_blocks = 2048;  // grid cap of the dense round kernel
     int dense_rounds = 8;     // frontier: rounds 1..dense_rounds run dense (the last one marks)
-    int wave_div = 0;         // frontier: k_sparse_wave once last known changes * wave_div <= n
-                              // (0 = never: measured slower than k_sparse_block at 10M agents)
     int sparse_blocks = 2048; // grid cap of k_sparse_block (8 resident workgroups per CU)
     Tuning() {
         dense_blocks = env_int("SWARM_DENSE_BLOCKS", 2048);
         dense_rounds = env_int("SWARM_DENSE_ROUNDS", 8);
-        wave_div = env_int("SWARM_WAVE_DIV", 0);
         sparse_blocks = env_int("SWARM_SPARSE_BLOCKS", 2048);
         if (dense_blocks < 1) dense_blocks = 1;
         if (dense_rounds < 0) dense_rounds = 0;
+        if (sparse_blocks < 1) sparse_blocks = 1;
     }
 };
 
@@ -541,22 +485,6 @@ int launch_dense_round(const Off *rp, const int32_t *col, const int32_t *lin, in
                            tot, act_w, t, guard);
     SW_LAUNCHED();
     return SWARM_OK;
-}
-
-// Workgroups of k_sparse_wave<Off> resident at once (its waves must all run together).
-template <typename Off>
-unsigned resident_blocks() {
-    static unsigned cached = 0;
-    if (!cached) {
-        int dev = 0, cus = 0, per_cu = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_sparse_wave<Off>, kBlock, 0) != hipSuccess ||
-            cus <= 0 || per_cu <= 0)
-            return 2048u;
-        cached = unsigned(cus) * unsigned(per_cu);
-    }
-    return cached;
 }
 
 // Frontier view of the ctx slots for n_rows owned agents of n_all.
@@ -593,16 +521,15 @@ int frontier_alloc(swarm_ctx *ctx, int64_t n_rows, int64_t n_all, int32_t *L0, i
     return SWARM_OK;
 }
 
-enum RoundKind { RK_DENSE = 0, RK_DENSE_MARK = 1, RK_SPARSE_BLOCK = 2, RK_SPARSE_WAVE = 3 };
+enum RoundKind { RK_DENSE = 0, RK_DENSE_MARK = 1, RK_SPARSE = 2 };
 
-// Kind of frontier round t given the last change count the host has read (-1: unknown).
-RoundKind plan_round(int t, int64_t n, int64_t last_changes) {
+// Kind of frontier round t: the first dense_rounds rounds dense (nearly every agent changes;
+// measured best at 8 for 10M agents), the last of them marking, then sparse.
+RoundKind plan_round(int t) {
     const int R = tuning().dense_rounds;
     if (t < R) return RK_DENSE;
     if (t == R) return RK_DENSE_MARK;
-    if (tuning().wave_div > 0 && last_changes >= 0 && last_changes * int64_t(tuning().wave_div) <= n)
-        return RK_SPARSE_WAVE;
-    return RK_SPARSE_BLOCK;
+    return RK_SPARSE;
 }
 
 template <typename Off>
@@ -611,15 +538,9 @@ int launch_frontier_round(const Off *rp, const int32_t *col, const Frontier &f, 
     if (k == RK_DENSE || k == RK_DENSE_MARK)
         return launch_dense_round<Off>(rp, col, f.L[(t - 1) & 1], f.L[t & 1], f.n_rows, f.ring, f.tot,
                                        k == RK_DENSE_MARK ? f.act[(t + 1) & 1] : nullptr, t, guard, s);
-    if (k == RK_SPARSE_WAVE) {
-        const unsigned grid = grid_for((f.n_rows + kWChunk - 1) / kWChunk, kWavesPerBlock, resident_blocks<Off>());
-        hipLaunchKernelGGL((k_sparse_wave<Off>), dim3(grid), dim3(kBlock), 0, s, rp, col, f, t, guard);
-    } else {
-        const int64_t nchunks = (f.n_rows + kChunk - 1) / kChunk;
-        const unsigned cap = tuning().sparse_blocks > 0 ? unsigned(tuning().sparse_blocks) : (1u << 20);
-        hipLaunchKernelGGL((k_sparse_block<Off>), dim3(grid_for(nchunks, 1, cap)), dim3(kBlock), 0, s, rp, col, f, t,
-                           guard);
-    }
+    const int64_t nchunks = (f.n_rows + kChunk - 1) / kChunk;
+    hipLaunchKernelGGL((k_sparse_block<Off>), dim3(grid_for(nchunks, 1, unsigned(tuning().sparse_blocks))), dim3(kBlock),
+                       0, s, rp, col, f, t, guard);
     SW_LAUNCHED();
     return SWARM_OK;
 }
@@ -681,7 +602,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     SW_ALLOC(dtot, ctx, S_ESTATS, size_t(kCounters) * 8 * kMaxBatch);
 
     int found = -1, t = 1, batch = 8, launched = 0;
-    int64_t act_sum = 0, edge_sum = 0, chg_sum = 0, dense_rounds = 0, last_changes = -1;
+    int64_t act_sum = 0, edge_sum = 0, chg_sum = 0, dense_rounds = 0;
     double bytes = 0.0;
     std::vector<RoundKind> kinds(kMaxBatch);
     // optional per-round timing: events before and after every round kernel
@@ -713,7 +634,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
                 rc = launch_dense_round<Off>(rp, col, bufs[(r - 1) & 1], bufs[r & 1], n, ring, nullptr, nullptr, r,
                                              1, s);
             } else {
-                kinds[r - t] = plan_round(r, n, last_changes);
+                kinds[r - t] = plan_round(r);
                 rc = launch_frontier_round<Off>(rp, col, f, r, kinds[r - t], 1, s);
             }
             if (rc) return rc;
@@ -737,7 +658,6 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
             chg_sum += c;
             dense_rounds += dn ? 1 : 0;
             bytes += round_bytes(dn, n, int64_t(e_total), act, ed);
-            last_changes = c;
             float x = 0;
             if (timed) {
                 SW_HIP(hipEventElapsedTime(&x, ev[2 * (r - t)], ev[2 * (r - t) + 1]));
@@ -780,16 +700,15 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
 
 }  // namespace
 
-// Internal entry points for comm.hip (the RCCL round loop): one stepper round (last_changes =
-// the newest global change count the caller has read, -1 if none), the ghost update of both
-// borders, and the device per-round totals (kCounters each) of rounds t0..t1.
+// Internal entry points for comm.hip (the RCCL round loop): one stepper round, the ghost update
+// of both borders, and the device per-round totals (kCounters each) of rounds t0..t1.
 int frontier_round_stepper(swarm_ctx *ctx, int t, const int32_t *rp, const int32_t *col, int32_t *L0,
-                           int32_t *L1, int64_t last_changes, hipStream_t s) {
+                           int32_t *L1, hipStream_t s) {
     Frontier f{};
     int rc = frontier_bind(ctx, L0, L1, &f);
     if (rc) return rc;
     if (f.n_rows == 0) return SWARM_OK;
-    return launch_frontier_round<int32_t>(rp, col, f, t, plan_round(t, f.n_rows, last_changes), /*guard=*/0, s);
+    return launch_frontier_round<int32_t>(rp, col, f, t, plan_round(t), /*guard=*/0, s);
 }
 
 int frontier_ghosts_both(swarm_ctx *ctx, int t, const int32_t *rp, const int32_t *col, int64_t b_lo, int64_t n_lo,
@@ -859,7 +778,7 @@ int swarm_frontier_step(swarm_ctx *ctx, int32_t t, const int32_t *row_ptr, const
     SW_ARG(t >= 1, "round must be >= 1");
     if (ctx->step_rows == 0) return SWARM_OK;
     SW_ARG(row_ptr && leader0 && leader1, "NULL array");
-    return frontier_round_stepper(ctx, t, row_ptr, col, leader0, leader1, -1, static_cast<hipStream_t>(stream));
+    return frontier_round_stepper(ctx, t, row_ptr, col, leader0, leader1, static_cast<hipStream_t>(stream));
 }
 
 int swarm_frontier_ghosts(swarm_ctx *ctx, int32_t t, int64_t begin, int64_t count,
