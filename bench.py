@@ -46,6 +46,27 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def pmc_traffic(kernel_prefix):
+    """HBM bytes per dispatch of a kernel from the newest committed rocprofv3 --pmc summary
+    (profiles/*/pmc_traffic.json, written by tools/gpu_pmc.sh + tools/pmc_summary.py: FETCH_SIZE
+    and WRITE_SIZE in separate passes, FETCH_SIZE doubled for gfx950).  bench.py cannot collect
+    PMC counters itself (that needs rocprofv3 around the process), so it reports the measured
+    figure of the same command with its source, or None."""
+    import glob
+    best = None
+    for path in glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        for k, v in d.items():
+            if k.startswith(kernel_prefix) and isinstance(v, dict):
+                m = path  # newest = last in name order (profiles/r1, r1_hybrid, r2, ...)
+                if best is None or m > best[2]:
+                    best = (v["hbm_bytes_per_dispatch"], os.path.relpath(path, ROOT), m)
+    return None if best is None else (best[0], f"rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE, {best[1]}")
+
+
 def main():
     args = parse()
     import torch
@@ -124,18 +145,19 @@ def main():
     t_elect_ms, t_alloc_ms = ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])
 
     # ---- per-kernel device time of the election (HIP events recorded by libswarm around every
-    # launch on the stream it launches on), one instrumented replay
+    # launch on the stream it launches on), one instrumented replay.  The dominant kernel is the
+    # sparse round (k_sparse_block); like rocprof, its average covers every launch, including the
+    # no-op rounds a batch issues after convergence.
     rt = sw.elect(mode=args.elect_mode, max_rounds=1 << 16, timed=True)
-    launches = max(rt.timed_launches, 1)
-    if args.elect_mode == "frontier":
-        # k_frontier_round algorithmic bytes, summed by libswarm from the per-round counters
-        # (DESIGN.md §4): dense rounds 12N + 8E + 4; sparse rounds N (stamps) + 16/marked agent
-        # + 8/edge
-        dom = {"kernel": "k_frontier_round (E2 round: dense sweep / marked-agent sparse gather)",
-               "bytes_per_launch": rt.bytes_total / launches,
-               "avg_launch_ms": rt.gather_ms / launches, "launches": launches,
-               "dense_rounds": rt.dense_rounds, "sparse_rounds": launches - rt.dense_rounds,
-               "edges_total": rt.edges_total}
+    if args.elect_mode == "frontier" and rt.sparse_launches:
+        pmc = pmc_traffic("k_sparse_block")
+        dom = {"kernel": "k_sparse_block (sparse E2 round: marked agents gather)",
+               "bytes_per_launch": rt.sparse_bytes / rt.sparse_launches,
+               "avg_launch_ms": rt.sparse_ms / rt.sparse_launches, "launches": rt.sparse_launches,
+               "traffic": pmc[0] if pmc else None, "traffic_source": pmc[1] if pmc else None,
+               "all_rounds": {"bytes_per_launch": rt.bytes_total / max(rt.timed_launches, 1),
+                              "avg_launch_ms": rt.gather_ms / max(rt.timed_launches, 1),
+                              "launches": rt.timed_launches, "dense_rounds": rt.dense_rounds}}
     else:
         dom = None
 
@@ -189,7 +211,7 @@ def main():
                           "achieved": dom["bytes_per_launch"] / (dom["avg_launch_ms"] * 1e-3) / 1e9,
                           "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": dom["bytes_per_launch"] / (dom["avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                          "traffic": None, **{k: v for k, v in dom.items() if k != "kernel"}}
+                          **{k: v for k, v in dom.items() if k != "kernel"}}
                          if dom else
                          {"kernel": "k_elect_dense (one E2 round)", "bound": "hbm",
                           "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

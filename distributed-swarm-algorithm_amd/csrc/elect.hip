@@ -602,9 +602,10 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     SW_ALLOC(dtot, ctx, S_ESTATS, size_t(kCounters) * 8 * kMaxBatch);
 
     int found = -1, t = 1, batch = 8, launched = 0;
-    int64_t act_sum = 0, edge_sum = 0, chg_sum = 0, dense_rounds = 0;
-    double bytes = 0.0;
+    int64_t act_sum = 0, edge_sum = 0, chg_sum = 0, dense_rounds = 0, sp_launches = 0;
+    double bytes = 0.0, sp_bytes = 0.0, sp_ms = 0.0;
     std::vector<RoundKind> kinds(kMaxBatch);
+    std::vector<float> ktime(kMaxBatch);
     // optional per-round timing: events before and after every round kernel
     std::vector<hipEvent_t> ev;
     double k_ms = 0;
@@ -646,6 +647,18 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         SW_LAUNCHED();
         SW_HIP(hipMemcpyAsync(hbuf, dtot, size_t(tend - t + 1) * kCounters * 8, hipMemcpyDeviceToHost, s));
         SW_HIP(hipStreamSynchronize(s));
+        for (int r = t; r <= tend; ++r) {  // every launched round's kernel time (rocprof's view)
+            if (!timed) break;
+            float x = 0;
+            SW_HIP(hipEventElapsedTime(&x, ev[2 * (r - t)], ev[2 * (r - t) + 1]));
+            k_ms += x;
+            ++timed_rounds;
+            if (kinds[r - t] == RK_SPARSE) {
+                sp_ms += x;
+                ++sp_launches;
+            }
+            ktime[r - t] = x;
+        }
         for (int r = t; r <= tend; ++r) {
             const unsigned long long *rb = hbuf + size_t(r - t) * kCounters;
             const int64_t c = int64_t(rb[C_CHG]);
@@ -657,16 +670,12 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
             edge_sum += ed;
             chg_sum += c;
             dense_rounds += dn ? 1 : 0;
-            bytes += round_bytes(dn, n, int64_t(e_total), act, ed);
-            float x = 0;
-            if (timed) {
-                SW_HIP(hipEventElapsedTime(&x, ev[2 * (r - t)], ev[2 * (r - t) + 1]));
-                k_ms += x;
-                ++timed_rounds;
-            }
+            const double rbytes = round_bytes(dn, n, int64_t(e_total), act, ed);
+            bytes += rbytes;
+            if (kinds[r - t] == RK_SPARSE) sp_bytes += rbytes;
             if (rlog)
                 fprintf(rlog, "%d %lld %lld %lld %d %.2f\n", r, (long long)c, (long long)act, (long long)ed,
-                        int(kinds[r - t]), x * 1e3);
+                        int(kinds[r - t]), timed ? ktime[r - t] * 1e3 : 0.0);
             if (c == 0) {
                 found = r;
                 break;
@@ -694,6 +703,9 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         st->edges_total = edge_sum;
         st->dense_rounds = dense_rounds;
         st->bytes_total = bytes;
+        st->sparse_ms = sp_ms;
+        st->sparse_launches = sp_launches;
+        st->sparse_bytes = sp_bytes;
     }
     return found > 0 ? SWARM_OK : SWARM_NOT_CONVERGED;
 }

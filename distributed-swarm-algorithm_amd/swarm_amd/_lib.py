@@ -48,7 +48,8 @@ class ElectStats(ctypes.Structure):
                 ("edges_total", ctypes.c_int64), ("changes_total", ctypes.c_int64),
                 ("gather_ms", ctypes.c_double), ("apply_ms", ctypes.c_double),
                 ("gather_launches", ctypes.c_int64), ("dense_rounds", ctypes.c_int64),
-                ("bytes_total", ctypes.c_double)]
+                ("bytes_total", ctypes.c_double), ("sparse_ms", ctypes.c_double),
+                ("sparse_launches", ctypes.c_int64), ("sparse_bytes", ctypes.c_double)]
 
 
 class Shard(ctypes.Structure):

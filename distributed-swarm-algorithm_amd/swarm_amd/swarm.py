@@ -169,6 +169,7 @@ class Swarm:
                           st.bytes_total)
         res.changes_total = st.changes_total
         res.gather_ms, res.apply_ms, res.timed_launches = st.gather_ms, st.apply_ms, st.gather_launches
+        res.sparse_ms, res.sparse_launches, res.sparse_bytes = st.sparse_ms, st.sparse_launches, st.sparse_bytes
         return res
 
     # ------------------------------------------------------------------ allocation

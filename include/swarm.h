@@ -71,11 +71,14 @@ typedef struct swarm_elect_stats {
     int64_t active_total;    /* agents gathered (DENSE: all; SPARSE: marked), rounds 1..rounds_exec */
     int64_t edges_total;     /* CSR edges visited, summed over rounds 1..rounds_exec */
     int64_t changes_total;   /* leader changes, summed over rounds */
-    double gather_ms;        /* SWARM_ELECT_TIMED: summed device time of the round kernels */
+    double gather_ms;        /* SWARM_ELECT_TIMED: device time of every launched round kernel */
     double apply_ms;         /* always 0 (one kernel per round); kept for layout stability */
-    int64_t gather_launches; /* launches behind gather_ms (rounds 1..rounds_exec) */
+    int64_t gather_launches; /* launches behind gather_ms (all launched rounds) */
     int64_t dense_rounds;    /* rounds executed as a full DENSE sweep */
     double bytes_total;      /* algorithmic HBM bytes of rounds 1..rounds_exec */
+    double sparse_ms;        /* SWARM_ELECT_TIMED: device time of every launched sparse round */
+    int64_t sparse_launches; /* SWARM_ELECT_TIMED: sparse rounds launched (incl. no-ops) */
+    double sparse_bytes;     /* algorithmic HBM bytes of the executed sparse rounds */
 } swarm_elect_stats;
 
 const char *swarm_last_error(void);

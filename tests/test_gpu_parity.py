@@ -342,7 +342,8 @@ def test_elect_timed_stats(sw, oracle_mod):
     r = s.elect(mode="frontier", timed=True)
     assert r.rounds_exec == int(g["rounds_exec"])
     assert r.changes_total == int(g["changes"].sum())
-    assert r.timed_launches == r.rounds_exec and r.gather_ms > 0 and r.apply_ms >= 0
+    assert r.timed_launches == r.rounds_launched >= r.rounds_exec and r.gather_ms > 0 and r.apply_ms >= 0
+    assert r.sparse_launches == r.rounds_launched - r.dense_rounds and r.sparse_ms > 0 and r.sparse_bytes > 0
     r2 = s.elect(mode="dense", timed=True)
     assert r2.rounds_exec == int(g["rounds_exec"]) and r2.gather_ms > 0
 
