@@ -25,6 +25,7 @@
 // records, per (task, tile), the max claim value and claim count; the chain then walks
 // tiles (ballot over tile maxima) and re-evaluates only the one tile a link lands in.
 #include "binning.h"
+#include "utility.h"
 
 #include <climits>
 
@@ -32,25 +33,6 @@ namespace swarm {
 namespace {
 
 constexpr int kCap = 2048;  // claims per task kept in LDS (beyond: exact recompute path)
-
-__device__ __forceinline__ double utility(double ax, double ay, uint32_t caps, double tx, double ty,
-                                          int rq, double u_scale) {
-    const double dx = ax - tx, dy = ay - ty;
-    const double d = sqrt(dx * dx + dy * dy);
-    const double has = (rq >= 0 && !((caps >> rq) & 1u)) ? 0.0 : 1.0;
-    return (u_scale / (1.0 + d)) * has;
-}
-
-// Could the reference (libm pow for the squares, <= 2 ulp away) decide or round differently?
-__device__ __forceinline__ bool guard_flag(double U, double thr) {
-    const double band = fmax(fabs(thr), fabs(U)) * 0x1p-49;
-    if (fabs(U - thr) <= band) return true;
-    if (U > thr) {
-        const double e = fabs(U) * 0x1p-50;
-        return float(U - e) != float(U + e);
-    }
-    return false;
-}
 
 __device__ __forceinline__ int block_min_int(int v, int *s_red) {
 #pragma unroll

@@ -1,0 +1,509 @@
+// Auction allocation on gfx950 (BASELINE config C4).
+//
+// The north star's "auction price update as a conflict-free bid kernel".  The reference has no
+// auction (its allocation is greedy claim + leader hysteresis, agent.py:292-325), so parity is
+// against the build's own CPU restatement (oracle/swarm_oracle.c orc_auction), bit-exact:
+// assignments, prices, per-round bidder counts and the round count.
+//
+// Problem: agents x tasks with value x(a,k) = f32(U(a,k)) for the admissible pairs U > claim_thr
+// -- the reference's claim rule (agent.py:297) and claim payload (agent.py:302) -- one task per
+// agent, one agent per task, maximise total value.  Jacobi Bertsekas auction: every round every
+// unassigned, active agent bids on its best task (net = x - price, ties -> lowest task index)
+// price + (best - second) + eps, the opt-out option (net 0) counting as a competitor; an agent
+// whose best net is <= 0 drops out for good.  Each task takes its highest bid, ties -> lowest
+// agent ID; the previous owner becomes unassigned.  Stops after the first round without bidders.
+//
+// Kernels:
+//   candidates   tasks binned in a uniform grid (cell >= claim radius); one thread per agent
+//                walks the cells its claim disc covers, fp64 utilities, and writes its
+//                admissible (task, f32 value) list (count pass, hipCUB scan, fill pass).
+//   k_auc_bid    one wave per agent: lanes sweep its list (price gathers), a wave reduction of
+//                (best, task, second); the bid is ONE 64-bit atomicMax per bidder on a packed
+//                key f32bits(bid) << 32 | ~id -- highest bid, then lowest ID, no conflicts.
+//   k_auc_resolve one thread per task: a non-zero key moves the task to its bidder.
+//   k_auc_tail   once few agents still bid (prices rising on a handful of contested tasks, the
+//                auction's long tail), ONE workgroup runs all remaining rounds with its bidder
+//                list in LDS and workgroup barriers between the phases: no kernel boundary per
+//                round.  Same rounds, same results.
+// Per-round bidder counts: 64-way sharded counters in a ring (multi-workgroup rounds), a log
+// written by the tail kernel; the host reads them every batch of rounds.
+#include <climits>
+#include <cmath>
+#include <vector>
+
+#include "binning.h"
+#include "utility.h"
+
+namespace swarm {
+namespace {
+
+constexpr int kAShards = 64;
+constexpr int kAStride = 16;       // u64 per shard: one 128-B line
+constexpr int kARing = 512;        // rounds of counter slots
+constexpr int kTailBlock = 1024;   // k_auc_tail: threads (16 waves)
+constexpr int kTailCap = 2048;     // k_auc_tail: bidder list capacity (LDS)
+
+__device__ __forceinline__ unsigned long long *aslot(unsigned long long *ring, int64_t r, int shard) {
+    return ring + size_t(r % kARing) * kAShards * kAStride + size_t(shard) * kAStride;
+}
+
+// ---------------------------------------------------------------- candidate lists
+struct CandIn {
+    const double2 *apos;
+    const uint32_t *acaps;
+    const double2 *tpos;
+    const int8_t *treq;
+    const int32_t *sorted;     // task indices, cell by cell
+    const uint32_t *cell_off;  // per-cell exclusive prefix into sorted
+    Grid g;
+    double rp, rp2, thr, u_scale;
+};
+
+// Walk agent a's admissible tasks: f(k, U) for every task with U > thr.
+template <typename F>
+__device__ __forceinline__ void for_admissible(const CandIn &c, int64_t a, unsigned long long &flagged, F f) {
+    const double2 p = c.apos[a];
+    const uint32_t caps = c.acaps[a];
+    const Grid &g = c.g;
+    if (p.x + c.rp < g.xmin || p.x - c.rp > g.xmax || p.y + c.rp < g.ymin || p.y - c.rp > g.ymax) return;
+    const int64_t x0 = cell_coord(p.x - c.rp, g.xmin, g.inv_cell, g.ncx);
+    const int64_t x1 = cell_coord(p.x + c.rp, g.xmin, g.inv_cell, g.ncx);
+    const int64_t y0 = cell_coord(p.y - c.rp, g.ymin, g.inv_cell, g.ncy);
+    const int64_t y1 = cell_coord(p.y + c.rp, g.ymin, g.inv_cell, g.ncy);
+    for (int64_t yy = y0; yy <= y1; ++yy) {
+        const uint32_t q0 = c.cell_off[yy * g.ncx + x0], q1 = c.cell_off[yy * g.ncx + x1 + 1];
+        for (uint32_t q = q0; q < q1; ++q) {
+            const int32_t k = c.sorted[q];
+            const double2 tp = c.tpos[k];
+            const double dx = p.x - tp.x, dy = p.y - tp.y;
+            if (dx * dx + dy * dy > c.rp2) continue;
+            const double U = utility(p.x, p.y, caps, tp.x, tp.y, c.treq[k], c.u_scale);
+            flagged += guard_flag(U, c.thr);
+            if (U > c.thr) f(k, U);
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_auc_count(CandIn c, int64_t n, int64_t *__restrict__ cnt,
+                                                     unsigned long long *__restrict__ flagged_out) {
+    unsigned long long fl = 0;
+    for (int64_t a = int64_t(blockIdx.x) * kBlock + threadIdx.x; a < n; a += int64_t(gridDim.x) * kBlock) {
+        int64_t m = 0;
+        for_admissible(c, a, fl, [&](int32_t, double) { ++m; });
+        cnt[a] = m;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) fl += __shfl_xor(fl, off, 64);
+    if ((threadIdx.x & 63) == 0 && fl) atomicAdd(flagged_out + (blockIdx.x & (kAShards - 1)) * kAStride, fl);
+}
+
+__global__ __launch_bounds__(kBlock) void k_auc_fill(CandIn c, int64_t n, const int64_t *__restrict__ off,
+                                                    int32_t *__restrict__ ck, float *__restrict__ cv) {
+    unsigned long long fl = 0;
+    for (int64_t a = int64_t(blockIdx.x) * kBlock + threadIdx.x; a < n; a += int64_t(gridDim.x) * kBlock) {
+        int64_t p = off[a];
+        for_admissible(c, a, fl, [&](int32_t k, double U) {
+            ck[p] = k;
+            cv[p] = float(U);
+            ++p;
+        });
+    }
+}
+
+// ---------------------------------------------------------------- bidding
+struct AucState {
+    const int64_t *off;
+    const int32_t *ck;
+    const float *cv;
+    const int32_t *ids;
+    const uint32_t *sorted_ids;  // ascending IDs ...
+    const int32_t *order;        // ... and their storage indices
+    float *price;
+    int32_t *owner;
+    int32_t *assigned;
+    uint8_t *out;
+    unsigned long long *key;
+    unsigned long long *ring;
+    int64_t n, t;
+    float eps;
+};
+
+// Best (ties -> lower task index) and second-best net over the lanes.
+struct Best {
+    float best, second;
+    int32_t bk;
+};
+
+__device__ __forceinline__ Best combine(Best x, Best y) {
+    Best r;
+    if (x.best > y.best || (x.best == y.best && x.bk < y.bk)) {
+        r.best = x.best;
+        r.bk = x.bk;
+        r.second = fmaxf(x.second, y.best);
+    } else {
+        r.best = y.best;
+        r.bk = y.bk;
+        r.second = fmaxf(y.second, x.best);
+    }
+    return r;
+}
+
+// The whole wave evaluates agent a (wave-uniform call).  Returns the bid key (0: drop out) and
+// the task in *bk.
+__device__ __forceinline__ unsigned long long wave_bid(const AucState &s, int64_t a, int32_t *bk_out) {
+    const int lane = threadIdx.x & 63;
+    Best m{-INFINITY, -INFINITY, INT_MAX};
+    const int64_t b = s.off[a], e = s.off[a + 1];
+    for (int64_t p = b + lane; p < e; p += 64) {
+        const int32_t k = s.ck[p];
+        const float net = s.cv[p] - s.price[k];
+        m = combine(m, Best{net, -INFINITY, k});
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        Best y;
+        y.best = __shfl_xor(m.best, o, 64);
+        y.second = __shfl_xor(m.second, o, 64);
+        y.bk = __shfl_xor(m.bk, o, 64);
+        m = combine(m, y);
+    }
+    *bk_out = m.bk;
+    if (!(m.best > 0.0f)) return 0ull;
+    const float second = m.second < 0.0f ? 0.0f : m.second;
+    const float inc = m.best - second;
+    float bid = s.price[m.bk] + inc;
+    bid = bid + s.eps;
+    return (static_cast<unsigned long long>(__float_as_uint(bid)) << 32) |
+           static_cast<unsigned long long>(0xFFFFFFFFu - static_cast<uint32_t>(s.ids[a]));
+}
+
+__device__ __forceinline__ int32_t index_of_id(const AucState &s, uint32_t id) {
+    int64_t lo = 0, hi = s.n - 1;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (s.sorted_ids[mid] < id) lo = mid + 1; else hi = mid;
+    }
+    return s.order[lo];
+}
+
+__global__ __launch_bounds__(kBlock) void k_auc_bid(AucState s, int64_t r) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = int64_t(gridDim.x) * (kBlock / kWave);
+    unsigned long long nb = 0;
+    for (int64_t a = int64_t(blockIdx.x) * (kBlock / kWave) + (threadIdx.x >> 6); a < s.n; a += nw) {
+        if (s.assigned[a] >= 0 || s.out[a]) continue;  // wave-uniform
+        ++nb;
+        int32_t bk;
+        const unsigned long long kk = wave_bid(s, a, &bk);
+        if (lane == 0) {
+            if (kk == 0) s.out[a] = 1;
+            else atomicMax(&s.key[bk], kk);
+        }
+    }
+    __shared__ unsigned long long s_nb[kBlock / kWave];
+    if (lane == 0) s_nb[threadIdx.x >> 6] = nb;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long v = 0;
+        for (int w = 0; w < kBlock / kWave; ++w) v += s_nb[w];
+        if (v) atomicAdd(aslot(s.ring, r, blockIdx.x & (kAShards - 1)), v);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_auc_resolve(AucState s, int64_t r) {
+    if (blockIdx.x == 0)  // recycle the counter slots of round r + kARing/2
+        for (int i = threadIdx.x; i < kAShards; i += kBlock) *aslot(s.ring, r + kARing / 2, i) = 0;
+    for (int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x; k < s.t; k += int64_t(gridDim.x) * kBlock) {
+        const unsigned long long kk = s.key[k];
+        if (!kk) continue;
+        const int32_t w = index_of_id(s, 0xFFFFFFFFu - static_cast<uint32_t>(kk & 0xFFFFFFFFull));
+        const int32_t prev = s.owner[k];
+        if (prev >= 0) s.assigned[prev] = -1;
+        s.owner[k] = w;
+        s.assigned[w] = int32_t(k);
+        s.price[k] = __uint_as_float(static_cast<uint32_t>(kk >> 32));
+        s.key[k] = 0;
+    }
+}
+
+// totals[i] = bidders of round r0 + i (one wave per round).
+__global__ void k_auc_totals(unsigned long long *ring, int64_t r0, unsigned long long *totals) {
+    unsigned long long v = *aslot(ring, r0 + blockIdx.x, threadIdx.x);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (threadIdx.x == 0) totals[blockIdx.x] = v;
+}
+
+// ---------------------------------------------------------------- the long tail, one workgroup
+// Rounds r0, r0+1, ... until no agent bids or max_rounds: bidder list in LDS (the unassigned,
+// active agents; it never grows: a round removes its winners and drop-outs and adds at most one
+// displaced owner per winner).  Phases per round, separated by workgroup barriers: bid (a wave
+// per listed agent, atomicMax on the task key), resolve (the bidder whose key stands wins),
+// key reset.  Task keys are read with agent-scope atomic loads (the atomics execute in L2).
+__global__ __launch_bounds__(kTailBlock) void k_auc_tail(AucState s, int64_t r0, int64_t max_rounds,
+                                                        int64_t *__restrict__ log, int64_t *__restrict__ done) {
+    __shared__ int32_t s_list[2][kTailCap];
+    __shared__ int32_t s_tgt[kTailCap];
+    __shared__ unsigned long long s_key[kTailCap];
+    __shared__ int s_cnt[2];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    constexpr int kWaves = kTailBlock / kWave;
+    if (threadIdx.x == 0) s_cnt[0] = s_cnt[1] = 0;
+    __syncthreads();
+    for (int64_t a = threadIdx.x; a < s.n; a += kTailBlock)
+        if (s.assigned[a] < 0 && !s.out[a]) {
+            const int p = atomicAdd(&s_cnt[0], 1);
+            if (p < kTailCap) s_list[0][p] = int32_t(a);
+        }
+    __syncthreads();
+    int cur = 0;
+    int64_t r = r0;
+    for (; r <= max_rounds; ++r) {
+        const int m = min(s_cnt[cur], kTailCap);
+        if (m == 0) break;
+        if (threadIdx.x == 0) log[r - r0] = m;
+        // bid
+        for (int i = wid; i < m; i += kWaves) {
+            const int32_t a = s_list[cur][i];
+            int32_t bk;
+            const unsigned long long kk = wave_bid(s, a, &bk);
+            if (lane == 0) {
+                s_tgt[i] = kk ? bk : -1;
+                s_key[i] = kk;
+                if (kk) atomicMax(&s.key[bk], kk);
+                else s.out[a] = 1;
+            }
+        }
+        if (threadIdx.x == 0) s_cnt[cur ^ 1] = 0;
+        __syncthreads();
+        // resolve: the standing key's bidder takes the task; losers bid again, the displaced
+        // owner joins them
+        for (int i = threadIdx.x; i < m; i += kTailBlock) {
+            const int32_t k = s_tgt[i];
+            if (k < 0) continue;
+            const int32_t a = s_list[cur][i];
+            const unsigned long long top = __hip_atomic_load(&s.key[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (top == s_key[i]) {
+                const int32_t prev = s.owner[k];
+                s.owner[k] = a;
+                s.assigned[a] = k;
+                s.price[k] = __uint_as_float(static_cast<uint32_t>(top >> 32));
+                if (prev >= 0) {
+                    s.assigned[prev] = -1;
+                    s_list[cur ^ 1][atomicAdd(&s_cnt[cur ^ 1], 1)] = prev;
+                }
+            } else {
+                s_list[cur ^ 1][atomicAdd(&s_cnt[cur ^ 1], 1)] = a;
+            }
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < m; i += kTailBlock)
+            if (s_tgt[i] >= 0 && s.owner[s_tgt[i]] == s_list[cur][i]) s.key[s_tgt[i]] = 0;
+        cur ^= 1;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *done = r - r0;  // rounds this kernel ran (all had bidders)
+}
+
+// Hand the rounds to k_auc_tail once a round had <= this many bidders (SWARM_AUCTION_TAIL,
+// read per call; 0 = never, tests use it to exercise both paths).
+int auc_tail_threshold() {
+    int tail = 512;
+    if (const char *e = getenv("SWARM_AUCTION_TAIL")) tail = atoi(e);
+    return tail < 0 ? 0 : (tail > kTailCap ? kTailCap : tail);
+}
+
+}  // namespace
+}  // namespace swarm
+
+extern "C" {
+
+int swarm_auction(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos, const uint32_t *acaps,
+                  int64_t t, const double *tpos, const int8_t *treq, double claim_thr, double u_scale, float eps,
+                  int32_t max_rounds, int32_t *owner, float *price, int32_t *assigned, int32_t *rounds_exec,
+                  int64_t *bidders_per_round, swarm_auction_stats *stats, void *stream) {
+    using namespace swarm;
+    SW_ARG(ctx != nullptr && rounds_exec != nullptr, "NULL argument");
+    SW_ARG(n >= 0 && n < (int64_t(1) << 31) && t >= 0 && t < (int64_t(1) << 31), "sizes out of range");
+    SW_ARG(max_rounds >= 1, "max_rounds < 1");
+    SW_ARG(std::isfinite(eps) && eps > 0.0f, "eps must be finite and > 0");
+    SW_ARG(std::isfinite(claim_thr) && claim_thr > 0.0 && std::isfinite(u_scale) && u_scale > 0.0,
+           "claim_thr and u_scale must be finite and > 0 (finite claim radius)");
+    SW_ARG(n == 0 || (ids && apos && acaps && assigned), "NULL agent array");
+    SW_ARG(t == 0 || (tpos && treq && owner && price), "NULL task array");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (stats) *stats = swarm_auction_stats{};
+    if (n) SW_HIP(hipMemsetAsync(assigned, 0xFF, size_t(n) * 4, s));  // -1
+    if (t) {
+        SW_HIP(hipMemsetAsync(owner, 0xFF, size_t(t) * 4, s));
+        SW_HIP(hipMemsetAsync(price, 0, size_t(t) * 4, s));
+    }
+    *rounds_exec = 0;
+    if (n == 0 || t == 0) {  // no tasks: round 1's bidders (every agent) all drop out
+        *rounds_exec = n ? 1 : 0;
+        if (n && bidders_per_round) bidders_per_round[0] = n;
+        if (stats) {
+            stats->rounds_launched = n ? 2 : 1;
+            stats->bids_total = n;
+        }
+        return SWARM_OK;
+    }
+    // ---- candidate lists
+    const double rc = u_scale / claim_thr - 1.0;  // U > thr  <=>  d < rc (has_cap)
+    int64_t *off;
+    unsigned long long *flag;
+    SW_ALLOC(off, ctx, S_AUC_OFF, size_t(n + 1) * 8);
+    SW_ALLOC(flag, ctx, S_ASTATS, size_t(kAShards) * kAStride * 8);
+    SW_HIP(hipMemsetAsync(flag, 0, size_t(kAShards) * kAStride * 8, s));
+    CandIn c{};
+    c.apos = reinterpret_cast<const double2 *>(apos);
+    c.acaps = acaps;
+    c.tpos = reinterpret_cast<const double2 *>(tpos);
+    c.treq = treq;
+    c.thr = claim_thr;
+    c.u_scale = u_scale;
+    int64_t npairs = 0;
+    if (rc > 0.0) {
+        c.rp = rc * (1.0 + 1e-9) + 1e-12;
+        c.rp2 = c.rp * c.rp;
+        int rcode = make_grid(ctx, t, tpos, c.rp, 2 * t + 1024, &c.g, s);
+        if (rcode) return rcode;
+        int32_t *sorted;
+        uint32_t *coff;
+        if ((rcode = bin_agents(ctx, t, tpos, c.g, &sorted, &coff, s))) return rcode;
+        c.sorted = sorted;
+        c.cell_off = coff;
+        const unsigned grid = grid_for(n, kBlock, 4096);
+        SW_HIP(hipMemsetAsync(off, 0, 8, s));
+        hipLaunchKernelGGL(k_auc_count, dim3(grid), dim3(kBlock), 0, s, c, n, off + 1, flag);
+        SW_LAUNCHED();
+        size_t tmp_bytes = 0;
+        SW_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tmp_bytes, off + 1, off + 1, int(n), s));
+        void *tmp;
+        SW_ALLOC(tmp, ctx, S_CUB_TMP, tmp_bytes);
+        SW_HIP(hipcub::DeviceScan::InclusiveSum(tmp, tmp_bytes, off + 1, off + 1, int(n), s));
+        SW_HIP(hipMemcpyAsync(&npairs, off + n, 8, hipMemcpyDeviceToHost, s));
+        SW_HIP(hipStreamSynchronize(s));
+    } else {
+        SW_HIP(hipMemsetAsync(off, 0, size_t(n + 1) * 8, s));
+    }
+    int32_t *ck;
+    float *cv;
+    SW_ALLOC(ck, ctx, S_AUC_K, size_t(npairs + 1) * 4);
+    SW_ALLOC(cv, ctx, S_AUC_V, size_t(npairs + 1) * 4);
+    if (npairs) {
+        hipLaunchKernelGGL(k_auc_fill, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s, c, n, off, ck, cv);
+        SW_LAUNCHED();
+    }
+    // ---- id -> storage index (ascending IDs), bid keys, flags, counters
+    uint32_t *kin, *kout;
+    int32_t *vin, *order;
+    SW_ALLOC(kin, ctx, S_KEYS_IN, size_t(n) * 4);
+    SW_ALLOC(kout, ctx, S_KEYS_OUT, size_t(n) * 4);
+    SW_ALLOC(vin, ctx, S_VALS_IN, size_t(n) * 4);
+    SW_ALLOC(order, ctx, S_ORDER, size_t(n) * 4);
+    {
+        SW_HIP(hipMemcpyAsync(kin, ids, size_t(n) * 4, hipMemcpyDeviceToDevice, s));
+        std::vector<int32_t> io(static_cast<size_t>(n));
+        for (int64_t i = 0; i < n; ++i) io[size_t(i)] = int32_t(i);
+        SW_HIP(hipMemcpyAsync(vin, io.data(), size_t(n) * 4, hipMemcpyHostToDevice, s));
+        size_t tmp_bytes = 0;
+        SW_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, kin, kout, vin, order, int(n), 0, 32, s));
+        void *tmp;
+        SW_ALLOC(tmp, ctx, S_CUB_TMP, tmp_bytes);
+        SW_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, order, int(n), 0, 32, s));
+        SW_HIP(hipStreamSynchronize(s));  // io leaves scope
+    }
+    AucState st{};
+    st.off = off;
+    st.ck = ck;
+    st.cv = cv;
+    st.ids = ids;
+    st.sorted_ids = kout;
+    st.order = order;
+    st.price = price;
+    st.owner = owner;
+    st.assigned = assigned;
+    st.n = n;
+    st.t = t;
+    st.eps = eps;
+    SW_ALLOC(st.out, ctx, S_AUC_OUT, size_t(n));
+    SW_ALLOC(st.key, ctx, S_AUC_KEY, size_t(t) * 8);
+    SW_ALLOC(st.ring, ctx, S_CHANGES, size_t(kARing) * kAShards * kAStride * 8);
+    SW_HIP(hipMemsetAsync(st.out, 0, size_t(n), s));
+    SW_HIP(hipMemsetAsync(st.key, 0, size_t(t) * 8, s));
+    SW_HIP(hipMemsetAsync(st.ring, 0, size_t(kARing) * kAShards * kAStride * 8, s));
+    constexpr int kMaxBatch = 256;
+    unsigned long long *dtot;
+    SW_ALLOC(dtot, ctx, S_ESTATS, size_t(kMaxBatch) * 8 + 64);
+    int64_t *dlog;
+    SW_ALLOC(dlog, ctx, S_TMP1, (size_t(max_rounds) + 2) * 8);
+    unsigned long long *h = static_cast<unsigned long long *>(pinned(ctx, size_t(kMaxBatch) * 8 + 64));
+    if (!h) return SWARM_ERR_OOM;
+
+    const unsigned bgrid = grid_for(n, kBlock / kWave, 8192), rgrid = grid_for(t, kBlock, 4096);
+    const int64_t tail_thr = auc_tail_threshold();
+    int64_t r = 1, found = -1, last_nb = n, launched = 0, tail_rounds = 0, total_bids = 0;
+    int batch = 8;
+    while (r <= max_rounds && found < 0) {
+        if (last_nb <= tail_thr) {  // the long tail: one workgroup runs every remaining round
+            int64_t *ddone = dlog + max_rounds;
+            hipLaunchKernelGGL(k_auc_tail, dim3(1), dim3(kTailBlock), 0, s, st, r, int64_t(max_rounds), dlog, ddone);
+            SW_LAUNCHED();
+            int64_t done = 0;
+            SW_HIP(hipMemcpyAsync(&done, ddone, 8, hipMemcpyDeviceToHost, s));
+            SW_HIP(hipStreamSynchronize(s));
+            std::vector<int64_t> lg(static_cast<size_t>(done) + 1);
+            if (done) SW_HIP(hipMemcpy(lg.data(), dlog, size_t(done) * 8, hipMemcpyDeviceToHost));
+            for (int64_t i = 0; i < done; ++i) {
+                if (bidders_per_round) bidders_per_round[r - 1 + i] = lg[size_t(i)];
+                total_bids += lg[size_t(i)];
+            }
+            tail_rounds = done;
+            launched = r + done;  // the round that found no bidder ran inside the kernel too
+            r += done;
+            if (r <= max_rounds) found = r;  // round r had no bidder
+            break;
+        }
+        const int64_t rend = (max_rounds - r + 1 < batch) ? max_rounds : r + batch - 1;
+        for (int64_t q = r; q <= rend; ++q) {
+            hipLaunchKernelGGL(k_auc_bid, dim3(bgrid), dim3(kBlock), 0, s, st, q);
+            SW_LAUNCHED();
+            hipLaunchKernelGGL(k_auc_resolve, dim3(rgrid), dim3(kBlock), 0, s, st, q);
+            SW_LAUNCHED();
+        }
+        launched = rend;
+        hipLaunchKernelGGL(k_auc_totals, dim3(rend - r + 1), dim3(kWave), 0, s, st.ring, r, dtot);
+        SW_LAUNCHED();
+        SW_HIP(hipMemcpyAsync(h, dtot, size_t(rend - r + 1) * 8, hipMemcpyDeviceToHost, s));
+        SW_HIP(hipStreamSynchronize(s));
+        for (int64_t q = r; q <= rend; ++q) {
+            const int64_t nb = int64_t(h[q - r]);
+            if (nb == 0) {
+                found = q;
+                break;
+            }
+            if (bidders_per_round) bidders_per_round[q - 1] = nb;
+            total_bids += nb;
+            last_nb = nb;
+        }
+        r = rend + 1;
+        batch = batch < kMaxBatch ? batch * 2 : kMaxBatch;
+    }
+    *rounds_exec = int32_t(found > 0 ? found - 1 : max_rounds);
+    if (stats) {
+        unsigned long long fl[kAShards * kAStride];
+        SW_HIP(hipMemcpyAsync(fl, flag, sizeof(fl), hipMemcpyDeviceToHost, s));
+        SW_HIP(hipStreamSynchronize(s));
+        int64_t nf = 0;
+        for (int i = 0; i < kAShards; ++i) nf += int64_t(fl[i * kAStride]);
+        stats->n_pairs = npairs;
+        stats->n_flagged = nf;
+        stats->rounds_launched = launched;
+        stats->tail_rounds = tail_rounds;
+        stats->bids_total = total_bids;
+    }
+    return found > 0 ? SWARM_OK : SWARM_NOT_CONVERGED;
+}
+
+}  // extern "C"

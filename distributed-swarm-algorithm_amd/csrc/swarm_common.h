@@ -39,6 +39,11 @@ enum Slot {
     S_ORDER,          // dense allocation: agents in ascending ID order
     S_TMP0,
     S_TMP1,
+    S_AUC_OFF,        // auction: candidate-list offsets (int64, n + 1)
+    S_AUC_K,          // auction: candidate tasks
+    S_AUC_V,          // auction: candidate values (f32)
+    S_AUC_OUT,        // auction: dropped-out flags
+    S_AUC_KEY,        // auction: per-task bid keys (u64)
     S_NUM
 };
 

@@ -1,0 +1,35 @@
+// The reference utility on the device, shared by the allocation and auction kernels.
+// _calculate_utility (agent.py:338-347): d = sqrt(dx**2 + dy**2), U = (100 / (1 + d)) * has_cap.
+// The reference squares with libm pow; this computes dx*dx (separately rounded products: the
+// library is built with -ffp-contract=off), IEEE sqrt and division.  guard_flag() marks the
+// values a <= 2-ulp difference could push across the claim threshold or an f32 rounding
+// boundary.
+#pragma once
+
+#include <cmath>
+#include <cstdint>
+
+namespace swarm {
+namespace {
+
+__device__ __forceinline__ double utility(double ax, double ay, uint32_t caps, double tx, double ty,
+                                          int rq, double u_scale) {
+    const double dx = ax - tx, dy = ay - ty;
+    const double d = sqrt(dx * dx + dy * dy);
+    const double has = (rq >= 0 && !((caps >> rq) & 1u)) ? 0.0 : 1.0;
+    return (u_scale / (1.0 + d)) * has;
+}
+
+// Could the reference (libm pow for the squares, <= 2 ulp away) decide or round differently?
+__device__ __forceinline__ bool guard_flag(double U, double thr) {
+    const double band = fmax(fabs(thr), fabs(U)) * 0x1p-49;
+    if (fabs(U - thr) <= band) return true;
+    if (U > thr) {
+        const double e = fabs(U) * 0x1p-50;
+        return float(U - e) != float(U + e);
+    }
+    return false;
+}
+
+}  // namespace
+}  // namespace swarm

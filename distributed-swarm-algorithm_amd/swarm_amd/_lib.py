@@ -28,7 +28,7 @@ EXPORTS = ("swarm_last_error", "swarm_version", "swarm_ctx_create", "swarm_ctx_d
            "swarm_utility", "swarm_build_rgg", "swarm_cell_order", "swarm_frontier_begin",
            "swarm_frontier_step", "swarm_frontier_ghosts", "swarm_frontier_changes",
            "swarm_comm_available", "swarm_comm_unique_id", "swarm_comm_create", "swarm_comm_destroy",
-           "swarm_elect_sharded")
+           "swarm_elect_sharded", "swarm_auction")
 
 
 class SwarmError(RuntimeError):
@@ -50,6 +50,12 @@ class ElectStats(ctypes.Structure):
                 ("gather_launches", ctypes.c_int64), ("dense_rounds", ctypes.c_int64),
                 ("bytes_total", ctypes.c_double), ("sparse_ms", ctypes.c_double),
                 ("sparse_launches", ctypes.c_int64), ("sparse_bytes", ctypes.c_double)]
+
+
+class AuctionStats(ctypes.Structure):
+    _fields_ = [("n_pairs", ctypes.c_int64), ("n_flagged", ctypes.c_int64),
+                ("rounds_launched", ctypes.c_int64), ("tail_rounds", ctypes.c_int64),
+                ("bids_total", ctypes.c_int64)]
 
 
 class Shard(ctypes.Structure):
@@ -99,6 +105,8 @@ def load(path: str = LIB_PATH):
         L.swarm_comm_create.argtypes = [ctypes.POINTER(P), ctypes.c_int, ctypes.c_int, P]
         L.swarm_comm_destroy.argtypes = [P]
         L.swarm_elect_sharded.argtypes = [P, P, ctypes.POINTER(Shard), P, P, i32, ctypes.POINTER(i32), P, P]
+        L.swarm_auction.argtypes = [P, i64, P, P, P, i64, P, P, d, d, ctypes.c_float, i32, P, P, P,
+                                    ctypes.POINTER(i32), P, P, P]
         for name in EXPORTS:
             if name not in ("swarm_last_error", "swarm_version"):
                 getattr(L, name).restype = ctypes.c_int

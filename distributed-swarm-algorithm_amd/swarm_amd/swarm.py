@@ -57,6 +57,17 @@ class ElectResult:
 
 
 @dataclass
+class AuctionResult:
+    owner: torch.Tensor                 # int32 [t] storage index of the task's agent (-1 = none)
+    price: torch.Tensor                 # float32 [t] final prices
+    assigned: torch.Tensor              # int32 [n] task index per agent (storage order, -1 = none)
+    rounds_exec: int                    # rounds that had bidders
+    bidders: np.ndarray                 # per-round bidder counts, rounds 1..rounds_exec
+    converged: bool = True
+    stats: dict = field(default_factory=dict)
+
+
+@dataclass
 class AllocResult:
     winner: torch.Tensor                # int32 [t] (-1 = unclaimed)
     util: torch.Tensor                  # float64 [t] winning claim value (f32-valued)
@@ -209,6 +220,31 @@ class Swarm:
                 ctypes.byref(st), _lib.stream()))
         stats = {k: getattr(st, k) for k, _ in _lib.AllocStats._fields_}
         return AllocResult(w, u, won, nclaim, nmsg, stats)
+
+    def auction(self, tx, ty, treq, *, eps: float = 0.1, claim_thr: float = 20.0, u_scale: float = 100.0,
+                max_rounds: int = 1 << 20) -> AuctionResult:
+        """Auction allocation over the admissible pairs (swarm_auction; SURVEY §8f f4, the north
+        star's auction price update): one task per agent, highest bid wins, ties to the lowest
+        ID.  No reference counterpart; parity against oracle.auction."""
+        dev = self.device
+        tpos = torch.stack([_to(tx, torch.float64, dev), _to(ty, torch.float64, dev)], 1).contiguous()
+        tq = _to(treq, torch.int8, dev)
+        t = tq.numel()
+        owner = torch.empty(max(t, 1), dtype=torch.int32, device=dev)
+        price = torch.empty(max(t, 1), dtype=torch.float32, device=dev)
+        assigned = torch.empty(max(self.n, 1), dtype=torch.int32, device=dev)
+        rounds = ctypes.c_int32(0)
+        bidders = np.zeros(int(max_rounds), np.int64)
+        st = _lib.AuctionStats()
+        with torch.cuda.device(dev):
+            rc = _lib.check(_lib.lib().swarm_auction(
+                _lib.ctx(), self.n, _lib.ptr(self.ids), _lib.ptr(self.pos), _lib.ptr(self.caps), t,
+                _lib.ptr(tpos), _lib.ptr(tq), float(claim_thr), float(u_scale), float(eps), int(max_rounds),
+                _lib.ptr(owner), _lib.ptr(price), _lib.ptr(assigned), ctypes.byref(rounds),
+                bidders.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st), _lib.stream()))
+        r = rounds.value
+        stats = {k: getattr(st, k) for k, _ in _lib.AuctionStats._fields_}
+        return AuctionResult(owner[:t], price[:t], assigned[: self.n], r, bidders[:r].copy(), rc == _lib.OK, stats)
 
     # ------------------------------------------------------------------ views / bridge
     def to_input_order(self, storage_tensor) -> np.ndarray:

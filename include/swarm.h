@@ -237,6 +237,35 @@ int swarm_build_rgg(swarm_ctx *ctx, int64_t n, const double *pos, double radius,
 int swarm_cell_order(swarm_ctx *ctx, int64_t n, const double *pos, double cell,
                      int32_t *perm, void *stream);
 
+/*
+ * Auction allocation (BASELINE config C4) -- the north star's "auction
+ * price update": no reference counterpart (the reference allocates by greedy claims and leader
+ * hysteresis, swarm_allocate above), parity against the build's CPU restatement
+ * (oracle/swarm_oracle.c orc_auction).  One task per agent and one agent per task over the
+ * admissible pairs U > claim_thr (agent.py:297), value x = f32(U) (the claim payload,
+ * agent.py:302).  Jacobi Bertsekas auction: each round every unassigned, active agent bids on
+ * its best task (net = x - price[k], ties -> lowest task index) the price price + (best -
+ * second) + eps, where the opt-out option (net 0) competes as a second best; an agent whose
+ * best net is <= 0 drops out for good.  Each task takes its highest bid, ties -> lowest agent
+ * ID; its previous owner becomes unassigned.  rounds_exec = rounds that had bidders (the auction
+ * stops at the first round without one).
+ * owner (device, t): storage index of the task's agent or -1; price (device, t, f32);
+ * assigned (device, n): task index or -1.  bidders_per_round (host, capacity max_rounds, may be
+ * NULL).  Returns SWARM_NOT_CONVERGED if max_rounds rounds all had bidders.
+ */
+typedef struct swarm_auction_stats {
+    int64_t n_pairs;         /* admissible (agent, task) pairs */
+    int64_t n_flagged;       /* pairs inside the libm guard band (see swarm_allocate) */
+    int64_t rounds_launched; /* rounds issued (>= rounds_exec + 1) */
+    int64_t tail_rounds;     /* rounds run by the single-workgroup tail kernel */
+    int64_t bids_total;      /* agent-rounds with a bidder, summed over rounds */
+} swarm_auction_stats;
+
+int swarm_auction(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos, const uint32_t *acaps,
+                  int64_t t, const double *tpos, const int8_t *treq, double claim_thr, double u_scale, float eps,
+                  int32_t max_rounds, int32_t *owner, float *price, int32_t *assigned, int32_t *rounds_exec,
+                  int64_t *bidders_per_round, swarm_auction_stats *stats, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

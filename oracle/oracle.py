@@ -52,6 +52,8 @@ def lib():
         L.orc_task_claims.argtypes = [l, P, P, P, P, d, d, ctypes.c_int8, d, d, i, P, P, l]
         L.orc_rgg_csr.restype = l
         L.orc_rgg_csr.argtypes = [l, P, P, d, P, P]
+        L.orc_auction.restype = l
+        L.orc_auction.argtypes = [l, P, P, P, P, l, P, P, P, d, d, i, ctypes.c_float, l, P, P, P, P, P]
         L.orc_num_threads.restype = i
         L.orc_set_threads.argtypes = [i]
         _lib = L
@@ -113,6 +115,26 @@ def allocate(ids, ax, ay, caps, tx, ty, treq, winner=None, util=None, claim_thr=
                                _p(nclaim), _p(nmsg), _p(won))
     return dict(winner=w, util=u, nclaim=nclaim, nmsg=nmsg, won=won, n_claims=int(total),
                 n_conflicts=int(nmsg.sum()))
+
+
+def auction(ids, ax, ay, caps, tx, ty, treq, eps=0.1, claim_thr=20.0, u_scale=100.0, use_pow=False,
+            max_rounds=1 << 20):
+    """Jacobi auction over the admissible pairs (swarm_oracle.c orc_auction) -> dict(owner, price,
+    assigned, rounds, bidders, n_pairs).  use_pow=False: the GPU's x*x utility arithmetic."""
+    ids = _c(ids, np.int32)
+    n, t = len(ids), len(tx)
+    owner = np.empty(t, np.int32)
+    price = np.empty(t, np.float32)
+    assigned = np.empty(n, np.int32)
+    bidders = np.zeros(max(1, min(max_rounds, 1 << 20)), np.int64)
+    npairs = np.zeros(1, np.int64)
+    arrs = [_c(ax, np.float64), _c(ay, np.float64), _c(caps, np.uint32)]
+    tarr = [_c(tx, np.float64), _c(ty, np.float64), _c(treq, np.int8)]
+    r = lib().orc_auction(n, _p(ids), *[_p(a) for a in arrs], t, *[_p(a) for a in tarr], claim_thr,
+                          u_scale, int(use_pow), float(eps), len(bidders), _p(owner), _p(price),
+                          _p(assigned), _p(bidders), _p(npairs))
+    return dict(owner=owner, price=price, assigned=assigned, rounds=int(r),
+                bidders=bidders[: max(r, 0)].copy(), n_pairs=int(npairs[0]))
 
 
 def task_claims(ids, ax, ay, caps, tx, ty, treq, claim_thr=20.0, u_scale=100.0, use_pow=True):
@@ -206,3 +228,58 @@ def allocate_py(ids, ax, ay, caps, tx, ty, treq, claim_thr=20.0, hysteresis=5.0)
         util.append(u)
         nmsg.append(m)
     return np.array(winner, np.int32), np.array(util), np.array(nmsg)
+
+
+def auction_py(ids, ax, ay, caps, tx, ty, treq, eps=0.1, claim_thr=20.0, max_rounds=100000):
+    """Straight restatement of the Jacobi auction (tiny inputs only): numpy float32 scalars
+    carry the f32 arithmetic, the x*x utility as on the GPU."""
+    n, t = len(ids), len(tx)
+    f = np.float32
+    cand = []
+    for a in range(n):
+        row = []
+        for k in range(t):
+            dx, dy = float(ax[a]) - float(tx[k]), float(ay[a]) - float(ty[k])
+            d = math.sqrt(dx * dx + dy * dy)
+            has = 0.0 if (int(treq[k]) >= 0 and not (int(caps[a]) >> int(treq[k])) & 1) else 1.0
+            U = (100.0 / (1.0 + d)) * has
+            if U > claim_thr:
+                row.append((k, f(U)))
+        cand.append(row)
+    price = [f(0.0)] * t
+    owner = [-1] * t
+    assigned = [-1] * n
+    out = [False] * n
+    rounds, bidders = 0, []
+    while rounds < max_rounds:
+        bids = {}
+        nb = 0
+        for a in range(n):
+            if assigned[a] >= 0 or out[a]:
+                continue
+            nb += 1
+            best, second, bk = f(-np.inf), f(-np.inf), None
+            for k, x in cand[a]:
+                net = f(x - price[k])
+                if net > best or (net == best and k < bk):
+                    second, best, bk = max(second, best), net, k
+                elif net > second:
+                    second = net
+            if not best > 0:
+                out[a] = True
+                continue
+            second = max(second, f(0.0))
+            bid = f(f(price[bk] + f(best - second)) + f(eps))
+            key = (bid, -int(ids[a]))
+            if bk not in bids or key > bids[bk][0]:
+                bids[bk] = (key, a)
+        if nb == 0:
+            break
+        bidders.append(nb)
+        rounds += 1
+        for k, (key, a) in bids.items():
+            if owner[k] >= 0:
+                assigned[owner[k]] = -1
+            owner[k], assigned[a], price[k] = a, k, key[0]
+    return dict(owner=np.array(owner, np.int32), price=np.array(price, np.float32),
+                assigned=np.array(assigned, np.int32), rounds=rounds, bidders=np.array(bidders, np.int64))

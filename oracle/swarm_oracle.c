@@ -22,6 +22,7 @@
  *                 every accepted claim and every rejected claim from a non-incumbent emits one
  *                 TASK_CONFLICT (322, 325).
  *   orc_rgg_csr   synthetic input builder (not reference code): edge iff dx*dx+dy*dy <= r*r.
+ *   orc_auction   the north star's auction allocation (no reference code; see its comment).
  */
 #include <math.h>
 #include <stdint.h>
@@ -240,4 +241,112 @@ long orc_rgg_csr(long n, const double *x, const double *y, double r, int64_t *ro
     free(start);
     free(kv);
     return (long)row_ptr[n];
+}
+
+/* ------------------------------------------------------------------ auction
+ * No reference counterpart: the north star's "auction price update" allocation, restated here
+ * as the checker of the GPU bid/resolve kernels (parity vs this restatement only).
+ * Jacobi (synchronous) Bertsekas auction over the admissible pairs U > claim_thr -- the
+ * reference's claim rule (agent.py:297) -- with value x = f32(U), the claim payload
+ * (agent.py:302).  Per round every unassigned, active agent a finds, over its admissible
+ * tasks, net = x - price[k] (f32), the best (ties -> lowest task index) and second-best net,
+ * with the opt-out option (net 0) as a competitor: best <= 0 -> a drops out for good (prices
+ * only rise); else it bids price[best] + (best - second) + eps (f32, in that order).  Each task
+ * takes its highest bid, ties -> lowest agent ID (packed key: f32 bits << 32 | ~id), the
+ * previous owner becomes unassigned.  Stops after the first round without bidders;
+ * rounds_exec = rounds that had bidders.  assigned[a] = task index or -1; owner[k] = agent
+ * storage index or -1; bidders[r] = active agents of round r+1. */
+static uint32_t f32_bits(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return u;
+}
+static float bits_f32(uint32_t u) {
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+
+long orc_auction(long n, const int32_t *ids, const double *ax, const double *ay, const uint32_t *caps,
+                 long t, const double *tx, const double *ty, const int8_t *treq, double claim_thr,
+                 double u_scale, int use_pow, float eps, long max_rounds, int32_t *owner, float *price,
+                 int32_t *assigned, int64_t *bidders, int64_t *n_pairs) {
+    int64_t *off = (int64_t *)calloc((size_t)n + 1, sizeof(int64_t));
+#pragma omp parallel for schedule(dynamic, 64)
+    for (long a = 0; a < n; ++a) {
+        int64_t c = 0;
+        for (long k = 0; k < t; ++k)
+            if (util_one(ax[a], ay[a], caps[a], tx[k], ty[k], treq[k], u_scale, use_pow) > claim_thr) ++c;
+        off[a + 1] = c;
+    }
+    for (long a = 0; a < n; ++a) off[a + 1] += off[a];
+    const int64_t np = off[n];
+    int32_t *ck = (int32_t *)malloc(sizeof(int32_t) * (size_t)(np > 0 ? np : 1));
+    float *cv = (float *)malloc(sizeof(float) * (size_t)(np > 0 ? np : 1));
+#pragma omp parallel for schedule(dynamic, 64)
+    for (long a = 0; a < n; ++a) {
+        int64_t p = off[a];
+        for (long k = 0; k < t; ++k) {
+            double U = util_one(ax[a], ay[a], caps[a], tx[k], ty[k], treq[k], u_scale, use_pow);
+            if (U > claim_thr) { ck[p] = (int32_t)k; cv[p] = (float)U; ++p; }
+        }
+    }
+    if (n_pairs) *n_pairs = np;
+    /* id -> storage index via the ascending-ID order */
+    long *order = (long *)malloc(sizeof(long) * (size_t)(n > 0 ? n : 1));
+    for (long i = 0; i < n; ++i) order[i] = i;
+    g_ids = ids;
+    qsort(order, (size_t)n, sizeof(long), cmp_by_id_g);
+    uint8_t *out = (uint8_t *)calloc((size_t)n + 1, 1);
+    uint64_t *key = (uint64_t *)calloc((size_t)t + 1, sizeof(uint64_t));
+    for (long k = 0; k < t; ++k) { owner[k] = -1; price[k] = 0.0f; }
+    for (long a = 0; a < n; ++a) assigned[a] = -1;
+    long r = 0, done = 0;
+    while (r < max_rounds) {
+        int64_t nb = 0;
+        for (long a = 0; a < n; ++a) {
+            if (assigned[a] >= 0 || out[a]) continue;
+            ++nb;
+            float best = -INFINITY, second = -INFINITY;
+            int32_t bk = INT32_MAX;
+            for (int64_t p = off[a]; p < off[a + 1]; ++p) {
+                const float net = cv[p] - price[ck[p]];
+                if (net > best || (net == best && ck[p] < bk)) {
+                    second = best > second ? best : second;
+                    best = net;
+                    bk = ck[p];
+                } else if (net > second) {
+                    second = net;
+                }
+            }
+            if (!(best > 0.0f)) { out[a] = 1; continue; }
+            if (second < 0.0f) second = 0.0f;
+            const float inc = best - second;
+            float bid = price[bk] + inc;
+            bid = bid + eps;
+            const uint64_t kk = ((uint64_t)f32_bits(bid) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)ids[a]);
+            if (kk > key[bk]) key[bk] = kk;
+        }
+        if (nb == 0) { done = 1; break; }
+        if (bidders) bidders[r] = nb;
+        ++r;
+        for (long k = 0; k < t; ++k) {
+            if (!key[k]) continue;
+            const int32_t wid = (int32_t)(0xFFFFFFFFu - (uint32_t)(key[k] & 0xFFFFFFFFu));
+            long lo = 0, hi = n - 1, w = -1;
+            while (lo <= hi) {
+                const long mid = (lo + hi) / 2;
+                const int32_t v = ids[order[mid]];
+                if (v == wid) { w = order[mid]; break; }
+                if (v < wid) lo = mid + 1; else hi = mid - 1;
+            }
+            if (owner[k] >= 0) assigned[owner[k]] = -1;
+            owner[k] = (int32_t)w;
+            assigned[w] = (int32_t)k;
+            price[k] = bits_f32((uint32_t)(key[k] >> 32));
+            key[k] = 0;
+        }
+    }
+    free(off); free(ck); free(cv); free(order); free(out); free(key);
+    return done ? r : -1;
 }
