@@ -1,0 +1,177 @@
+// Physics / formation step on gfx950.
+//
+// Replaces SwarmAgent._update_physics (agent.py:94-181) run by every agent of the swarm, as one
+// synchronous step (contract P1, tools/gen_golden.py): every agent reads the step-start snapshot
+// of all positions (pos_in) and writes its new position to pos_out (double-buffered), so the
+// result does not depend on the order agents are updated in.
+//   formation  a FOLLOWER with a leader targets its V slot behind the leader's position as the
+//              heartbeat carries it ('!ff': f32-rounded, agent.py:256-258, 283-289):
+//              x - 2 id, y + 2 id (even id) / y - 2 id (odd id)  (agent.py:96-111)
+//   forces     attraction to the target beyond 0.5 (118-125); obstacle repulsion, obstacles in
+//              list order (128-146); neighbour separation within 2.0, neighbours in CSR order
+//              (149-160) -- sums in the reference's order, so the result is bit-exact against
+//              the CPU restatement's x*x arithmetic (the reference squares with libm pow: <= 1
+//              ulp per square, checked with a tolerance against its fixtures)
+//   update     speed clamp to max_speed (169-174), Euler step (177-178).
+// One thread per agent (fp64 VALU + the neighbour gathers; the snapshot of the neighbourhood is
+// the HBM traffic: 16 B per edge + 80 B per agent); obstacles staged in LDS per workgroup.
+// A zero distance to an obstacle centre or a neighbour makes the reference raise
+// ZeroDivisionError; here it yields non-finite values and is counted (n_singular).
+#include <cmath>
+
+#include "swarm_common.h"
+
+namespace swarm {
+namespace {
+
+constexpr int kObsLds = 1024;  // obstacles staged in LDS per pass (3 doubles each)
+
+__global__ __launch_bounds__(kBlock) void k_physics(int64_t n, const int32_t *__restrict__ ids,
+                                                   const uint8_t *__restrict__ state,
+                                                   const int32_t *__restrict__ leader,
+                                                   const double2 *__restrict__ pin, double2 *__restrict__ pout,
+                                                   double2 *__restrict__ vel, double2 *__restrict__ tgt,
+                                                   uint8_t *__restrict__ has_t, int64_t m,
+                                                   const double *__restrict__ obs, const int32_t *__restrict__ rp,
+                                                   const int32_t *__restrict__ col, double dt, double max_speed,
+                                                   unsigned long long *__restrict__ singular) {
+    __shared__ double s_obs[kObsLds * 3];
+    unsigned long long sing = 0;
+    for (int64_t base = int64_t(blockIdx.x) * kBlock; base < n; base += int64_t(gridDim.x) * kBlock) {
+        const int64_t i = base + threadIdx.x;
+        const bool valid = i < n;
+        double px = 0, py = 0, frx = 0.0, fry = 0.0;
+        bool moving = false;
+        double2 t = make_double2(0, 0);
+        if (valid) {
+            const double2 p = pin[i];
+            px = p.x;
+            py = p.y;
+            t = tgt[i];
+            bool has = has_t[i] != 0;
+            const int32_t L = leader[i];
+            if (state[i] == SWARM_FOLLOWER && L >= 0) {
+                const double2 lp = pin[L];
+                const double lx = double(float(lp.x)), ly = double(float(lp.y));
+                const double rank = double(ids[i]);
+                const double xo = -2.0 * rank;
+                const double yo = (ids[i] % 2 == 0) ? 2.0 * rank : -2.0 * rank;
+                t = make_double2(lx + xo, ly + yo);
+                tgt[i] = t;
+                if (!has) has_t[i] = 1;
+                has = true;
+            }
+            moving = has;
+        }
+        // obstacles: every workgroup stages them through LDS (all lanes join the barriers)
+        for (int64_t o0 = 0; o0 < m; o0 += kObsLds) {
+            const int64_t cnt = (m - o0 < kObsLds) ? m - o0 : kObsLds;
+            __syncthreads();
+            for (int64_t q = threadIdx.x; q < 3 * cnt; q += kBlock) s_obs[q] = obs[3 * o0 + q];
+            __syncthreads();
+            if (moving)
+                for (int64_t o = 0; o < cnt; ++o) {
+                    const double ox = s_obs[3 * o], oy = s_obs[3 * o + 1], r = s_obs[3 * o + 2];
+                    const double ex = px - ox, ey = py - oy;
+                    double d = sqrt(ex * ex + ey * ey) - r;
+                    if (d <= 0.001) d = 0.001;
+                    if (d < 5.0) {
+                        const double mag = 50.0 * (1.0 / d - 1.0 / 5.0) / (d * d);
+                        const double nrm = sqrt(ex * ex + ey * ey);
+                        sing += nrm == 0.0;
+                        frx += (ex / nrm) * mag;
+                        fry += (ey / nrm) * mag;
+                    }
+                }
+        }
+        if (!moving) continue;
+        double fax = 0.0, fay = 0.0;
+        const double gx = t.x - px, gy = t.y - py;
+        if (sqrt(gx * gx + gy * gy) > 0.5) {
+            fax = 1.0 * gx;
+            fay = 1.0 * gy;
+        }
+        double fsx = 0.0, fsy = 0.0;
+        for (int32_t k = rp[i], e = rp[i + 1]; k < e; ++k) {
+            const double2 q = pin[col[k]];
+            const double ex = px - q.x, ey = py - q.y;
+            double d = sqrt(ex * ex + ey * ey);
+            if (d < 2.0) {
+                if (d <= 0.001) d = 0.001;
+                const double mag = 20.0 / (d * d);
+                const double nrm = sqrt(ex * ex + ey * ey);
+                sing += nrm == 0.0;
+                fsx += (ex / nrm) * mag;
+                fsy += (ey / nrm) * mag;
+            }
+        }
+        const double f0 = fax + frx + fsx, f1 = fay + fry + fsy;
+        const double vmag = sqrt(f0 * f0 + f1 * f1);
+        double2 v;
+        if (vmag > max_speed) {
+            const double scale = max_speed / vmag;
+            v = make_double2(f0 * scale, f1 * scale);
+        } else {
+            v = make_double2(f0, f1);
+        }
+        vel[i] = v;
+        pout[i] = make_double2(px + v.x * dt, py + v.y * dt);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) sing += __shfl_xor(sing, off, 64);
+    if ((threadIdx.x & 63) == 0 && sing) atomicAdd(singular, sing);
+}
+
+// Agents that do not move keep their position in the output buffer.
+__global__ __launch_bounds__(kBlock) void k_physics_copy(int64_t n, const uint8_t *__restrict__ has_t,
+                                                        const uint8_t *__restrict__ state,
+                                                        const int32_t *__restrict__ leader,
+                                                        const double2 *__restrict__ pin, double2 *__restrict__ pout) {
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock)
+        if (!has_t[i] && !(state[i] == SWARM_FOLLOWER && leader[i] >= 0)) pout[i] = pin[i];
+}
+
+}  // namespace
+}  // namespace swarm
+
+extern "C" {
+
+int swarm_physics_step(swarm_ctx *ctx, int64_t n, const int32_t *ids, const uint8_t *state,
+                       const int32_t *leader_index, const double *pos_in, double *pos_out, double *vel,
+                       double *target, uint8_t *has_target, int64_t m, const double *obstacles,
+                       const int32_t *row_ptr, const int32_t *col, double dt, double max_speed,
+                       int64_t *n_singular, void *stream) {
+    using namespace swarm;
+    SW_ARG(ctx != nullptr, "ctx is NULL");
+    SW_ARG(n >= 0 && n < (int64_t(1) << 31) && m >= 0, "sizes out of range");
+    SW_ARG(std::isfinite(dt) && std::isfinite(max_speed), "dt / max_speed must be finite");
+    SW_ARG(n == 0 || (ids && state && leader_index && pos_in && pos_out && vel && target && has_target && row_ptr),
+           "NULL agent array");
+    SW_ARG(m == 0 || obstacles != nullptr, "obstacles is NULL");
+    SW_ARG(pos_in != pos_out || n == 0, "pos_in and pos_out must differ (synchronous step)");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (n_singular) *n_singular = 0;
+    if (n == 0) return SWARM_OK;
+    unsigned long long *d_sing;
+    SW_ALLOC(d_sing, ctx, S_TMP0, 64);
+    SW_HIP(hipMemsetAsync(d_sing, 0, 8, s));
+    // order matters: k_physics_copy reads has_target before k_physics may set it (followers)
+    hipLaunchKernelGGL(k_physics_copy, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s, n, has_target, state,
+                       leader_index, reinterpret_cast<const double2 *>(pos_in), reinterpret_cast<double2 *>(pos_out));
+    SW_LAUNCHED();
+    hipLaunchKernelGGL(k_physics, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, n, ids, state, leader_index,
+                       reinterpret_cast<const double2 *>(pos_in), reinterpret_cast<double2 *>(pos_out),
+                       reinterpret_cast<double2 *>(vel), reinterpret_cast<double2 *>(target), has_target, m, obstacles,
+                       row_ptr, col, dt, max_speed, d_sing);
+    SW_LAUNCHED();
+    if (n_singular) {
+        unsigned long long *h = static_cast<unsigned long long *>(pinned(ctx, 64));
+        if (!h) return SWARM_ERR_OOM;
+        SW_HIP(hipMemcpyAsync(h, d_sing, 8, hipMemcpyDeviceToHost, s));
+        SW_HIP(hipStreamSynchronize(s));
+        *n_singular = int64_t(*h);
+    }
+    return SWARM_OK;
+}
+
+}  // extern "C"

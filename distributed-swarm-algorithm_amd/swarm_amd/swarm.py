@@ -246,6 +246,55 @@ class Swarm:
         stats = {k: getattr(st, k) for k, _ in _lib.AuctionStats._fields_}
         return AuctionResult(owner[:t], price[:t], assigned[: self.n], r, bidders[:r].copy(), rc == _lib.OK, stats)
 
+    # ------------------------------------------------------------------ physics
+    def leader_index(self, leader: torch.Tensor | None = None) -> torch.Tensor:
+        """Storage index of each FOLLOWER's leader (-1 for leaders / unknown IDs), from the
+        election's leader IDs (self.leader after elect())."""
+        leader = self.leader if leader is None else _to(leader, torch.int32, self.device)
+        out = torch.full((self.n,), -1, dtype=torch.int32, device=self.device)
+        idx = self.id_index()
+        if idx is None or self.n == 0:
+            srt, order = torch.sort(self.ids.long())
+            pos = torch.searchsorted(srt, leader.long()).clamp(max=max(self.n - 1, 0))
+            hit = srt[pos] == leader.long()
+            cand = torch.where(hit, order[pos].int(), out)
+        else:
+            ok = (leader >= 0) & (leader < idx.numel())
+            cand = torch.where(ok, idx[leader.clamp(0, idx.numel() - 1).long()], out)
+        return torch.where(self.state == _lib.FOLLOWER, cand, out).contiguous()
+
+    def physics_step(self, obstacles=None, *, sensors=None, leader_index=None, dt: float = 0.1,
+                     max_speed: float = 5.0, steps: int = 1) -> dict:
+        """`steps` synchronous _update_physics steps (agent.py:94-181) of every agent, in place on
+        self.pos (contract P1; swarm_physics_step).  obstacles: (m, 3) [x, y, r]; sensors:
+        (row_ptr, col) over storage indices (default: the neighbour graph); leader_index:
+        default self.leader_index().  Velocity / target state lives on the Swarm."""
+        dev, n = self.device, self.n
+        if not hasattr(self, "vel"):
+            self.vel = torch.zeros((n, 2), dtype=torch.float64, device=dev)
+            self.target = torch.zeros((n, 2), dtype=torch.float64, device=dev)
+            self.has_target = torch.zeros(n, dtype=torch.uint8, device=dev)
+        obs = torch.zeros((0, 3), dtype=torch.float64, device=dev) if obstacles is None else \
+            _to(obstacles, torch.float64, dev).reshape(-1, 3).contiguous()
+        rp, col = sensors if sensors is not None else (self.row_ptr, self.col)
+        if rp is None:
+            raise RuntimeError("no sensor graph: pass sensors=(row_ptr, col) or build_graph()")
+        rp, col = _to(rp, torch.int32, dev), _to(col, torch.int32, dev)
+        li = self.leader_index() if leader_index is None else _to(leader_index, torch.int32, dev)
+        other = torch.empty_like(self.pos)
+        sing = ctypes.c_int64(0)
+        total = 0
+        with torch.cuda.device(dev):
+            for _ in range(int(steps)):
+                _lib.check(_lib.lib().swarm_physics_step(
+                    _lib.ctx(), n, _lib.ptr(self.ids), _lib.ptr(self.state), _lib.ptr(li), _lib.ptr(self.pos),
+                    _lib.ptr(other), _lib.ptr(self.vel), _lib.ptr(self.target), _lib.ptr(self.has_target),
+                    obs.shape[0], _lib.ptr(obs) if obs.numel() else None, _lib.ptr(rp), _lib.ptr(col) if col.numel() else None,
+                    float(dt), float(max_speed), ctypes.byref(sing), _lib.stream()))
+                total += sing.value
+                self.pos, other = other, self.pos
+        return {"singular": total}
+
     # ------------------------------------------------------------------ views / bridge
     def to_input_order(self, storage_tensor) -> np.ndarray:
         """Host copy of a per-agent tensor re-ordered to the caller's input numbering."""

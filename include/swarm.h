@@ -266,6 +266,26 @@ int swarm_auction(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *a
                   int32_t max_rounds, int32_t *owner, float *price, int32_t *assigned, int32_t *rounds_exec,
                   int64_t *bidders_per_round, swarm_auction_stats *stats, void *stream);
 
+/*
+ * Physics / formation step: SwarmAgent._update_physics (agent.py:94-181)
+ * for every agent, as one synchronous step (contract P1): all agents read the step-start
+ * positions pos_in (n x 2 f64) and write pos_out (must differ).  A FOLLOWER (state) with
+ * leader_index >= 0 (storage index of its leader, -1 none) targets its V-formation slot behind
+ * the f32-rounded leader position (the '!ff' heartbeat payload); target (n x 2 f64) /
+ * has_target (n u8) are in/out (agent.py:53 self.target, None = 0).  obstacles: m x 3 f64
+ * (x, y, radius), shared by every agent, applied in order; row_ptr/col: each agent's sensed
+ * neighbours, applied in CSR order.  vel (n x 2 f64): out for every moving agent.  Agents
+ * without a target keep position and velocity (agent.py:113-114).  Arithmetic: fp64, the
+ * reference's order of operations, squares as x*x (the reference uses libm pow; <= 1 ulp per
+ * square).  n_singular (host, may be NULL): zero distances to an obstacle centre or a
+ * neighbour (the reference raises ZeroDivisionError there).
+ */
+int swarm_physics_step(swarm_ctx *ctx, int64_t n, const int32_t *ids, const uint8_t *state,
+                       const int32_t *leader_index, const double *pos_in, double *pos_out, double *vel,
+                       double *target, uint8_t *has_target, int64_t m, const double *obstacles,
+                       const int32_t *row_ptr, const int32_t *col, double dt, double max_speed,
+                       int64_t *n_singular, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

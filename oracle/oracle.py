@@ -54,6 +54,8 @@ def lib():
         L.orc_rgg_csr.argtypes = [l, P, P, d, P, P]
         L.orc_auction.restype = l
         L.orc_auction.argtypes = [l, P, P, P, P, l, P, P, P, d, d, i, ctypes.c_float, l, P, P, P, P, P]
+        L.orc_physics.restype = l
+        L.orc_physics.argtypes = [l, P, P, P, P, P, P, P, P, P, P, l, P, P, P, d, d, l, i]
         L.orc_num_threads.restype = i
         L.orc_set_threads.argtypes = [i]
         _lib = L
@@ -135,6 +137,23 @@ def auction(ids, ax, ay, caps, tx, ty, treq, eps=0.1, claim_thr=20.0, u_scale=10
                           _p(assigned), _p(bidders), _p(npairs))
     return dict(owner=owner, price=price, assigned=assigned, rounds=int(r),
                 bidders=bidders[: max(r, 0)].copy(), n_pairs=int(npairs[0]))
+
+
+def physics(ids, state, leader, x, y, vx, vy, tx, ty, has_t, obs, row_ptr, col, dt=0.1, max_speed=5.0,
+            steps=1, use_pow=True):
+    """Physics steps under contract P1 (swarm_oracle.c orc_physics) -> dict of the new state
+    (x, y, vx, vy, tx, ty, has_t) and `singular` (reference ZeroDivisionError cases)."""
+    o = dict(x=_c(x, np.float64).copy(), y=_c(y, np.float64).copy(), vx=_c(vx, np.float64).copy(),
+             vy=_c(vy, np.float64).copy(), tx=_c(tx, np.float64).copy(), ty=_c(ty, np.float64).copy(),
+             has_t=_c(has_t, np.uint8).copy())
+    ids = _c(ids, np.int32)
+    obs = _c(np.asarray(obs, np.float64).reshape(-1, 3), np.float64)
+    sing = lib().orc_physics(len(ids), _p(ids), _p(_c(state, np.uint8)), _p(_c(leader, np.int32)), _p(o["x"]),
+                             _p(o["y"]), _p(o["vx"]), _p(o["vy"]), _p(o["tx"]), _p(o["ty"]), _p(o["has_t"]),
+                             len(obs), _p(obs), _p(_c(row_ptr, np.int64)), _p(_c(col, np.int32)), float(dt),
+                             float(max_speed), int(steps), int(use_pow))
+    o["singular"] = int(sing)
+    return o
 
 
 def task_claims(ids, ax, ay, caps, tx, ty, treq, claim_thr=20.0, u_scale=100.0, use_pow=True):

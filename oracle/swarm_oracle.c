@@ -23,6 +23,7 @@
  *                 TASK_CONFLICT (322, 325).
  *   orc_rgg_csr   synthetic input builder (not reference code): edge iff dx*dx+dy*dy <= r*r.
  *   orc_auction   the north star's auction allocation (no reference code; see its comment).
+ *   orc_physics   _update_physics (94-181) under the synchronous step contract P1.
  */
 #include <math.h>
 #include <stdint.h>
@@ -349,4 +350,95 @@ long orc_auction(long n, const int32_t *ids, const double *ax, const double *ay,
     }
     free(off); free(ck); free(cv); free(order); free(out); free(key);
     return done ? r : -1;
+}
+
+/* ------------------------------------------------------------------ physics
+ * _update_physics (agent.py:94-181) under the synchronous step contract P1 (tools/gen_golden.py):
+ * every agent reads the step-start snapshot of all positions; a FOLLOWER with a leader targets
+ * the V-formation slot behind the f32-rounded leader position (the '!ff' heartbeat payload,
+ * agent.py:256-258, 283-289): x - 2 id, y + 2 id (even id) or y - 2 id (odd id) (agent.py:96-111);
+ * no target -> no motion (113-114).  Forces (fp64, the reference's order of operations):
+ * attraction (target - p) if |target - p| > 0.5 (118-125); obstacles in list order, d = |p - o| - r
+ * clamped to 0.001, if d < 5: 50 (1/d - 1/5) / d^2 along (p - o)/|p - o| (128-146); neighbours
+ * in CSR order, d = |p - q|, if d < 2: clamped, 20 / d^2 along (p - q)/|p - q| (149-160); speed
+ * clamp to max_speed (169-174); Euler step (177-178).  `**2` is libm pow (use_pow) or x*x.
+ * A zero |p - o| or |p - q| makes the reference raise ZeroDivisionError; here it yields
+ * non-finite values and is counted (return value). */
+long orc_physics(long n, const int32_t *ids, const uint8_t *state, const int32_t *leader, double *x, double *y,
+                 double *vx, double *vy, double *tx, double *ty, uint8_t *has_t, long m, const double *obs,
+                 const int64_t *row_ptr, const int32_t *col, double dt, double max_speed, long steps,
+                 int use_pow) {
+    double *sx = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    double *sy = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    long singular = 0;
+#define SQ(v) (use_pow ? pow((v), 2.0) : (v) * (v))
+    for (long st = 0; st < steps; ++st) {
+        memcpy(sx, x, sizeof(double) * (size_t)n);
+        memcpy(sy, y, sizeof(double) * (size_t)n);
+#pragma omp parallel for schedule(static) reduction(+ : singular)
+        for (long i = 0; i < n; ++i) {
+            const double px = sx[i], py = sy[i];
+            if (state[i] == ST_FOLLOWER && leader[i] >= 0) {
+                const double lx = (double)(float)sx[leader[i]], ly = (double)(float)sy[leader[i]];
+                const double rank = (double)ids[i];
+                const double xo = -2.0 * rank;
+                const double yo = (ids[i] % 2 == 0) ? 2.0 * rank : -2.0 * rank;
+                tx[i] = lx + xo;
+                ty[i] = ly + yo;
+                has_t[i] = 1;
+            }
+            if (!has_t[i]) continue;
+            double fax = 0.0, fay = 0.0;
+            const double dtg = sqrt(SQ(tx[i] - px) + SQ(ty[i] - py));
+            if (dtg > 0.5) {
+                fax = 1.0 * (tx[i] - px);
+                fay = 1.0 * (ty[i] - py);
+            }
+            double frx = 0.0, fry = 0.0;
+            for (long o = 0; o < m; ++o) {
+                const double ox = obs[3 * o], oy = obs[3 * o + 1], r = obs[3 * o + 2];
+                double d = sqrt(SQ(px - ox) + SQ(py - oy)) - r;
+                if (d <= 0.001) d = 0.001;
+                if (d < 5.0) {
+                    const double mag = 50.0 * (1.0 / d - 1.0 / 5.0) / SQ(d);
+                    const double dx = px - ox, dy = py - oy;
+                    const double nrm = sqrt(SQ(dx) + SQ(dy));
+                    if (nrm == 0.0) ++singular;
+                    frx += (dx / nrm) * mag;
+                    fry += (dy / nrm) * mag;
+                }
+            }
+            double fsx = 0.0, fsy = 0.0;
+            for (int64_t k = row_ptr[i]; k < row_ptr[i + 1]; ++k) {
+                const long j = col[k];
+                const double qx = sx[j], qy = sy[j];
+                double d = sqrt(SQ(px - qx) + SQ(py - qy));
+                if (d < 2.0) {
+                    if (d <= 0.001) d = 0.001;
+                    const double mag = 20.0 / SQ(d);
+                    const double dx = px - qx, dy = py - qy;
+                    const double nrm = sqrt(SQ(dx) + SQ(dy));
+                    if (nrm == 0.0) ++singular;
+                    fsx += (dx / nrm) * mag;
+                    fsy += (dy / nrm) * mag;
+                }
+            }
+            const double f0 = fax + frx + fsx, f1 = fay + fry + fsy;
+            const double vmag = sqrt(SQ(f0) + SQ(f1));
+            if (vmag > max_speed) {
+                const double scale = max_speed / vmag;
+                vx[i] = f0 * scale;
+                vy[i] = f1 * scale;
+            } else {
+                vx[i] = f0;
+                vy[i] = f1;
+            }
+            x[i] = px + vx[i] * dt;
+            y[i] = py + vy[i] * dt;
+        }
+    }
+#undef SQ
+    free(sx);
+    free(sy);
+    return singular;
 }

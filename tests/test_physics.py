@@ -1,0 +1,91 @@
+"""Physics / formation step: _update_physics (agent.py:94-181) under the
+synchronous step contract P1 (tools/gen_golden.py).
+
+Parity is pinned by the reference itself: tests/golden/physics_*.npz were produced by driving
+the real _update_physics.  The C oracle (libm pow, as the reference squares with `**2`) must
+reproduce them bit-exactly; the GPU squares with x*x, so it is checked bit-exactly against the
+oracle's x*x restatement and within 1e-12 relative of the reference's fixtures.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_names, load_golden
+
+PHYS = golden_names("physics_")
+KEYS = ("x", "y", "vx", "vy", "tx", "ty", "has_t")
+
+
+def _oracle(oracle_mod, g, use_pow, steps=None):
+    return oracle_mod.physics(g["ids"], g["state"], g["leader"], g["x"], g["y"], g["vx"], g["vy"], g["tx"],
+                              g["ty"], g["has_t"], g["obs"], g["row_ptr"], g["col"], float(g["dt"]), 5.0,
+                              int(g["steps"] if steps is None else steps), use_pow=use_pow)
+
+
+@pytest.mark.parametrize("name", PHYS)
+def test_oracle_matches_reference_fixture(oracle_mod, name):
+    g = load_golden(name)
+    o = _oracle(oracle_mod, g, use_pow=True)
+    for k in KEYS:
+        np.testing.assert_array_equal(o[k], g[k + "_out"], err_msg=k)
+    assert o["singular"] == 0
+    # the x*x arithmetic (the GPU's) stays within a few ulp of the reference's libm pow
+    o2 = _oracle(oracle_mod, g, use_pow=False)
+    for k in ("x", "y", "vx", "vy"):
+        np.testing.assert_allclose(o2[k], g[k + "_out"], rtol=1e-12, atol=1e-12)
+
+
+def _random_case(n, seed, side, m_obs=16, radius=2.5):
+    from swarm_amd import gen
+    rng = np.random.default_rng(seed)
+    x, y = rng.uniform(0, side, n), rng.uniform(0, side, n)
+    ids = rng.permutation(n).astype(np.int32)
+    state = np.where(rng.uniform(size=n) < 0.02, 3, 1).astype(np.uint8)
+    leaders = np.nonzero(state == 3)[0]
+    leader = np.where((state == 1) & (rng.uniform(size=n) < 0.7), rng.choice(leaders, n), -1).astype(np.int32)
+    has_t = (rng.uniform(size=n) < 0.3).astype(np.uint8)
+    tx, ty = rng.uniform(0, side, n), rng.uniform(0, side, n)
+    obs = np.stack([rng.uniform(0, side, m_obs), rng.uniform(0, side, m_obs), rng.uniform(0.2, 2, m_obs)], 1)
+    rp, col = gen.rgg_csr(x, y, radius)
+    return dict(ids=ids, state=state, leader=leader, x=x, y=y, vx=np.zeros(n), vy=np.zeros(n), tx=tx, ty=ty,
+                has_t=has_t, obs=obs, row_ptr=rp, col=col, dt=np.float64(0.1), steps=np.int64(3))
+
+
+def _gpu(g):
+    from swarm_amd.swarm import Swarm
+    s = Swarm(g["ids"], g["x"], g["y"], layout="input", device="cuda")
+    s.state = torch.as_tensor(g["state"], device="cuda")
+    n = len(g["ids"])
+    s.vel = torch.as_tensor(np.stack([g["vx"], g["vy"]], 1), device="cuda").contiguous()
+    s.target = torch.as_tensor(np.stack([g["tx"], g["ty"]], 1), device="cuda").contiguous()
+    s.has_target = torch.as_tensor(g["has_t"], device="cuda")
+    rp = torch.as_tensor(np.asarray(g["row_ptr"], np.int32), device="cuda")
+    col = torch.as_tensor(np.asarray(g["col"], np.int32), device="cuda")
+    r = s.physics_step(g["obs"], sensors=(rp, col), leader_index=g["leader"], dt=float(g["dt"]),
+                       steps=int(g["steps"]))
+    p, v, t = s.pos.cpu().numpy(), s.vel.cpu().numpy(), s.target.cpu().numpy()
+    return dict(x=p[:, 0], y=p[:, 1], vx=v[:, 0], vy=v[:, 1], tx=t[:, 0], ty=t[:, 1],
+                has_t=s.has_target.cpu().numpy(), singular=r["singular"]), n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", PHYS)
+def test_gpu_physics_matches_oracle_and_reference(oracle_mod, name):
+    g = load_golden(name)
+    got, _ = _gpu(g)
+    want = _oracle(oracle_mod, g, use_pow=False)
+    for k in KEYS:
+        np.testing.assert_array_equal(got[k], want[k], err_msg=k)
+    for k in ("x", "y", "vx", "vy"):
+        np.testing.assert_allclose(got[k], g[k + "_out"], rtol=1e-12, atol=1e-12)
+    assert got["singular"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,seed,side", [(5000, 1, 40.0), (200000, 2, 300.0)])
+def test_gpu_physics_random_swarms(oracle_mod, n, seed, side):
+    g = _random_case(n, seed, side)
+    got, _ = _gpu(g)
+    want = _oracle(oracle_mod, g, use_pow=False)
+    for k in KEYS:
+        np.testing.assert_array_equal(got[k], want[k], err_msg=k)

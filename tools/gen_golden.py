@@ -327,6 +327,84 @@ def ref_utility_kat(mod, m=20000, seed=31):
                 claim=(U > 20.0))
 
 
+# ------------------------------------------------------------------ physics (contract P1)
+# _update_physics (agent.py:94-181), batched as synchronous steps.  Step
+# contract P1: snapshot S of every agent's position; every agent gets
+#   sensors['obstacles'] = the shared obstacle list (ox, oy, r), in list order;
+#   sensors['neighbors'] = [(id_u, S[u]) for u in N(v)] in CSR order;
+#   leader_pos = the f32-rounded S[leader] -- the '!ff' heartbeat payload (agent.py:256-258,
+#                283-289) -- for a FOLLOWER with a leader;
+# then runs _update_physics(dt) (position / velocity / target updated in place).
+PHYSICS_CASES = {
+    "physics_n400": dict(n=400, side=18.0, m_obs=12, radius=2.5, steps=3, seed=41),
+    "physics_dense_n200": dict(n=200, side=7.0, m_obs=6, radius=3.0, steps=2, seed=42),
+}
+
+
+def make_physics_inputs(c):
+    n, side, rng = c["n"], c["side"], np.random.default_rng(c["seed"])
+    x = rng.uniform(0, side, n)
+    y = rng.uniform(0, side, n)
+    ids = rng.permutation(n).astype(np.int32)
+    # leaders: the 3 highest IDs; followers: 80 % of the rest follow one of them
+    lead_idx = np.argsort(ids)[-3:]
+    state = np.full(n, 1, np.uint8)
+    state[lead_idx] = 3
+    leader = np.full(n, -1, np.int32)
+    fol = (state == 1) & (rng.uniform(size=n) < 0.8)
+    leader[fol] = lead_idx[rng.integers(0, 3, n)][fol]
+    # explicit targets for the leaders and some free agents; the rest stay put
+    has_t = np.zeros(n, np.uint8)
+    tx = np.zeros(n)
+    ty = np.zeros(n)
+    pick = (state == 3) | ((leader < 0) & (rng.uniform(size=n) < 0.5))
+    has_t[pick] = 1
+    tx[pick] = rng.uniform(-side, 2 * side, pick.sum())
+    ty[pick] = rng.uniform(-side, 2 * side, pick.sum())
+    near = rng.choice(n, size=4, replace=False)  # some targets within the 0.5 tolerance
+    has_t[near] = 1
+    tx[near] = x[near] + rng.uniform(-0.3, 0.3, 4)
+    ty[near] = y[near] + rng.uniform(-0.3, 0.3, 4)
+    vx = rng.uniform(-1, 1, n)
+    vy = rng.uniform(-1, 1, n)
+    obs = np.stack([rng.uniform(0, side, c["m_obs"]), rng.uniform(0, side, c["m_obs"]),
+                    rng.uniform(0.2, 1.5, c["m_obs"])], 1)
+    row_ptr, col = gen.rgg_csr(x, y, c["radius"])
+    return dict(ids=ids, state=state, leader=leader, x=x, y=y, vx=vx, vy=vy, tx=tx, ty=ty, has_t=has_t,
+                obs=obs, row_ptr=np.asarray(row_ptr, np.int64), col=np.asarray(col, np.int32),
+                dt=np.float64(0.1), steps=np.int64(c["steps"]))
+
+
+def ref_physics(mod, inp):
+    n = len(inp["ids"])
+    ags = []
+    for i in range(n):
+        a = mod.SwarmAgent(int(inp["ids"][i]), n)
+        a.state = mod.AgentState(int(inp["state"][i]))
+        a.position = [float(inp["x"][i]), float(inp["y"][i])]
+        a.velocity = [float(inp["vx"][i]), float(inp["vy"][i])]
+        a.target = (float(inp["tx"][i]), float(inp["ty"][i])) if inp["has_t"][i] else None
+        ags.append(a)
+    obstacles = [tuple(float(v) for v in o) for o in inp["obs"]]
+    rp, col = inp["row_ptr"], inp["col"]
+    for _ in range(int(inp["steps"])):
+        snap = [(a.position[0], a.position[1]) for a in ags]
+        for i, a in enumerate(ags):
+            nb = [(int(inp["ids"][j]), snap[j][0], snap[j][1]) for j in col[rp[i]:rp[i + 1]]]
+            a.update_sensors(obstacles, nb)
+            L = int(inp["leader"][i])
+            if L >= 0:  # the heartbeat payload: '!ff' of the leader's position
+                a.leader_pos = struct.unpack("!ff", struct.pack("!ff", *snap[L]))
+        for a in ags:
+            a._update_physics(float(inp["dt"]))
+    out = dict(x_out=np.array([a.position[0] for a in ags]), y_out=np.array([a.position[1] for a in ags]),
+               vx_out=np.array([a.velocity[0] for a in ags]), vy_out=np.array([a.velocity[1] for a in ags]),
+               has_t_out=np.array([a.target is not None for a in ags], np.uint8),
+               tx_out=np.array([a.target[0] if a.target else 0.0 for a in ags]),
+               ty_out=np.array([a.target[1] if a.target else 0.0 for a in ags]))
+    return out
+
+
 def sha_prefix(path):
     with open(path, "rb") as f:
         return hashlib.sha256(f.read()).hexdigest()[:16]
@@ -385,6 +463,18 @@ def main():
                                        edge=bool(c.get("edge")), n_claims=int(out["n_claims"]),
                                        n_conflicts=int(out["n_conflicts"]))
         print(name, "claims", int(out["n_claims"]), "%.1fs" % (time.time() - t0))
+
+    for name, c in PHYSICS_CASES.items():
+        if not want(name):
+            continue
+        inp = make_physics_inputs(c)
+        out = ref_physics(mod, inp)
+        arrays = dict(inp)
+        arrays.update(out)
+        np.savez_compressed(os.path.join(OUT, name + ".npz"), **arrays)
+        index["fixtures"][name] = dict(kind="physics", contract="P1", n=c["n"], steps=c["steps"],
+                                       seed=c["seed"], obstacles=c["m_obs"], radius=c["radius"])
+        print(name, "moved", int((out["x_out"] != inp["x"]).sum()))
 
     if want("utility_kat"):
         kat = ref_utility_kat(mod)
