@@ -28,7 +28,8 @@ EXPORTS = ("swarm_last_error", "swarm_version", "swarm_ctx_create", "swarm_ctx_d
            "swarm_utility", "swarm_build_rgg", "swarm_cell_order", "swarm_frontier_begin",
            "swarm_frontier_step", "swarm_frontier_ghosts", "swarm_frontier_changes",
            "swarm_comm_available", "swarm_comm_unique_id", "swarm_comm_create", "swarm_comm_destroy",
-           "swarm_elect_sharded", "swarm_auction", "swarm_physics_step")
+           "swarm_elect_sharded", "swarm_auction", "swarm_physics_step", "swarm_codec_encode",
+           "swarm_codec_decode")
 
 
 class SwarmError(RuntimeError):
@@ -106,6 +107,8 @@ def load(path: str = LIB_PATH):
         L.swarm_comm_destroy.argtypes = [P]
         L.swarm_elect_sharded.argtypes = [P, P, ctypes.POINTER(Shard), P, P, i32, ctypes.POINTER(i32), P, P]
         L.swarm_physics_step.argtypes = [P, i64, P, P, P, P, P, P, P, P, i64, P, P, P, d, d, ctypes.POINTER(i64), P]
+        L.swarm_codec_encode.argtypes = [P, i64, P, P, P, P, P, P, P, i32, P, i64, P, P, ctypes.POINTER(i64), P]
+        L.swarm_codec_decode.argtypes = [P, i64, P, P, i32, P, P, P, P, P, P, P, P, P, P]
         L.swarm_auction.argtypes = [P, i64, P, P, P, i64, P, P, d, d, ctypes.c_float, i32, P, P, P,
                                     ctypes.POINTER(i32), P, P, P]
         for name in EXPORTS:

@@ -286,6 +286,38 @@ int swarm_physics_step(swarm_ctx *ctx, int64_t n, const int32_t *ids, const uint
                        const int32_t *row_ptr, const int32_t *col, double dt, double max_speed,
                        int64_t *n_singular, void *stream);
 
+/*
+ * Batched wire codec: the reference's transport framing, agent.py:184-214,
+ * for m messages at once.  Big-endian '!BBI' header (type, sender, tick) + payload by type:
+ * 1 HEARTBEAT '!ff' (a, b = leader x, y), 2 ELECTION_ACCLAIM '!B' (the sender ID), 3 COORDINATOR
+ * (none), 4 TASK_CLAIM '!If' (task, a = utility), 5 TASK_CONFLICT '!IB' (task, winner).
+ * wide != 0 widens every u8 ID field to u32 ('!BII' header, '!I' acclaim, '!II' conflict), an
+ * extension for swarms with IDs > 255 that the reference cannot frame.
+ *
+ * encode (device arrays of m; integer fields int64 so out-of-range values are representable):
+ * status[i] = 0 ok, 1 struct.error (an integer field out of range), 2 OverflowError (a finite
+ * value beyond f32), 3 unknown type -- payload checked before header, as the reference packs
+ * them; an errored message takes no bytes.  offsets (device, m+1) = packet offsets into out,
+ * offsets[m] = *total_bytes (host).  out == NULL: sizing call (status/offsets/total only);
+ * otherwise cap must be >= the total (SWARM_ERR_RANGE).  Synchronises the stream (total_bytes).
+ */
+int swarm_codec_encode(swarm_ctx *ctx, int64_t m, const int64_t *type, const int64_t *sender, const int64_t *tick,
+                       const double *a, const double *b, const int64_t *task, const int64_t *winner, int32_t wide,
+                       uint8_t *out, int64_t cap, int64_t *offsets, int8_t *status, int64_t *total_bytes,
+                       void *stream);
+
+/*
+ * decode: packet i is buf[offsets[i] .. offsets[i+1]) (device).  status: 0 handled, 1 dropped
+ * (shorter than the header, agent.py:198-199), 2 unknown type (ignored, no handler), 3 the
+ * handler's unpack raises struct.error (TASK_CLAIM payload != 8 bytes, TASK_CONFLICT != 5 (8
+ * wide)).  Fields not carried by the type are 0; a HEARTBEAT carries a position (has_pos = 1,
+ * a/b as f32) only when its payload is exactly 8 bytes (agent.py:256-258).  TASK_CLAIM
+ * utility -> a.  Asynchronous on stream.
+ */
+int swarm_codec_decode(swarm_ctx *ctx, int64_t m, const uint8_t *buf, const int64_t *offsets, int32_t wide,
+                       int8_t *status, int64_t *type, int64_t *sender, int64_t *tick, float *a, float *b,
+                       int64_t *task, int64_t *winner, uint8_t *has_pos, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -302,3 +302,89 @@ def auction_py(ids, ax, ay, caps, tx, ty, treq, eps=0.1, claim_thr=20.0, max_rou
             owner[k], assigned[a], price[k] = a, k, key[0]
     return dict(owner=np.array(owner, np.int32), price=np.array(price, np.float32),
                 assigned=np.array(assigned, np.int32), rounds=rounds, bidders=np.array(bidders, np.int64))
+
+
+# ----------------------------------------------------------------------------- wire codec (f3)
+# Restatement of the transport framing: SwarmAgent._pack_header / _send_msg (agent.py:184-194),
+# the senders' payloads (heartbeat '!ff' agent.py:283-289, acclaim '!B' 240, coordinator 241,
+# claim '!If' 302, conflict '!IB' 322/325) and on_message_received's dispatch (agent.py:197-214)
+# with the handlers' first unpack (256-258, 305, 328).  Pinned by tests/golden/codec_kat.npz.
+HB, ACCLAIM, COORD, CLAIM, CONFLICT = 1, 2, 3, 4, 5
+
+
+def codec_encode_py(typ, sender, tick, a, b, task, winner, wide=False):
+    """Per message: status (0 ok, 1 struct.error, 2 OverflowError, 3 unknown type) and packet
+    bytes (b"" on error).  Payload packed before the header, as the senders do."""
+    idf = "I" if wide else "B"
+    out_st, out_pk = [], []
+    for ty, s, tk, x, y, t, w in zip(typ, sender, tick, a, b, task, winner):
+        ty, s, tk, t, w = int(ty), int(s), int(tk), int(t), int(w)
+        try:
+            if ty == HB:
+                pl = struct.pack("!ff", float(x), float(y))
+            elif ty == ACCLAIM:
+                pl = struct.pack("!" + idf, s)
+            elif ty == COORD:
+                pl = b""
+            elif ty == CLAIM:
+                pl = struct.pack("!If", t, float(x))
+            elif ty == CONFLICT:
+                pl = struct.pack("!I" + idf, t, w)
+            else:
+                out_st.append(3)
+                out_pk.append(b"")
+                continue
+            pk = struct.pack("!B" + idf + "I", ty, s, tk) + pl
+            out_st.append(0)
+            out_pk.append(pk)
+        except struct.error:
+            out_st.append(1)
+            out_pk.append(b"")
+        except OverflowError:
+            out_st.append(2)
+            out_pk.append(b"")
+    return np.array(out_st, np.int8), out_pk
+
+
+def codec_decode_py(packets, wide=False):
+    """Per packet: the receiver's dispatch.  status 0 handled, 1 dropped (< header), 2 unknown
+    type, 3 the handler's unpack raises; fields as the handler sees them (0 where absent)."""
+    hdr, idf = (9, "I") if wide else (6, "B")
+    keys = ("status", "type", "sender", "tick", "task", "winner", "has_pos")
+    rows = {k: [] for k in keys + ("a", "b")}
+    for pk in packets:
+        r = dict(status=1, type=0, sender=0, tick=0, task=0, winner=0, has_pos=0, a=0.0, b=0.0)
+        if len(pk) >= hdr:
+            r["type"], r["sender"], r["tick"] = struct.unpack("!B" + idf + "I", pk[:hdr])
+            pl = pk[hdr:]
+            r["status"] = 0
+            if r["type"] == HB:
+                if len(pl) == 8:
+                    r["a"], r["b"] = struct.unpack("!ff", pl)
+                    r["has_pos"] = 1
+            elif r["type"] in (ACCLAIM, COORD):
+                pass
+            elif r["type"] == CLAIM:
+                try:
+                    r["task"], r["a"] = struct.unpack("!If", pl)
+                except struct.error:
+                    r["status"] = 3
+            elif r["type"] == CONFLICT:
+                try:
+                    r["task"], r["winner"] = struct.unpack("!I" + idf, pl)
+                except struct.error:
+                    r["status"] = 3
+            else:
+                r["status"] = 2
+        for k in rows:
+            rows[k].append(r[k])
+    out = {k: np.array(rows[k], np.int64) for k in keys}
+    out["a"] = np.array(rows["a"], np.float32)
+    out["b"] = np.array(rows["b"], np.float32)
+    return out
+
+
+def split_packets(buf, lens):
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    raw = bytes(np.asarray(buf, np.uint8))
+    return [raw[off[i]:off[i + 1]] for i in range(len(lens))], off

@@ -1,0 +1,174 @@
+"""Batched wire codec: the transport framing of agent.py:184-214.
+
+Parity is pinned by the reference itself: tests/golden/codec_kat.npz holds messages framed by
+the real senders (_send_heartbeat, _check_election_timeout, _process_tasks,
+_handle_task_claim -> _pack_header) with the exception each raised, and packets (the encoded
+ones plus malformed ones) parsed by the real on_message_received (tools/gen_golden.py
+ref_codec).  The struct-based restatement (oracle.codec_*_py) must reproduce it exactly; the GPU
+(libswarm swarm_codec_encode / swarm_codec_decode) must reproduce both bit-exactly, and at
+large sizes an encode -> decode round trip must return every field (f32-rounded floats).
+"""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+
+DEC_KEYS = ("status", "type", "sender", "tick", "task", "winner", "has_pos", "a", "b")
+
+
+@pytest.fixture(scope="module")
+def kat():
+    return load_golden("codec_kat")
+
+
+def _fields(g):
+    return [g["enc_" + k] for k in ("type", "sender", "tick", "a", "b", "task", "winner")]
+
+
+def test_kat_covers_every_outcome(kat):
+    assert set(np.unique(kat["enc_status"])) == {0, 1, 2}
+    assert set(np.unique(kat["dec_status"])) == {0, 1, 2, 3}
+    assert set(np.unique(kat["enc_type"])) == {1, 2, 3, 4, 5}
+    assert kat["dec_has_pos"].any() and not kat["dec_has_pos"].all()
+
+
+def test_oracle_encode_matches_reference(oracle_mod, kat):
+    st, pk = oracle_mod.codec_encode_py(*_fields(kat))
+    np.testing.assert_array_equal(st, kat["enc_status"])
+    np.testing.assert_array_equal([len(p) for p in pk], kat["enc_len"])
+    np.testing.assert_array_equal(np.frombuffer(b"".join(pk), np.uint8), kat["enc_bytes"])
+
+
+def test_oracle_decode_matches_reference(oracle_mod, kat):
+    pk, _ = oracle_mod.split_packets(kat["dec_bytes"], kat["dec_len"])
+    d = oracle_mod.codec_decode_py(pk)
+    for k in DEC_KEYS:
+        np.testing.assert_array_equal(d[k], kat["dec_" + k], err_msg=k)
+
+
+def _random_msgs(m, seed, wide=False, bad=True):
+    rng = np.random.default_rng(seed)
+    id_max = 2**32 if wide else 256
+    ty = rng.integers(1, 6, m)
+    if bad:
+        ty[rng.uniform(size=m) < 0.01] = rng.integers(6, 9)
+    snd = rng.integers(0, id_max, m)
+    tick = rng.integers(0, 2**32, m)
+    task = rng.integers(0, 2**32, m)
+    win = rng.integers(0, id_max, m)
+    a = rng.normal(0, 1e3, m)
+    b = rng.normal(0, 1e3, m)
+    if bad:
+        for arr, hi in ((snd, id_max), (tick, 2**32), (task, 2**32), (win, id_max)):
+            sel = rng.uniform(size=m) < 0.01
+            arr[sel] = np.where(rng.uniform(size=sel.sum()) < 0.5, -1 - rng.integers(0, 5, sel.sum()),
+                                hi + rng.integers(0, 5, sel.sum()))
+        a[rng.uniform(size=m) < 0.01] = 3.5e38 * np.sign(rng.normal())
+        b[rng.uniform(size=m) < 0.005] = np.inf
+        a[rng.uniform(size=m) < 0.005] = np.nan
+        a[rng.uniform(size=m) < 0.005] = 3.4028235677973366e38  # rounds to FLT_MAX, no overflow
+    return [ty, snd, tick, a, b, task, win]
+
+
+@pytest.mark.parametrize("wide", [False, True])
+def test_oracle_round_trip(oracle_mod, wide):
+    f = _random_msgs(3000, 3, wide=wide)
+    st, pk = oracle_mod.codec_encode_py(*f, wide=wide)
+    assert {0, 1, 2, 3} <= set(np.unique(st))
+    ok = st == 0
+    d = oracle_mod.codec_decode_py([p for p in pk if p], wide=wide)
+    assert (d["status"] == 0).all()
+    for k, v in zip(("type", "sender", "tick"), f[:3]):
+        np.testing.assert_array_equal(d[k], v[ok])
+
+
+# ----------------------------------------------------------------------------- GPU
+
+@pytest.mark.gpu
+def test_gpu_encode_matches_reference(kat):
+    from swarm_amd import codec
+    e = codec.encode(*_fields(kat), device="cuda")
+    np.testing.assert_array_equal(e.status.cpu().numpy(), kat["enc_status"])
+    np.testing.assert_array_equal(np.diff(e.offsets.cpu().numpy()), kat["enc_len"])
+    assert e.total_bytes == kat["enc_bytes"].size
+    np.testing.assert_array_equal(e.buf.cpu().numpy(), kat["enc_bytes"])
+
+
+@pytest.mark.gpu
+def test_gpu_decode_matches_reference(kat):
+    from swarm_amd import codec
+    off = np.concatenate([[0], np.cumsum(kat["dec_len"])])
+    d = codec.decode(kat["dec_bytes"], off, device="cuda")
+    for k in DEC_KEYS:
+        np.testing.assert_array_equal(getattr(d, k).cpu().numpy(), kat["dec_" + k], err_msg=k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wide", [False, True])
+def test_gpu_matches_oracle_random(oracle_mod, wide):
+    from swarm_amd import codec
+    f = _random_msgs(20000, 11 + wide, wide=wide)
+    st, pk = oracle_mod.codec_encode_py(*f, wide=wide)
+    e = codec.encode(*f, wide=wide, device="cuda")
+    np.testing.assert_array_equal(e.status.cpu().numpy(), st)
+    np.testing.assert_array_equal(e.buf.cpu().numpy(), np.frombuffer(b"".join(pk), np.uint8))
+    # decode: the encoded packets with malformed ones spliced in
+    rng = np.random.default_rng(5)
+    pk = [p for p in pk if p]
+    for i in rng.choice(len(pk), 400, replace=False):
+        pk[i] = pk[i][:int(rng.integers(0, len(pk[i])))]
+    want = oracle_mod.codec_decode_py(pk, wide=wide)
+    buf, off = oracle_mod.split_packets(np.frombuffer(b"".join(pk), np.uint8), [len(p) for p in pk])
+    d = codec.decode(np.frombuffer(b"".join(pk), np.uint8), off, wide=wide, device="cuda")
+    assert {0, 1, 3} <= set(np.unique(want["status"]))
+    for k in DEC_KEYS:
+        np.testing.assert_array_equal(getattr(d, k).cpu().numpy(), want[k], err_msg=k)
+
+
+@pytest.mark.gpu
+def test_gpu_round_trip_large():
+    """4M messages: encode -> decode returns every field (size-independent property)."""
+    import torch
+    from swarm_amd import codec
+    m = 1 << 22
+    f = _random_msgs(m, 21, bad=False)
+    e = codec.encode(*f, device="cuda")
+    assert int((e.status != 0).sum()) == 0
+    d = codec.decode(e.buf, e.offsets, device="cuda")
+    assert int((d.status != 0).sum()) == 0
+    ty = torch.as_tensor(f[0], device="cuda")
+    for k, v in zip(("type", "sender", "tick"), f[:3]):
+        assert torch.equal(getattr(d, k), torch.as_tensor(v, device="cuda")), k
+    a32 = torch.as_tensor(f[3], device="cuda").float()
+    b32 = torch.as_tensor(f[4], device="cuda").float()
+    hb, cl, cf = ty == 1, ty == 4, ty == 5
+    assert torch.equal(d.a[hb], a32[hb]) and torch.equal(d.b[hb], b32[hb]) and bool(d.has_pos[hb].all())
+    assert torch.equal(d.a[cl], a32[cl])
+    task = torch.as_tensor(f[5], device="cuda")
+    assert torch.equal(d.task[cl | cf], task[cl | cf])
+    assert torch.equal(d.winner[cf], torch.as_tensor(f[6], device="cuda")[cf])
+
+
+@pytest.mark.gpu
+def test_gpu_empty_and_errors():
+    import torch
+    from swarm_amd import _lib, codec
+    e = codec.encode(np.zeros(0, np.int64), [], [], device="cuda")
+    assert e.total_bytes == 0 and e.offsets.cpu().tolist() == [0]
+    d = codec.decode(np.zeros(0, np.uint8), [0], device="cuda")
+    assert d.status.numel() == 0
+    with pytest.raises(ValueError):
+        codec.decode(np.zeros(4, np.uint8), [0, 6], device="cuda")
+    # undersized output buffer: SWARM_ERR_RANGE, not a write past the end
+    ty = torch.ones(4, dtype=torch.int64, device="cuda")
+    z = torch.zeros(4, dtype=torch.int64, device="cuda")
+    zf = torch.zeros(4, dtype=torch.float64, device="cuda")
+    off = torch.empty(5, dtype=torch.int64, device="cuda")
+    st = torch.empty(4, dtype=torch.int8, device="cuda")
+    buf = torch.empty(10, dtype=torch.uint8, device="cuda")
+    import ctypes
+    tot = ctypes.c_int64()
+    rc = _lib.lib().swarm_codec_encode(_lib.ctx(), 4, *[_lib.ptr(t) for t in (ty, z, z, zf, zf, z, z)], 0,
+                                       _lib.ptr(buf), 10, _lib.ptr(off), _lib.ptr(st), ctypes.byref(tot),
+                                       _lib.stream())
+    assert rc == _lib.ERR_RANGE and tot.value == 56

@@ -405,6 +405,152 @@ def ref_physics(mod, inp):
     return out
 
 
+# ------------------------------------------------------------------ wire codec
+# Encode: messages produced by the reference's own senders (_send_heartbeat, the
+# _check_election_timeout win, _process_tasks, _handle_task_claim) on agents with seeded IDs,
+# ticks and positions, captured at the _send_msg seam (type, payload) and framed with the real
+# _pack_header (agent.py:184-194).  Decode: those packets plus malformed ones through the real
+# on_message_received (agent.py:197-214) with the five handlers replaced by recorders.
+MSG_FIELDS = ("type", "sender", "tick", "a", "b", "task", "winner")
+
+
+class _Rec:
+    def __init__(self):
+        self.calls = []
+
+    def __call__(self, *args, **kw):
+        self.calls.append(args)
+
+    def sent(self):  # _send_msg(msg_type, payload=b'') calls as (type, payload)
+        return [(int(c[0]), c[1] if len(c) > 1 else b"") for c in self.calls]
+
+
+def ref_codec(mod, m=600, seed=51):
+    rng = np.random.default_rng(seed)
+    msgs, packets, status = [], [], []
+
+    def emit(a, mt, payload, fields):
+        try:
+            pkt = a._pack_header(mt) + payload
+            st = 0
+        except struct.error:
+            pkt, st = b"", 1
+        msgs.append(fields)
+        packets.append(pkt)
+        status.append(st)
+
+    for i in range(m):
+        kind = i % 5
+        aid = int(rng.integers(0, 256)) if rng.uniform() > 0.05 else int(rng.integers(256, 1000))
+        a = mod.SwarmAgent(aid, 8)
+        a.tick = int(rng.integers(0, 2**32)) if rng.uniform() > 0.03 else 2**32 + int(rng.integers(0, 9))
+        rec = _Rec()
+        a._send_msg = rec
+        if kind == 0:  # heartbeat: position as '!ff'
+            a.tick -= a.tick % 10
+            big = i % 40 == 0  # beyond the f32 range: struct.pack('!ff') raises OverflowError
+            a.position = [float(rng.uniform(-1e6, 1e6)) * (1e34 if big else 1), float(rng.normal() * 50)]
+            try:
+                a._send_heartbeat()
+            except OverflowError:
+                msgs.append((1, aid, a.tick, a.position[0], a.position[1], 0, 0))
+                packets.append(b"")
+                status.append(2)
+                continue
+            for mt, pl in rec.sent():
+                emit(a, mt, pl, (1, aid, a.tick, a.position[0], a.position[1], 0, 0))
+        elif kind == 1:  # election win: ACCLAIM (!B own id) + COORDINATOR
+            a.state = mod.AgentState.ELECTION_WAIT
+            a.election_wait_start = time.time() - 5.0
+            a.election_delay = 0.0
+            try:
+                a._check_election_timeout()
+            except struct.error:  # '!B' of an ID > 255
+                msgs.append((2, aid, a.tick, 0.0, 0.0, 0, 0))
+                packets.append(b"")
+                status.append(1)
+                continue
+            for mt, pl in rec.sent():
+                emit(a, int(mt), pl, (int(mt), aid, a.tick, 0.0, 0.0, 0, 0))
+        elif kind == 2:  # task claim: '!If' (task id, f32 utility)
+            tid = int(rng.integers(0, 2**32))
+            a.position = [0.0, 0.0]
+            a.tasks = {tid: {"status": "OPEN", "pos": (float(rng.uniform(0, 3)), float(rng.uniform(0, 3)))}}
+            a._process_tasks()
+            util = a._calculate_utility(a.tasks[tid])
+            for mt, pl in rec.sent():
+                emit(a, int(mt), pl, (4, aid, a.tick, util, 0.0, tid, 0))
+        else:  # task conflict: '!IB' (task id, winner)
+            a.state = mod.AgentState.LEADER
+            tid = int(rng.integers(0, 2**32))
+            sender = int(rng.integers(0, 256)) if kind == 3 else int(rng.integers(0, 300))
+            try:
+                a._handle_task_claim(sender, struct.pack("!If", tid, 50.0))
+            except struct.error:
+                msgs.append((5, aid, a.tick, 0.0, 0.0, tid, sender))
+                packets.append(b"")
+                status.append(1)
+                continue
+            for mt, pl in rec.sent():
+                emit(a, int(mt), pl, (int(mt), aid, a.tick, 0.0, 0.0, tid, sender))
+    # decode: the encoded packets + malformed ones
+    dec_in = [p for p in packets if p]
+    for j in range(60):
+        t = int(rng.integers(0, 8))
+        n_pl = int(rng.integers(0, 12))
+        raw = bytes(rng.integers(0, 256, size=int(rng.integers(0, 6)), dtype=np.uint8)) if j % 6 == 0 else \
+            struct.pack("!BBI", t, int(rng.integers(0, 256)), int(rng.integers(0, 2**32))) + \
+            bytes(rng.integers(0, 256, size=n_pl, dtype=np.uint8))
+        dec_in.append(raw)
+    recv = mod.SwarmAgent(7, 8)
+    names = ("_handle_heartbeat", "_handle_election_acclaim", "_handle_coordinator", "_handle_task_claim",
+             "_handle_task_conflict")
+    dec = []
+    for pkt in dec_in:
+        recs = {nm: _Rec() for nm in names}
+        for nm in names:
+            setattr(recv, nm, recs[nm])
+        recv.on_message_received(pkt)
+        hit = [(nm, r.calls[0]) for nm, r in recs.items() if r.calls]
+        row = dict(status=1 if len(pkt) < 6 else 2, type=0, sender=0, tick=0, a=0.0, b=0.0, task=0,
+                   winner=0, has_pos=0)
+        if len(pkt) >= 6:
+            row["type"], row["sender"], row["tick"] = struct.unpack("!BBI", pkt[:6])
+        if hit:
+            nm, args = hit[0]
+            row["status"] = 0
+            pl = args[1] if len(args) > 1 else b""
+            if nm == "_handle_heartbeat" and len(pl) == 8:
+                row["a"], row["b"] = struct.unpack("!ff", pl)
+                row["has_pos"] = 1
+            elif nm == "_handle_task_claim":
+                # the real handler unpacks '!If' first thing: a wrong length raises struct.error
+                try:
+                    row["task"], row["a"] = struct.unpack("!If", pl)
+                except struct.error:
+                    row["status"] = 3
+            elif nm == "_handle_task_conflict":
+                try:
+                    row["task"], row["winner"] = struct.unpack("!IB", pl)
+                except struct.error:
+                    row["status"] = 3
+        dec.append(row)
+    fields = np.array(msgs, dtype=object)
+    out = dict(enc_type=fields[:, 0].astype(np.int64), enc_sender=fields[:, 1].astype(np.int64),
+               enc_tick=fields[:, 2].astype(np.int64), enc_a=fields[:, 3].astype(np.float64),
+               enc_b=fields[:, 4].astype(np.float64), enc_task=fields[:, 5].astype(np.int64),
+               enc_winner=fields[:, 6].astype(np.int64), enc_status=np.array(status, np.int8),
+               enc_len=np.array([len(p) for p in packets], np.int64),
+               enc_bytes=np.frombuffer(b"".join(packets), np.uint8).copy(),
+               dec_len=np.array([len(p) for p in dec_in], np.int64),
+               dec_bytes=np.frombuffer(b"".join(dec_in), np.uint8).copy())
+    for k in ("status", "type", "sender", "tick", "task", "winner", "has_pos"):
+        out["dec_" + k] = np.array([r[k] for r in dec], np.int64)
+    for k in ("a", "b"):
+        out["dec_" + k] = np.array([r[k] for r in dec], np.float32)
+    return out
+
+
 def sha_prefix(path):
     with open(path, "rb") as f:
         return hashlib.sha256(f.read()).hexdigest()[:16]
@@ -475,6 +621,14 @@ def main():
         index["fixtures"][name] = dict(kind="physics", contract="P1", n=c["n"], steps=c["steps"],
                                        seed=c["seed"], obstacles=c["m_obs"], radius=c["radius"])
         print(name, "moved", int((out["x_out"] != inp["x"]).sum()))
+
+    if want("codec_kat"):
+        kat = ref_codec(mod)
+        np.savez_compressed(os.path.join(OUT, "codec_kat.npz"), **kat)
+        index["fixtures"]["codec_kat"] = dict(kind="codec", messages=len(kat["enc_type"]),
+                                              packets=len(kat["dec_len"]), seed=51)
+        print("codec_kat", len(kat["enc_type"]), "messages", len(kat["dec_len"]), "packets",
+              "errors", int((kat["enc_status"] != 0).sum()))
 
     if want("utility_kat"):
         kat = ref_utility_kat(mod)
