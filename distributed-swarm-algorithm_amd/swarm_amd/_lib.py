@@ -29,13 +29,18 @@ EXPORTS = ("swarm_last_error", "swarm_version", "swarm_ctx_create", "swarm_ctx_d
            "swarm_frontier_step", "swarm_frontier_ghosts", "swarm_frontier_changes",
            "swarm_comm_available", "swarm_comm_unique_id", "swarm_comm_create", "swarm_comm_destroy",
            "swarm_elect_sharded", "swarm_auction", "swarm_physics_step", "swarm_codec_encode",
-           "swarm_codec_decode")
+           "swarm_codec_decode", "swarm_protocol_run")
 
 
 class SwarmError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f"libswarm error {code}: {msg}")
         self.code = code
+
+
+class Fsm(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_void_p) for k in ("state", "leader", "last_hb", "wait_start", "delay", "leader_pos",
+                                               "has_leader_pos", "alive", "outbox")]
 
 
 class AllocStats(ctypes.Structure):
@@ -109,6 +114,8 @@ def load(path: str = LIB_PATH):
         L.swarm_physics_step.argtypes = [P, i64, P, P, P, P, P, P, P, P, i64, P, P, P, d, d, ctypes.POINTER(i64), P]
         L.swarm_codec_encode.argtypes = [P, i64, P, P, P, P, P, P, P, i32, P, i64, P, P, ctypes.POINTER(i64), P]
         L.swarm_codec_decode.argtypes = [P, i64, P, P, i32, P, P, P, P, P, P, P, P, P, P]
+        L.swarm_protocol_run.argtypes = [P, i64, P, P, P, P, P, ctypes.POINTER(Fsm), i64, i32, d, d, d,
+                                         ctypes.c_uint64, P, i32, P, P]
         L.swarm_auction.argtypes = [P, i64, P, P, P, i64, P, P, d, d, ctypes.c_float, i32, P, P, P,
                                     ctypes.POINTER(i32), P, P, P]
         for name in EXPORTS:

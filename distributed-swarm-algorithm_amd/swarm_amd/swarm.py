@@ -39,7 +39,10 @@ def _dev(device):
 def _to(a, dtype, device):
     if isinstance(a, torch.Tensor):
         return a.to(device=device, dtype=dtype).contiguous()
-    return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype, device=device)
+    a = np.ascontiguousarray(a)
+    if not a.flags.writeable:  # torch refuses read-only buffers (np.frombuffer, np.load views)
+        a = a.copy()
+    return torch.as_tensor(a, dtype=dtype, device=device)
 
 
 @dataclass
@@ -294,6 +297,59 @@ class Swarm:
                 total += sing.value
                 self.pos, other = other, self.pos
         return {"singular": total}
+
+    # ------------------------------------------------------------------ timer FSM (f2)
+    def _storage(self, a, dtype):
+        """Per-agent array in INPUT order -> storage order on the device."""
+        t = _to(a, dtype, self.device)
+        if t.numel() != self.n:
+            raise ValueError(f"expected {self.n} values, got {t.numel()}")
+        return t[self.perm.long()].contiguous() if self.layout != "input" else t
+
+    def protocol_reset(self, tick_off=None, last_hb=None):
+        """Every agent as SwarmAgent.__init__ leaves it (agent.py:31-39): FOLLOWER, no leader,
+        no leader position, alive, nothing in flight; last_heartbeat_time = last_hb (input
+        order, default 0.0 = the clock at tick 0); tick_off: each agent's tick-counter phase
+        (input order, default 0 = lock-step).  Tick counter restarts at 0."""
+        n, dev = self.n, self.device
+        z = lambda dt: torch.zeros(n, dtype=dt, device=dev)  # noqa: E731
+        self.state.fill_(_lib.FOLLOWER)
+        self.leader.fill_(-1)
+        self.fsm = dict(last_hb=z(torch.float64) if last_hb is None else self._storage(last_hb, torch.float64),
+                        wait_start=z(torch.float64), delay=z(torch.float64),
+                        leader_pos=torch.zeros((n, 2), dtype=torch.float32, device=dev),
+                        has_leader_pos=z(torch.uint8), alive=torch.ones(n, dtype=torch.uint8, device=dev),
+                        outbox=torch.zeros(2 * n, dtype=torch.uint8, device=dev))
+        self.tick_off = z(torch.int32) if tick_off is None else self._storage(tick_off, torch.int32)
+        self.fsm_tick = 0
+        return self
+
+    def protocol_run(self, ticks: int, *, kill_ticks=(), dt: float = 0.1, timeout: float = 3.0,
+                     jitter: float = 0.2, seed: int = 0) -> np.ndarray:
+        """Advance the timer FSM + election handlers `ticks` ticks under contract T1
+        (swarm_protocol_run; agent.py:66-80, 217-289), messages along the neighbour graph.
+        kill_ticks: absolute ticks at whose start every alive LEADER dies.  Returns counts
+        (ticks x 4): alive LEADERs, alive ELECTION_WAITs, ACCLAIM senders, HEARTBEAT senders."""
+        if self.row_ptr is None:
+            raise RuntimeError("no neighbour graph: call build_graph() or set_graph()")
+        if not hasattr(self, "fsm"):
+            self.protocol_reset()
+        f = self.fsm
+        fs = _lib.Fsm(*[_lib.ptr(t) if self.n else None for t in
+                        (self.state, self.leader, f["last_hb"], f["wait_start"], f["delay"], f["leader_pos"],
+                         f["has_leader_pos"], f["alive"], f["outbox"])])
+        kt = np.ascontiguousarray(np.asarray(kill_ticks, np.int64))
+        counts = np.zeros((int(ticks), 4), np.int64)
+        with torch.cuda.device(self.device):
+            _lib.check(_lib.lib().swarm_protocol_run(
+                _lib.ctx(), self.n, _lib.ptr(self.ids) if self.n else None, _lib.ptr(self.pos) if self.n else None,
+                _lib.ptr(self.row_ptr, torch.int32), _lib.ptr(self.col, torch.int32) if self.n_edges else None,
+                _lib.ptr(self.tick_off) if self.n else None, ctypes.byref(fs), self.fsm_tick, int(ticks),
+                float(dt), float(timeout), float(jitter), ctypes.c_uint64(int(seed)),
+                kt.ctypes.data_as(ctypes.c_void_p) if kt.size else None, kt.size,
+                counts.ctypes.data_as(ctypes.c_void_p), _lib.stream()))
+        self.fsm_tick += int(ticks)
+        return counts
 
     # ------------------------------------------------------------------ views / bridge
     def to_input_order(self, storage_tensor) -> np.ndarray:

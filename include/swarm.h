@@ -318,6 +318,40 @@ int swarm_codec_decode(swarm_ctx *ctx, int64_t m, const uint8_t *buf, const int6
                        int8_t *status, int64_t *type, int64_t *sender, int64_t *tick, float *a, float *b,
                        int64_t *task, int64_t *winner, uint8_t *has_pos, void *stream);
 
+/*
+ * Timer FSM / protocol ticks: every agent's update_loop tick
+ * (agent.py:66-80) at once -- inbound ELECTION_ACCLAIM / COORDINATOR / HEARTBEAT handling
+ * (243-281) from the CSR neighbours' previous-tick sends, then _check_election_timeout
+ * (217-241) and the leader's _send_heartbeat (283-289) -- for ticks t0+1 .. t0+ticks under
+ * contract T1 (tools/gen_golden.py ref_fsm): clock = t * dt; agent i's own tick counter is
+ * t + tick_off[i] (heartbeats when it is a multiple of 10); the election jitter is
+ * jitter * u(seed, id, t) with u the splitmix64 hash of tools/gen_golden.py jitter_u.
+ * fsm: device state, in/out (n each unless noted): state (SWARM_*), leader (ID, -1 = None),
+ * last_hb / wait_start / delay (f64 seconds: last_heartbeat_time, election_wait_start,
+ * election_delay), leader_pos (n x 2 f32, the '!ff' heartbeat payload; (0, 0) when None),
+ * has_leader_pos, alive, outbox (2n bytes, tick-parity double buffer: the bytes at parity
+ * (t0 & 1) are the tick-t0 sends; bit 0 ACCLAIM+COORDINATOR, bit 1 HEARTBEAT).
+ * kill_ticks (host, n_kill): at the start of each such tick every alive LEADER dies.
+ * counts (host, ticks x 4, may be NULL): per tick, alive LEADERs, alive ELECTION_WAITs, ACCLAIM
+ * senders, HEARTBEAT senders.  Synchronises the stream when counts != NULL.
+ */
+typedef struct {
+    uint8_t *state;
+    int32_t *leader;
+    double *last_hb;
+    double *wait_start;
+    double *delay;
+    float *leader_pos;
+    uint8_t *has_leader_pos;
+    uint8_t *alive;
+    uint8_t *outbox;
+} swarm_fsm;
+
+int swarm_protocol_run(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *pos, const int32_t *row_ptr,
+                       const int32_t *col, const int32_t *tick_off, const swarm_fsm *fsm, int64_t t0, int32_t ticks,
+                       double dt, double timeout, double jitter, uint64_t seed, const int64_t *kill_ticks,
+                       int32_t n_kill, int64_t *counts, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -50,6 +50,9 @@ def lib():
         L.orc_allocate.argtypes = [l, P, P, P, P, l, P, P, P, d, d, d, i, P, P, P, P, P]
         L.orc_task_claims.restype = l
         L.orc_task_claims.argtypes = [l, P, P, P, P, d, d, ctypes.c_int8, d, d, i, P, P, l]
+        L.orc_protocol.restype = None
+        L.orc_protocol.argtypes = [l, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, l, l, d, d, d,
+                                   ctypes.c_uint64, P, l, P]
         L.orc_rgg_csr.restype = l
         L.orc_rgg_csr.argtypes = [l, P, P, d, P, P]
         L.orc_auction.restype = l
@@ -153,6 +156,34 @@ def physics(ids, state, leader, x, y, vx, vy, tx, ty, has_t, obs, row_ptr, col, 
                              len(obs), _p(obs), _p(_c(row_ptr, np.int64)), _p(_c(col, np.int32)), float(dt),
                              float(max_speed), int(steps), int(use_pow))
     o["singular"] = int(sing)
+    return o
+
+
+def protocol(ids, x, y, row_ptr, col, tick_off, ticks, *, state=None, leader=None, last_hb=None,
+             wait_start=None, delay=None, lpos=None, has_lpos=None, alive=None, outbox=None, t0=0, dt=0.1,
+             timeout=3.0, jitter=0.2, seed=0, kill_ticks=()):
+    """Timer FSM ticks t0+1 .. t0+ticks under contract T1 (swarm_oracle.c orc_protocol) -> dict
+    of the state after the last tick and counts (ticks x 4).  Defaults: the reference's initial
+    agent (FOLLOWER, no leader, last_heartbeat_time 0, alive)."""
+    n = len(ids)
+    o = dict(state=np.full(n, FOLLOWER, np.uint8) if state is None else _c(state, np.uint8).copy(),
+             leader=np.full(n, -1, np.int32) if leader is None else _c(leader, np.int32).copy(),
+             last_hb=np.zeros(n) if last_hb is None else _c(last_hb, np.float64).copy(),
+             wait_start=np.zeros(n) if wait_start is None else _c(wait_start, np.float64).copy(),
+             delay=np.zeros(n) if delay is None else _c(delay, np.float64).copy(),
+             lpos=np.zeros((n, 2), np.float32) if lpos is None else _c(lpos, np.float32).reshape(n, 2).copy(),
+             has_lpos=np.zeros(n, np.uint8) if has_lpos is None else _c(has_lpos, np.uint8).copy(),
+             alive=np.ones(n, np.uint8) if alive is None else _c(alive, np.uint8).copy(),
+             outbox=np.zeros(2 * n, np.uint8) if outbox is None else _c(outbox, np.uint8).copy())
+    kt = _c(np.asarray(kill_ticks, np.int64), np.int64)
+    counts = np.zeros((int(ticks), 4), np.int64)
+    lib().orc_protocol(n, _p(_c(ids, np.int32)), _p(_c(x, np.float64)), _p(_c(y, np.float64)),
+                       _p(_c(row_ptr, np.int64)), _p(_c(col, np.int32)), _p(_c(tick_off, np.int32)),
+                       _p(o["state"]), _p(o["leader"]), _p(o["last_hb"]), _p(o["wait_start"]), _p(o["delay"]),
+                       _p(o["lpos"]), _p(o["has_lpos"]), _p(o["alive"]), _p(o["outbox"]), int(t0), int(ticks),
+                       float(dt), float(timeout), float(jitter), ctypes.c_uint64(int(seed)), _p(kt), len(kt),
+                       _p(counts))
+    o["counts"] = counts
     return o
 
 

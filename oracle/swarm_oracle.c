@@ -24,6 +24,8 @@
  *   orc_rgg_csr   synthetic input builder (not reference code): edge iff dx*dx+dy*dy <= r*r.
  *   orc_auction   the north star's auction allocation (no reference code; see its comment).
  *   orc_physics   _update_physics (94-181) under the synchronous step contract P1.
+ *   orc_protocol  the timer FSM (_check_election_timeout 217-241, _send_heartbeat 283-289) and
+ *                 the election handlers (243-281) ticking under contract T1.
  */
 #include <math.h>
 #include <stdint.h>
@@ -441,4 +443,124 @@ long orc_physics(long n, const int32_t *ids, const uint8_t *state, const int32_t
     free(sx);
     free(sy);
     return singular;
+}
+
+
+/* ---------------------------------------------------------------------- timer FSM (T1) */
+#define ST_WAIT 2
+#define OB_ACCLAIM 1u /* ELECTION_ACCLAIM followed by COORDINATOR (agent.py:240-241) */
+#define OB_HB 2u      /* HEARTBEAT (289) */
+
+/* random.uniform(0, 0.2)'s u: splitmix64 finaliser of (seed, id, tick), 53 high bits
+ * (tools/gen_golden.py jitter_u). */
+static double jitter_u(uint64_t seed, int32_t id, int64_t t) {
+    uint64_t x = seed ^ ((uint64_t)(uint32_t)id * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)t * 0xD1B54A32D192ED03ull);
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    x ^= x >> 31;
+    return (double)(x >> 11) * (1.0 / 9007199254740992.0);
+}
+
+/* Ticks t = t0+1 .. t0+ticks of contract T1 (tools/gen_golden.py ref_fsm).  At tick t (clock
+ * now = t*dt; agent i's own tick counter t + tick_off[i]):
+ *   kills      if t is in kill_ticks, every alive LEADER dies (stops receiving and sending)
+ *   receive    each alive agent handles what its CSR neighbours sent during tick t-1, in CSR
+ *              order; one sender's packets within a tick are ACCLAIM, COORDINATOR, HEARTBEAT or
+ *              just HEARTBEAT(s) -- a bully HEARTBEAT (249-251, 272-275) needs state LEADER,
+ *              which rules out an ACCLAIM in the same tick, and a repeated HEARTBEAT is
+ *              idempotent -- so a two-bit outbox carries them exactly:
+ *                ACCLAIM (263-275): higher sender -> FOLLOWER, leader, liveness;
+ *                  lower sender while LEADER / ELECTION_WAIT -> LEADER, bully heartbeat
+ *                COORDINATOR (277-281): unconditional takeover
+ *                HEARTBEAT (243-261): LEADER hearing a lower sender bullies back and stops;
+ *                  else yield if LEADER, follow, liveness, leader_pos = f32 sender position,
+ *                  ELECTION_WAIT -> FOLLOWER
+ *              a heartbeat is sent only when the agent's own tick % 10 == 0 (288)
+ *   logic      _check_election_timeout (217-241) then the LEADER's _send_heartbeat.
+ * outbox: 2n bytes, tick parity double buffer (in: the tick-t0 outbox at parity t0&1).
+ * counts (ticks x 4): alive LEADERs, alive ELECTION_WAITs, ACCLAIM senders, HEARTBEAT senders. */
+void orc_protocol(long n, const int32_t *ids, const double *x, const double *y, const int64_t *row_ptr,
+                  const int32_t *col, const int32_t *tick_off, uint8_t *state, int32_t *leader, double *last_hb,
+                  double *wait_start, double *delay, float *lpos, uint8_t *has_lpos, uint8_t *alive,
+                  uint8_t *outbox, long t0, long ticks, double dt, double timeout, double jitter, uint64_t seed,
+                  const int64_t *kill_ticks, long n_kill, int64_t *counts) {
+    for (long t = t0 + 1; t <= t0 + ticks; ++t) {
+        const double now = (double)t * dt;
+        const uint8_t *ob_in = outbox + (size_t)((t - 1) & 1) * (size_t)n;
+        uint8_t *ob_out = outbox + (size_t)(t & 1) * (size_t)n;
+        int kill = 0;
+        for (long k = 0; k < n_kill; ++k) kill |= kill_ticks[k] == t;
+        int64_t *cnt = counts + 4 * (t - t0 - 1);
+        cnt[0] = cnt[1] = cnt[2] = cnt[3] = 0;
+        for (long i = 0; i < n; ++i)
+            if (kill && alive[i] && state[i] == ST_LEADER) alive[i] = 0;
+        for (long i = 0; i < n; ++i) {
+            uint8_t ob = 0;
+            if (!alive[i]) {
+                ob_out[i] = 0;
+                continue;
+            }
+            const int32_t me = ids[i];
+            const int hb_tick = ((t + tick_off[i]) % 10) == 0;
+            uint8_t st = state[i];
+            for (int64_t k = row_ptr[i]; k < row_ptr[i + 1]; ++k) {
+                const int32_t j = col[k];
+                const uint8_t o = ob_in[j];
+                const int32_t s = ids[j];
+                if (o & OB_ACCLAIM) {
+                    if (s > me) {
+                        st = ST_FOLLOWER;
+                        leader[i] = s;
+                        last_hb[i] = now;
+                    } else if (s < me && (st == ST_LEADER || st == ST_WAIT)) {
+                        if (st == ST_WAIT) {
+                            st = ST_LEADER;
+                            leader[i] = me;
+                        }
+                        if (hb_tick) ob |= OB_HB;
+                    }
+                    leader[i] = s; /* COORDINATOR */
+                    st = ST_FOLLOWER;
+                    last_hb[i] = now;
+                }
+                if (o & OB_HB) {
+                    if (st == ST_LEADER && s < me) {
+                        if (hb_tick) ob |= OB_HB;
+                    } else {
+                        if (st == ST_LEADER && s > me) st = ST_FOLLOWER;
+                        leader[i] = s;
+                        last_hb[i] = now;
+                        lpos[2 * i] = (float)x[j];
+                        lpos[2 * i + 1] = (float)y[j];
+                        has_lpos[i] = 1;
+                        if (st == ST_WAIT) st = ST_FOLLOWER;
+                    }
+                }
+            }
+            if (st != ST_LEADER) {
+                if (st == ST_FOLLOWER && now - last_hb[i] > timeout) {
+                    st = ST_WAIT;
+                    wait_start[i] = now;
+                    delay[i] = 0.0 + jitter * jitter_u(seed, me, t);
+                    leader[i] = -1;
+                    has_lpos[i] = 0; /* leader_pos = None: stored as (0, 0) */
+                    lpos[2 * i] = lpos[2 * i + 1] = 0.0f;
+                }
+                if (st == ST_WAIT && now - wait_start[i] > delay[i]) {
+                    st = ST_LEADER;
+                    leader[i] = me;
+                    ob |= OB_ACCLAIM;
+                }
+            }
+            if (st == ST_LEADER && hb_tick) ob |= OB_HB;
+            state[i] = st;
+            ob_out[i] = ob;
+        }
+        for (long i = 0; i < n; ++i) {
+            cnt[0] += alive[i] && state[i] == ST_LEADER;
+            cnt[1] += alive[i] && state[i] == ST_WAIT;
+            cnt[2] += (ob_out[i] & OB_ACCLAIM) != 0;
+            cnt[3] += (ob_out[i] & OB_HB) != 0;
+        }
+    }
 }

@@ -1,0 +1,153 @@
+"""Timer FSM / protocol ticks: _check_election_timeout (agent.py:217-241),
+_send_heartbeat (283-289) and the election handlers (243-281) ticking under contract T1.
+
+Parity is pinned by the reference itself: tests/golden/fsm_*.npz were produced by ticking real
+SwarmAgent objects (their clock and jitter draw patched to the contract's, packets framed by
+_pack_header and delivered through on_message_received; tools/gen_golden.py ref_fsm), with
+phase-shifted agents and leader kills (fsm_n200, fsm_wide_n800) and in lock-step
+(fsm_lockstep_n150, where the optimistic COORDINATOR takeover makes simultaneous winners
+depose each other).  The C oracle must reproduce them exactly, and the GPU
+(swarm_protocol_run) must match both bit for bit.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden_names, load_golden
+
+FSM = golden_names("fsm_")
+OUT = ("state", "leader", "last_hb", "wait_start", "delay", "has_lpos", "lpos", "alive")
+F, W, L = 1, 2, 3
+
+
+def _run_oracle(oracle_mod, g, **kw):
+    return oracle_mod.protocol(g["ids"], g["x"], g["y"], g["row_ptr"], g["col"], g["tick_off"], int(g["ticks"]),
+                               last_hb=g["last_hb0"], dt=float(g["dt"]), seed=int(g["seed"]),
+                               kill_ticks=g["kill_ticks"], **kw)
+
+
+@pytest.mark.parametrize("name", FSM)
+def test_oracle_matches_reference_fixture(oracle_mod, name):
+    g = load_golden(name)
+    o = _run_oracle(oracle_mod, g)
+    for k in OUT:
+        np.testing.assert_array_equal(o[k], g[k + "_out"], err_msg=k)
+    np.testing.assert_array_equal(o["counts"], g["counts"])
+
+
+def test_fixtures_exercise_the_fsm():
+    g = load_golden("fsm_n200")
+    c = g["counts"]
+    assert c[:, 0].max() > 0 and c[:, 1].sum() > 0 and c[:, 2].sum() > 0 and c[:, 3].sum() > 0
+    assert g["alive_out"].sum() < len(g["ids"])           # the kills removed leaders
+    k = int(g["kill_ticks"][0])
+    assert c[k - 1, 0] < c[k - 2, 0]                       # ... and leadership dropped at the kill
+    assert c[k - 1 + 28:, 0].max() > 0                     # ... and re-election follows the timeout
+    lock = load_golden("fsm_lockstep_n150")["counts"]
+    assert lock[:, 2].sum() > 0 and lock[-20:, 0].max() == 0  # winners depose each other
+
+
+def test_oracle_chunked_equals_one_run(oracle_mod):
+    g = load_golden("fsm_wide_n800")
+    full = _run_oracle(oracle_mod, g)
+    a = oracle_mod.protocol(g["ids"], g["x"], g["y"], g["row_ptr"], g["col"], g["tick_off"], 77,
+                            last_hb=g["last_hb0"], dt=float(g["dt"]), seed=int(g["seed"]), kill_ticks=g["kill_ticks"])
+    b = oracle_mod.protocol(g["ids"], g["x"], g["y"], g["row_ptr"], g["col"], g["tick_off"], int(g["ticks"]) - 77,
+                            t0=77, dt=float(g["dt"]), seed=int(g["seed"]), kill_ticks=g["kill_ticks"],
+                            **{k: a[k] for k in OUT + ("outbox",) if k in a})
+    for k in OUT:
+        np.testing.assert_array_equal(b[k], full[k], err_msg=k)
+    np.testing.assert_array_equal(np.concatenate([a["counts"], b["counts"]]), full["counts"])
+
+
+def test_oracle_reference_unit_scenarios(oracle_mod):
+    """test_election.py's FSM cases (22-71) restated as ticks of one / two agents."""
+    empty = np.zeros(2, np.int64), np.zeros(0, np.int32)
+    # timeout trigger (22-30): 5 s of silence > 3 s -> ELECTION_WAIT, wait started
+    o = oracle_mod.protocol([1], [0.0], [0.0], *empty, [1], 1, last_hb=[-4.9], dt=0.1)
+    assert o["state"][0] == W and o["wait_start"][0] == 0.1 and 0.0 <= o["delay"][0] < 0.2
+    # victory after the wait (32-45): LEADER, leader_id = self, ACCLAIM (+ COORDINATOR) sent
+    o = oracle_mod.protocol([1], [0.0], [0.0], *empty, [1], 1, state=[W], wait_start=[-1.0], delay=[0.1], dt=0.1)
+    assert o["state"][0] == L and o["leader"][0] == 1 and o["counts"][0, 2] == 1
+    # submission to a higher acclaim (47-56) and bullying a lower one (58-71): agents 1 and 2,
+    # both LEADER; 2 has just sent ACCLAIM, 1 hears it and backs down ...
+    rp, col = np.array([0, 1, 2]), np.array([1, 0], np.int32)
+    ob = np.zeros(4, np.uint8)
+    ob[1] = 1  # tick-0 outbox (parity 0): agent index 1 (ID 2) acclaimed
+    o = oracle_mod.protocol([1, 2], [0.0, 1.0], [0.0, 0.0], rp, col, [0, 0], 1, state=[L, L], leader=[1, 2],
+                            outbox=ob, dt=0.1)
+    assert o["state"][0] == F and o["leader"][0] == 2
+    # ... while 2, hearing 1's acclaim on a heartbeat tick (own tick % 10 == 0), bullies back
+    ob = np.zeros(4, np.uint8)
+    ob[0] = 1
+    o = oracle_mod.protocol([1, 2], [0.0, 1.0], [0.0, 0.0], rp, col, [0, 9], 1, state=[L, L], leader=[1, 2],
+                            outbox=ob, dt=0.1)
+    assert o["outbox"][2 + 1] & 2  # heartbeat sent by ID 2 (the COORDINATOR then takes it over)
+
+
+# ----------------------------------------------------------------------------- GPU
+
+def _gpu_swarm(g, layout="spatial"):
+    from swarm_amd.swarm import Swarm
+    s = Swarm(g["ids"], g["x"], g["y"], layout=layout, device="cuda")
+    s.set_graph(g["row_ptr"], g["col"])
+    s.protocol_reset(tick_off=g["tick_off"], last_hb=g["last_hb0"])
+    return s
+
+
+def _gpu_state(s):
+    f = s.fsm
+    out = dict(state=s.state, leader=s.leader, last_hb=f["last_hb"], wait_start=f["wait_start"], delay=f["delay"],
+               has_lpos=f["has_leader_pos"], lpos=f["leader_pos"], alive=f["alive"])
+    return {k: s.to_input_order(v) for k, v in out.items()}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", FSM)
+@pytest.mark.parametrize("layout", ["spatial", "input"])
+def test_gpu_matches_reference_fixture(name, layout):
+    g = load_golden(name)
+    s = _gpu_swarm(g, layout)
+    counts = s.protocol_run(int(g["ticks"]), kill_ticks=g["kill_ticks"], dt=float(g["dt"]), seed=int(g["seed"]))
+    got = _gpu_state(s)
+    for k in OUT:
+        np.testing.assert_array_equal(got[k], g[k + "_out"], err_msg=k)
+    np.testing.assert_array_equal(counts, g["counts"])
+
+
+def _random_case(n, seed, side):
+    from swarm_amd import gen
+    rng = np.random.default_rng(seed)
+    x, y = rng.uniform(0, side, n), rng.uniform(0, side, n)
+    ids = rng.permutation(n).astype(np.int32)
+    rp, col = gen.rgg_csr(x, y, 1.0)
+    off = rng.integers(0, 40, n).astype(np.int32)
+    return dict(ids=ids, x=x, y=y, row_ptr=np.asarray(rp, np.int64), col=np.asarray(col, np.int32), tick_off=off,
+                last_hb0=-(off * 0.1), dt=np.float64(0.1), seed=np.uint64(seed))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,seed,side", [(20000, 1, 50.0), (300000, 2, 180.0)])
+def test_gpu_matches_oracle_random(oracle_mod, n, seed, side):
+    g = _random_case(n, seed, side)
+    g["ticks"], g["kill_ticks"] = np.int64(150), np.array([60, 61, 110], np.int64)
+    want = _run_oracle(oracle_mod, g)
+    s = _gpu_swarm(g)
+    c1 = s.protocol_run(64, kill_ticks=g["kill_ticks"], seed=seed)   # in two chunks: the state and the
+    c2 = s.protocol_run(86, kill_ticks=g["kill_ticks"], seed=seed)   # in-flight outbox carry over
+    got = _gpu_state(s)
+    for k in OUT:
+        np.testing.assert_array_equal(got[k], want[k], err_msg=k)
+    np.testing.assert_array_equal(np.concatenate([c1, c2]), want["counts"])
+    assert want["counts"][:, 0].max() > 0 and want["alive"].sum() < n
+
+
+@pytest.mark.gpu
+def test_gpu_empty_and_isolated():
+    from swarm_amd.swarm import Swarm
+    s = Swarm(np.zeros(0, np.int32), [], [], device="cuda")
+    s.set_graph(np.zeros(1, np.int64), np.zeros(0, np.int32))
+    assert s.protocol_run(5).shape == (5, 4)
+    s = Swarm(np.arange(3, dtype=np.int32), [0.0, 10.0, 20.0], [0.0, 0.0, 0.0], device="cuda")
+    s.set_graph(np.zeros(4, np.int64), np.zeros(0, np.int32))  # nobody hears anybody
+    c = s.protocol_run(40)
+    assert c[30, 1] == 3 and c[-1, 0] == 3  # all time out at t=31 (3.1 s > 3.0 s), then all lead

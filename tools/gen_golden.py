@@ -382,6 +382,7 @@ def ref_physics(mod, inp):
         a = mod.SwarmAgent(int(inp["ids"][i]), n)
         a.state = mod.AgentState(int(inp["state"][i]))
         a.position = [float(inp["x"][i]), float(inp["y"][i])]
+        a.last_heartbeat_time = float(inp["last_hb0"][i])
         a.velocity = [float(inp["vx"][i]), float(inp["vy"][i])]
         a.target = (float(inp["tx"][i]), float(inp["ty"][i])) if inp["has_t"][i] else None
         ags.append(a)
@@ -551,6 +552,125 @@ def ref_codec(mod, m=600, seed=51):
     return out
 
 
+
+# ----------------------------------------------------------------------------- timer FSM (f2)
+# Contract T1 (lock-step protocol simulation): time advances in ticks of dt; at tick t
+# (clock = t * dt, self.tick = t + tick_off[i]: agents' loops run at the same rate but out of
+# phase, and were started at different times: last_heartbeat_time starts at last_hb0[i]) every
+# alive agent first receives, through the real
+# on_message_received, the packets its sensor neighbours sent during tick t-1 (neighbours in
+# CSR order, each neighbour's packets in the order it sent them), then runs the real
+# _process_logic (_check_election_timeout, the leader's _send_heartbeat, _process_tasks with
+# no tasks).  random.uniform(a, b) inside the FSM is a + (b - a) * u with u = jitter_u(seed,
+# id, t) (a counter-based hash, so every implementation draws the same jitter).  Agents killed
+# at the start of tick t (kill_ticks: every agent that is LEADER then) stop receiving and
+# sending; packets they sent before still arrive.
+
+def jitter_u(seed, agent_id, t):
+    """u in [0, 1): splitmix64 finaliser of (seed, id, tick); 53 high bits."""
+    M = (1 << 64) - 1
+    x = (seed ^ ((agent_id & 0xFFFFFFFF) * 0x9E3779B97F4A7C15) ^ (t * 0xD1B54A32D192ED03)) & M
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & M
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & M
+    x ^= x >> 31
+    return (x >> 11) * (1.0 / (1 << 53))
+
+
+class _FsmWide(WideStruct):
+    _MAP = {"!B": "!I", "!IB": "!II", "!BBI": "!BII"}
+
+
+FSM_CASES = {
+    "fsm_n200": dict(n=200, side=14.0, radius=2.5, ticks=260, kill_ticks=(90, 180), seed=61, dt=0.1),
+    "fsm_lockstep_n150": dict(n=150, side=12.0, radius=2.5, ticks=120, kill_ticks=(), seed=63, dt=0.1, phase=1),
+    "fsm_wide_n800": dict(n=800, side=22.0, radius=2.2, ticks=200, kill_ticks=(70, 140), seed=62, dt=0.1,
+                          id_scale=5),
+}
+
+
+def make_fsm_inputs(c):
+    n, rng = c["n"], np.random.default_rng(c["seed"])
+    x = rng.uniform(0, c["side"], n)
+    y = rng.uniform(0, c["side"], n)
+    ids = (rng.permutation(n) * c.get("id_scale", 1) + rng.integers(0, c.get("id_scale", 1), n)).astype(np.int32)
+    row_ptr, col = gen.rgg_csr(x, y, c["radius"])
+    off = rng.integers(0, c.get("phase", 40), n).astype(np.int32)
+    return dict(ids=ids, x=x, y=y, row_ptr=np.asarray(row_ptr, np.int64), col=np.asarray(col, np.int32),
+                tick_off=off, last_hb0=-(off * c["dt"]), ticks=np.int64(c["ticks"]), kill_ticks=np.asarray(c["kill_ticks"], np.int64),
+                seed=np.uint64(c["seed"] * 7919), dt=np.float64(c["dt"]))
+
+
+def ref_fsm(mod, inp):
+    import types
+    n = len(inp["ids"])
+    ids, rp, col = inp["ids"], inp["row_ptr"], inp["col"]
+    wide = int(ids.max()) > 255
+    mod.struct = _FsmWide(struct) if wide else struct
+    clock = [0.0]
+    cur = [0, 0]
+    seed, dt = int(inp["seed"]), float(inp["dt"])
+    mod.time = types.SimpleNamespace(time=lambda: clock[0], sleep=_noop)
+    mod.random = types.SimpleNamespace(uniform=lambda a, b: a + (b - a) * jitter_u(seed, cur[0], cur[1]))
+    agents = [mod.SwarmAgent(int(ids[i]), n) for i in range(n)]  # last_heartbeat_time = clock 0.0
+    out_prev = [[] for _ in range(n)]
+    out_cur = [[] for _ in range(n)]
+    for i, a in enumerate(agents):
+        a.position = [float(inp["x"][i]), float(inp["y"][i])]
+        a.last_heartbeat_time = float(inp["last_hb0"][i])
+
+        def send(mt, payload=b"", a=a, i=i):
+            out_cur[i].append(a._pack_header(mt) + payload)
+        a._send_msg = send
+    alive = np.ones(n, bool)
+    kills = set(int(k) for k in inp["kill_ticks"])
+    L, W = mod.AgentState.LEADER, mod.AgentState.ELECTION_WAIT
+    counts = np.zeros((int(inp["ticks"]), 4), np.int64)  # leaders, waiting, acclaim senders, hb senders
+    for t in range(1, int(inp["ticks"]) + 1):
+        clock[0] = t * dt
+        if t in kills:
+            for i, a in enumerate(agents):
+                if alive[i] and a.state == L:
+                    alive[i] = False
+        for i, a in enumerate(agents):
+            if not alive[i]:
+                continue
+            a.tick = t + int(inp["tick_off"][i])
+            for k in range(rp[i], rp[i + 1]):
+                for pkt in out_prev[col[k]]:
+                    if wide:  # on_message_received slices a 6-byte header: dispatch as it does
+                        mt, snd, _ = struct.unpack("!BII", pkt[:9])
+                        pl = pkt[9:]
+                        {1: lambda: a._handle_heartbeat(snd, pl), 2: lambda: a._handle_election_acclaim(snd),
+                         3: lambda: a._handle_coordinator(snd)}[mt]()
+                    else:
+                        a.on_message_received(pkt)
+        for i, a in enumerate(agents):
+            if not alive[i]:
+                continue
+            cur[0], cur[1] = int(ids[i]), t
+            a.tick = t + int(inp["tick_off"][i])
+            a._process_logic()
+        for i, a in enumerate(agents):
+            types_sent = {pk[0] for pk in out_cur[i]}
+            counts[t - 1, 2] += 2 in types_sent
+            counts[t - 1, 3] += 1 in types_sent
+            if alive[i]:
+                counts[t - 1, 0] += a.state == L
+                counts[t - 1, 1] += a.state == W
+        out_prev, out_cur = out_cur, [[] for _ in range(n)]
+    mod.struct, mod.time, mod.random = struct, time, __import__("random")
+    st = np.array([a.state.value for a in agents], np.uint8)
+    return dict(state_out=st, leader_out=np.array([-1 if a.leader_id is None else a.leader_id for a in agents],
+                                                   np.int32),
+                last_hb_out=np.array([a.last_heartbeat_time for a in agents], np.float64),
+                wait_start_out=np.array([a.election_wait_start for a in agents], np.float64),
+                delay_out=np.array([a.election_delay for a in agents], np.float64),
+                has_lpos_out=np.array([a.leader_pos is not None for a in agents], np.uint8),
+                lpos_out=np.array([a.leader_pos if a.leader_pos is not None else (0.0, 0.0) for a in agents],
+                                  np.float32).reshape(n, 2),
+                alive_out=alive.astype(np.uint8), counts=counts)
+
+
 def sha_prefix(path):
     with open(path, "rb") as f:
         return hashlib.sha256(f.read()).hexdigest()[:16]
@@ -621,6 +741,20 @@ def main():
         index["fixtures"][name] = dict(kind="physics", contract="P1", n=c["n"], steps=c["steps"],
                                        seed=c["seed"], obstacles=c["m_obs"], radius=c["radius"])
         print(name, "moved", int((out["x_out"] != inp["x"]).sum()))
+
+    for name, c in FSM_CASES.items():
+        if not want(name):
+            continue
+        t0 = time.time()
+        inp = make_fsm_inputs(c)
+        out = ref_fsm(mod, inp)
+        arrays = dict(inp)
+        arrays.update(out)
+        np.savez_compressed(os.path.join(OUT, name + ".npz"), **arrays)
+        index["fixtures"][name] = dict(kind="fsm", contract="T1", n=c["n"], ticks=c["ticks"], seed=c["seed"],
+                                       kill_ticks=list(c["kill_ticks"]), radius=c["radius"],
+                                       final_leaders=int(out["counts"][-1, 0]))
+        print(name, "leaders per 10 ticks", out["counts"][::10, 0].tolist(), "%.1fs" % (time.time() - t0))
 
     if want("codec_kat"):
         kat = ref_codec(mod)
