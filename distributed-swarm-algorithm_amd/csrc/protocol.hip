@@ -14,16 +14,26 @@
 //             ELECTION_WAIT past its delay -> LEADER + ELECTION_ACCLAIM + COORDINATOR;
 //   sends     into its outbox byte (tick-parity double buffer): bit 0 ACCLAIM+COORDINATOR,
 //             bit 1 HEARTBEAT -- exact, see swarm_oracle.c orc_protocol.
-// A tick reads, per agent, its ~24 B of state plus a CSR row (4 B per edge) and one outbox byte
-// per neighbour (spatially ordered agents: mostly L2 hits); sender IDs and positions are read
-// only for neighbours that sent something.  HBM-bound, no arithmetic worth the name.
+// Push mode (the hearers CSR given), three launches per tick:
+//   k_compact  the mail bitmap (1 bit per agent, set by last tick's senders) -> a list of
+//              receivers (one workgroup-aggregated atomic per workgroup pass), words cleared;
+//   k_receive  one thread per listed receiver walks its CSR row (col / outbox loads in chunks
+//              of kRecv, all in flight) and applies the handlers in CSR order;
+//   k_sweep    one thread per agent: timers, sends, mail bits for the hearers of every sender
+//              (64-bit atomicOr, combined per word), per-tick counters.
+// A quiet agent costs ~12 B (alive, state, outbox byte, its 8-byte timer); only receivers pay
+// for their rows.  Pull mode (no hearers CSR): one fused launch in which every agent walks
+// its row -- the cross-check.  Both are latency-bound gathers, no arithmetic worth the name.
 // Agents killed at a kill tick (every alive LEADER then) stop receiving and sending.
+#include <cmath>
+
 #include "swarm_common.h"
 
 namespace swarm {
 namespace {
 
 constexpr uint8_t kAcclaim = 1, kHeartbeat = 2;
+constexpr int kRecv = 8;  // CSR entries loaded per receive chunk
 constexpr uint8_t ST_F = SWARM_FOLLOWER, ST_W = SWARM_ELECTION_WAIT, ST_L = SWARM_LEADER;
 
 __device__ __forceinline__ double jitter_u(uint64_t seed, int32_t id, int64_t t) {
@@ -48,13 +58,142 @@ __global__ __launch_bounds__(kBlock) void k_kill_leaders(int64_t n, const uint8_
         if (alive[i] && state[i] == ST_L) alive[i] = 0;
 }
 
-__global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int32_t *__restrict__ ids,
-                                                const double2 *__restrict__ pos, const int32_t *__restrict__ rp,
-                                                const int32_t *__restrict__ col,
-                                                const int32_t *__restrict__ tick_off, Fsm f,
-                                                const uint8_t *__restrict__ ob_in, uint8_t *__restrict__ ob_out,
-                                                double dt, double timeout, double jitter, uint64_t seed,
-                                                unsigned long long *__restrict__ counts) {
+// Handlers for everything agent (me) hears in CSR row [b, e) (see the header).  The row in
+// chunks of kRecv: all column loads, then all outbox loads in flight, then the handlers in CSR
+// order on registers; sender IDs only for neighbours that sent something.
+struct Heard {
+    uint8_t st, ob;
+    bool live, lead_set;
+    int32_t lead, hb_from;  // hb_from: the last accepted heartbeat's sender (its position -> leader_pos)
+};
+
+__device__ __forceinline__ void receive_row(int32_t b, int32_t e, const int32_t *__restrict__ col,
+                                            const uint8_t *__restrict__ ob_in, const int32_t *__restrict__ ids,
+                                            int32_t me, bool hb_tick, Heard &h) {
+    for (int32_t k0 = b; k0 < e; k0 += kRecv) {
+        int32_t jj[kRecv];
+        uint8_t oo[kRecv];
+#pragma unroll
+        for (int u = 0; u < kRecv; ++u) jj[u] = k0 + u < e ? col[k0 + u] : -1;
+        uint8_t any = 0;
+#pragma unroll
+        for (int u = 0; u < kRecv; ++u) {
+            oo[u] = jj[u] >= 0 ? ob_in[jj[u]] : uint8_t(0);
+            any |= oo[u];
+        }
+        if (!any) continue;
+        int32_t ss[kRecv];  // the senders' IDs, all loads in flight
+#pragma unroll
+        for (int u = 0; u < kRecv; ++u) ss[u] = oo[u] ? ids[jj[u]] : 0;
+#pragma unroll
+        for (int u = 0; u < kRecv; ++u) {
+            const uint8_t o = oo[u] & (kAcclaim | kHeartbeat);
+            if (!o) continue;
+            const int32_t s = ss[u];
+            if (o & kAcclaim) {
+                if (s < me && (h.st == ST_L || h.st == ST_W) && hb_tick) h.ob |= kHeartbeat;  // bully back
+                h.lead = s;  // (higher sender: follow) then COORDINATOR: unconditional takeover
+                h.lead_set = true;
+                h.st = ST_F;
+                h.live = true;
+            }
+            if (o & kHeartbeat) {
+                if (h.st == ST_L && s < me) {
+                    if (hb_tick) h.ob |= kHeartbeat;
+                } else {
+                    h.st = ST_F;  // yield (LEADER) / stop waiting (ELECTION_WAIT) / stay FOLLOWER
+                    h.lead = s;
+                    h.lead_set = true;
+                    h.live = true;
+                    h.hb_from = jj[u];
+                }
+            }
+        }
+    }
+}
+
+// Write back the liveness proof and the heartbeat's leader position (state / leader: caller).
+__device__ __forceinline__ void apply_heard(int64_t i, const Heard &h, double now, const double2 *__restrict__ pos,
+                                            const Fsm &f) {
+    if (h.live) f.last_hb[i] = now;
+    if (h.hb_from >= 0) {
+        const double2 q = pos[h.hb_from];
+        f.lpos[i] = make_float2(float(q.x), float(q.y));
+        f.has_lpos[i] = 1;
+    }
+}
+
+// _check_election_timeout (217-241) and the leader's heartbeat (283-289) for agent i in state
+// st; `heard`: it got a liveness proof this tick (its last_hb is now).  Returns the sends.
+__device__ __forceinline__ uint8_t timers(int64_t i, uint8_t &st, bool heard, int32_t &lead, bool &lead_set,
+                                          int64_t t, double now, double timeout, double jitter, uint64_t seed,
+                                          const int32_t *__restrict__ ids, const int32_t *__restrict__ tick_off,
+                                          const Fsm &f) {
+    uint8_t ob = 0;
+    if (st == ST_F && !heard && now - f.last_hb[i] > timeout) {
+        st = ST_W;
+        f.wait_start[i] = now;
+        f.delay[i] = 0.0 + jitter * jitter_u(seed, ids[i], t);
+        lead = -1;
+        lead_set = true;
+        f.has_lpos[i] = 0;
+        f.lpos[i] = make_float2(0.f, 0.f);
+    }
+    if (st == ST_W && now - f.wait_start[i] > f.delay[i]) {
+        st = ST_L;
+        lead = ids[i];
+        lead_set = true;
+        ob |= kAcclaim;
+    }
+    if (st == ST_L && ((t + tick_off[i]) % 10) == 0) ob |= kHeartbeat;
+    return ob;
+}
+
+// Per-tick counters: wave reduce, one LDS atomic per wave, one global atomic per workgroup into
+// one of kShards copies (blockIdx-interleaved; k_sum_counts adds them up).  A single copy made
+// every workgroup's 4 atomics queue on the same 4 addresses: ~50 us per tick at 4 096
+// workgroups, ~470 us at one agent per thread (measured).
+constexpr int kShards = 64;
+
+__device__ __forceinline__ void add_counts(unsigned c0, unsigned c1, unsigned c2, unsigned c3, unsigned *s_cnt,
+                                           unsigned long long *counts) {
+    counts += 4 * (blockIdx.x & (kShards - 1));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        c0 += __shfl_xor(c0, off, 64);
+        c1 += __shfl_xor(c1, off, 64);
+        c2 += __shfl_xor(c2, off, 64);
+        c3 += __shfl_xor(c3, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (c0) atomicAdd(&s_cnt[0], c0);
+        if (c1) atomicAdd(&s_cnt[1], c1);
+        if (c2) atomicAdd(&s_cnt[2], c2);
+        if (c3) atomicAdd(&s_cnt[3], c3);
+    }
+    __syncthreads();
+    if (threadIdx.x < 4 && s_cnt[threadIdx.x]) atomicAdd(&counts[threadIdx.x], (unsigned long long)s_cnt[threadIdx.x]);
+}
+
+// counts[t][shard][c] -> out[t][c]
+__global__ __launch_bounds__(kBlock) void k_sum_counts(int64_t ticks, const unsigned long long *__restrict__ part,
+                                                      unsigned long long *__restrict__ out) {
+    for (int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x; q < ticks * 4; q += int64_t(gridDim.x) * kBlock) {
+        const int64_t t = q / 4, c = q % 4;
+        unsigned long long sum = 0;
+        for (int sh = 0; sh < kShards; ++sh) sum += part[(t * kShards + sh) * 4 + c];
+        out[q] = sum;
+    }
+}
+
+// ---------------------------------------------------------------- pull mode: one fused launch
+__global__ __launch_bounds__(kBlock) void k_tick_pull(int64_t n, int64_t t, const int32_t *__restrict__ ids,
+                                                     const double2 *__restrict__ pos, const int32_t *__restrict__ rp,
+                                                     const int32_t *__restrict__ col,
+                                                     const int32_t *__restrict__ tick_off, Fsm f,
+                                                     const uint8_t *__restrict__ ob_in, uint8_t *__restrict__ ob_out,
+                                                     double dt, double timeout, double jitter, uint64_t seed,
+                                                     unsigned long long *__restrict__ counts) {
     __shared__ unsigned s_cnt[4];
     if (threadIdx.x < 4) s_cnt[threadIdx.x] = 0;
     __syncthreads();
@@ -65,87 +204,164 @@ __global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int
             ob_out[i] = 0;
             continue;
         }
-        const int32_t me = ids[i];
-        const bool hb_tick = ((t + tick_off[i]) % 10) == 0;
-        uint8_t st = f.state[i], ob = 0;
-        const uint8_t st0 = st;
-        int32_t lead = f.leader[i];
-        const int32_t lead0 = lead;
-        bool live = false, pos_set = false;
-        float2 lp;
-        for (int32_t k = rp[i], e = rp[i + 1]; k < e; ++k) {
-            const int32_t j = col[k];
-            const uint8_t o = ob_in[j];
-            if (!o) continue;
-            const int32_t s = ids[j];
-            if (o & kAcclaim) {
-                if (s > me) {
-                    live = true;
-                } else if (s < me && (st == ST_L || st == ST_W)) {
-                    if (hb_tick) ob |= kHeartbeat;  // bully back (state/leader: overwritten below)
-                }
-                lead = s;  // COORDINATOR: unconditional takeover
-                st = ST_F;
-                live = true;
-            }
-            if (o & kHeartbeat) {
-                if (st == ST_L && s < me) {
-                    if (hb_tick) ob |= kHeartbeat;
-                } else {
-                    st = ST_F;  // yield (LEADER) / stop waiting (ELECTION_WAIT) / stay FOLLOWER
-                    lead = s;
-                    live = true;
-                    const double2 q = pos[j];
-                    lp = make_float2(float(q.x), float(q.y));
-                    pos_set = true;
-                }
-            }
-        }
-        if (live) f.last_hb[i] = now;
-        if (pos_set) {
-            f.lpos[i] = lp;
-            f.has_lpos[i] = 1;
-        }
-        if (st != ST_L) {
-            if (st == ST_F && now - (live ? now : f.last_hb[i]) > timeout) {
-                st = ST_W;
-                f.wait_start[i] = now;
-                f.delay[i] = 0.0 + jitter * jitter_u(seed, me, t);
-                lead = -1;
-                f.has_lpos[i] = 0;
-                f.lpos[i] = make_float2(0.f, 0.f);
-            }
-            if (st == ST_W && now - f.wait_start[i] > f.delay[i]) {
-                st = ST_L;
-                lead = me;
-                ob |= kAcclaim;
-            }
-        }
-        if (st == ST_L && hb_tick) ob |= kHeartbeat;
-        if (st != st0) f.state[i] = st;
-        if (lead != lead0) f.leader[i] = lead;
+        const uint8_t st0 = f.state[i];
+        Heard h{st0, 0, false, false, 0, -1};
+        receive_row(rp[i], rp[i + 1], col, ob_in, ids, ids[i], ((t + tick_off[i]) % 10) == 0, h);
+        apply_heard(i, h, now, pos, f);
+        const uint8_t ob = h.ob | timers(i, h.st, h.live, h.lead, h.lead_set, t, now, timeout, jitter, seed, ids,
+                                         tick_off, f);
+        if (h.st != st0) f.state[i] = h.st;
+        if (h.lead_set) f.leader[i] = h.lead;
         ob_out[i] = ob;
+        c_lead += h.st == ST_L;
+        c_wait += h.st == ST_W;
+        c_acc += (ob & kAcclaim) != 0;
+        c_hb += (ob & kHeartbeat) != 0;
+    }
+    add_counts(c_lead, c_wait, c_acc, c_hb, s_cnt, counts);
+}
+
+// ---------------------------------------------------------------- push mode
+constexpr uint8_t kFresh = 0x80;  // outbox byte written by k_receive this tick
+constexpr uint8_t kHeard = 0x04;  // ... whose receiver got a liveness proof
+
+// Mail bits for the hearers of agent i (hearers CSR), one atomicOr per distinct 64-agent word.
+// (Plain byte marks were tried: the scan of 1-byte marks dirtied by scattered byte stores costs
+// 5x the 64-bit bitmap's, more than the atomics save.)
+__device__ __forceinline__ void mail_hearers(int32_t b, int32_t e, const int32_t *__restrict__ tcol,
+                                             unsigned long long *__restrict__ mail) {
+    int32_t w = -1;
+    unsigned long long bits = 0;
+    for (int32_t k0 = b; k0 < e; k0 += kRecv) {
+        int32_t rr[kRecv];  // all hearer loads of the chunk in flight
+#pragma unroll
+        for (int u = 0; u < kRecv; ++u) rr[u] = k0 + u < e ? tcol[k0 + u] : -1;
+#pragma unroll
+        for (int u = 0; u < kRecv; ++u) {
+            const int32_t r = rr[u];
+            if (r < 0) continue;
+            if ((r >> 6) != w) {
+                if (bits) atomicOr(&mail[w], bits);  // no return value: fire and forget
+                w = r >> 6;
+                bits = 0;
+            }
+            bits |= 1ull << (r & 63);
+        }
+    }
+    if (bits) atomicOr(&mail[w], bits);
+}
+
+// Resumed run: mail for the receivers of tick t0's sends.
+__global__ __launch_bounds__(kBlock) void k_mail_from_outbox(int64_t n, const uint8_t *__restrict__ ob,
+                                                            const int32_t *__restrict__ trp,
+                                                            const int32_t *__restrict__ tcol,
+                                                            unsigned long long *__restrict__ mail) {
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock)
+        if (ob[i]) mail_hearers(trp[i], trp[i + 1], tcol, mail);
+}
+
+// Mail bitmap -> receiver list, words cleared.  One atomicAdd per workgroup pass.
+__global__ __launch_bounds__(kBlock) void k_compact(int64_t n_words, unsigned long long *__restrict__ mail,
+                                                   int32_t *__restrict__ list, unsigned *__restrict__ n_list) {
+    __shared__ unsigned s_wave[kBlock / kWave];
+    __shared__ unsigned s_base;
+    const unsigned lane = threadIdx.x & (kWave - 1);
+    const int wv = threadIdx.x / kWave;
+    for (int64_t base = int64_t(blockIdx.x) * kBlock; base < n_words; base += int64_t(gridDim.x) * kBlock) {
+        const int64_t w = base + threadIdx.x;
+        unsigned long long bits = 0;
+        if (w < n_words) {
+            bits = mail[w];
+            if (bits) mail[w] = 0;
+        }
+        const unsigned c = unsigned(__popcll(bits));
+        unsigned incl = c;  // wave inclusive scan
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) {
+            const unsigned v = __shfl_up(incl, off, kWave);
+            if (lane >= unsigned(off)) incl += v;
+        }
+        if (lane == kWave - 1) s_wave[wv] = incl;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned tot = 0;
+            for (int q = 0; q < kBlock / kWave; ++q) {
+                const unsigned v = s_wave[q];
+                s_wave[q] = tot;
+                tot += v;
+            }
+            s_base = tot ? atomicAdd(n_list, tot) : 0u;
+        }
+        __syncthreads();
+        unsigned o = s_base + s_wave[wv] + incl - c;
+        while (bits) {
+            const int b = __ffsll((long long)bits) - 1;
+            bits &= bits - 1;
+            list[o++] = int32_t(w * 64 + b);
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_receive(int64_t t, const int32_t *__restrict__ list,
+                                                   const unsigned *__restrict__ n_list, unsigned *__restrict__ n_next,
+                                                   const int32_t *__restrict__ ids, const double2 *__restrict__ pos,
+                                                   const int32_t *__restrict__ rp, const int32_t *__restrict__ col,
+                                                   const int32_t *__restrict__ tick_off, Fsm f,
+                                                   const uint8_t *__restrict__ ob_in, uint8_t *__restrict__ ob_out,
+                                                   double dt) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *n_next = 0;  // the next tick's list counter
+    const int64_t m = *n_list;
+    const double now = double(t) * dt;
+    for (int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x; q < m; q += int64_t(gridDim.x) * kBlock) {
+        const int32_t i = list[q];
+        if (!f.alive[i]) continue;
+        const uint8_t st0 = f.state[i];
+        Heard h{st0, 0, false, false, 0, -1};
+        receive_row(rp[i], rp[i + 1], col, ob_in, ids, ids[i], ((t + tick_off[i]) % 10) == 0, h);
+        apply_heard(i, h, now, pos, f);
+        if (h.st != st0) f.state[i] = h.st;
+        if (h.lead_set) f.leader[i] = h.lead;
+        ob_out[i] = uint8_t(kFresh | h.ob | (h.live ? kHeard : 0));
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_sweep(int64_t n, int64_t t, const int32_t *__restrict__ ids,
+                                                 const int32_t *__restrict__ trp, const int32_t *__restrict__ tcol,
+                                                 const int32_t *__restrict__ tick_off, Fsm f,
+                                                 uint8_t *__restrict__ ob_out, unsigned long long *__restrict__ mail,
+                                                 double dt, double timeout, double jitter, uint64_t seed,
+                                                 unsigned long long *__restrict__ counts) {
+    __shared__ unsigned s_cnt[4];
+    if (threadIdx.x < 4) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const double now = double(t) * dt;
+    unsigned c_lead = 0, c_wait = 0, c_acc = 0, c_hb = 0;
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+        const uint8_t alive = f.alive[i];
+        const uint8_t prev = ob_out[i];  // this tick's receive result, or a stale tick t-2 byte
+        uint8_t st = f.state[i];
+        if (!alive) {
+            if (prev) ob_out[i] = 0;
+            continue;
+        }
+        const uint8_t rb = (prev & kFresh) ? prev : uint8_t(0);
+        const uint8_t st0 = st;
+        int32_t lead = 0;
+        bool lead_set = false;
+        const uint8_t ob = uint8_t((rb & (kAcclaim | kHeartbeat)) |
+                                   timers(i, st, (rb & kHeard) != 0, lead, lead_set, t, now, timeout, jitter, seed,
+                                          ids, tick_off, f));
+        if (st != st0) f.state[i] = st;
+        if (lead_set) f.leader[i] = lead;
+        if (ob != prev) ob_out[i] = ob;
+        if (ob) mail_hearers(trp[i], trp[i + 1], tcol, mail);
         c_lead += st == ST_L;
         c_wait += st == ST_W;
         c_acc += (ob & kAcclaim) != 0;
         c_hb += (ob & kHeartbeat) != 0;
     }
-    // wave reduce, then one LDS atomic per wave and one global atomic per workgroup
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        c_lead += __shfl_xor(c_lead, off, 64);
-        c_wait += __shfl_xor(c_wait, off, 64);
-        c_acc += __shfl_xor(c_acc, off, 64);
-        c_hb += __shfl_xor(c_hb, off, 64);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&s_cnt[0], c_lead);
-        atomicAdd(&s_cnt[1], c_wait);
-        atomicAdd(&s_cnt[2], c_acc);
-        atomicAdd(&s_cnt[3], c_hb);
-    }
-    __syncthreads();
-    if (threadIdx.x < 4 && s_cnt[threadIdx.x]) atomicAdd(&counts[threadIdx.x], (unsigned long long)s_cnt[threadIdx.x]);
+    add_counts(c_lead, c_wait, c_acc, c_hb, s_cnt, counts);
 }
 
 }  // namespace
@@ -154,13 +370,16 @@ __global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int
 extern "C" {
 
 int swarm_protocol_run(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *pos, const int32_t *row_ptr,
-                       const int32_t *col, const int32_t *tick_off, const swarm_fsm *fsm, int64_t t0, int32_t ticks,
+                       const int32_t *col, const int32_t *hear_row_ptr, const int32_t *hear_col,
+                       const int32_t *tick_off, const swarm_fsm *fsm, int64_t t0, int32_t ticks,
                        double dt, double timeout, double jitter, uint64_t seed, const int64_t *kill_ticks,
                        int32_t n_kill, int64_t *counts, void *stream) {
     using namespace swarm;
     SW_ARG(ctx != nullptr && fsm != nullptr, "NULL argument");
     SW_ARG(n >= 0 && n < (int64_t(1) << 31) && ticks >= 0 && t0 >= 0 && n_kill >= 0, "sizes out of range");
     SW_ARG(n_kill == 0 || kill_ticks != nullptr, "kill_ticks is NULL");
+    SW_ARG(std::isfinite(dt) && timeout >= 0.0 && jitter >= 0.0, "dt / timeout / jitter out of range");
+    SW_ARG(hear_row_ptr != nullptr || hear_col == nullptr, "hear_col without hear_row_ptr");
     SW_ARG(n == 0 || (ids && pos && row_ptr && tick_off && fsm->state && fsm->leader && fsm->last_hb &&
                       fsm->wait_start && fsm->delay && fsm->leader_pos && fsm->has_leader_pos && fsm->alive &&
                       fsm->outbox),
@@ -170,12 +389,28 @@ int swarm_protocol_run(swarm_ctx *ctx, int64_t n, const int32_t *ids, const doub
         return SWARM_OK;
     }
     hipStream_t s = static_cast<hipStream_t>(stream);
-    unsigned long long *d_cnt;
-    SW_ALLOC(d_cnt, ctx, S_TMP0, size_t(ticks) * 4 * 8);
-    SW_HIP(hipMemsetAsync(d_cnt, 0, size_t(ticks) * 4 * 8, s));
+    unsigned long long *d_cnt;  // per tick: kShards x 4 partial counters, then the 4 sums
+    const size_t part_bytes = size_t(ticks) * kShards * 4 * 8;
+    SW_ALLOC(d_cnt, ctx, S_TMP0, part_bytes + size_t(ticks) * 4 * 8);
+    SW_HIP(hipMemsetAsync(d_cnt, 0, part_bytes, s));
+    unsigned long long *d_sum = d_cnt + size_t(ticks) * kShards * 4;
     const Fsm f{fsm->state, fsm->leader, fsm->last_hb, fsm->wait_start, fsm->delay,
                 reinterpret_cast<float2 *>(fsm->leader_pos), fsm->has_leader_pos, fsm->alive};
     const unsigned grid = grid_for(n, kBlock, 4096);
+    const bool push = hear_row_ptr != nullptr;
+    const int64_t n_words = (n + 63) / 64;
+    unsigned long long *mail = nullptr;
+    int32_t *list = nullptr;
+    unsigned *n_list = nullptr;
+    if (push) {  // mail bitmap + the two list counters (tick parity) after it
+        SW_ALLOC(mail, ctx, S_FSM_MAIL, size_t(n_words) * 8 + 64);
+        SW_ALLOC(list, ctx, S_FSM_LIST, size_t(n) * 4);
+        n_list = reinterpret_cast<unsigned *>(mail + n_words);
+        SW_HIP(hipMemsetAsync(mail, 0, size_t(n_words) * 8 + 64, s));
+        hipLaunchKernelGGL(k_mail_from_outbox, dim3(grid), dim3(kBlock), 0, s, n,
+                           fsm->outbox + size_t(t0 & 1) * size_t(n), hear_row_ptr, hear_col, mail);
+        SW_LAUNCHED();
+    }
     for (int64_t t = t0 + 1; t <= t0 + ticks; ++t) {
         bool kill = false;
         for (int32_t k = 0; k < n_kill; ++k) kill |= kill_ticks[k] == t;
@@ -185,13 +420,29 @@ int swarm_protocol_run(swarm_ctx *ctx, int64_t n, const int32_t *ids, const doub
         }
         const uint8_t *ob_in = fsm->outbox + size_t((t - 1) & 1) * size_t(n);
         uint8_t *ob_out = fsm->outbox + size_t(t & 1) * size_t(n);
-        hipLaunchKernelGGL(k_tick, dim3(grid), dim3(kBlock), 0, s, n, t, ids,
-                           reinterpret_cast<const double2 *>(pos), row_ptr, col, tick_off, f, ob_in, ob_out, dt,
-                           timeout, jitter, seed, d_cnt + 4 * (t - t0 - 1));
+        unsigned long long *cnt = d_cnt + size_t(t - t0 - 1) * kShards * 4;
+        if (push) {
+            unsigned *nl = n_list + (t & 1), *nl_next = n_list + ((t + 1) & 1);
+            hipLaunchKernelGGL(k_compact, dim3(grid_for(n_words, kBlock, 2048)), dim3(kBlock), 0, s, n_words, mail,
+                               list, nl);
+            SW_LAUNCHED();
+            hipLaunchKernelGGL(k_receive, dim3(2048), dim3(kBlock), 0, s, t, list, nl, nl_next, ids,
+                               reinterpret_cast<const double2 *>(pos), row_ptr, col, tick_off, f, ob_in, ob_out, dt);
+            SW_LAUNCHED();
+            hipLaunchKernelGGL(k_sweep, dim3(grid), dim3(kBlock), 0, s, n, t, ids, hear_row_ptr, hear_col, tick_off,
+                               f, ob_out, mail, dt, timeout, jitter, seed, cnt);
+        } else {
+            hipLaunchKernelGGL(k_tick_pull, dim3(grid), dim3(kBlock), 0, s, n, t, ids,
+                               reinterpret_cast<const double2 *>(pos), row_ptr, col, tick_off, f, ob_in, ob_out, dt,
+                               timeout, jitter, seed, cnt);
+        }
         SW_LAUNCHED();
     }
     if (counts) {
-        SW_HIP(hipMemcpyAsync(counts, d_cnt, size_t(ticks) * 4 * 8, hipMemcpyDeviceToHost, s));
+        hipLaunchKernelGGL(k_sum_counts, dim3(grid_for(int64_t(ticks) * 4, kBlock, 256)), dim3(kBlock), 0, s,
+                           int64_t(ticks), d_cnt, d_sum);
+        SW_LAUNCHED();
+        SW_HIP(hipMemcpyAsync(counts, d_sum, size_t(ticks) * 4 * 8, hipMemcpyDeviceToHost, s));
         SW_HIP(hipStreamSynchronize(s));
     }
     return SWARM_OK;

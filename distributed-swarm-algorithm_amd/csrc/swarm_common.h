@@ -44,6 +44,8 @@ enum Slot {
     S_AUC_V,          // auction: candidate values (f32)
     S_AUC_OUT,        // auction: dropped-out flags
     S_AUC_KEY,        // auction: per-task bid keys (u64)
+    S_FSM_MAIL,       // protocol: mail bitmap (1 bit per agent) + list counters
+    S_FSM_LIST,       // protocol: receivers of the current tick
     S_NUM
 };
 

@@ -138,6 +138,7 @@ class Swarm:
                                          _lib.ptr(row_ptr), _lib.ptr(col), col.numel(), ctypes.byref(ne),
                                          _lib.stream()))
         self.row_ptr, self.col = row_ptr, col[: ne.value]
+        self._hear = None  # a radius graph is symmetric: its own transpose
         return self
 
     def set_graph(self, row_ptr, col):
@@ -158,6 +159,18 @@ class Swarm:
             rp = new_rp
         self.row_ptr = torch.as_tensor(rp.astype(np.int32), device=self.device)
         self.col = torch.as_tensor(cl.astype(np.int32), device=self.device)
+        # hearers (transpose) CSR for the protocol's push marks: the same arrays when symmetric
+        src = np.repeat(np.arange(self.n, dtype=np.int64), np.diff(rp))
+        fwd = np.sort(src * max(self.n, 1) + cl)
+        bwd = np.sort(cl * max(self.n, 1) + src)
+        if np.array_equal(fwd, bwd):
+            self._hear = None
+        else:
+            order = np.argsort(cl, kind="stable")
+            trp = np.zeros(self.n + 1, np.int64)
+            trp[1:] = np.cumsum(np.bincount(cl, minlength=self.n))
+            self._hear = (torch.as_tensor(trp.astype(np.int32), device=self.device),
+                          torch.as_tensor(src[order].astype(np.int32), device=self.device))
         return self
 
     # ------------------------------------------------------------------ election
@@ -325,11 +338,13 @@ class Swarm:
         return self
 
     def protocol_run(self, ticks: int, *, kill_ticks=(), dt: float = 0.1, timeout: float = 3.0,
-                     jitter: float = 0.2, seed: int = 0) -> np.ndarray:
+                     jitter: float = 0.2, seed: int = 0, mode: str = "push") -> np.ndarray:
         """Advance the timer FSM + election handlers `ticks` ticks under contract T1
         (swarm_protocol_run; agent.py:66-80, 217-289), messages along the neighbour graph.
         kill_ticks: absolute ticks at whose start every alive LEADER dies.  Returns counts
-        (ticks x 4): alive LEADERs, alive ELECTION_WAITs, ACCLAIM senders, HEARTBEAT senders."""
+        (ticks x 4): alive LEADERs, alive ELECTION_WAITs, ACCLAIM senders, HEARTBEAT senders.
+        mode "push": senders mark their hearers and only marked agents scan their row; "pull":
+        every agent scans its row every tick (same results)."""
         if self.row_ptr is None:
             raise RuntimeError("no neighbour graph: call build_graph() or set_graph()")
         if not hasattr(self, "fsm"):
@@ -339,12 +354,17 @@ class Swarm:
                         (self.state, self.leader, f["last_hb"], f["wait_start"], f["delay"], f["leader_pos"],
                          f["has_leader_pos"], f["alive"], f["outbox"])])
         kt = np.ascontiguousarray(np.asarray(kill_ticks, np.int64))
+        if mode not in ("push", "pull"):
+            raise ValueError(f"unknown mode {mode!r}")
+        h = getattr(self, "_hear", None) or (self.row_ptr, self.col)
+        hear = (None, None) if mode == "pull" or self.n == 0 else \
+            (_lib.ptr(h[0], torch.int32), _lib.ptr(h[1], torch.int32) if h[1].numel() else None)
         counts = np.zeros((int(ticks), 4), np.int64)
         with torch.cuda.device(self.device):
             _lib.check(_lib.lib().swarm_protocol_run(
                 _lib.ctx(), self.n, _lib.ptr(self.ids) if self.n else None, _lib.ptr(self.pos) if self.n else None,
                 _lib.ptr(self.row_ptr, torch.int32), _lib.ptr(self.col, torch.int32) if self.n_edges else None,
-                _lib.ptr(self.tick_off) if self.n else None, ctypes.byref(fs), self.fsm_tick, int(ticks),
+                *hear, _lib.ptr(self.tick_off) if self.n else None, ctypes.byref(fs), self.fsm_tick, int(ticks),
                 float(dt), float(timeout), float(jitter), ctypes.c_uint64(int(seed)),
                 kt.ctypes.data_as(ctypes.c_void_p) if kt.size else None, kt.size,
                 counts.ctypes.data_as(ctypes.c_void_p), _lib.stream()))

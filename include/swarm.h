@@ -331,6 +331,9 @@ int swarm_codec_decode(swarm_ctx *ctx, int64_t m, const uint8_t *buf, const int6
  * election_delay), leader_pos (n x 2 f32, the '!ff' heartbeat payload; (0, 0) when None),
  * has_leader_pos, alive, outbox (2n bytes, tick-parity double buffer: the bytes at parity
  * (t0 & 1) are the tick-t0 sends; bit 0 ACCLAIM+COORDINATOR, bit 1 HEARTBEAT).
+ * row_ptr/col: whom each agent hears (its receive order); hear_row_ptr/hear_col: the transpose
+ * (who hears each agent; the same arrays for a symmetric graph), or NULL: with it only agents
+ * something was sent to walk their row each tick (push marks), without it every agent does.
  * kill_ticks (host, n_kill): at the start of each such tick every alive LEADER dies.
  * counts (host, ticks x 4, may be NULL): per tick, alive LEADERs, alive ELECTION_WAITs, ACCLAIM
  * senders, HEARTBEAT senders.  Synchronises the stream when counts != NULL.
@@ -348,7 +351,8 @@ typedef struct {
 } swarm_fsm;
 
 int swarm_protocol_run(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *pos, const int32_t *row_ptr,
-                       const int32_t *col, const int32_t *tick_off, const swarm_fsm *fsm, int64_t t0, int32_t ticks,
+                       const int32_t *col, const int32_t *hear_row_ptr, const int32_t *hear_col,
+                       const int32_t *tick_off, const swarm_fsm *fsm, int64_t t0, int32_t ticks,
                        double dt, double timeout, double jitter, uint64_t seed, const int64_t *kill_ticks,
                        int32_t n_kill, int64_t *counts, void *stream);
 

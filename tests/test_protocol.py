@@ -103,11 +103,12 @@ def _gpu_state(s):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", FSM)
-@pytest.mark.parametrize("layout", ["spatial", "input"])
-def test_gpu_matches_reference_fixture(name, layout):
+@pytest.mark.parametrize("layout,mode", [("spatial", "push"), ("input", "push"), ("spatial", "pull")])
+def test_gpu_matches_reference_fixture(name, layout, mode):
     g = load_golden(name)
     s = _gpu_swarm(g, layout)
-    counts = s.protocol_run(int(g["ticks"]), kill_ticks=g["kill_ticks"], dt=float(g["dt"]), seed=int(g["seed"]))
+    counts = s.protocol_run(int(g["ticks"]), kill_ticks=g["kill_ticks"], dt=float(g["dt"]), seed=int(g["seed"]),
+                            mode=mode)
     got = _gpu_state(s)
     for k in OUT:
         np.testing.assert_array_equal(got[k], g[k + "_out"], err_msg=k)
@@ -125,15 +126,34 @@ def _random_case(n, seed, side):
                 last_hb0=-(off * 0.1), dt=np.float64(0.1), seed=np.uint64(seed))
 
 
+def _directed(g, seed):
+    """Drop a third of the edges one way: agent i may hear j while j does not hear i."""
+    rng = np.random.default_rng(seed)
+    rp, col = g["row_ptr"], g["col"]
+    keep = rng.uniform(size=col.size) > 0.33
+    deg = np.add.reduceat(keep, rp[:-1]) if col.size else np.zeros(len(rp) - 1, np.int64)
+    deg[np.diff(rp) == 0] = 0
+    g = dict(g)
+    g["row_ptr"] = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    g["col"] = col[keep]
+    return g
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,seed,side", [(20000, 1, 50.0), (300000, 2, 180.0)])
-def test_gpu_matches_oracle_random(oracle_mod, n, seed, side):
+@pytest.mark.parametrize("n,seed,side,mode,directed", [(20000, 1, 50.0, "push", False),
+                                                       (20000, 3, 50.0, "push", True),
+                                                       (20000, 4, 50.0, "pull", True),
+                                                       (300000, 2, 180.0, "push", False)])
+def test_gpu_matches_oracle_random(oracle_mod, n, seed, side, mode, directed):
     g = _random_case(n, seed, side)
+    if directed:
+        g = _directed(g, seed)
     g["ticks"], g["kill_ticks"] = np.int64(150), np.array([60, 61, 110], np.int64)
     want = _run_oracle(oracle_mod, g)
     s = _gpu_swarm(g)
-    c1 = s.protocol_run(64, kill_ticks=g["kill_ticks"], seed=seed)   # in two chunks: the state and the
-    c2 = s.protocol_run(86, kill_ticks=g["kill_ticks"], seed=seed)   # in-flight outbox carry over
+    assert (s._hear is not None) == directed
+    c1 = s.protocol_run(64, kill_ticks=g["kill_ticks"], seed=seed, mode=mode)  # in two chunks: the state
+    c2 = s.protocol_run(86, kill_ticks=g["kill_ticks"], seed=seed, mode=mode)  # and in-flight sends carry over
     got = _gpu_state(s)
     for k in OUT:
         np.testing.assert_array_equal(got[k], want[k], err_msg=k)

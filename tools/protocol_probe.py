@@ -35,6 +35,17 @@ for rep in range(2):
     c = s.protocol_run(a.ticks, kill_ticks=(80, 150), seed=5)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+# per-chunk timing (10 ticks per call) to separate quiet ticks from election storms
+s.protocol_reset(tick_off=off, last_hb=-(off * 0.1))
+chunks = []
+for k in range(a.ticks // 10):
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    cc = s.protocol_run(10, kill_ticks=(80, 150), seed=5)
+    torch.cuda.synchronize()
+    chunks.append((round(1e3 * (time.perf_counter() - t1) / 10, 4), int(cc[:, 1].sum()), int(cc[:, 2].sum()),
+                   int(cc[:, 3].sum())))
+print(json.dumps(dict(chunk_ms_per_tick_waits_acclaims_hbs=chunks)))
 res = dict(agents=a.agents, edges=s.n_edges, ticks=a.ticks, ms_per_tick=1e3 * dt / a.ticks,
            agent_ticks_per_s=a.agents * a.ticks / dt,
            bytes_per_tick_est=a.agents * 26 + 5 * s.n_edges,
