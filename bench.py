@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--roofline-rounds", type=int, default=20)
     ap.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the oracle timing")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--rows", type=int, default=1,
+                    help="0 to skip the other SURVEY §8 rows (C2, C4 auction, physics, protocol, codec)")
     return ap.parse_args()
 
 
@@ -227,6 +229,9 @@ def main():
                             "dense_rounds": r.dense_rounds, "changes_total": rt.changes_total},
             "alloc_stats": a.stats,
         }
+    # ---- the other §8 rows, each timed once at its own scale (informational; not `value`)
+    if rank == 0 and args.rows:
+        out["rows"] = rows_bench(sw, dev, args)
     # ---- CPU baseline: the oracle restatement on the host cores, bounded sample
     if rank == 0 and args.cpu_baseline:
         from oracle import oracle
@@ -264,6 +269,86 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _timed(fn, reps=1):
+    """Wall time of fn() (device work included) in ms, best of reps, after one warm call."""
+    import torch
+    fn()
+    torch.cuda.synchronize()
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        res = fn()
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) * 1e3
+        best = ms if best is None or ms < best else best
+    return best, res
+
+
+def rows_bench(sw, dev, args):
+    """One measurement per SURVEY §8 row beside the headline (C3): C2 election, C4 auction,
+    f1 physics, f2 timer FSM ticks, f3 codec.  Synthetic seeded inputs, resident in HBM."""
+    import torch
+    from swarm_amd import codec, gen
+    from swarm_amd.swarm import Swarm
+
+    rows = {}
+    # C2: 100k-agent RGG, election to convergence
+    d2 = gen.swarm_inputs(100_000, args.seed + 1, deg=args.deg)
+    s2 = Swarm(d2["ids"], d2["x"], d2["y"], device=dev).build_graph(1.0)
+    ms, r2 = _timed(lambda: s2.elect(max_rounds=1 << 16), reps=3)
+    rows["C2_elect_100k"] = {"ms": ms, "rounds_exec": r2.rounds_exec,
+                             "agent_rounds_per_s": s2.n * r2.rounds_exec / (ms * 1e-3)}
+    # C4: 100k agents x 100k tasks auction (eps 0.1)
+    d4 = gen.swarm_inputs(100_000, args.seed + 2, t=100_000)
+    s4 = Swarm(d4["ids"], d4["x"], d4["y"], d4["caps"], device=dev)
+    tq = [torch.as_tensor(d4[k], device=dev) for k in ("tx", "ty", "treq")]
+    ms, r4 = _timed(lambda: s4.auction(*tq), reps=2)
+    rows["C4_auction_100k_x_100k"] = {"ms": ms, "rounds": r4.rounds_exec, "pairs": r4.stats["n_pairs"],
+                                      "bids": r4.stats["bids_total"],
+                                      "assigned": int((r4.assigned >= 0).sum())}
+    del s2, s4
+    # f1: synchronous physics steps of the C3 swarm (formation behind the elected leaders,
+    # 16 obstacles, separation over the sensor graph)
+    g = np.random.default_rng(args.seed + 3)
+    side = float(sw.pos[:, 0].max())
+    obs = np.stack([g.uniform(0, side, 16), g.uniform(0, side, 16), g.uniform(0.2, 1.5, 16)], 1)
+    li = sw.leader_index()
+    steps = 5
+    ms, _ = _timed(lambda: sw.physics_step(obs, leader_index=li, steps=steps), reps=1)
+    n, e = sw.n, sw.n_edges
+    rows["f1_physics_step"] = {"agents": n, "ms_per_step": ms / steps,
+                               "agent_steps_per_s": n * steps / (ms * 1e-3),
+                               "algorithmic_GBps": (80 * n + 16 * e) / (ms / steps * 1e-3) / 1e9}
+    # f3: codec, 10M messages of every type (encode: fields -> packets; decode: packets -> fields)
+    m = 10_000_000
+    g = np.random.default_rng(args.seed + 4)
+    f = [torch.as_tensor(v, device=dev) for v in (g.integers(1, 6, m), g.integers(0, 256, m),
+                                                  g.integers(0, 2**32, m), g.normal(0, 1e3, m),
+                                                  g.normal(0, 1e3, m), g.integers(0, 2**32, m),
+                                                  g.integers(0, 256, m))]
+    ms_e, enc = _timed(lambda: codec.encode(*f, device=dev), reps=3)
+    ms_d, _ = _timed(lambda: codec.decode(enc.buf, enc.offsets, device=dev), reps=3)
+    rows["f3_codec"] = {"messages": m, "bytes": enc.total_bytes, "encode_ms": ms_e, "decode_ms": ms_d,
+                        "encode_msgs_per_s": m / (ms_e * 1e-3), "decode_msgs_per_s": m / (ms_d * 1e-3)}
+    # f2: timer FSM ticks of the C3 swarm (phase-shifted agents, a leader kill at tick 80)
+    off = (np.arange(n, dtype=np.int64) * 7919 % 40).astype(np.int32)
+    ticks = 200
+
+    def run_fsm():
+        sw.protocol_reset(tick_off=off, last_hb=-(off * 0.1))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        c = sw.protocol_run(ticks, kill_ticks=(80, 150), seed=5)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) * 1e3, c
+    run_fsm()
+    ms, c = run_fsm()
+    rows["f2_protocol_ticks"] = {"agents": n, "ticks": ticks, "ms_per_tick": ms / ticks,
+                                 "agent_ticks_per_s": n * ticks / (ms * 1e-3),
+                                 "leaders_final": int(c[-1, 0]), "heartbeats": int(c[:, 3].sum())}
+    return rows
 
 
 def sharded(args, rank, world, dev):

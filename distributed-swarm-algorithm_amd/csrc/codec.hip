@@ -19,6 +19,8 @@
 //           unknown type -> ignored (2); TASK_CLAIM / TASK_CONFLICT whose payload is not
 //           exactly '!If' / '!IB' sized -> the handler's struct.unpack raises (3); a HEARTBEAT
 //           payload carries a position only when it is exactly 8 bytes (agent.py:256-258).
+//           A packet whose offsets fall outside [0, buf_len] or run backwards is not read
+//           (status 4).
 #include <hipcub/hipcub.hpp>
 
 #include <cmath>
@@ -143,17 +145,19 @@ struct DecOut {
     uint8_t *has_pos;
 };
 
-__global__ __launch_bounds__(kBlock) void k_decode(int64_t m, const uint8_t *__restrict__ buf,
+__global__ __launch_bounds__(kBlock) void k_decode(int64_t m, const uint8_t *__restrict__ buf, int64_t buf_len,
                                                   const int64_t *__restrict__ off, int wide, DecOut o) {
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < m; i += int64_t(gridDim.x) * kBlock) {
-        const uint8_t *p = buf + off[i];
-        const int64_t len = off[i + 1] - off[i];
+        const int64_t pb = off[i], pe = off[i + 1];
+        const bool inside = 0 <= pb && pb <= pe && pe <= buf_len;  // else status 4, nothing read
+        const uint8_t *p = buf + (inside ? pb : 0);
+        const int64_t len = inside ? pe - pb : 0;
         const int hdr = wide ? 9 : 6;
-        int st = 1;
+        int st = inside ? 1 : 4;
         int64_t ty = 0, snd = 0, tick = 0, task = 0, win = 0;
         float a = 0.f, b = 0.f;
         uint8_t hp = 0;
-        if (len >= hdr) {
+        if (inside && len >= hdr) {
             ty = p[0];
             snd = wide ? int64_t(get_u32(p + 1)) : int64_t(p[1]);
             tick = int64_t(get_u32(p + (wide ? 5 : 2)));
@@ -246,18 +250,20 @@ int swarm_codec_encode(swarm_ctx *ctx, int64_t m, const int64_t *type, const int
     return SWARM_OK;
 }
 
-int swarm_codec_decode(swarm_ctx *ctx, int64_t m, const uint8_t *buf, const int64_t *offsets, int32_t wide,
+int swarm_codec_decode(swarm_ctx *ctx, int64_t m, const uint8_t *buf, int64_t buf_len, const int64_t *offsets,
+                       int32_t wide,
                        int8_t *status, int64_t *type, int64_t *sender, int64_t *tick, float *a, float *b,
                        int64_t *task, int64_t *winner, uint8_t *has_pos, void *stream) {
     using namespace swarm;
     SW_ARG(ctx != nullptr, "ctx is NULL");
-    SW_ARG(m >= 0 && m < (int64_t(1) << 31), "m out of range");
+    SW_ARG(m >= 0 && m < (int64_t(1) << 31) && buf_len >= 0, "m / buf_len out of range");
+    SW_ARG(buf != nullptr || buf_len == 0, "buf is NULL");
     SW_ARG(m == 0 || (offsets && status && type && sender && tick && a && b && task && winner && has_pos),
            "NULL array");
     if (m == 0) return SWARM_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const DecOut o{status, type, sender, tick, task, winner, a, b, has_pos};
-    hipLaunchKernelGGL(k_decode, dim3(grid_for(m, kBlock, 4096)), dim3(kBlock), 0, s, m, buf, offsets,
+    hipLaunchKernelGGL(k_decode, dim3(grid_for(m, kBlock, 4096)), dim3(kBlock), 0, s, m, buf, buf_len, offsets,
                        int(wide != 0), o);
     SW_LAUNCHED();
     return SWARM_OK;

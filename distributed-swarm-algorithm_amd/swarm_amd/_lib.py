@@ -113,7 +113,7 @@ def load(path: str = LIB_PATH):
         L.swarm_elect_sharded.argtypes = [P, P, ctypes.POINTER(Shard), P, P, i32, ctypes.POINTER(i32), P, P]
         L.swarm_physics_step.argtypes = [P, i64, P, P, P, P, P, P, P, P, i64, P, P, P, d, d, ctypes.POINTER(i64), P]
         L.swarm_codec_encode.argtypes = [P, i64, P, P, P, P, P, P, P, i32, P, i64, P, P, ctypes.POINTER(i64), P]
-        L.swarm_codec_decode.argtypes = [P, i64, P, P, i32, P, P, P, P, P, P, P, P, P, P]
+        L.swarm_codec_decode.argtypes = [P, i64, P, i64, P, i32, P, P, P, P, P, P, P, P, P, P]
         L.swarm_protocol_run.argtypes = [P, i64, P, P, P, P, P, P, P, ctypes.POINTER(Fsm), i64, i32, d, d, d,
                                          ctypes.c_uint64, P, i32, P, P]
         L.swarm_auction.argtypes = [P, i64, P, P, P, i64, P, P, d, d, ctypes.c_float, i32, P, P, P,

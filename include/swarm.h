@@ -310,11 +310,13 @@ int swarm_codec_encode(swarm_ctx *ctx, int64_t m, const int64_t *type, const int
  * decode: packet i is buf[offsets[i] .. offsets[i+1]) (device).  status: 0 handled, 1 dropped
  * (shorter than the header, agent.py:198-199), 2 unknown type (ignored, no handler), 3 the
  * handler's unpack raises struct.error (TASK_CLAIM payload != 8 bytes, TASK_CONFLICT != 5 (8
- * wide)).  Fields not carried by the type are 0; a HEARTBEAT carries a position (has_pos = 1,
+ * wide)), 4 offsets outside [0, buf_len] or decreasing (packet not read).  Fields not carried by
+ * the type are 0; a HEARTBEAT carries a position (has_pos = 1,
  * a/b as f32) only when its payload is exactly 8 bytes (agent.py:256-258).  TASK_CLAIM
  * utility -> a.  Asynchronous on stream.
  */
-int swarm_codec_decode(swarm_ctx *ctx, int64_t m, const uint8_t *buf, const int64_t *offsets, int32_t wide,
+int swarm_codec_decode(swarm_ctx *ctx, int64_t m, const uint8_t *buf, int64_t buf_len, const int64_t *offsets,
+                       int32_t wide,
                        int8_t *status, int64_t *type, int64_t *sender, int64_t *tick, float *a, float *b,
                        int64_t *task, int64_t *winner, uint8_t *has_pos, void *stream);
 

@@ -157,8 +157,8 @@ def test_gpu_empty_and_errors():
     assert e.total_bytes == 0 and e.offsets.cpu().tolist() == [0]
     d = codec.decode(np.zeros(0, np.uint8), [0], device="cuda")
     assert d.status.numel() == 0
-    with pytest.raises(ValueError):
-        codec.decode(np.zeros(4, np.uint8), [0, 6], device="cuda")
+    d = codec.decode(np.zeros(12, np.uint8), [0, 6, 20, 3, 9], device="cuda")  # ok, past the end, backwards
+    assert d.status.cpu().tolist() == [2, 4, 4, 2]  # type 0 is unknown; bad offsets are not read
     # undersized output buffer: SWARM_ERR_RANGE, not a write past the end
     ty = torch.ones(4, dtype=torch.int64, device="cuda")
     z = torch.zeros(4, dtype=torch.int64, device="cuda")
