@@ -23,8 +23,8 @@
 //   k_auc_resolve one thread per task: a non-zero key moves the task to its bidder.
 //   k_auc_tail   once few agents still bid (prices rising on a handful of contested tasks, the
 //                auction's long tail), ONE workgroup runs all remaining rounds with its bidder
-//                list in LDS and workgroup barriers between the phases: no kernel boundary per
-//                round.  Same rounds, same results.
+//                list in LDS, workgroup barriers between the phases and workgroup-scoped key
+//                atomics: no kernel boundary per round.  Same rounds, same results.
 // Per-round bidder counts: 64-way sharded counters in a ring (multi-workgroup rounds), a log
 // written by the tail kernel; the host reads them every batch of rounds.
 #include <climits>
@@ -42,6 +42,7 @@ constexpr int kAStride = 16;       // u64 per shard: one 128-B line
 constexpr int kARing = 512;        // rounds of counter slots
 constexpr int kTailBlock = 1024;   // k_auc_tail: threads (16 waves)
 constexpr int kTailCap = 2048;     // k_auc_tail: bidder list capacity (LDS)
+constexpr int kBidU = 4;           // wave_bid: list entries per lane per pass
 
 __device__ __forceinline__ unsigned long long *aslot(unsigned long long *ring, int64_t r, int shard) {
     return ring + size_t(r % kARing) * kAShards * kAStride + size_t(shard) * kAStride;
@@ -128,9 +129,10 @@ struct AucState {
     float eps;
 };
 
-// Best (ties -> lower task index) and second-best net over the lanes.
+// Best (ties -> lower task index) and second-best net over the lanes; bp: the best task's price
+// as the lane loaded it (saves re-reading it after the reduction).
 struct Best {
-    float best, second;
+    float best, second, bp;
     int32_t bk;
 };
 
@@ -139,10 +141,12 @@ __device__ __forceinline__ Best combine(Best x, Best y) {
     if (x.best > y.best || (x.best == y.best && x.bk < y.bk)) {
         r.best = x.best;
         r.bk = x.bk;
+        r.bp = x.bp;
         r.second = fmaxf(x.second, y.best);
     } else {
         r.best = y.best;
         r.bk = y.bk;
+        r.bp = y.bp;
         r.second = fmaxf(y.second, x.best);
     }
     return r;
@@ -152,18 +156,32 @@ __device__ __forceinline__ Best combine(Best x, Best y) {
 // the task in *bk.
 __device__ __forceinline__ unsigned long long wave_bid(const AucState &s, int64_t a, int32_t *bk_out) {
     const int lane = threadIdx.x & 63;
-    Best m{-INFINITY, -INFINITY, INT_MAX};
+    Best m{-INFINITY, -INFINITY, 0.0f, INT_MAX};
     const int64_t b = s.off[a], e = s.off[a + 1];
-    for (int64_t p = b + lane; p < e; p += 64) {
-        const int32_t k = s.ck[p];
-        const float net = s.cv[p] - s.price[k];
-        m = combine(m, Best{net, -INFINITY, k});
+    const uint32_t id = static_cast<uint32_t>(s.ids[a]);  // loaded beside the list bounds
+    // kBidU list entries per lane per pass, all loads of a pass in flight (the result does not
+    // depend on the combine order: ties go to the lower task index, second is a max)
+    for (int64_t p0 = b + lane; p0 < e; p0 += 64 * kBidU) {
+        int32_t kk[kBidU];
+        float vv[kBidU], pr[kBidU];
+#pragma unroll
+        for (int u = 0; u < kBidU; ++u) {
+            const int64_t p = p0 + 64 * u;
+            kk[u] = p < e ? s.ck[p] : -1;
+            vv[u] = p < e ? s.cv[p] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < kBidU; ++u) pr[u] = kk[u] >= 0 ? s.price[kk[u]] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < kBidU; ++u)
+            if (kk[u] >= 0) m = combine(m, Best{vv[u] - pr[u], -INFINITY, pr[u], kk[u]});
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         Best y;
         y.best = __shfl_xor(m.best, o, 64);
         y.second = __shfl_xor(m.second, o, 64);
+        y.bp = __shfl_xor(m.bp, o, 64);
         y.bk = __shfl_xor(m.bk, o, 64);
         m = combine(m, y);
     }
@@ -171,10 +189,10 @@ __device__ __forceinline__ unsigned long long wave_bid(const AucState &s, int64_
     if (!(m.best > 0.0f)) return 0ull;
     const float second = m.second < 0.0f ? 0.0f : m.second;
     const float inc = m.best - second;
-    float bid = s.price[m.bk] + inc;
+    float bid = m.bp + inc;
     bid = bid + s.eps;
     return (static_cast<unsigned long long>(__float_as_uint(bid)) << 32) |
-           static_cast<unsigned long long>(0xFFFFFFFFu - static_cast<uint32_t>(s.ids[a]));
+           static_cast<unsigned long long>(0xFFFFFFFFu - id);
 }
 
 __device__ __forceinline__ int32_t index_of_id(const AucState &s, uint32_t id) {
@@ -237,13 +255,16 @@ __global__ void k_auc_totals(unsigned long long *ring, int64_t r0, unsigned long
 // ---------------------------------------------------------------- the long tail, one workgroup
 // Rounds r0, r0+1, ... until no agent bids or max_rounds: bidder list in LDS (the unassigned,
 // active agents; it never grows: a round removes its winners and drop-outs and adds at most one
-// displaced owner per winner).  Phases per round, separated by workgroup barriers: bid (a wave
-// per listed agent, atomicMax on the task key), resolve (the bidder whose key stands wins),
-// key reset.  Task keys are read with agent-scope atomic loads (the atomics execute in L2).
+// displaced owner per winner).  Per round, two phases separated by workgroup barriers: bid (a
+// wave per listed agent, atomicMax on the task key) and resolve (the bidder whose key stands
+// wins; losers and displaced owners form the next list).  Keys are double-buffered by round
+// parity, so the resolve phase also clears the previous round's keys -- no third phase.  The
+// kernel is one workgroup on one XCD: its key atomics and loads are workgroup-scoped and stay
+// in that XCD's L2 instead of travelling to the device-coherence point.
 __global__ __launch_bounds__(kTailBlock) void k_auc_tail(AucState s, int64_t r0, int64_t max_rounds,
                                                         int64_t *__restrict__ log, int64_t *__restrict__ done) {
     __shared__ int32_t s_list[2][kTailCap];
-    __shared__ int32_t s_tgt[kTailCap];
+    __shared__ int32_t s_tgt[2][kTailCap];
     __shared__ unsigned long long s_key[kTailCap];
     __shared__ int s_cnt[2];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -256,11 +277,12 @@ __global__ __launch_bounds__(kTailBlock) void k_auc_tail(AucState s, int64_t r0,
             if (p < kTailCap) s_list[0][p] = int32_t(a);
         }
     __syncthreads();
-    int cur = 0;
+    int cur = 0, m_prev = 0;
     int64_t r = r0;
     for (; r <= max_rounds; ++r) {
         const int m = min(s_cnt[cur], kTailCap);
         if (m == 0) break;
+        unsigned long long *key = s.key + ((r & 1) ? s.t : 0), *key_prev = s.key + ((r & 1) ? 0 : s.t);
         if (threadIdx.x == 0) log[r - r0] = m;
         // bid
         for (int i = wid; i < m; i += kWaves) {
@@ -268,23 +290,23 @@ __global__ __launch_bounds__(kTailBlock) void k_auc_tail(AucState s, int64_t r0,
             int32_t bk;
             const unsigned long long kk = wave_bid(s, a, &bk);
             if (lane == 0) {
-                s_tgt[i] = kk ? bk : -1;
+                s_tgt[cur][i] = kk ? bk : -1;
                 s_key[i] = kk;
-                if (kk) atomicMax(&s.key[bk], kk);
+                if (kk) __hip_atomic_fetch_max(&key[bk], kk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 else s.out[a] = 1;
             }
         }
         if (threadIdx.x == 0) s_cnt[cur ^ 1] = 0;
         __syncthreads();
         // resolve: the standing key's bidder takes the task; losers bid again, the displaced
-        // owner joins them
+        // owner joins them.  Then clear the keys the previous round left.
         for (int i = threadIdx.x; i < m; i += kTailBlock) {
-            const int32_t k = s_tgt[i];
+            const int32_t k = s_tgt[cur][i];
             if (k < 0) continue;
             const int32_t a = s_list[cur][i];
-            const unsigned long long top = __hip_atomic_load(&s.key[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long top = __hip_atomic_load(&key[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int32_t prev = s.owner[k];  // issued beside the key load
             if (top == s_key[i]) {
-                const int32_t prev = s.owner[k];
                 s.owner[k] = a;
                 s.assigned[a] = k;
                 s.price[k] = __uint_as_float(static_cast<uint32_t>(top >> 32));
@@ -296,11 +318,19 @@ __global__ __launch_bounds__(kTailBlock) void k_auc_tail(AucState s, int64_t r0,
                 s_list[cur ^ 1][atomicAdd(&s_cnt[cur ^ 1], 1)] = a;
             }
         }
-        __syncthreads();
-        for (int i = threadIdx.x; i < m; i += kTailBlock)
-            if (s_tgt[i] >= 0 && s.owner[s_tgt[i]] == s_list[cur][i]) s.key[s_tgt[i]] = 0;
+        for (int i = threadIdx.x; i < m_prev; i += kTailBlock) {
+            const int32_t k = s_tgt[cur ^ 1][i];
+            if (k >= 0) __hip_atomic_store(&key_prev[k], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        m_prev = m;
         cur ^= 1;
         __syncthreads();
+    }
+    // the last round's keys
+    unsigned long long *key_last = s.key + (((r - 1) & 1) ? s.t : 0);
+    for (int i = threadIdx.x; i < m_prev; i += kTailBlock) {
+        const int32_t k = s_tgt[cur ^ 1][i];
+        if (k >= 0) key_last[k] = 0;
     }
     if (threadIdx.x == 0) *done = r - r0;  // rounds this kernel ran (all had bidders)
 }
@@ -428,10 +458,10 @@ int swarm_auction(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *a
     st.t = t;
     st.eps = eps;
     SW_ALLOC(st.out, ctx, S_AUC_OUT, size_t(n));
-    SW_ALLOC(st.key, ctx, S_AUC_KEY, size_t(t) * 8);
+    SW_ALLOC(st.key, ctx, S_AUC_KEY, size_t(t) * 16);  // two halves: k_auc_tail double-buffers by round
     SW_ALLOC(st.ring, ctx, S_CHANGES, size_t(kARing) * kAShards * kAStride * 8);
     SW_HIP(hipMemsetAsync(st.out, 0, size_t(n), s));
-    SW_HIP(hipMemsetAsync(st.key, 0, size_t(t) * 8, s));
+    SW_HIP(hipMemsetAsync(st.key, 0, size_t(t) * 16, s));
     SW_HIP(hipMemsetAsync(st.ring, 0, size_t(kARing) * kAShards * kAStride * 8, s));
     constexpr int kMaxBatch = 256;
     unsigned long long *dtot;
