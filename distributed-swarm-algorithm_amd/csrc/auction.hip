@@ -343,41 +343,11 @@ int auc_tail_threshold() {
     return tail < 0 ? 0 : (tail > kTailCap ? kTailCap : tail);
 }
 
-}  // namespace
-}  // namespace swarm
-
-extern "C" {
-
-int swarm_auction(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos, const uint32_t *acaps,
-                  int64_t t, const double *tpos, const int8_t *treq, double claim_thr, double u_scale, float eps,
-                  int32_t max_rounds, int32_t *owner, float *price, int32_t *assigned, int32_t *rounds_exec,
-                  int64_t *bidders_per_round, swarm_auction_stats *stats, void *stream) {
-    using namespace swarm;
-    SW_ARG(ctx != nullptr && rounds_exec != nullptr, "NULL argument");
-    SW_ARG(n >= 0 && n < (int64_t(1) << 31) && t >= 0 && t < (int64_t(1) << 31), "sizes out of range");
-    SW_ARG(max_rounds >= 1, "max_rounds < 1");
-    SW_ARG(std::isfinite(eps) && eps > 0.0f, "eps must be finite and > 0");
-    SW_ARG(std::isfinite(claim_thr) && claim_thr > 0.0 && std::isfinite(u_scale) && u_scale > 0.0,
-           "claim_thr and u_scale must be finite and > 0 (finite claim radius)");
-    SW_ARG(n == 0 || (ids && apos && acaps && assigned), "NULL agent array");
-    SW_ARG(t == 0 || (tpos && treq && owner && price), "NULL task array");
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    if (stats) *stats = swarm_auction_stats{};
-    if (n) SW_HIP(hipMemsetAsync(assigned, 0xFF, size_t(n) * 4, s));  // -1
-    if (t) {
-        SW_HIP(hipMemsetAsync(owner, 0xFF, size_t(t) * 4, s));
-        SW_HIP(hipMemsetAsync(price, 0, size_t(t) * 4, s));
-    }
-    *rounds_exec = 0;
-    if (n == 0 || t == 0) {  // no tasks: round 1's bidders (every agent) all drop out
-        *rounds_exec = n ? 1 : 0;
-        if (n && bidders_per_round) bidders_per_round[0] = n;
-        if (stats) {
-            stats->rounds_launched = n ? 2 : 1;
-            stats->bids_total = n;
-        }
-        return SWARM_OK;
-    }
+// Candidate lists, ascending-ID index, drop-out flags and round counters for n agents against t
+// tasks (n, t > 0): everything but the task keys and the price / owner / assigned arrays.
+int auc_prepare(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos, const uint32_t *acaps, int64_t t,
+                const double *tpos, const int8_t *treq, double claim_thr, double u_scale, float eps, AucState *out_st,
+                int64_t *npairs_out, unsigned long long **flag_out, hipStream_t s) {
     // ---- candidate lists
     const double rc = u_scale / claim_thr - 1.0;  // U > thr  <=>  d < rc (has_cap)
     int64_t *off;
@@ -444,25 +414,144 @@ int swarm_auction(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *a
         SW_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, order, int(n), 0, 32, s));
         SW_HIP(hipStreamSynchronize(s));  // io leaves scope
     }
-    AucState st{};
+    AucState &st = *out_st;
+    st = AucState{};
     st.off = off;
     st.ck = ck;
     st.cv = cv;
     st.ids = ids;
     st.sorted_ids = kout;
     st.order = order;
-    st.price = price;
-    st.owner = owner;
-    st.assigned = assigned;
     st.n = n;
     st.t = t;
     st.eps = eps;
     SW_ALLOC(st.out, ctx, S_AUC_OUT, size_t(n));
-    SW_ALLOC(st.key, ctx, S_AUC_KEY, size_t(t) * 16);  // two halves: k_auc_tail double-buffers by round
     SW_ALLOC(st.ring, ctx, S_CHANGES, size_t(kARing) * kAShards * kAStride * 8);
     SW_HIP(hipMemsetAsync(st.out, 0, size_t(n), s));
-    SW_HIP(hipMemsetAsync(st.key, 0, size_t(t) * 16, s));
     SW_HIP(hipMemsetAsync(st.ring, 0, size_t(kARing) * kAShards * kAStride * 8, s));
+    *npairs_out = npairs;
+    *flag_out = flag;
+    return SWARM_OK;
+}
+
+// ---------------------------------------------------------------- sharded rounds
+// Agents partitioned over ranks, tasks replicated.  Round r on every rank: its bidders bid into
+// the key array (t task keys + one bidder-count word per rank), one element-wise MAX all-reduce
+// makes the keys global, and every rank resolves all tasks identically (owners are agent IDs;
+// each rank updates `assigned` of its own agents only).  Same rounds, bidder counts, prices and
+// assignments as the single-GPU auction over the union of the agents.
+
+// Storage index of agent ID `id` among this rank's agents, or -1.
+__device__ __forceinline__ int32_t local_index(const AucState &s, uint32_t id) {
+    if (s.n == 0) return -1;
+    int64_t lo = 0, hi = s.n - 1;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (s.sorted_ids[mid] < id) lo = mid + 1; else hi = mid;
+    }
+    return s.sorted_ids[lo] == id ? s.order[lo] : -1;
+}
+
+// This rank's bidders of round r (the ring slot's shards) -> *slot; the ring slot is recycled.
+__global__ void k_auc_post_count(unsigned long long *ring, int64_t r, unsigned long long *slot) {
+    unsigned long long *p = aslot(ring, r, threadIdx.x);
+    unsigned long long v = *p;
+    *p = 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (threadIdx.x == 0) *slot = v;
+}
+
+// All tasks, after the all-reduce: keys[0..t) task keys, keys[t..t+world) bidder counts.
+__global__ __launch_bounds__(kBlock) void k_auc_resolve_ids(AucState s, int world, int64_t r,
+                                                           int64_t *__restrict__ log) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        unsigned long long tot = 0;
+        for (int q = 0; q < world; ++q) {
+            tot += s.key[s.t + q];
+            s.key[s.t + q] = 0;
+        }
+        log[r] = int64_t(tot);
+    }
+    for (int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x; k < s.t; k += int64_t(gridDim.x) * kBlock) {
+        const unsigned long long kk = s.key[k];
+        if (!kk) continue;
+        const uint32_t w = 0xFFFFFFFFu - static_cast<uint32_t>(kk & 0xFFFFFFFFull);
+        const int32_t prev = s.owner[k];
+        if (prev >= 0) {
+            const int32_t pi = local_index(s, uint32_t(prev));
+            if (pi >= 0) s.assigned[pi] = -1;
+        }
+        s.owner[k] = int32_t(w);
+        const int32_t wi = local_index(s, w);
+        if (wi >= 0) s.assigned[wi] = int32_t(k);
+        s.price[k] = __uint_as_float(static_cast<uint32_t>(kk >> 32));
+        s.key[k] = 0;
+    }
+}
+
+AucState auc_from_ctx(const swarm_ctx *ctx) {
+    const AucPersist &p = ctx->auc;
+    AucState st{};
+    st.off = p.off;
+    st.ck = p.ck;
+    st.cv = p.cv;
+    st.ids = p.ids;
+    st.sorted_ids = p.sorted_ids;
+    st.order = p.order;
+    st.out = p.out;
+    st.ring = p.ring;
+    st.n = p.n;
+    st.t = p.t;
+    st.eps = p.eps;
+    return st;
+}
+
+}  // namespace
+}  // namespace swarm
+
+extern "C" {
+
+int swarm_auction(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos, const uint32_t *acaps,
+                  int64_t t, const double *tpos, const int8_t *treq, double claim_thr, double u_scale, float eps,
+                  int32_t max_rounds, int32_t *owner, float *price, int32_t *assigned, int32_t *rounds_exec,
+                  int64_t *bidders_per_round, swarm_auction_stats *stats, void *stream) {
+    using namespace swarm;
+    SW_ARG(ctx != nullptr && rounds_exec != nullptr, "NULL argument");
+    SW_ARG(n >= 0 && n < (int64_t(1) << 31) && t >= 0 && t < (int64_t(1) << 31), "sizes out of range");
+    SW_ARG(max_rounds >= 1, "max_rounds < 1");
+    SW_ARG(std::isfinite(eps) && eps > 0.0f, "eps must be finite and > 0");
+    SW_ARG(std::isfinite(claim_thr) && claim_thr > 0.0 && std::isfinite(u_scale) && u_scale > 0.0,
+           "claim_thr and u_scale must be finite and > 0 (finite claim radius)");
+    SW_ARG(n == 0 || (ids && apos && acaps && assigned), "NULL agent array");
+    SW_ARG(t == 0 || (tpos && treq && owner && price), "NULL task array");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (stats) *stats = swarm_auction_stats{};
+    if (n) SW_HIP(hipMemsetAsync(assigned, 0xFF, size_t(n) * 4, s));  // -1
+    if (t) {
+        SW_HIP(hipMemsetAsync(owner, 0xFF, size_t(t) * 4, s));
+        SW_HIP(hipMemsetAsync(price, 0, size_t(t) * 4, s));
+    }
+    *rounds_exec = 0;
+    if (n == 0 || t == 0) {  // no tasks: round 1's bidders (every agent) all drop out
+        *rounds_exec = n ? 1 : 0;
+        if (n && bidders_per_round) bidders_per_round[0] = n;
+        if (stats) {
+            stats->rounds_launched = n ? 2 : 1;
+            stats->bids_total = n;
+        }
+        return SWARM_OK;
+    }
+    AucState st{};
+    int64_t npairs = 0;
+    unsigned long long *flag = nullptr;
+    if (int rc = auc_prepare(ctx, n, ids, apos, acaps, t, tpos, treq, claim_thr, u_scale, eps, &st, &npairs, &flag, s))
+        return rc;
+    st.price = price;
+    st.owner = owner;
+    st.assigned = assigned;
+    SW_ALLOC(st.key, ctx, S_AUC_KEY, size_t(t) * 16);  // two halves: k_auc_tail double-buffers by round
+    SW_HIP(hipMemsetAsync(st.key, 0, size_t(t) * 16, s));
     constexpr int kMaxBatch = 256;
     unsigned long long *dtot;
     SW_ALLOC(dtot, ctx, S_ESTATS, size_t(kMaxBatch) * 8 + 64);
@@ -531,6 +620,165 @@ int swarm_auction(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *a
         stats->n_flagged = nf;
         stats->rounds_launched = launched;
         stats->tail_rounds = tail_rounds;
+        stats->bids_total = total_bids;
+    }
+    return found > 0 ? SWARM_OK : SWARM_NOT_CONVERGED;
+}
+
+int swarm_auction_begin(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos, const uint32_t *acaps,
+                        int64_t t, const double *tpos, const int8_t *treq, double claim_thr, double u_scale, float eps,
+                        int32_t *owner_id, float *price, int32_t *assigned, swarm_auction_stats *stats,
+                        void *stream) {
+    using namespace swarm;
+    SW_ARG(ctx != nullptr, "ctx is NULL");
+    SW_ARG(n >= 0 && n < (int64_t(1) << 31) && t >= 0 && t < (int64_t(1) << 31), "sizes out of range");
+    SW_ARG(std::isfinite(eps) && eps > 0.0f, "eps must be finite and > 0");
+    SW_ARG(std::isfinite(claim_thr) && claim_thr > 0.0 && std::isfinite(u_scale) && u_scale > 0.0,
+           "claim_thr and u_scale must be finite and > 0 (finite claim radius)");
+    SW_ARG(n == 0 || (ids && apos && acaps && assigned), "NULL agent array");
+    SW_ARG(t == 0 || (tpos && treq && owner_id && price), "NULL task array");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    ctx->auc = AucPersist{};
+    if (stats) *stats = swarm_auction_stats{};
+    if (n) SW_HIP(hipMemsetAsync(assigned, 0xFF, size_t(n) * 4, s));
+    if (t) {
+        SW_HIP(hipMemsetAsync(owner_id, 0xFF, size_t(t) * 4, s));
+        SW_HIP(hipMemsetAsync(price, 0, size_t(t) * 4, s));
+    }
+    AucState st{};
+    int64_t npairs = 0;
+    unsigned long long *flag = nullptr;
+    if (n > 0 && t > 0) {
+        if (int rc = auc_prepare(ctx, n, ids, apos, acaps, t, tpos, treq, claim_thr, u_scale, eps, &st, &npairs, &flag,
+                                 s))
+            return rc;
+    } else {  // nothing admissible: empty lists, every agent drops out in round 1
+        int64_t *off0;
+        SW_ALLOC(off0, ctx, S_AUC_OFF, size_t(n + 1) * 8);
+        SW_HIP(hipMemsetAsync(off0, 0, size_t(n + 1) * 8, s));
+        st.off = off0;
+        SW_ALLOC(st.out, ctx, S_AUC_OUT, size_t(n) + 1);
+        SW_HIP(hipMemsetAsync(st.out, 0, size_t(n) + 1, s));
+        SW_ALLOC(st.ring, ctx, S_CHANGES, size_t(kARing) * kAShards * kAStride * 8);
+        SW_HIP(hipMemsetAsync(st.ring, 0, size_t(kARing) * kAShards * kAStride * 8, s));
+        st.ids = ids;
+        st.n = n;
+        st.t = t;
+        st.eps = eps;
+    }
+    AucPersist &p = ctx->auc;
+    p.n = n;
+    p.t = t;
+    p.npairs = npairs;
+    p.eps = eps;
+    p.ids = ids;
+    p.off = const_cast<int64_t *>(st.off);
+    p.ck = const_cast<int32_t *>(st.ck);
+    p.cv = const_cast<float *>(st.cv);
+    p.sorted_ids = const_cast<uint32_t *>(st.sorted_ids);
+    p.order = const_cast<int32_t *>(st.order);
+    p.out = st.out;
+    p.ring = st.ring;
+    p.ready = true;
+    if (stats) {
+        stats->n_pairs = npairs;
+        if (flag) {
+            unsigned long long fl[kAShards * kAStride];
+            SW_HIP(hipMemcpyAsync(fl, flag, sizeof(fl), hipMemcpyDeviceToHost, s));
+            SW_HIP(hipStreamSynchronize(s));
+            for (int i = 0; i < kAShards; ++i) stats->n_flagged += int64_t(fl[i * kAStride]);
+        }
+    }
+    return SWARM_OK;
+}
+
+int swarm_auction_bid(swarm_ctx *ctx, int64_t r, int32_t rank, int32_t world, uint64_t *keys, const float *price,
+                      int32_t *assigned, void *stream) {
+    using namespace swarm;
+    SW_ARG(ctx != nullptr && ctx->auc.ready, "no swarm_auction_begin on this ctx");
+    SW_ARG(r >= 1 && world >= 1 && rank >= 0 && rank < world && keys != nullptr, "bad round / rank / keys");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    AucState st = auc_from_ctx(ctx);
+    st.key = reinterpret_cast<unsigned long long *>(keys);
+    st.price = const_cast<float *>(price);
+    st.assigned = assigned;
+    hipLaunchKernelGGL(k_auc_bid, dim3(grid_for(st.n, kBlock / kWave, 8192)), dim3(kBlock), 0, s, st, r);
+    SW_LAUNCHED();
+    hipLaunchKernelGGL(k_auc_post_count, dim3(1), dim3(kWave), 0, s, st.ring, r, st.key + st.t + rank);
+    SW_LAUNCHED();
+    return SWARM_OK;
+}
+
+int swarm_auction_resolve(swarm_ctx *ctx, int64_t r, int32_t world, uint64_t *keys, int32_t *owner_id, float *price,
+                          int32_t *assigned, int64_t *log, void *stream) {
+    using namespace swarm;
+    SW_ARG(ctx != nullptr && ctx->auc.ready, "no swarm_auction_begin on this ctx");
+    SW_ARG(r >= 1 && world >= 1 && keys != nullptr && log != nullptr, "bad round / keys / log");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    AucState st = auc_from_ctx(ctx);
+    st.key = reinterpret_cast<unsigned long long *>(keys);
+    st.owner = owner_id;
+    st.price = price;
+    st.assigned = assigned;
+    hipLaunchKernelGGL(k_auc_resolve_ids, dim3(grid_for(st.t, kBlock, 4096)), dim3(kBlock), 0, s, st, int(world), r,
+                       log);
+    SW_LAUNCHED();
+    return SWARM_OK;
+}
+
+int swarm_auction_sharded(swarm_ctx *ctx, swarm_comm *comm, int64_t n, const int32_t *ids, const double *apos,
+                          const uint32_t *acaps, int64_t t, const double *tpos, const int8_t *treq, double claim_thr,
+                          double u_scale, float eps, int32_t max_rounds, int32_t *owner_id, float *price,
+                          int32_t *assigned, int32_t *rounds_exec, int64_t *bidders_per_round,
+                          swarm_auction_stats *stats, void *stream) {
+    using namespace swarm;
+    SW_ARG(rounds_exec != nullptr && max_rounds >= 1, "rounds_exec NULL or max_rounds < 1");
+    int rank = 0, world = 1;
+    if (int rc = comm_rank(comm, &rank, &world)) return rc;
+    if (int rc = swarm_auction_begin(ctx, n, ids, apos, acaps, t, tpos, treq, claim_thr, u_scale, eps, owner_id, price,
+                                     assigned, stats, stream))
+        return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    unsigned long long *keys;
+    int64_t *dlog;
+    SW_ALLOC(keys, ctx, S_AUC_KEY, size_t(t + world) * 8);
+    SW_ALLOC(dlog, ctx, S_TMP1, (size_t(max_rounds) + 2) * 8);
+    SW_HIP(hipMemsetAsync(keys, 0, size_t(t + world) * 8, s));
+    constexpr int kMaxBatch = 256;
+    int64_t *h = static_cast<int64_t *>(pinned(ctx, size_t(kMaxBatch) * 8 + 64));
+    if (!h) return SWARM_ERR_OOM;
+    int64_t r = 1, found = -1, launched = 0, total_bids = 0;
+    int batch = 8;
+    *rounds_exec = 0;
+    while (r <= max_rounds && found < 0) {
+        const int64_t rend = (max_rounds - r + 1 < batch) ? max_rounds : r + batch - 1;
+        for (int64_t q = r; q <= rend; ++q) {
+            if (int rc = swarm_auction_bid(ctx, q, rank, world, reinterpret_cast<uint64_t *>(keys), price, assigned,
+                                           stream))
+                return rc;
+            if (int rc = comm_allreduce_max_u64(comm, keys, size_t(t + world), s)) return rc;
+            if (int rc = swarm_auction_resolve(ctx, q, world, reinterpret_cast<uint64_t *>(keys), owner_id, price,
+                                               assigned, dlog, stream))
+                return rc;
+        }
+        launched = rend;
+        SW_HIP(hipMemcpyAsync(h, dlog + r, size_t(rend - r + 1) * 8, hipMemcpyDeviceToHost, s));
+        SW_HIP(hipStreamSynchronize(s));
+        for (int64_t q = r; q <= rend; ++q) {
+            const int64_t nb = h[q - r];
+            if (nb == 0) {
+                found = q;
+                break;
+            }
+            if (bidders_per_round) bidders_per_round[q - 1] = nb;
+            total_bids += nb;
+        }
+        r = rend + 1;
+        batch = batch < kMaxBatch ? batch * 2 : kMaxBatch;
+    }
+    *rounds_exec = int32_t(found > 0 ? found - 1 : max_rounds);
+    if (stats) {
+        stats->rounds_launched = launched;
         stats->bids_total = total_bids;
     }
     return found > 0 ? SWARM_OK : SWARM_NOT_CONVERGED;

@@ -85,6 +85,29 @@ __global__ __launch_bounds__(kBlock) void k_pack(const int32_t *__restrict__ L, 
 }
 
 }  // namespace
+
+// Element-wise MAX all-reduce of u64 words in place on the device stream (the auction's
+// per-round bid keys, csrc/auction.hip).  comm->nranks == 1 is a no-op.
+int comm_allreduce_max_u64(swarm_comm *comm, unsigned long long *buf, size_t count, hipStream_t s) {
+    if (comm == nullptr) {
+        set_error("NULL communicator");
+        return SWARM_ERR_ARG;
+    }
+    if (comm->nranks <= 1 || count == 0) return SWARM_OK;
+    SW_NCCL(rccl().allReduce(buf, buf, count, ncclUint64, ncclMax, comm->comm, s));
+    return SWARM_OK;
+}
+
+int comm_rank(const swarm_comm *comm, int *rank, int *nranks) {
+    if (comm == nullptr) {
+        set_error("NULL communicator");
+        return SWARM_ERR_ARG;
+    }
+    *rank = comm->rank;
+    *nranks = comm->nranks;
+    return SWARM_OK;
+}
+
 }  // namespace swarm
 
 // the frontier round launcher lives in elect.hip

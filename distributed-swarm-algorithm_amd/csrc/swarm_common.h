@@ -51,7 +51,26 @@ enum Slot {
 
 }  // namespace swarm
 
+namespace swarm {
+// Sharded auction state kept between swarm_auction_begin and the per-round calls (pointers into
+// this ctx's scratch slots; see auction.hip).
+struct AucPersist {
+    int64_t n = 0, t = 0, npairs = 0;
+    float eps = 0.f;
+    const int32_t *ids = nullptr;
+    int64_t *off = nullptr;
+    int32_t *ck = nullptr;
+    float *cv = nullptr;
+    uint32_t *sorted_ids = nullptr;
+    int32_t *order = nullptr;
+    uint8_t *out = nullptr;
+    unsigned long long *ring = nullptr;
+    bool ready = false;
+};
+}  // namespace swarm
+
 struct swarm_ctx {
+    swarm::AucPersist auc;         // sharded auction between begin and the round calls
     int device = 0;
     void *slot[swarm::S_NUM] = {};
     size_t cap[swarm::S_NUM] = {};
@@ -62,6 +81,9 @@ struct swarm_ctx {
 };
 
 namespace swarm {
+
+int comm_allreduce_max_u64(swarm_comm *comm, unsigned long long *buf, size_t count, hipStream_t s);
+int comm_rank(const swarm_comm *comm, int *rank, int *nranks);
 
 // Returns a device buffer of at least `bytes` for `s` (nullptr + error on failure).
 void *scratch(swarm_ctx *ctx, Slot s, size_t bytes);

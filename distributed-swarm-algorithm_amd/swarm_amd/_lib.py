@@ -29,7 +29,8 @@ EXPORTS = ("swarm_last_error", "swarm_version", "swarm_ctx_create", "swarm_ctx_d
            "swarm_frontier_step", "swarm_frontier_ghosts", "swarm_frontier_changes",
            "swarm_comm_available", "swarm_comm_unique_id", "swarm_comm_create", "swarm_comm_destroy",
            "swarm_elect_sharded", "swarm_auction", "swarm_physics_step", "swarm_codec_encode",
-           "swarm_codec_decode", "swarm_protocol_run")
+           "swarm_codec_decode", "swarm_protocol_run", "swarm_auction_begin",
+           "swarm_auction_bid", "swarm_auction_resolve", "swarm_auction_sharded")
 
 
 class SwarmError(RuntimeError):
@@ -116,6 +117,11 @@ def load(path: str = LIB_PATH):
         L.swarm_codec_decode.argtypes = [P, i64, P, i64, P, i32, P, P, P, P, P, P, P, P, P, P]
         L.swarm_protocol_run.argtypes = [P, i64, P, P, P, P, P, P, P, ctypes.POINTER(Fsm), i64, i32, d, d, d,
                                          ctypes.c_uint64, P, i32, P, P]
+        L.swarm_auction_begin.argtypes = [P, i64, P, P, P, i64, P, P, d, d, ctypes.c_float, P, P, P, P, P]
+        L.swarm_auction_bid.argtypes = [P, i64, i32, i32, P, P, P, P]
+        L.swarm_auction_resolve.argtypes = [P, i64, i32, P, P, P, P, P, P]
+        L.swarm_auction_sharded.argtypes = [P, P, i64, P, P, P, i64, P, P, d, d, ctypes.c_float, i32, P, P, P,
+                                            ctypes.POINTER(i32), P, P, P]
         L.swarm_auction.argtypes = [P, i64, P, P, P, i64, P, P, d, d, ctypes.c_float, i32, P, P, P,
                                     ctypes.POINTER(i32), P, P, P]
         for name in EXPORTS:

@@ -20,6 +20,11 @@ receives the neighbour ranks' agents within Rp of the border (positions, IDs, ca
 runs swarm_allocate over owned + halo agents, and sends the halo agents' won counts back to
 their owners.  No data-path all-gather; one small all-reduce for the global counters.
 
+Auction (exact, config C4 on several GPUs).  Tasks are replicated, agents stay partitioned:
+every round, each rank's bidders bid into the task-key array, one MAX all-reduce of the keys
+(+ one bidder-count word per rank) makes them global, and every rank resolves every task the
+same way (owners as agent IDs).  Same rounds, prices and owners as one GPU over all agents.
+
 Exchanges per election round: 2 x (boundary agents x 4 B) per neighbour; ~20k agents per
 border at 10M agents per GPU, i.e. ~80 KB -- latency-bound, a few microseconds over xGMI.
 """
@@ -86,6 +91,17 @@ class Halo:
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
         return t.cpu().numpy()
 
+    def all_reduce_max_(self, t):
+        """In-place element-wise MAX over ranks of an int64 tensor (the auction's bid keys)."""
+        if self.world > 1:
+            if self.host_staged and t.is_cuda:
+                h = t.cpu()
+                dist.all_reduce(h, op=dist.ReduceOp.MAX, group=self.group)
+                t.copy_(h)
+            else:
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return t
+
     def exchange_counts(self, n_to_lo, n_to_hi):
         dev = "cpu" if self.host_staged else self.device
         t = torch.tensor([n_to_lo], dtype=torch.int64, device=dev)
@@ -93,6 +109,17 @@ class Halo:
         a, b = self.exchange(t if self.lo is not None else t[:0], u if self.hi is not None else u[:0],
                              1 if self.lo is not None else 0, 1 if self.hi is not None else 0, t)
         return (int(a.item()) if a.numel() else 0), (int(b.item()) if b.numel() else 0)
+
+
+@dataclass
+class ShardAuctionResult:
+    rounds_exec: int
+    bidders: np.ndarray        # GLOBAL bidders per round, rounds 1..rounds_exec
+    owner_id: torch.Tensor     # per task: the owning agent's ID or -1 (replicated on every rank)
+    price: torch.Tensor        # per task, f32 (replicated)
+    assigned: torch.Tensor     # owned agents (storage order): task index or -1
+    converged: bool
+    stats: dict
 
 
 @dataclass
@@ -198,6 +225,59 @@ class GpuBackend:
                                                L.stream()))
         return out
 
+    # ---- sharded auction (swarm_auction_begin / _bid / _resolve, or the native RCCL loop)
+    def auction_begin(self, ids, pos, caps, tx, ty, treq, claim_thr, u_scale, eps):
+        import ctypes
+        L, dev = self.L, self.device
+        n, t = ids.numel(), tx.numel()
+        tpos = torch.stack([tx, ty], 1).contiguous()
+        st = dict(owner_id=torch.empty(t, dtype=torch.int32, device=dev),
+                  price=torch.empty(t, dtype=torch.float32, device=dev),
+                  assigned=torch.empty(n, dtype=torch.int32, device=dev), tpos=tpos, treq=treq)
+        stats = L.AuctionStats()
+        L.check(L.lib().swarm_auction_begin(
+            L.ctx(), n, L.ptr(ids) if n else None, L.ptr(pos) if n else None, L.ptr(caps) if n else None, t,
+            L.ptr(tpos) if t else None, L.ptr(treq) if t else None, float(claim_thr), float(u_scale), float(eps),
+            L.ptr(st["owner_id"]) if t else None, L.ptr(st["price"]) if t else None,
+            L.ptr(st["assigned"]) if n else None, ctypes.byref(stats), L.stream()))
+        st["stats"] = {k: int(getattr(stats, k)) for k, _ in L.AuctionStats._fields_}
+        return st
+
+    def auction_bid(self, r, rank, world, keys, st):
+        L = self.L
+        L.check(L.lib().swarm_auction_bid(L.ctx(), r, rank, world, L.ptr(keys),
+                                          L.ptr(st["price"]) if st["price"].numel() else None,
+                                          L.ptr(st["assigned"]) if st["assigned"].numel() else None, L.stream()))
+
+    def auction_resolve(self, r, world, keys, st, log):
+        L = self.L
+        L.check(L.lib().swarm_auction_resolve(L.ctx(), r, world, L.ptr(keys),
+                                              L.ptr(st["owner_id"]) if st["owner_id"].numel() else None,
+                                              L.ptr(st["price"]) if st["price"].numel() else None,
+                                              L.ptr(st["assigned"]) if st["assigned"].numel() else None,
+                                              L.ptr(log), L.stream()))
+
+    def auction_native(self, comm, ids, pos, caps, tx, ty, treq, claim_thr, u_scale, eps, max_rounds):
+        import ctypes
+        L, dev = self.L, self.device
+        n, t = ids.numel(), tx.numel()
+        tpos = torch.stack([tx, ty], 1).contiguous()
+        owner = torch.empty(t, dtype=torch.int32, device=dev)
+        price = torch.empty(t, dtype=torch.float32, device=dev)
+        assigned = torch.empty(n, dtype=torch.int32, device=dev)
+        rounds = ctypes.c_int32(0)
+        bidders = np.zeros(max_rounds, np.int64)
+        stats = L.AuctionStats()
+        rc = L.check(L.lib().swarm_auction_sharded(
+            L.ctx(), comm, n, L.ptr(ids) if n else None, L.ptr(pos) if n else None, L.ptr(caps) if n else None, t,
+            L.ptr(tpos) if t else None, L.ptr(treq) if t else None, float(claim_thr), float(u_scale), float(eps),
+            int(max_rounds), L.ptr(owner) if t else None, L.ptr(price) if t else None,
+            L.ptr(assigned) if n else None, ctypes.byref(rounds), bidders.ctypes.data_as(ctypes.c_void_p),
+            ctypes.byref(stats), L.stream()))
+        r = rounds.value
+        return ShardAuctionResult(r, bidders[:r].copy(), owner, price, assigned, rc == L.OK,
+                                  {k: int(getattr(stats, k)) for k, _ in L.AuctionStats._fields_})
+
     def allocate(self, ids, pos, caps, tx, ty, treq, **kw):
         from .swarm import Swarm
         s = Swarm.__new__(Swarm)  # a view over already-resident tensors (no reordering)
@@ -295,6 +375,51 @@ class ShardedSwarm:
         g_hi = cur[self.n_own + self.n_glo:self.n_own + self.n_glo + self.n_ghi]
         if not (torch.equal(in_lo, g_lo) and torch.equal(in_hi, g_hi)):
             raise RuntimeError("sharded election: ghost leaders disagree with their owners")
+
+    # ------------------------------------------------------------------ auction (C4 sharded)
+    def auction(self, tx, ty, treq, *, eps: float = 0.1, claim_thr: float = 20.0, u_scale: float = 100.0,
+                max_rounds: int = 1 << 20, check_every: int = 16, native: bool | None = None) -> ShardAuctionResult:
+        """Jacobi auction of this rank's agents against the SAME task set on every rank (tasks
+        replicated, agents partitioned): per round, local bids -> one MAX all-reduce of the
+        task keys (+ a bidder-count word per rank) -> identical resolution everywhere.  Equal
+        to Swarm.auction over the union of all ranks' agents.  native (default: when an RCCL
+        communicator is available) runs the whole loop in libswarm on the device stream."""
+        be, h = self.backend, self.halo
+        dev = self.device
+        tx = torch.as_tensor(np.ascontiguousarray(tx), dtype=torch.float64).to(dev)
+        ty = torch.as_tensor(np.ascontiguousarray(ty), dtype=torch.float64).to(dev)
+        treq = torch.as_tensor(np.ascontiguousarray(treq), dtype=torch.int8).to(dev)
+        if native is None or native:
+            if getattr(self, "_native", "unset") == "unset":
+                self._native = be.native_comm(h) if hasattr(be, "native_comm") else None
+            if self._native is not None:
+                return be.auction_native(self._native, self.ids, self.pos, self.caps, tx, ty, treq, claim_thr,
+                                         u_scale, eps, max_rounds)
+            if native:
+                raise RuntimeError("no RCCL communicator for the native sharded auction")
+        t, world, rank = tx.numel(), h.world, h.rank
+        st = be.auction_begin(self.ids, self.pos, self.caps, tx, ty, treq, claim_thr, u_scale, eps)
+        keys = torch.zeros(t + world, dtype=torch.int64, device=dev)
+        log = torch.zeros(max_rounds + 2, dtype=torch.int64, device=dev)
+        bidders = []
+        r, found = 1, -1
+        check_every = max(1, int(check_every))
+        while r <= max_rounds and found < 0:
+            rend = min(max_rounds, r + check_every - 1)
+            for q in range(r, rend + 1):
+                be.auction_bid(q, rank, world, keys, st)
+                h.all_reduce_max_(keys)
+                be.auction_resolve(q, world, keys, st, log)
+            for q, nb in zip(range(r, rend + 1), log[r:rend + 1].cpu().tolist()):
+                if nb == 0:
+                    found = q
+                    break
+                bidders.append(int(nb))
+            r = rend + 1
+        rounds = found - 1 if found > 0 else max_rounds
+        stats = dict(st.get("stats", {}), rounds_launched=min(r - 1, max_rounds), bids_total=int(sum(bidders)))
+        return ShardAuctionResult(rounds, np.array(bidders[:rounds], np.int64), st["owner_id"], st["price"],
+                                  st["assigned"], found > 0, stats)
 
     # ------------------------------------------------------------------ allocation
     def allocate(self, tx, ty, treq, *, claim_thr: float = 20.0, hysteresis: float = 5.0,

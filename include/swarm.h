@@ -267,6 +267,37 @@ int swarm_auction(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *a
                   int64_t *bidders_per_round, swarm_auction_stats *stats, void *stream);
 
 /*
+ * Sharded auction (BASELINE config C4 on several GPUs): agents partitioned over
+ * ranks, tasks replicated on every rank.  Round r: this rank's unassigned, active agents bid
+ * into keys (t task keys, packed as in swarm_auction, + one bidder-count word per rank: t + world
+ * u64, zero on the first call), the keys are MAX-all-reduced over ranks, and every rank resolves
+ * every task identically.  owner_id holds the owning agent's ID (-1 none; replicated), price is
+ * replicated, assigned (n, this rank's agents) the task index or -1.  Results equal
+ * swarm_auction over the union of all ranks' agents (rounds, bidder counts, prices, owners).
+ *   swarm_auction_begin    candidate lists of this rank's agents; initialises owner_id, price,
+ *                          assigned; keeps its state in ctx until the next begin (no other
+ *                          libswarm call on this ctx in between)
+ *   swarm_auction_bid      round r's bids -> keys (then the caller all-reduces keys with MAX)
+ *   swarm_auction_resolve  round r's resolution from the reduced keys; log[r] = the round's global
+ *                          bidder count (device int64, indexed by round); zeroes keys again
+ *   swarm_auction_sharded  the whole loop on the device stream with an RCCL all-reduce per round
+ *                          (comm from swarm_comm_create); returns as swarm_auction
+ */
+int swarm_auction_begin(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos, const uint32_t *acaps,
+                        int64_t t, const double *tpos, const int8_t *treq, double claim_thr, double u_scale, float eps,
+                        int32_t *owner_id, float *price, int32_t *assigned, swarm_auction_stats *stats,
+                        void *stream);
+int swarm_auction_bid(swarm_ctx *ctx, int64_t r, int32_t rank, int32_t world, uint64_t *keys, const float *price,
+                      int32_t *assigned, void *stream);
+int swarm_auction_resolve(swarm_ctx *ctx, int64_t r, int32_t world, uint64_t *keys, int32_t *owner_id, float *price,
+                          int32_t *assigned, int64_t *log, void *stream);
+int swarm_auction_sharded(swarm_ctx *ctx, swarm_comm *comm, int64_t n, const int32_t *ids, const double *apos,
+                          const uint32_t *acaps, int64_t t, const double *tpos, const int8_t *treq, double claim_thr,
+                          double u_scale, float eps, int32_t max_rounds, int32_t *owner_id, float *price,
+                          int32_t *assigned, int32_t *rounds_exec, int64_t *bidders_per_round,
+                          swarm_auction_stats *stats, void *stream);
+
+/*
  * Physics / formation step: SwarmAgent._update_physics (agent.py:94-181)
  * for every agent, as one synchronous step (contract P1): all agents read the step-start
  * positions pos_in (n x 2 f64) and write pos_out (must differ).  A FOLLOWER (state) with

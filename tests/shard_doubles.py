@@ -83,6 +83,73 @@ class NumpyBackend:
         return out
 
 
+    # ---- sharded auction, restated (the per-round contract of swarm_auction_begin/_bid/_resolve)
+    def auction_begin(self, ids, pos, caps, tx, ty, treq, claim_thr, u_scale, eps):
+        import math
+        p = pos.numpy()
+        tx_, ty_, tq = tx.numpy(), ty.numpy(), treq.numpy()
+        cp = caps.numpy().view(np.uint32)
+        cand = []
+        for a in range(ids.numel()):
+            row = []
+            for k in range(len(tx_)):
+                dx, dy = float(p[a, 0]) - float(tx_[k]), float(p[a, 1]) - float(ty_[k])
+                d = math.sqrt(dx * dx + dy * dy)
+                has = 0.0 if (int(tq[k]) >= 0 and not (int(cp[a]) >> int(tq[k])) & 1) else 1.0
+                U = (u_scale / (1.0 + d)) * has
+                if U > claim_thr:
+                    row.append((k, np.float32(U)))
+            cand.append(row)
+        t = len(tx_)
+        return dict(cand=cand, ids=ids.numpy().astype(np.int64), eps=np.float32(eps),
+                    index={int(v): i for i, v in enumerate(ids.numpy())},
+                    out=np.zeros(ids.numel(), bool), owner_id=torch.full((t,), -1, dtype=torch.int32),
+                    price=torch.zeros(t, dtype=torch.float32), assigned=torch.full((ids.numel(),), -1, dtype=torch.int32),
+                    stats=dict(n_pairs=sum(len(c) for c in cand), n_flagged=0))
+
+    def auction_bid(self, r, rank, world, keys, st):
+        f = np.float32
+        price, assigned, kv = st["price"].numpy(), st["assigned"].numpy(), keys.numpy()
+        t = price.size
+        nb = 0
+        for a, row in enumerate(st["cand"]):
+            if assigned[a] >= 0 or st["out"][a]:
+                continue
+            nb += 1
+            best, second, bk = f(-np.inf), f(-np.inf), None
+            for k, x in row:
+                net = f(x - price[k])
+                if net > best or (net == best and k < bk):
+                    second, best, bk = max(second, best), net, k
+                elif net > second:
+                    second = net
+            if not best > 0:
+                st["out"][a] = True
+                continue
+            second = max(second, f(0.0))
+            bid = f(f(price[bk] + f(best - second)) + st["eps"])
+            key = (int(np.array(bid, np.float32).view(np.uint32)) << 32) | (0xFFFFFFFF - int(st["ids"][a]))
+            kv[bk] = max(int(kv[bk]), key)
+        kv[t + rank] = nb
+
+    def auction_resolve(self, r, world, keys, st, log):
+        kv, owner, price, assigned = keys.numpy(), st["owner_id"].numpy(), st["price"].numpy(), st["assigned"].numpy()
+        t = price.size
+        for k in np.nonzero(kv[:t])[0]:
+            key = int(kv[k])
+            w = 0xFFFFFFFF - (key & 0xFFFFFFFF)
+            prev = int(owner[k])
+            if prev >= 0 and prev in st["index"]:
+                assigned[st["index"][prev]] = -1
+            owner[k] = w
+            if w in st["index"]:
+                assigned[st["index"][w]] = k
+            price[k] = np.array([key >> 32], np.uint32).view(np.float32)[0]
+            kv[k] = 0
+        log.numpy()[r] = int(kv[t:t + world].sum())
+        kv[t:t + world] = 0
+
+
 class ThreadHalo:
     """In-process strip chain for shards driven by threads (one per shard)."""
 
@@ -120,6 +187,17 @@ class ThreadHalo:
                 t = torch.tensor([n_to_lo]), torch.tensor([n_to_hi])
                 a, b = self.exchange(t[0], t[1], 1 if self.lo is not None else 0, 1 if self.hi is not None else 0, t[0])
                 return (int(a[0]) if a.numel() else 0), (int(b[0]) if b.numel() else 0)
+
+            def all_reduce_max_(self, t):
+                with hub.lock:
+                    hub.sums.setdefault("max", []).append(t.clone())
+                hub.barrier.wait()
+                t.copy_(torch.stack(hub.sums["max"]).max(0).values)
+                hub.barrier.wait()
+                with hub.lock:
+                    hub.sums.pop("max", None)
+                hub.barrier.wait()
+                return t
 
             def all_reduce_sum(self, arr):
                 arr = np.asarray(arr)

@@ -132,3 +132,99 @@ def test_gpu_auction_edge_cases(oracle_mod):
     r = s.auction(d["tx"], d["ty"], d["treq"], max_rounds=2)  # not converged in 2 rounds
     want = oracle_mod.auction(d["ids"], d["x"], d["y"], d["caps"], d["tx"], d["ty"], d["treq"])
     assert want["rounds"] > 2 and not r.converged and r.rounds_exec == 2
+
+
+# ----------------------------------------------------------------------------- sharded (C4 on N GPUs)
+
+@pytest.mark.gpu
+def test_gpu_sharded_auction_two_shards_on_one_gpu(oracle_mod):
+    """swarm_auction_begin/_bid/_resolve through ShardedSwarm.auction: two shards (two threads,
+    one GPU, in-process MAX reduce of the keys), tasks replicated; the union auction is the
+    reference (oracle.auction over all agents)."""
+    import threading
+
+    import torch
+    from shard_doubles import ThreadHalo
+    from swarm_amd import gen
+    from swarm_amd.dist import ShardedSwarm
+    world, n_per, t_per = 2, 6000, 3000
+    ds = [gen.shard_inputs(n_per, 12, world, k, t=t_per) for k in range(world)]
+    cat = lambda k: np.concatenate([d[k] for d in ds])  # noqa: E731
+    tx, ty, tq = cat("tx"), cat("ty"), cat("treq")
+    hub = ThreadHalo(world)
+    outs, errs = {}, []
+
+    def run(rank):
+        try:
+            torch.cuda.set_device(0)
+            d = ds[rank]
+            sh = ShardedSwarm(d["ids"], d["x"], d["y"], d["caps"], d["strip"], device="cuda:0",
+                              halo=hub.member(rank))
+            r = sh.auction(tx, ty, tq, check_every=32)
+            torch.cuda.synchronize()
+            outs[rank] = dict(r=r, ids=sh.ids.cpu().numpy(), owner=r.owner_id.cpu().numpy(),
+                              price=r.price.cpu().numpy(), assigned=r.assigned.cpu().numpy())
+        except Exception as e:  # surfaced below
+            errs.append(e)
+            hub.barrier.abort()
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errs, errs
+    ids = cat("ids")
+    want = oracle_mod.auction(ids, cat("x"), cat("y"), cat("caps"), tx, ty, tq)
+    owner_id = np.where(want["owner"] >= 0, ids[np.maximum(want["owner"], 0)], -1)
+    by_id = dict(zip(ids.tolist(), want["assigned"].tolist()))
+    for k in range(world):
+        o = outs[k]
+        assert o["r"].converged and o["r"].rounds_exec == want["rounds"]
+        np.testing.assert_array_equal(o["r"].bidders, want["bidders"])
+        np.testing.assert_array_equal(o["owner"], owner_id)
+        np.testing.assert_array_equal(o["price"], want["price"])
+        assert all(by_id[int(i)] == int(a) for i, a in zip(o["ids"], o["assigned"]))
+
+
+@pytest.mark.gpu
+def test_gpu_native_sharded_auction_single_rank_rccl():
+    """swarm_auction_sharded (RCCL all-reduce per round) on a 1-rank communicator equals
+    swarm_auction on the same agents: rounds, bidders, prices, owners (as IDs), assignments."""
+    import ctypes
+
+    import torch
+    from swarm_amd import _lib as L
+    from swarm_amd.swarm import Swarm
+    if not L.lib().swarm_comm_available():
+        pytest.skip("RCCL not resolvable in this process")
+    d = _inputs(20000, 5)
+    s = Swarm(d["ids"], d["x"], d["y"], d["caps"], device="cuda")
+    want = s.auction(d["tx"], d["ty"], d["treq"])
+    uid = (ctypes.c_uint8 * 128)()
+    L.check(L.lib().swarm_comm_unique_id(ctypes.cast(uid, ctypes.c_void_p)))
+    comm = ctypes.c_void_p()
+    L.check(L.lib().swarm_comm_create(ctypes.byref(comm), 1, 0, ctypes.cast(uid, ctypes.c_void_p)))
+    try:
+        t = len(d["tx"])
+        tpos = torch.as_tensor(np.stack([d["tx"], d["ty"]], 1), device="cuda").contiguous()
+        treq = torch.as_tensor(d["treq"], device="cuda")
+        owner = torch.empty(t, dtype=torch.int32, device="cuda")
+        price = torch.empty(t, dtype=torch.float32, device="cuda")
+        assigned = torch.empty(s.n, dtype=torch.int32, device="cuda")
+        rounds = ctypes.c_int32(0)
+        bid = np.zeros(1 << 16, np.int64)
+        L.check(L.lib().swarm_auction_sharded(
+            L.ctx(), comm, s.n, L.ptr(s.ids), L.ptr(s.pos), L.ptr(s.caps), t, L.ptr(tpos), L.ptr(treq), 20.0, 100.0,
+            0.1, len(bid), L.ptr(owner), L.ptr(price), L.ptr(assigned), ctypes.byref(rounds),
+            bid.ctypes.data_as(ctypes.c_void_p), None, L.stream()))
+        r = rounds.value
+        assert r == want.rounds_exec
+        np.testing.assert_array_equal(bid[:r], want.bidders)
+        np.testing.assert_array_equal(price.cpu().numpy(), want.price.cpu().numpy())
+        ids = s.ids.cpu().numpy()
+        wo = want.owner.cpu().numpy()
+        np.testing.assert_array_equal(owner.cpu().numpy(), np.where(wo >= 0, ids[np.maximum(wo, 0)], -1))
+        np.testing.assert_array_equal(assigned.cpu().numpy(), want.assigned.cpu().numpy())
+    finally:
+        L.lib().swarm_comm_destroy(comm)

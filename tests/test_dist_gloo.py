@@ -98,3 +98,57 @@ def test_shard_ids_are_a_global_permutation():
     from swarm_amd import gen
     ids = np.concatenate([gen.shard_inputs(777, 3, 5, r)["ids"] for r in range(5)])
     assert (np.sort(ids) == np.arange(777 * 5)).all()
+
+
+# ----------------------------------------------------------------------------- sharded auction
+A_PER, A_T = 300, 60
+
+
+def _auction_worker(rank, world, port, out_q, check_every):
+    import sys
+    for p in (PKG, ROOT, os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from shard_doubles import NumpyBackend
+        from swarm_amd import gen
+        from swarm_amd.dist import ShardedSwarm
+        ds = [gen.shard_inputs(A_PER, SEED + 1, world, r, t=A_T) for r in range(world)]
+        d = ds[rank]
+        tx, ty, tq = (np.concatenate([e[k] for e in ds]) for k in ("tx", "ty", "treq"))  # replicated tasks
+        sh = ShardedSwarm(d["ids"], d["x"], d["y"], d["caps"], d["strip"], device="cpu", backend=NumpyBackend())
+        r = sh.auction(tx, ty, tq, check_every=check_every)
+        out_q.put(dict(rank=rank, rounds=r.rounds_exec, bidders=r.bidders, owner=r.owner_id.numpy().copy(),
+                       price=r.price.numpy().copy(), assigned=r.assigned.numpy().copy(), ids=sh.ids.numpy().copy(),
+                       converged=r.converged))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,check_every", [(2, 5), (3, 16)])
+def test_sharded_auction_matches_single_auction(world, check_every, oracle_mod):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_auction_worker, args=(r, world, port, q, check_every)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=300) for _ in range(world)], key=lambda o: o["rank"])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from swarm_amd import gen
+    ds = [gen.shard_inputs(A_PER, SEED + 1, world, r, t=A_T) for r in range(world)]
+    cat = lambda k: np.concatenate([d[k] for d in ds])  # noqa: E731
+    ids = cat("ids")
+    want = oracle_mod.auction(ids, cat("x"), cat("y"), cat("caps"), cat("tx"), cat("ty"), cat("treq"))
+    owner_id = np.where(want["owner"] >= 0, ids[np.maximum(want["owner"], 0)], -1)
+    assert want["rounds"] > 3 and (want["owner"] >= 0).sum() > 0
+    by_id = dict(zip(ids.tolist(), want["assigned"].tolist()))
+    for o in outs:
+        assert o["converged"] and o["rounds"] == want["rounds"]
+        np.testing.assert_array_equal(o["bidders"], want["bidders"])
+        np.testing.assert_array_equal(o["owner"], owner_id)
+        np.testing.assert_array_equal(o["price"], want["price"])
+        assert all(by_id[int(i)] == int(a) for i, a in zip(o["ids"], o["assigned"]))
