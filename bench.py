@@ -416,8 +416,41 @@ def sharded(args, rank, world, dev):
             "roofline": None,
             "cpu_baseline": None,
         }
+    # C4 on N GPUs beside the headline: 100k agents split over the ranks, 100k tasks replicated,
+    # the native sharded auction (one RCCL MAX all-reduce of the task keys per round)
+    if args.rows:
+        c4 = sharded_auction_row(args, rank, world, dev)
+        if rank == 0:
+            out["rows"] = {"C4_auction_sharded": c4}
+    if rank == 0:
         print(json.dumps(out), flush=True)
     dist.destroy_process_group()
+
+
+def sharded_auction_row(args, rank, world, dev):
+    import torch
+    import torch.distributed as dist
+
+    from swarm_amd import gen
+    from swarm_amd.dist import ShardedSwarm
+    n_tot = 100_000
+    ds = [gen.shard_inputs(n_tot // world, args.seed + 2, world, r, t=n_tot // world) for r in range(world)]
+    d = ds[rank]
+    tx, ty, tq = (np.concatenate([e[k] for e in ds]) for k in ("tx", "ty", "treq"))
+    sh = ShardedSwarm(d["ids"], d["x"], d["y"], d["caps"], d["strip"], device=dev)
+    sh.auction(tx, ty, tq)  # warm-up (communicator, scratch)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    r = sh.auction(tx, ty, tq)
+    torch.cuda.synchronize()
+    dist.barrier()
+    ms = torch.tensor([(time.perf_counter() - t0) * 1e3], dtype=torch.float64,
+                      device=dev if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+    return {"ms": float(ms[0]), "agents": n_tot, "tasks": len(tx), "gpus": world, "rounds": r.rounds_exec,
+            "bids": int(r.bidders.sum()), "converged": r.converged,
+            "path": "native RCCL loop" if getattr(sh, "_native", None) is not None else "per-round torch.distributed"}
 
 
 if __name__ == "__main__":
