@@ -25,6 +25,7 @@ namespace swarm {
 namespace {
 
 constexpr int kObsLds = 1024;  // obstacles staged in LDS per pass (3 doubles each)
+constexpr int kNb = 8;         // neighbour positions gathered in flight per thread
 
 __global__ __launch_bounds__(kBlock) void k_physics(int64_t n, const int32_t *__restrict__ ids,
                                                    const uint8_t *__restrict__ state,
@@ -92,17 +93,28 @@ __global__ __launch_bounds__(kBlock) void k_physics(int64_t n, const int32_t *__
             fay = 1.0 * gy;
         }
         double fsx = 0.0, fsy = 0.0;
-        for (int32_t k = rp[i], e = rp[i + 1]; k < e; ++k) {
-            const double2 q = pin[col[k]];
-            const double ex = px - q.x, ey = py - q.y;
-            double d = sqrt(ex * ex + ey * ey);
-            if (d < 2.0) {
-                if (d <= 0.001) d = 0.001;
-                const double mag = 20.0 / (d * d);
-                const double nrm = sqrt(ex * ex + ey * ey);
-                sing += nrm == 0.0;
-                fsx += (ex / nrm) * mag;
-                fsy += (ey / nrm) * mag;
+        // the row in chunks of kNb: all column loads, then all position gathers in flight, then
+        // the separation terms summed in CSR order (the reference's order: bit-exact)
+        for (int32_t k0 = rp[i], e = rp[i + 1]; k0 < e; k0 += kNb) {
+            int32_t jj[kNb];
+#pragma unroll
+            for (int u = 0; u < kNb; ++u) jj[u] = k0 + u < e ? col[k0 + u] : -1;
+            double2 qq[kNb];
+#pragma unroll
+            for (int u = 0; u < kNb; ++u) qq[u] = jj[u] >= 0 ? pin[jj[u]] : make_double2(0.0, 0.0);
+#pragma unroll
+            for (int u = 0; u < kNb; ++u) {
+                if (jj[u] < 0) continue;
+                const double ex = px - qq[u].x, ey = py - qq[u].y;
+                double d = sqrt(ex * ex + ey * ey);
+                if (d < 2.0) {
+                    if (d <= 0.001) d = 0.001;
+                    const double mag = 20.0 / (d * d);
+                    const double nrm = sqrt(ex * ex + ey * ey);
+                    sing += nrm == 0.0;
+                    fsx += (ex / nrm) * mag;
+                    fsy += (ey / nrm) * mag;
+                }
             }
         }
         const double f0 = fax + frx + fsx, f1 = fay + fry + fsy;

@@ -1,0 +1,26 @@
+"""Time swarm_physics_step at bench scale (10M agents, deg-16 sensor graph, 16 obstacles).
+python tools/physics_probe.py [N]"""
+import sys
+import time
+
+sys.path.insert(0, "distributed-swarm-algorithm_amd")
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from swarm_amd import gen  # noqa: E402
+from swarm_amd.swarm import Swarm  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
+d = gen.swarm_inputs(n, 2026)
+s = Swarm(d["ids"], d["x"], d["y"], device="cuda:0").build_graph(1.0)
+s.elect()
+li = s.leader_index()
+g = np.random.default_rng(3)
+side = float(s.pos[:, 0].max())
+obs = np.stack([g.uniform(0, side, 16), g.uniform(0, side, 16), g.uniform(0.2, 1.5, 16)], 1)
+s.physics_step(obs, leader_index=li, steps=2)
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+s.physics_step(obs, leader_index=li, steps=10)
+torch.cuda.synchronize()
+ms = (time.perf_counter() - t0) * 1e3 / 10
+print(f"n={n} E={s.n_edges} physics ms/step {ms:.3f}  algorithmic {(80 * n + 16 * s.n_edges) / (ms * 1e-3) / 1e9:.0f} GB/s")
