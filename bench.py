@@ -286,12 +286,32 @@ def _timed(fn, reps=1):
     return best, res
 
 
+def _roof(alg_bytes, ms, kernel, pmc_kernel=None, note=None):
+    """Row roofline: algorithmic bytes of one unit of work over its measured time (device work
+    of the unit, wall-clock around a synchronised call), traffic from the committed PMC summary."""
+    gbs = alg_bytes / (ms * 1e-3) / 1e9
+    t = pmc_traffic(pmc_kernel) if pmc_kernel else None
+    out = {"bound": "hbm", "kernel": kernel, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": gbs / HBM_PEAK_GBS, "algorithmic_bytes": alg_bytes, "ms": ms,
+           "traffic_per_dispatch": t[0] if t else None, "traffic_source": t[1] if t else None}
+    if note:
+        out["note"] = note
+    return out
+
+
 def rows_bench(sw, dev, args):
     """One measurement per SURVEY §8 row beside the headline (C3): C2 election, C4 auction,
-    f1 physics, f2 timer FSM ticks, f3 codec.  Synthetic seeded inputs, resident in HBM."""
+    f1 physics, f2 timer FSM ticks, f3 codec -- each with its roofline figure and its CPU
+    restatement (oracle/) timed on a bounded sample of the host cores.  Synthetic seeded inputs,
+    resident in HBM."""
     import torch
     from swarm_amd import codec, gen
     from swarm_amd.swarm import Swarm
+    cpu = bool(args.cpu_baseline)
+    if cpu:
+        from oracle import oracle
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        oracle.set_threads(threads)
 
     rows = {}
     # C2: 100k-agent RGG, election to convergence
@@ -299,15 +319,41 @@ def rows_bench(sw, dev, args):
     s2 = Swarm(d2["ids"], d2["x"], d2["y"], device=dev).build_graph(1.0)
     ms, r2 = _timed(lambda: s2.elect(max_rounds=1 << 16), reps=3)
     rows["C2_elect_100k"] = {"ms": ms, "rounds_exec": r2.rounds_exec,
-                             "agent_rounds_per_s": s2.n * r2.rounds_exec / (ms * 1e-3)}
+                             "agent_rounds_per_s": s2.n * r2.rounds_exec / (ms * 1e-3),
+                             "roofline": _roof(float(r2.bytes_total), ms, "k_elect_dense + k_sparse_block",
+                                               note="all rounds' algorithmic bytes (DESIGN §4) over the election")}
+    if cpu:
+        rp2 = s2.row_ptr.cpu().numpy().astype(np.int64)
+        t1 = time.perf_counter()
+        oracle.elect(rp2, s2.col.cpu().numpy(), s2.ids.cpu().numpy())
+        cms = (time.perf_counter() - t1) * 1e3
+        rows["C2_elect_100k"]["cpu_baseline"] = {
+            "value": s2.n * r2.rounds_exec / (cms * 1e-3), "unit": "agent-rounds/s", "cores": threads,
+            "kind": "port", "sample": f"the whole C2 election, C oracle (OpenMP x{threads}): {cms:.0f} ms"}
     # C4: 100k agents x 100k tasks auction (eps 0.1)
     d4 = gen.swarm_inputs(100_000, args.seed + 2, t=100_000)
     s4 = Swarm(d4["ids"], d4["x"], d4["y"], d4["caps"], device=dev)
     tq = [torch.as_tensor(d4[k], device=dev) for k in ("tx", "ty", "treq")]
     ms, r4 = _timed(lambda: s4.auction(*tq), reps=2)
     rows["C4_auction_100k_x_100k"] = {"ms": ms, "rounds": r4.rounds_exec, "pairs": r4.stats["n_pairs"],
-                                      "bids": r4.stats["bids_total"],
-                                      "assigned": int((r4.assigned >= 0).sum())}
+                                      "bids": r4.stats["bids_total"], "us_per_round": ms * 1e3 / max(r4.rounds_exec, 1),
+                                      "assigned": int((r4.assigned >= 0).sum()),
+                                      "roofline": {"bound": "latency", "note": "rounds are dependent; a round is a "
+                                                   "few dependent memory steps and <= 2 launches (DESIGN §4b)"}}
+    if cpu:  # bounded sample: 20k x 20k, GPU timed on the same sample
+        ds = gen.swarm_inputs(20_000, args.seed + 5, t=20_000)
+        t1 = time.perf_counter()
+        rs = oracle.auction(ds["ids"], ds["x"], ds["y"], ds["caps"], ds["tx"], ds["ty"], ds["treq"])
+        cms = (time.perf_counter() - t1) * 1e3
+        ss = Swarm(ds["ids"], ds["x"], ds["y"], ds["caps"], device=dev)
+        tqs = [torch.as_tensor(ds[k], device=dev) for k in ("tx", "ty", "treq")]
+        gms, rg = _timed(lambda: ss.auction(*tqs), reps=2)
+        assert rg.rounds_exec == rs["rounds"]
+        rows["C4_auction_100k_x_100k"]["cpu_baseline"] = {
+            "value": cms, "unit": "ms (20k x 20k sample)", "cores": 1, "kind": "port",
+            "sample": f"C oracle orc_auction on 20k agents x 20k tasks ({rs['rounds']} rounds): {cms:.0f} ms; "
+                      f"the GPU on the same sample: {gms:.1f} ms"}
+        del ss
     del s2, s4
     # f1: synchronous physics steps of the C3 swarm (formation behind the elected leaders,
     # 16 obstacles, separation over the sensor graph)
@@ -315,23 +361,55 @@ def rows_bench(sw, dev, args):
     side = float(sw.pos[:, 0].max())
     obs = np.stack([g.uniform(0, side, 16), g.uniform(0, side, 16), g.uniform(0.2, 1.5, 16)], 1)
     li = sw.leader_index()
+    n_fol = int((li >= 0).sum())
     steps = 5
     ms, _ = _timed(lambda: sw.physics_step(obs, leader_index=li, steps=steps), reps=1)
     n, e = sw.n, sw.n_edges
     rows["f1_physics_step"] = {"agents": n, "ms_per_step": ms / steps,
                                "agent_steps_per_s": n * steps / (ms * 1e-3),
-                               "algorithmic_GBps": (80 * n + 16 * e) / (ms / steps * 1e-3) / 1e9}
+                               "roofline": _roof(82.0 * n + 20.0 * e + 16.0 * n_fol, ms / steps,
+                                                 "k_physics + k_physics_copy", "k_physics",
+                                                 note="82 B/agent + 20 B/edge + 16 B per follower's leader gather")}
+    if cpu:
+        dp = gen.swarm_inputs(1_000_000, args.seed + 6)
+        rpp, colp = oracle.rgg_csr(dp["x"], dp["y"], 1.0)
+        m1 = len(dp["ids"])
+        t1 = time.perf_counter()
+        oracle.physics(dp["ids"], np.full(m1, 1, np.uint8), np.full(m1, -1, np.int32), dp["x"], dp["y"], np.zeros(m1),
+                       np.zeros(m1), dp["x"] + 1.0, dp["y"], np.ones(m1, np.uint8), obs, rpp, colp, use_pow=False)
+        cs = time.perf_counter() - t1
+        rows["f1_physics_step"]["cpu_baseline"] = {
+            "value": m1 / cs, "unit": "agent-steps/s", "cores": threads, "kind": "port",
+            "sample": f"C oracle orc_physics (OpenMP x{threads}), 1 step of 1M agents: {cs * 1e3:.0f} ms"}
     # f3: codec, 10M messages of every type (encode: fields -> packets; decode: packets -> fields)
     m = 10_000_000
     g = np.random.default_rng(args.seed + 4)
-    f = [torch.as_tensor(v, device=dev) for v in (g.integers(1, 6, m), g.integers(0, 256, m),
-                                                  g.integers(0, 2**32, m), g.normal(0, 1e3, m),
-                                                  g.normal(0, 1e3, m), g.integers(0, 2**32, m),
-                                                  g.integers(0, 256, m))]
+    fields = (g.integers(1, 6, m), g.integers(0, 256, m), g.integers(0, 2**32, m), g.normal(0, 1e3, m),
+              g.normal(0, 1e3, m), g.integers(0, 2**32, m), g.integers(0, 256, m))
+    f = [torch.as_tensor(v, device=dev) for v in fields]
     ms_e, enc = _timed(lambda: codec.encode(*f, device=dev), reps=3)
     ms_d, _ = _timed(lambda: codec.decode(enc.buf, enc.offsets, device=dev), reps=3)
-    rows["f3_codec"] = {"messages": m, "bytes": enc.total_bytes, "encode_ms": ms_e, "decode_ms": ms_d,
-                        "encode_msgs_per_s": m / (ms_e * 1e-3), "decode_msgs_per_s": m / (ms_d * 1e-3)}
+    pk = enc.total_bytes
+    rows["f3_codec"] = {"messages": m, "bytes": pk, "encode_ms": ms_e, "decode_ms": ms_d,
+                        "encode_msgs_per_s": m / (ms_e * 1e-3), "decode_msgs_per_s": m / (ms_d * 1e-3),
+                        "roofline_encode": _roof(146.0 * m + pk, ms_e, "k_enc_len + scan + k_enc_write", "k_enc_write",
+                                                 note="fields read twice (56 B x 2), lengths/offsets/status 34 B, "
+                                                      "packet bytes written; the sizing call's host sync included"),
+                        "roofline_decode": _roof(66.0 * m + pk, ms_d, "k_decode", "k_decode",
+                                                 note="offsets 16 B + fields written 50 B per packet + packet bytes")}
+    if cpu:
+        mc = 200_000
+        sub = [v[:mc] for v in fields]
+        t1 = time.perf_counter()
+        _, pks = oracle.codec_encode_py(*sub)
+        t2 = time.perf_counter()
+        oracle.codec_decode_py(pks)
+        t3 = time.perf_counter()
+        rows["f3_codec"]["cpu_baseline"] = {
+            "value": mc / (t2 - t1), "unit": "encoded msgs/s", "cores": 1, "kind": "port",
+            "decode_msgs_per_s": mc / (t3 - t2),
+            "sample": f"struct-based restatement (the reference's own struct calls), {mc} messages: encode "
+                      f"{(t2 - t1) * 1e3:.0f} ms, decode {(t3 - t2) * 1e3:.0f} ms"}
     # f2: timer FSM ticks of the C3 swarm (phase-shifted agents, a leader kill at tick 80)
     off = (np.arange(n, dtype=np.int64) * 7919 % 40).astype(np.int32)
     ticks = 200
@@ -347,7 +425,21 @@ def rows_bench(sw, dev, args):
     ms, c = run_fsm()
     rows["f2_protocol_ticks"] = {"agents": n, "ticks": ticks, "ms_per_tick": ms / ticks,
                                  "agent_ticks_per_s": n * ticks / (ms * 1e-3),
-                                 "leaders_final": int(c[-1, 0]), "heartbeats": int(c[:, 3].sum())}
+                                 "leaders_final": int(c[-1, 0]), "heartbeats": int(c[:, 3].sum()),
+                                 "roofline": _roof(12.0 * n, ms / ticks, "k_compact + k_receive + k_sweep", "k_sweep",
+                                                   note="sweep bytes only (alive, state, outbox r/w, 8-B timer per "
+                                                        "agent); receivers' rows not counted: a lower bound")}
+    if cpu:
+        dq = gen.swarm_inputs(1_000_000, args.seed + 7)
+        rpq, colq = oracle.rgg_csr(dq["x"], dq["y"], 1.0)
+        m2 = len(dq["ids"])
+        offq = (np.arange(m2) * 7919 % 40).astype(np.int32)
+        t1 = time.perf_counter()
+        oracle.protocol(dq["ids"], dq["x"], dq["y"], rpq, colq, offq, 20, last_hb=-(offq * 0.1), seed=5)
+        cs = time.perf_counter() - t1
+        rows["f2_protocol_ticks"]["cpu_baseline"] = {
+            "value": m2 * 20 / cs, "unit": "agent-ticks/s", "cores": 1, "kind": "port",
+            "sample": f"C oracle orc_protocol (1 thread), 20 ticks of 1M agents: {cs * 1e3:.0f} ms"}
     return rows
 
 
