@@ -228,3 +228,17 @@ def test_gpu_native_sharded_auction_single_rank_rccl():
         np.testing.assert_array_equal(assigned.cpu().numpy(), want.assigned.cpu().numpy())
     finally:
         L.lib().swarm_comm_destroy(comm)
+
+
+@pytest.mark.gpu
+def test_gpu_auction_large_ids(oracle_mod):
+    """IDs at the top of the int32 range: the packed key's ~id tie-break and the ID index."""
+    from swarm_amd.swarm import Swarm
+    d = _inputs(3000, 13)
+    d["ids"] = (np.int64(2**31 - 1) - np.random.default_rng(1).permutation(len(d["ids"])) * 7).astype(np.int32)
+    want = oracle_mod.auction(d["ids"], d["x"], d["y"], d["caps"], d["tx"], d["ty"], d["treq"])
+    s = Swarm(d["ids"], d["x"], d["y"], d["caps"], device="cuda")
+    r = s.auction(d["tx"], d["ty"], d["treq"])
+    assert r.rounds_exec == want["rounds"]
+    np.testing.assert_array_equal(r.price.cpu().numpy(), want["price"])
+    np.testing.assert_array_equal(s.to_input_order(r.assigned), want["assigned"])

@@ -89,3 +89,35 @@ def test_gpu_physics_random_swarms(oracle_mod, n, seed, side):
     want = _oracle(oracle_mod, g, use_pow=False)
     for k in KEYS:
         np.testing.assert_array_equal(got[k], want[k], err_msg=k)
+
+
+def _singular_case():
+    """Agents sitting exactly on an obstacle centre and on each other (the reference raises
+    ZeroDivisionError there, agent.py:137-145, 157-160): counted, and the same non-finite bits."""
+    g = _random_case(300, 7, 12.0, m_obs=4)
+    g["obs"][0, :2] = g["x"][5], g["y"][5]
+    g["x"][9], g["y"][9] = g["x"][8], g["y"][8]
+    for k in (5, 8, 9):
+        g["has_t"][k] = 1
+        g["state"][k] = 3
+    from swarm_amd import gen
+    g["row_ptr"], g["col"] = gen.rgg_csr(g["x"], g["y"], 2.5)
+    g["steps"] = np.int64(1)
+    return g
+
+
+def test_oracle_counts_singular_cases(oracle_mod):
+    g = _singular_case()
+    o = _oracle(oracle_mod, g, use_pow=False)
+    assert o["singular"] >= 3  # the obstacle hit + both members of the coincident pair
+    assert not np.isfinite(o["x"][5]) and not np.isfinite(o["x"][8])
+
+
+@pytest.mark.gpu
+def test_gpu_physics_singular_cases_match_oracle(oracle_mod):
+    g = _singular_case()
+    got, _ = _gpu(g)
+    want = _oracle(oracle_mod, g, use_pow=False)
+    assert got["singular"] == want["singular"]
+    for k in KEYS:
+        np.testing.assert_array_equal(got[k], want[k], err_msg=k)

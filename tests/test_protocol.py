@@ -171,3 +171,18 @@ def test_gpu_empty_and_isolated():
     s.set_graph(np.zeros(4, np.int64), np.zeros(0, np.int32))  # nobody hears anybody
     c = s.protocol_run(40)
     assert c[30, 1] == 3 and c[-1, 0] == 3  # all time out at t=31 (3.1 s > 3.0 s), then all lead
+
+
+@pytest.mark.gpu
+def test_gpu_large_ids_match_oracle(oracle_mod):
+    """IDs at the top of the int32 range (jitter hash, ID comparisons, leader IDs)."""
+    g = _random_case(20000, 9, 50.0)
+    g["ids"] = (np.int64(2**31 - 1) - np.random.default_rng(2).permutation(20000) * 3).astype(np.int32)
+    g["ticks"], g["kill_ticks"] = np.int64(120), np.array([70], np.int64)
+    want = _run_oracle(oracle_mod, g)
+    s = _gpu_swarm(g)
+    c = s.protocol_run(120, kill_ticks=g["kill_ticks"], seed=int(g["seed"]))
+    got = _gpu_state(s)
+    for k in OUT:
+        np.testing.assert_array_equal(got[k], want[k], err_msg=k)
+    np.testing.assert_array_equal(c, want["counts"])
