@@ -19,8 +19,10 @@
 //              receivers (one workgroup-aggregated atomic per workgroup pass), words cleared;
 //   k_receive  one thread per listed receiver walks its CSR row (col / outbox loads in chunks
 //              of kRecv, all in flight) and applies the handlers in CSR order;
-//   k_sweep    one thread per agent: timers, sends, mail bits for the hearers of every sender
-//              (64-bit atomicOr, combined per word), per-tick counters.
+//   k_sweep    one thread per agent: timers, sends (senders listed in the workgroup's own
+//              segment: no global atomics), per-tick counters;
+//   k_mail     per segment, mail bits for the hearers of every sender (64-bit atomicOr,
+//              combined per word, all hearer loads in flight).
 // A quiet agent costs ~12 B (alive, state, outbox byte, its 8-byte timer); only receivers pay
 // for their rows.  Pull mode (no hearers CSR): one fused launch in which every agent walks
 // its row -- the cross-check.  Both are latency-bound gathers, no arithmetic worth the name.
@@ -327,14 +329,17 @@ __global__ __launch_bounds__(kBlock) void k_receive(int64_t t, const int32_t *__
 }
 
 __global__ __launch_bounds__(kBlock) void k_sweep(int64_t n, int64_t t, const int32_t *__restrict__ ids,
-                                                 const int32_t *__restrict__ trp, const int32_t *__restrict__ tcol,
                                                  const int32_t *__restrict__ tick_off, Fsm f,
-                                                 uint8_t *__restrict__ ob_out, unsigned long long *__restrict__ mail,
+                                                 uint8_t *__restrict__ ob_out, int32_t *__restrict__ senders,
+                                                 int64_t seg_cap, int32_t *__restrict__ seg_count,
                                                  double dt, double timeout, double jitter, uint64_t seed,
                                                  unsigned long long *__restrict__ counts) {
     __shared__ unsigned s_cnt[4];
+    __shared__ int s_ns;
     if (threadIdx.x < 4) s_cnt[threadIdx.x] = 0;
+    if (threadIdx.x == 0) s_ns = 0;
     __syncthreads();
+    int32_t *seg = senders + int64_t(blockIdx.x) * seg_cap;
     const double now = double(t) * dt;
     unsigned c_lead = 0, c_wait = 0, c_acc = 0, c_hb = 0;
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
@@ -355,13 +360,27 @@ __global__ __launch_bounds__(kBlock) void k_sweep(int64_t n, int64_t t, const in
         if (st != st0) f.state[i] = st;
         if (lead_set) f.leader[i] = lead;
         if (ob != prev) ob_out[i] = ob;
-        if (ob) mail_hearers(trp[i], trp[i + 1], tcol, mail);
+        if (ob) seg[atomicAdd(&s_ns, 1)] = int32_t(i);  // this workgroup's sender segment (LDS counter)
         c_lead += st == ST_L;
         c_wait += st == ST_W;
         c_acc += (ob & kAcclaim) != 0;
         c_hb += (ob & kHeartbeat) != 0;
     }
-    add_counts(c_lead, c_wait, c_acc, c_hb, s_cnt, counts);
+    add_counts(c_lead, c_wait, c_acc, c_hb, s_cnt, counts);  // (ends with a barrier: s_ns is final)
+    if (threadIdx.x == 0) seg_count[blockIdx.x] = s_ns;
+}
+
+// Mail for the hearers of every sender the sweep listed: workgroup b walks segment b.
+__global__ __launch_bounds__(kBlock) void k_mail(const int32_t *__restrict__ senders, int64_t seg_cap,
+                                                const int32_t *__restrict__ seg_count,
+                                                const int32_t *__restrict__ trp, const int32_t *__restrict__ tcol,
+                                                unsigned long long *__restrict__ mail) {
+    const int m = seg_count[blockIdx.x];
+    const int32_t *seg = senders + int64_t(blockIdx.x) * seg_cap;
+    for (int q = threadIdx.x; q < m; q += kBlock) {
+        const int32_t i = seg[q];
+        mail_hearers(trp[i], trp[i + 1], tcol, mail);
+    }
 }
 
 }  // namespace
@@ -400,11 +419,17 @@ int swarm_protocol_run(swarm_ctx *ctx, int64_t n, const int32_t *ids, const doub
     const bool push = hear_row_ptr != nullptr;
     const int64_t n_words = (n + 63) / 64;
     unsigned long long *mail = nullptr;
-    int32_t *list = nullptr;
+    int32_t *list = nullptr, *senders = nullptr, *seg_count = nullptr;
+    int64_t seg_cap = 0;
     unsigned *n_list = nullptr;
     if (push) {  // mail bitmap + the two list counters (tick parity) after it
         SW_ALLOC(mail, ctx, S_FSM_MAIL, size_t(n_words) * 8 + 64);
         SW_ALLOC(list, ctx, S_FSM_LIST, size_t(n) * 4);
+        // per-workgroup sender segments of the sweep (grid-stride: each workgroup sees at most
+        // seg_cap agents), then their counts
+        seg_cap = (n + int64_t(grid) * kBlock - 1) / (int64_t(grid) * kBlock) * kBlock;
+        SW_ALLOC(senders, ctx, S_FSM_SEND, size_t(seg_cap) * grid * 4 + size_t(grid) * 4);
+        seg_count = senders + seg_cap * grid;
         n_list = reinterpret_cast<unsigned *>(mail + n_words);
         SW_HIP(hipMemsetAsync(mail, 0, size_t(n_words) * 8 + 64, s));
         hipLaunchKernelGGL(k_mail_from_outbox, dim3(grid), dim3(kBlock), 0, s, n,
@@ -429,8 +454,11 @@ int swarm_protocol_run(swarm_ctx *ctx, int64_t n, const int32_t *ids, const doub
             hipLaunchKernelGGL(k_receive, dim3(2048), dim3(kBlock), 0, s, t, list, nl, nl_next, ids,
                                reinterpret_cast<const double2 *>(pos), row_ptr, col, tick_off, f, ob_in, ob_out, dt);
             SW_LAUNCHED();
-            hipLaunchKernelGGL(k_sweep, dim3(grid), dim3(kBlock), 0, s, n, t, ids, hear_row_ptr, hear_col, tick_off,
-                               f, ob_out, mail, dt, timeout, jitter, seed, cnt);
+            hipLaunchKernelGGL(k_sweep, dim3(grid), dim3(kBlock), 0, s, n, t, ids, tick_off, f, ob_out, senders,
+                               seg_cap, seg_count, dt, timeout, jitter, seed, cnt);
+            SW_LAUNCHED();
+            hipLaunchKernelGGL(k_mail, dim3(grid), dim3(kBlock), 0, s, senders, seg_cap, seg_count, hear_row_ptr,
+                               hear_col, mail);
         } else {
             hipLaunchKernelGGL(k_tick_pull, dim3(grid), dim3(kBlock), 0, s, n, t, ids,
                                reinterpret_cast<const double2 *>(pos), row_ptr, col, tick_off, f, ob_in, ob_out, dt,

@@ -46,6 +46,7 @@ enum Slot {
     S_AUC_KEY,        // auction: per-task bid keys (u64)
     S_FSM_MAIL,       // protocol: mail bitmap (1 bit per agent) + list counters
     S_FSM_LIST,       // protocol: receivers of the current tick
+    S_FSM_SEND,       // protocol: per-workgroup sender segments + counts
     S_NUM
 };
 
