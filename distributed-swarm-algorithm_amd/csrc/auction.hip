@@ -17,10 +17,13 @@
 //   candidates   tasks binned in a uniform grid (cell >= claim radius); one thread per agent
 //                walks the cells its claim disc covers, fp64 utilities, and writes its
 //                admissible (task, f32 value) list (count pass, hipCUB scan, fill pass).
-//   k_auc_bid    one wave per agent: lanes sweep its list (price gathers), a wave reduction of
+//   k_auc_bid_list  one wave per listed bidder (the unassigned, active agents; the list never
+//                grows): lanes sweep its candidate list (price gathers), a wave reduction of
 //                (best, task, second); the bid is ONE 64-bit atomicMax per bidder on a packed
 //                key f32bits(bid) << 32 | ~id -- highest bid, then lowest ID, no conflicts.
-//   k_auc_resolve one thread per task: a non-zero key moves the task to its bidder.
+//   k_auc_resolve_list  one thread per list entry: the standing key's bidder takes the task;
+//                losers and displaced owners form the next round's list.
+//   (k_auc_bid / k_auc_resolve: the same over every agent / task, for the sharded rounds.)
 //   k_auc_tail   once few agents still bid (prices rising on a handful of contested tasks, the
 //                auction's long tail), ONE workgroup runs all remaining rounds with its bidder
 //                list in LDS, workgroup barriers between the phases and workgroup-scoped key
@@ -154,30 +157,33 @@ __device__ __forceinline__ Best combine(Best x, Best y) {
 
 // The whole wave evaluates agent a (wave-uniform call).  Returns the bid key (0: drop out) and
 // the task in *bk.
-__device__ __forceinline__ unsigned long long wave_bid(const AucState &s, int64_t a, int32_t *bk_out) {
-    const int lane = threadIdx.x & 63;
+// W lanes (a power of two <= 64, aligned within the wave) evaluate agent a together, U list
+// entries per lane per pass.
+template <int W, int U>
+__device__ __forceinline__ unsigned long long group_bid(const AucState &s, int64_t a, int32_t *bk_out) {
+    const int lane = threadIdx.x & (W - 1);
     Best m{-INFINITY, -INFINITY, 0.0f, INT_MAX};
     const int64_t b = s.off[a], e = s.off[a + 1];
     const uint32_t id = static_cast<uint32_t>(s.ids[a]);  // loaded beside the list bounds
     // kBidU list entries per lane per pass, all loads of a pass in flight (the result does not
     // depend on the combine order: ties go to the lower task index, second is a max)
-    for (int64_t p0 = b + lane; p0 < e; p0 += 64 * kBidU) {
-        int32_t kk[kBidU];
-        float vv[kBidU], pr[kBidU];
+    for (int64_t p0 = b + lane; p0 < e; p0 += W * U) {
+        int32_t kk[U];
+        float vv[U], pr[U];
 #pragma unroll
-        for (int u = 0; u < kBidU; ++u) {
-            const int64_t p = p0 + 64 * u;
+        for (int u = 0; u < U; ++u) {
+            const int64_t p = p0 + W * u;
             kk[u] = p < e ? s.ck[p] : -1;
             vv[u] = p < e ? s.cv[p] : 0.0f;
         }
 #pragma unroll
-        for (int u = 0; u < kBidU; ++u) pr[u] = kk[u] >= 0 ? s.price[kk[u]] : 0.0f;
+        for (int u = 0; u < U; ++u) pr[u] = kk[u] >= 0 ? s.price[kk[u]] : 0.0f;
 #pragma unroll
-        for (int u = 0; u < kBidU; ++u)
+        for (int u = 0; u < U; ++u)
             if (kk[u] >= 0) m = combine(m, Best{vv[u] - pr[u], -INFINITY, pr[u], kk[u]});
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
+    for (int o = W / 2; o > 0; o >>= 1) {
         Best y;
         y.best = __shfl_xor(m.best, o, 64);
         y.second = __shfl_xor(m.second, o, 64);
@@ -193,6 +199,10 @@ __device__ __forceinline__ unsigned long long wave_bid(const AucState &s, int64_
     bid = bid + s.eps;
     return (static_cast<unsigned long long>(__float_as_uint(bid)) << 32) |
            static_cast<unsigned long long>(0xFFFFFFFFu - id);
+}
+
+__device__ __forceinline__ unsigned long long wave_bid(const AucState &s, int64_t a, int32_t *bk_out) {
+    return group_bid<64, kBidU>(s, a, bk_out);
 }
 
 __device__ __forceinline__ int32_t index_of_id(const AucState &s, uint32_t id) {
@@ -244,6 +254,103 @@ __global__ __launch_bounds__(kBlock) void k_auc_resolve(AucState s, int64_t r) {
     }
 }
 
+// ---------------------------------------------------------------- list-driven rounds
+// The multi-workgroup rounds keep the bidder list (the unassigned, active agents: it never grows)
+// instead of scanning every agent and every task: round r's list -> bids (a wave per bidder) ->
+// resolution per list entry (the standing key's bidder wins; losers and displaced owners form
+// round r+1's list, appended with one global atomic per workgroup).  Task keys alternate
+// halves by round parity; round r's resolution clears the keys round r-1 left.
+struct AucList {
+    int32_t *L[2];               // bidder lists by round parity
+    int32_t *tgt[2];             // per entry: the task bid on (-1: dropped out)
+    unsigned long long *mykey;   // per entry: this round's bid key
+    unsigned *cnt;               // [2] list lengths by round parity
+    int64_t *log;                // bidders per round, indexed by round
+};
+
+__global__ __launch_bounds__(kBlock) void k_auc_iota(int32_t *__restrict__ L, int64_t n) {
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock)
+        L[i] = int32_t(i);
+}
+
+__global__ __launch_bounds__(kBlock) void k_auc_bid_list(AucState s, AucList l, int64_t r) {
+    const unsigned m = l.cnt[r & 1];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        l.log[r] = m;
+        l.cnt[(r + 1) & 1] = 0;  // round r+1's list is appended by this round's resolution
+    }
+    unsigned long long *key = s.key + ((r & 1) ? s.t : 0);
+    const int lane = threadIdx.x & 63;
+    const int32_t *L = l.L[r & 1];
+    int32_t *tgt = l.tgt[r & 1];
+    const int64_t nw = int64_t(gridDim.x) * (kBlock / kWave);
+    for (int64_t i = int64_t(blockIdx.x) * (kBlock / kWave) + (threadIdx.x >> 6); i < m; i += nw) {
+        const int32_t a = L[i];
+        int32_t bk;
+        const unsigned long long kk = wave_bid(s, a, &bk);
+        if (lane == 0) {
+            tgt[i] = kk ? bk : -1;
+            l.mykey[i] = kk;
+            if (kk) atomicMax(&key[bk], kk);
+            else s.out[a] = 1;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_auc_resolve_list(AucState s, AucList l, int64_t r) {
+    __shared__ int s_n;
+    __shared__ unsigned s_base;
+    const int64_t m = l.log[r], mprev = r > 1 ? l.log[r - 1] : 0;
+    unsigned long long *key = s.key + ((r & 1) ? s.t : 0), *key_prev = s.key + ((r & 1) ? 0 : s.t);
+    const int32_t *L = l.L[r & 1], *tgt = l.tgt[r & 1], *tgt_prev = l.tgt[(r + 1) & 1];
+    int32_t *Lnext = l.L[(r + 1) & 1];
+    const int64_t span = m > mprev ? m : mprev;
+    for (int64_t base = int64_t(blockIdx.x) * kBlock; base < span; base += int64_t(gridDim.x) * kBlock) {
+        const int64_t i = base + threadIdx.x;
+        if (i < mprev) {
+            const int32_t k = tgt_prev[i];
+            if (k >= 0) key_prev[k] = 0;
+        }
+        int32_t app = -1;
+        if (i < m) {
+            const int32_t k = tgt[i];
+            if (k >= 0) {
+                const int32_t a = L[i];
+                const unsigned long long top = key[k];
+                const int32_t prev = s.owner[k];
+                if (top == l.mykey[i]) {
+                    s.owner[k] = a;
+                    s.assigned[a] = k;
+                    s.price[k] = __uint_as_float(static_cast<uint32_t>(top >> 32));
+                    if (prev >= 0) {
+                        s.assigned[prev] = -1;
+                        app = prev;
+                    }
+                } else {
+                    app = a;
+                }
+            }
+        }
+        if (threadIdx.x == 0) s_n = 0;
+        __syncthreads();
+        const int pos = app >= 0 ? atomicAdd(&s_n, 1) : -1;
+        __syncthreads();
+        if (threadIdx.x == 0 && s_n) s_base = atomicAdd(&l.cnt[(r + 1) & 1], unsigned(s_n));
+        __syncthreads();
+        if (pos >= 0) Lnext[s_base + pos] = app;
+        __syncthreads();
+    }
+}
+
+// Before the tail kernel takes over at round r: clear the keys round r-1 left.
+__global__ __launch_bounds__(kBlock) void k_auc_clear_keys(AucState s, AucList l, int64_t r) {
+    const int64_t m = l.log[r - 1];
+    unsigned long long *key = s.key + (((r - 1) & 1) ? s.t : 0);
+    const int32_t *tgt = l.tgt[(r - 1) & 1];
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < m; i += int64_t(gridDim.x) * kBlock)
+        if (tgt[i] >= 0) key[tgt[i]] = 0;
+}
+
 // totals[i] = bidders of round r0 + i (one wave per round).
 __global__ void k_auc_totals(unsigned long long *ring, int64_t r0, unsigned long long *totals) {
     unsigned long long v = *aslot(ring, r0 + blockIdx.x, threadIdx.x);
@@ -284,16 +391,28 @@ __global__ __launch_bounds__(kTailBlock) void k_auc_tail(AucState s, int64_t r0,
         if (m == 0) break;
         unsigned long long *key = s.key + ((r & 1) ? s.t : 0), *key_prev = s.key + ((r & 1) ? 0 : s.t);
         if (threadIdx.x == 0) log[r - r0] = m;
-        // bid
-        for (int i = wid; i < m; i += kWaves) {
-            const int32_t a = s_list[cur][i];
-            int32_t bk;
-            const unsigned long long kk = wave_bid(s, a, &bk);
-            if (lane == 0) {
-                s_tgt[cur][i] = kk ? bk : -1;
-                s_key[i] = kk;
-                if (kk) __hip_atomic_fetch_max(&key[bk], kk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                else s.out[a] = 1;
+        // bid: a wave per bidder while there are at most as many bidders as waves, else 16-lane
+        // groups (4 bidders per wave at once: fewer bidders in sequence per wave)
+        auto post = [&](int i, int32_t a, unsigned long long kk, int32_t bk) {
+            s_tgt[cur][i] = kk ? bk : -1;
+            s_key[i] = kk;
+            if (kk) __hip_atomic_fetch_max(&key[bk], kk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            else s.out[a] = 1;
+        };
+        if (m <= kWaves) {
+            for (int i = wid; i < m; i += kWaves) {
+                const int32_t a = s_list[cur][i];
+                int32_t bk;
+                const unsigned long long kk = wave_bid(s, a, &bk);
+                if (lane == 0) post(i, a, kk, bk);
+            }
+        } else {
+            constexpr int kGl = 16;
+            for (int i = threadIdx.x / kGl; i < m; i += kTailBlock / kGl) {
+                const int32_t a = s_list[cur][i];
+                int32_t bk;
+                const unsigned long long kk = group_bid<kGl, 8>(s, a, &bk);
+                if ((threadIdx.x & (kGl - 1)) == 0) post(i, a, kk, bk);
             }
         }
         if (threadIdx.x == 0) s_cnt[cur ^ 1] = 0;
@@ -338,7 +457,7 @@ __global__ __launch_bounds__(kTailBlock) void k_auc_tail(AucState s, int64_t r0,
 // Hand the rounds to k_auc_tail once a round had <= this many bidders (SWARM_AUCTION_TAIL,
 // read per call; 0 = never, tests use it to exercise both paths).
 int auc_tail_threshold() {
-    int tail = 512;
+    int tail = 128;  // C4 sweep: 16..512 -> best at 96..128
     if (const char *e = getenv("SWARM_AUCTION_TAIL")) tail = atoi(e);
     return tail < 0 ? 0 : (tail > kTailCap ? kTailCap : tail);
 }
@@ -560,12 +679,36 @@ int swarm_auction(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *a
     unsigned long long *h = static_cast<unsigned long long *>(pinned(ctx, size_t(kMaxBatch) * 8 + 64));
     if (!h) return SWARM_ERR_OOM;
 
-    const unsigned bgrid = grid_for(n, kBlock / kWave, 8192), rgrid = grid_for(t, kBlock, 4096);
+    // bidder lists (round parity), per-entry targets and keys, list counters, per-round log
+    AucList al{};
+    {
+        char *p;
+        const size_t nb = size_t(n) * 4;
+        SW_ALLOC(p, ctx, S_AUC_LIST, 4 * nb + size_t(n) * 8 + 64 + (size_t(max_rounds) + 2) * 8);
+        al.L[0] = reinterpret_cast<int32_t *>(p);
+        al.L[1] = reinterpret_cast<int32_t *>(p + nb);
+        al.tgt[0] = reinterpret_cast<int32_t *>(p + 2 * nb);
+        al.tgt[1] = reinterpret_cast<int32_t *>(p + 3 * nb);
+        al.mykey = reinterpret_cast<unsigned long long *>(p + 4 * nb);
+        al.cnt = reinterpret_cast<unsigned *>(p + 4 * nb + size_t(n) * 8);
+        al.log = reinterpret_cast<int64_t *>(p + 4 * nb + size_t(n) * 8 + 64);
+        const unsigned c0[2] = {0u, unsigned(n)};  // round 1 reads parity 1: every agent bids
+        SW_HIP(hipMemcpyAsync(al.cnt, c0, 8, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_auc_iota, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s, al.L[1], n);
+        SW_LAUNCHED();
+        SW_HIP(hipMemsetAsync(al.log, 0, (size_t(max_rounds) + 2) * 8, s));
+        SW_HIP(hipStreamSynchronize(s));  // c0 leaves scope
+    }
     const int64_t tail_thr = auc_tail_threshold();
     int64_t r = 1, found = -1, last_nb = n, launched = 0, tail_rounds = 0, total_bids = 0;
     int batch = 8;
     while (r <= max_rounds && found < 0) {
         if (last_nb <= tail_thr) {  // the long tail: one workgroup runs every remaining round
+            if (r > 1) {
+                hipLaunchKernelGGL(k_auc_clear_keys, dim3(grid_for(last_nb, kBlock, 1024)), dim3(kBlock), 0, s, st, al,
+                                   r);
+                SW_LAUNCHED();
+            }
             int64_t *ddone = dlog + max_rounds;
             hipLaunchKernelGGL(k_auc_tail, dim3(1), dim3(kTailBlock), 0, s, st, r, int64_t(max_rounds), dlog, ddone);
             SW_LAUNCHED();
@@ -585,16 +728,16 @@ int swarm_auction(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *a
             break;
         }
         const int64_t rend = (max_rounds - r + 1 < batch) ? max_rounds : r + batch - 1;
+        // grids sized by the last known bidder count: an upper bound (lists never grow)
+        const unsigned bgrid = grid_for(last_nb, kBlock / kWave, 8192), rgrid = grid_for(last_nb, kBlock, 4096);
         for (int64_t q = r; q <= rend; ++q) {
-            hipLaunchKernelGGL(k_auc_bid, dim3(bgrid), dim3(kBlock), 0, s, st, q);
+            hipLaunchKernelGGL(k_auc_bid_list, dim3(bgrid), dim3(kBlock), 0, s, st, al, q);
             SW_LAUNCHED();
-            hipLaunchKernelGGL(k_auc_resolve, dim3(rgrid), dim3(kBlock), 0, s, st, q);
+            hipLaunchKernelGGL(k_auc_resolve_list, dim3(rgrid), dim3(kBlock), 0, s, st, al, q);
             SW_LAUNCHED();
         }
         launched = rend;
-        hipLaunchKernelGGL(k_auc_totals, dim3(rend - r + 1), dim3(kWave), 0, s, st.ring, r, dtot);
-        SW_LAUNCHED();
-        SW_HIP(hipMemcpyAsync(h, dtot, size_t(rend - r + 1) * 8, hipMemcpyDeviceToHost, s));
+        SW_HIP(hipMemcpyAsync(h, al.log + r, size_t(rend - r + 1) * 8, hipMemcpyDeviceToHost, s));
         SW_HIP(hipStreamSynchronize(s));
         for (int64_t q = r; q <= rend; ++q) {
             const int64_t nb = int64_t(h[q - r]);

@@ -44,6 +44,7 @@ enum Slot {
     S_AUC_V,          // auction: candidate values (f32)
     S_AUC_OUT,        // auction: dropped-out flags
     S_AUC_KEY,        // auction: per-task bid keys (u64)
+    S_AUC_LIST,       // auction: bidder lists, targets, keys, counters, per-round log
     S_FSM_MAIL,       // protocol: mail bitmap (1 bit per agent) + list counters
     S_FSM_LIST,       // protocol: receivers of the current tick
     S_FSM_SEND,       // protocol: per-workgroup sender segments + counts
