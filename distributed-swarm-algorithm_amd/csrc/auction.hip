@@ -23,7 +23,7 @@
 //                key f32bits(bid) << 32 | ~id -- highest bid, then lowest ID, no conflicts.
 //   k_auc_resolve_list  one thread per list entry: the standing key's bidder takes the task;
 //                losers and displaced owners form the next round's list.
-//   (k_auc_bid / k_auc_resolve: the same over every agent / task, for the sharded rounds.)
+//   (k_auc_bid / k_auc_resolve_ids: every agent / task per round, for the sharded rounds.)
 //   k_auc_tail   once few agents still bid (prices rising on a handful of contested tasks, the
 //                auction's long tail), ONE workgroup runs all remaining rounds with its bidder
 //                list in LDS, workgroup barriers between the phases and workgroup-scoped key
@@ -238,22 +238,6 @@ __global__ __launch_bounds__(kBlock) void k_auc_bid(AucState s, int64_t r) {
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_auc_resolve(AucState s, int64_t r) {
-    if (blockIdx.x == 0)  // recycle the counter slots of round r + kARing/2
-        for (int i = threadIdx.x; i < kAShards; i += kBlock) *aslot(s.ring, r + kARing / 2, i) = 0;
-    for (int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x; k < s.t; k += int64_t(gridDim.x) * kBlock) {
-        const unsigned long long kk = s.key[k];
-        if (!kk) continue;
-        const int32_t w = index_of_id(s, 0xFFFFFFFFu - static_cast<uint32_t>(kk & 0xFFFFFFFFull));
-        const int32_t prev = s.owner[k];
-        if (prev >= 0) s.assigned[prev] = -1;
-        s.owner[k] = w;
-        s.assigned[w] = int32_t(k);
-        s.price[k] = __uint_as_float(static_cast<uint32_t>(kk >> 32));
-        s.key[k] = 0;
-    }
-}
-
 // ---------------------------------------------------------------- list-driven rounds
 // The multi-workgroup rounds keep the bidder list (the unassigned, active agents: it never grows)
 // instead of scanning every agent and every task: round r's list -> bids (a wave per bidder) ->
@@ -349,14 +333,6 @@ __global__ __launch_bounds__(kBlock) void k_auc_clear_keys(AucState s, AucList l
     const int32_t *tgt = l.tgt[(r - 1) & 1];
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < m; i += int64_t(gridDim.x) * kBlock)
         if (tgt[i] >= 0) key[tgt[i]] = 0;
-}
-
-// totals[i] = bidders of round r0 + i (one wave per round).
-__global__ void k_auc_totals(unsigned long long *ring, int64_t r0, unsigned long long *totals) {
-    unsigned long long v = *aslot(ring, r0 + blockIdx.x, threadIdx.x);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (threadIdx.x == 0) totals[blockIdx.x] = v;
 }
 
 // ---------------------------------------------------------------- the long tail, one workgroup
@@ -672,8 +648,6 @@ int swarm_auction(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *a
     SW_ALLOC(st.key, ctx, S_AUC_KEY, size_t(t) * 16);  // two halves: k_auc_tail double-buffers by round
     SW_HIP(hipMemsetAsync(st.key, 0, size_t(t) * 16, s));
     constexpr int kMaxBatch = 256;
-    unsigned long long *dtot;
-    SW_ALLOC(dtot, ctx, S_ESTATS, size_t(kMaxBatch) * 8 + 64);
     int64_t *dlog;
     SW_ALLOC(dlog, ctx, S_TMP1, (size_t(max_rounds) + 2) * 8);
     unsigned long long *h = static_cast<unsigned long long *>(pinned(ctx, size_t(kMaxBatch) * 8 + 64));
