@@ -38,9 +38,11 @@ def _worker(rank, world, port, out_q, n_per, deg, check_every):
         sh = ShardedSwarm(d["ids"], d["x"], d["y"], d["caps"], d["strip"], device="cpu", backend=NumpyBackend())
         r = sh.elect(check_every=check_every)
         res, won, gst = sh.allocate(d["tx"], d["ty"], d["treq"])
+        res0, won0, _ = sh.allocate(d["tx"], d["ty"], d["treq"], hysteresis=0.0)  # argmax (h = 0) mode
         out_q.put(dict(rank=rank, rounds=r.rounds_exec, changes=r.changes, ids=sh.ids.numpy(),
                        leader=r.leader.numpy(), state=r.state.numpy(), winner=res.winner.numpy(),
                        util=res.util.numpy(), won=won.numpy(), gstats=gst,
+                       winner0=res0.winner.numpy(), won0=won0.numpy(),
                        n_ghost=(sh.n_glo, sh.n_ghi)))
     finally:
         dist.destroy_process_group()
@@ -92,6 +94,12 @@ def test_sharded_election_and_allocation_match_single_graph(world, oracle_mod):
         assert all(won_want[int(i)] == int(w) for i, w in zip(o["ids"], o["won"]))
         assert o["gstats"]["n_claims"] == wa["n_claims"]
         assert o["gstats"]["n_conflicts"] == wa["n_conflicts"]
+    # hysteresis 0: the argmax (lowest-ID tie-break) resolution through the same sharded path
+    w0 = oracle_mod.allocate(ids, x, y, caps, cat("tx"), cat("ty"), cat("treq"), hysteresis=0.0)
+    np.testing.assert_array_equal(np.concatenate([o["winner0"] for o in outs]), w0["winner"])
+    won0 = dict(zip(ids.tolist(), w0["won"].tolist()))
+    for o in outs:
+        assert all(won0[int(i)] == int(w) for i, w in zip(o["ids"], o["won0"]))
 
 
 def test_shard_ids_are_a_global_permutation():
