@@ -96,45 +96,75 @@ __global__ __launch_bounds__(kBlock) void k_enc_len(int64_t m, EncIn in, int wid
     }
 }
 
+// Packet bytes of message i at p (status 0).
+__device__ __forceinline__ void write_packet(uint8_t *p, const EncIn &in, int64_t i, int wide) {
+    const int ty = int(in.type[i]);
+    p[0] = uint8_t(ty);
+    int h;
+    if (wide) {
+        put_u32(p + 1, uint32_t(in.sender[i]));
+        put_u32(p + 5, uint32_t(in.tick[i]));
+        h = 9;
+    } else {
+        p[1] = uint8_t(in.sender[i]);
+        put_u32(p + 2, uint32_t(in.tick[i]));
+        h = 6;
+    }
+    p += h;
+    switch (ty) {
+        case T_HB:
+            put_u32(p, __float_as_uint(float(in.a[i])));
+            put_u32(p + 4, __float_as_uint(float(in.b[i])));
+            break;
+        case T_ACCLAIM:
+            if (wide) put_u32(p, uint32_t(in.sender[i]));
+            else p[0] = uint8_t(in.sender[i]);
+            break;
+        case T_CLAIM:
+            put_u32(p, uint32_t(in.task[i]));
+            put_u32(p + 4, __float_as_uint(float(in.a[i])));
+            break;
+        case T_CONFLICT:
+            put_u32(p, uint32_t(in.task[i]));
+            if (wide) put_u32(p + 4, uint32_t(in.winner[i]));
+            else p[4] = uint8_t(in.winner[i]);
+            break;
+        default:
+            break;
+    }
+}
+
+// Messages [c0, c0 + kEncPer) per workgroup: packets are assembled in LDS at the same 16-byte
+// alignment they have in `out`, then the workgroup's contiguous output range is stored with
+// 16-byte vector stores (its partial first / last 16 bytes byte by byte: they share lines with
+// the neighbouring workgroups' packets).
+constexpr int kEncJ = 4, kEncPer = kBlock * kEncJ, kMaxPkt = 17;
+constexpr int kEncLds = (kEncPer * kMaxPkt + 32 + 15) / 16;  // uint4 words
+
 __global__ __launch_bounds__(kBlock) void k_enc_write(int64_t m, EncIn in, int wide, const int64_t *__restrict__ off,
                                                      const int8_t *__restrict__ status, uint8_t *__restrict__ out) {
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < m; i += int64_t(gridDim.x) * kBlock) {
-        if (status[i]) continue;
-        uint8_t *p = out + off[i];
-        const int ty = int(in.type[i]);
-        p[0] = uint8_t(ty);
-        int h;
-        if (wide) {
-            put_u32(p + 1, uint32_t(in.sender[i]));
-            put_u32(p + 5, uint32_t(in.tick[i]));
-            h = 9;
+    __shared__ uint4 s_buf[kEncLds];
+    uint8_t *lb = reinterpret_cast<uint8_t *>(s_buf);
+    for (int64_t c0 = int64_t(blockIdx.x) * kEncPer; c0 < m; c0 += int64_t(gridDim.x) * kEncPer) {
+        const int64_t c1 = c0 + kEncPer < m ? c0 + kEncPer : m;
+        const int64_t base = off[c0], end = off[c1], abase = base & ~int64_t(15);
+#pragma unroll
+        for (int j = 0; j < kEncJ; ++j) {
+            const int64_t i = c0 + j * kBlock + threadIdx.x;
+            if (i < c1 && status[i] == 0) write_packet(lb + (off[i] - abase), in, i, wide);
+        }
+        __syncthreads();
+        const int64_t A = (base + 15) & ~int64_t(15), B = end & ~int64_t(15);
+        if (A >= B) {  // no whole 16-byte block: bytewise
+            for (int64_t x = base + threadIdx.x; x < end; x += kBlock) out[x] = lb[x - abase];
         } else {
-            p[1] = uint8_t(in.sender[i]);
-            put_u32(p + 2, uint32_t(in.tick[i]));
-            h = 6;
+            if (threadIdx.x < A - base) out[base + threadIdx.x] = lb[base + threadIdx.x - abase];
+            if (threadIdx.x < end - B) out[B + threadIdx.x] = lb[B + threadIdx.x - abase];
+            uint4 *dst = reinterpret_cast<uint4 *>(out + A);
+            const uint4 *src = s_buf + (A - abase) / 16;
+            for (int64_t q = threadIdx.x; q < (B - A) / 16; q += kBlock) dst[q] = src[q];
         }
-        p += h;
-        switch (ty) {
-            case T_HB:
-                put_u32(p, __float_as_uint(float(in.a[i])));
-                put_u32(p + 4, __float_as_uint(float(in.b[i])));
-                break;
-            case T_ACCLAIM:
-                if (wide) put_u32(p, uint32_t(in.sender[i]));
-                else p[0] = uint8_t(in.sender[i]);
-                break;
-            case T_CLAIM:
-                put_u32(p, uint32_t(in.task[i]));
-                put_u32(p + 4, __float_as_uint(float(in.a[i])));
-                break;
-            case T_CONFLICT:
-                put_u32(p, uint32_t(in.task[i]));
-                if (wide) put_u32(p + 4, uint32_t(in.winner[i]));
-                else p[4] = uint8_t(in.winner[i]);
-                break;
-            default:
-                break;
-        }
+        __syncthreads();  // s_buf reused by the next chunk
     }
 }
 
@@ -245,7 +275,8 @@ int swarm_codec_encode(swarm_ctx *ctx, int64_t m, const int64_t *type, const int
         set_error("output buffer holds %lld bytes, the packets need %lld", (long long)cap, (long long)*total_bytes);
         return SWARM_ERR_RANGE;
     }
-    hipLaunchKernelGGL(k_enc_write, dim3(grid), dim3(kBlock), 0, s, m, in, int(wide != 0), offsets, status, out);
+    hipLaunchKernelGGL(k_enc_write, dim3(grid_for(m, kEncPer, 4096)), dim3(kBlock), 0, s, m, in, int(wide != 0),
+                       offsets, status, out);
     SW_LAUNCHED();
     return SWARM_OK;
 }

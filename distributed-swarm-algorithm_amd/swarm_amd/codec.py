@@ -25,6 +25,8 @@ from . import _lib
 from .swarm import _dev, _to
 
 HEARTBEAT, ELECTION_ACCLAIM, COORDINATOR, TASK_CLAIM, TASK_CONFLICT = 1, 2, 3, 4, 5
+MAX_PACKET, MAX_PACKET_WIDE = 14, 17   # '!BBI' + '!ff' / '!If';  '!BII' + '!II'
+WORST_CASE_LIMIT = 1 << 31              # bytes: above it, size the buffer with a first call
 
 
 @dataclass
@@ -68,15 +70,18 @@ def encode(type, sender, tick, a=None, b=None, task=None, winner=None, *, wide=F
     total = ctypes.c_int64(0)
     L = _lib.lib()
     args = [ty, snd, tk, fa, fb, tsk, win]
+    worst = m * (MAX_PACKET_WIDE if wide else MAX_PACKET)
     with torch.cuda.device(dev):
         p = [_lib.ptr(t) if m else None for t in args]
-        _lib.check(L.swarm_codec_encode(_lib.ctx(), m, *p, int(bool(wide)), None, 0, _lib.ptr(offsets),
-                                        _lib.ptr(status) if m else None, ctypes.byref(total), _lib.stream()))
-        buf = torch.empty(max(total.value, 1), dtype=torch.uint8, device=dev)
-        if m:
-            _lib.check(L.swarm_codec_encode(_lib.ctx(), m, *p, int(bool(wide)), _lib.ptr(buf), buf.numel(),
-                                            _lib.ptr(offsets), _lib.ptr(status), ctypes.byref(total),
-                                            _lib.stream()))
+        if worst <= WORST_CASE_LIMIT:  # one call into a worst-case buffer
+            buf = torch.empty(max(worst, 1), dtype=torch.uint8, device=dev)
+        else:  # a sizing call first
+            _lib.check(L.swarm_codec_encode(_lib.ctx(), m, *p, int(bool(wide)), None, 0, _lib.ptr(offsets),
+                                            _lib.ptr(status) if m else None, ctypes.byref(total), _lib.stream()))
+            buf = torch.empty(max(total.value, 1), dtype=torch.uint8, device=dev)
+        _lib.check(L.swarm_codec_encode(_lib.ctx(), m, *p, int(bool(wide)), _lib.ptr(buf), buf.numel(),
+                                        _lib.ptr(offsets), _lib.ptr(status) if m else None, ctypes.byref(total),
+                                        _lib.stream()))
     return Encoded(buf[:total.value], offsets, status, total.value)
 
 

@@ -1,0 +1,32 @@
+"""Time the batch codec at 10M messages of every type: encode (fields -> packets) and decode.
+python tools/codec_probe.py [M] [wide]"""
+import sys
+import time
+
+sys.path.insert(0, "distributed-swarm-algorithm_amd")
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from swarm_amd import codec  # noqa: E402
+
+m = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
+wide = len(sys.argv) > 2 and sys.argv[2] == "wide"
+g = np.random.default_rng(1)
+idm = 2**31 if wide else 256
+f = [torch.as_tensor(v, device="cuda") for v in (g.integers(1, 6, m), g.integers(0, idm, m), g.integers(0, 2**32, m),
+                                                 g.normal(0, 1e3, m), g.normal(0, 1e3, m), g.integers(0, 2**32, m),
+                                                 g.integers(0, idm, m))]
+best_e = best_d = 1e9
+for rep in range(4):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e = codec.encode(*f, wide=wide)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    d = codec.decode(e.buf, e.offsets, wide=wide)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    if rep:
+        best_e, best_d = min(best_e, t1 - t0), min(best_d, t2 - t1)
+pk = e.total_bytes
+print(f"m={m} wide={wide} bytes={pk} encode {best_e * 1e3:.3f} ms ({(146 * m + pk) / best_e / 1e9:.0f} GB/s alg) "
+      f"decode {best_d * 1e3:.3f} ms ({(66 * m + pk) / best_d / 1e9:.0f} GB/s alg)")
