@@ -69,6 +69,29 @@ struct Heard {
     int32_t lead, hb_from;  // hb_from: the last accepted heartbeat's sender (its position -> leader_pos)
 };
 
+// What one sender's packets of a tick do to the receiver (s: sender ID, j: its index), in the
+// order it sent them: ACCLAIM then COORDINATOR, then HEARTBEAT.
+__device__ __forceinline__ void hear(Heard &h, uint8_t o, int32_t s, int32_t j, int32_t me, bool hb_tick) {
+    if (o & kAcclaim) {
+        if (s < me && (h.st == ST_L || h.st == ST_W) && hb_tick) h.ob |= kHeartbeat;  // bully back
+        h.lead = s;  // (higher sender: follow) then COORDINATOR: unconditional takeover
+        h.lead_set = true;
+        h.st = ST_F;
+        h.live = true;
+    }
+    if (o & kHeartbeat) {
+        if (h.st == ST_L && s < me) {
+            if (hb_tick) h.ob |= kHeartbeat;
+        } else {
+            h.st = ST_F;  // yield (LEADER) / stop waiting (ELECTION_WAIT) / stay FOLLOWER
+            h.lead = s;
+            h.lead_set = true;
+            h.live = true;
+            h.hb_from = j;
+        }
+    }
+}
+
 __device__ __forceinline__ void receive_row(int32_t b, int32_t e, const int32_t *__restrict__ col,
                                             const uint8_t *__restrict__ ob_in, const int32_t *__restrict__ ids,
                                             int32_t me, bool hb_tick, Heard &h) {
@@ -90,26 +113,7 @@ __device__ __forceinline__ void receive_row(int32_t b, int32_t e, const int32_t 
 #pragma unroll
         for (int u = 0; u < kRecv; ++u) {
             const uint8_t o = oo[u] & (kAcclaim | kHeartbeat);
-            if (!o) continue;
-            const int32_t s = ss[u];
-            if (o & kAcclaim) {
-                if (s < me && (h.st == ST_L || h.st == ST_W) && hb_tick) h.ob |= kHeartbeat;  // bully back
-                h.lead = s;  // (higher sender: follow) then COORDINATOR: unconditional takeover
-                h.lead_set = true;
-                h.st = ST_F;
-                h.live = true;
-            }
-            if (o & kHeartbeat) {
-                if (h.st == ST_L && s < me) {
-                    if (hb_tick) h.ob |= kHeartbeat;
-                } else {
-                    h.st = ST_F;  // yield (LEADER) / stop waiting (ELECTION_WAIT) / stay FOLLOWER
-                    h.lead = s;
-                    h.lead_set = true;
-                    h.live = true;
-                    h.hb_from = jj[u];
-                }
-            }
+            if (o) hear(h, o, ss[u], jj[u], me, hb_tick);
         }
     }
 }
@@ -227,11 +231,30 @@ __global__ __launch_bounds__(kBlock) void k_tick_pull(int64_t n, int64_t t, cons
 constexpr uint8_t kFresh = 0x80;  // outbox byte written by k_receive this tick
 constexpr uint8_t kHeard = 0x04;  // ... whose receiver got a liveness proof
 
-// Mail bits for the hearers of agent i (hearers CSR), one atomicOr per distinct 64-agent word.
-// (Plain byte marks were tried: the scan of 1-byte marks dirtied by scattered byte stores costs
-// 5x the 64-bit bitmap's, more than the atomics save.)
-__device__ __forceinline__ void mail_hearers(int32_t b, int32_t e, const int32_t *__restrict__ tcol,
-                                             unsigned long long *__restrict__ mail) {
+// Mail for the hearers of sender i: one bit per agent (one atomicOr per distinct 64-agent word).
+// The atomic returns the word's previous bits: a hearer whose bit was clear gets from[r] = i (its
+// only sender so far); one whose bit was already set gets its `multi` bit (several senders: it
+// walks its row).  (Plain byte marks were tried: the scan of 1-byte marks dirtied by scattered
+// byte stores costs 5x the 64-bit bitmap's, more than the atomics save.)
+struct Mail {
+    unsigned long long *bits, *multi;
+    int32_t *from;
+};
+
+__device__ __forceinline__ void mail_flush(const Mail &m, int32_t w, unsigned long long bits, int32_t sender) {
+    const unsigned long long old = atomicOr(&m.bits[w], bits);
+    const unsigned long long dup = old & bits;
+    if (dup) atomicOr(&m.multi[w], dup);
+    unsigned long long fresh = bits & ~old;
+    while (fresh) {
+        const int q = __ffsll((long long)fresh) - 1;
+        fresh &= fresh - 1;
+        m.from[int64_t(w) * 64 + q] = sender;
+    }
+}
+
+__device__ __forceinline__ void mail_hearers(int32_t b, int32_t e, const int32_t *__restrict__ tcol, const Mail &m,
+                                             int32_t sender) {
     int32_t w = -1;
     unsigned long long bits = 0;
     for (int32_t k0 = b; k0 < e; k0 += kRecv) {
@@ -243,38 +266,44 @@ __device__ __forceinline__ void mail_hearers(int32_t b, int32_t e, const int32_t
             const int32_t r = rr[u];
             if (r < 0) continue;
             if ((r >> 6) != w) {
-                if (bits) atomicOr(&mail[w], bits);  // no return value: fire and forget
+                if (bits) mail_flush(m, w, bits, sender);
                 w = r >> 6;
                 bits = 0;
             }
             bits |= 1ull << (r & 63);
         }
     }
-    if (bits) atomicOr(&mail[w], bits);
+    if (bits) mail_flush(m, w, bits, sender);
 }
 
 // Resumed run: mail for the receivers of tick t0's sends.
 __global__ __launch_bounds__(kBlock) void k_mail_from_outbox(int64_t n, const uint8_t *__restrict__ ob,
                                                             const int32_t *__restrict__ trp,
-                                                            const int32_t *__restrict__ tcol,
-                                                            unsigned long long *__restrict__ mail) {
+                                                            const int32_t *__restrict__ tcol, Mail m) {
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock)
-        if (ob[i]) mail_hearers(trp[i], trp[i + 1], tcol, mail);
+        if (ob[i]) mail_hearers(trp[i], trp[i + 1], tcol, m, int32_t(i));
 }
 
 // Mail bitmap -> receiver list, words cleared.  One atomicAdd per workgroup pass.
-__global__ __launch_bounds__(kBlock) void k_compact(int64_t n_words, unsigned long long *__restrict__ mail,
-                                                   int32_t *__restrict__ list, unsigned *__restrict__ n_list) {
+// List entries carry the multi-sender flag in bit 31 (agent indices are < 2^31).
+constexpr uint32_t kMulti = 0x80000000u;
+
+__global__ __launch_bounds__(kBlock) void k_compact(int64_t n_words, Mail mail, int32_t *__restrict__ list,
+                                                   unsigned *__restrict__ n_list) {
     __shared__ unsigned s_wave[kBlock / kWave];
     __shared__ unsigned s_base;
     const unsigned lane = threadIdx.x & (kWave - 1);
     const int wv = threadIdx.x / kWave;
     for (int64_t base = int64_t(blockIdx.x) * kBlock; base < n_words; base += int64_t(gridDim.x) * kBlock) {
         const int64_t w = base + threadIdx.x;
-        unsigned long long bits = 0;
+        unsigned long long bits = 0, multi = 0;
         if (w < n_words) {
-            bits = mail[w];
-            if (bits) mail[w] = 0;
+            bits = mail.bits[w];
+            if (bits) {
+                mail.bits[w] = 0;
+                multi = mail.multi[w];
+                if (multi) mail.multi[w] = 0;
+            }
         }
         const unsigned c = unsigned(__popcll(bits));
         unsigned incl = c;  // wave inclusive scan
@@ -299,13 +328,14 @@ __global__ __launch_bounds__(kBlock) void k_compact(int64_t n_words, unsigned lo
         while (bits) {
             const int b = __ffsll((long long)bits) - 1;
             bits &= bits - 1;
-            list[o++] = int32_t(w * 64 + b);
+            list[o++] = int32_t(uint32_t(w * 64 + b) | (((multi >> b) & 1ull) ? kMulti : 0u));
         }
         __syncthreads();
     }
 }
 
 __global__ __launch_bounds__(kBlock) void k_receive(int64_t t, const int32_t *__restrict__ list,
+                                                   const int32_t *__restrict__ from,
                                                    const unsigned *__restrict__ n_list, unsigned *__restrict__ n_next,
                                                    const int32_t *__restrict__ ids, const double2 *__restrict__ pos,
                                                    const int32_t *__restrict__ rp, const int32_t *__restrict__ col,
@@ -316,11 +346,20 @@ __global__ __launch_bounds__(kBlock) void k_receive(int64_t t, const int32_t *__
     const int64_t m = *n_list;
     const double now = double(t) * dt;
     for (int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x; q < m; q += int64_t(gridDim.x) * kBlock) {
-        const int32_t i = list[q];
+        const uint32_t entry = uint32_t(list[q]);
+        const int32_t i = int32_t(entry & ~kMulti);
         if (!f.alive[i]) continue;
         const uint8_t st0 = f.state[i];
         Heard h{st0, 0, false, false, 0, -1};
-        receive_row(rp[i], rp[i + 1], col, ob_in, ids, ids[i], ((t + tick_off[i]) % 10) == 0, h);
+        const int32_t me = ids[i];
+        const bool hb_tick = ((t + tick_off[i]) % 10) == 0;
+        if (entry & kMulti) {  // several senders: the row, in CSR order
+            receive_row(rp[i], rp[i + 1], col, ob_in, ids, me, hb_tick, h);
+        } else {  // exactly one sender: no row walk
+            const int32_t j = from[i];
+            const uint8_t o = ob_in[j] & (kAcclaim | kHeartbeat);
+            if (o) hear(h, o, ids[j], j, me, hb_tick);
+        }
         apply_heard(i, h, now, pos, f);
         if (h.st != st0) f.state[i] = h.st;
         if (h.lead_set) f.leader[i] = h.lead;
@@ -374,12 +413,12 @@ __global__ __launch_bounds__(kBlock) void k_sweep(int64_t n, int64_t t, const in
 __global__ __launch_bounds__(kBlock) void k_mail(const int32_t *__restrict__ senders, int64_t seg_cap,
                                                 const int32_t *__restrict__ seg_count,
                                                 const int32_t *__restrict__ trp, const int32_t *__restrict__ tcol,
-                                                unsigned long long *__restrict__ mail) {
+                                                Mail mail) {
     const int m = seg_count[blockIdx.x];
     const int32_t *seg = senders + int64_t(blockIdx.x) * seg_cap;
     for (int q = threadIdx.x; q < m; q += kBlock) {
         const int32_t i = seg[q];
-        mail_hearers(trp[i], trp[i + 1], tcol, mail);
+        mail_hearers(trp[i], trp[i + 1], tcol, mail, i);
     }
 }
 
@@ -418,20 +457,24 @@ int swarm_protocol_run(swarm_ctx *ctx, int64_t n, const int32_t *ids, const doub
     const unsigned grid = grid_for(n, kBlock, 4096);
     const bool push = hear_row_ptr != nullptr;
     const int64_t n_words = (n + 63) / 64;
-    unsigned long long *mail = nullptr;
+    Mail mail{};
     int32_t *list = nullptr, *senders = nullptr, *seg_count = nullptr;
     int64_t seg_cap = 0;
     unsigned *n_list = nullptr;
     if (push) {  // mail bitmap + the two list counters (tick parity) after it
-        SW_ALLOC(mail, ctx, S_FSM_MAIL, size_t(n_words) * 8 + 64);
+        unsigned long long *mw;  // mail bits, multi-sender bits, then the two list counters
+        SW_ALLOC(mw, ctx, S_FSM_MAIL, size_t(n_words) * 16 + 64);
+        mail.bits = mw;
+        mail.multi = mw + n_words;
+        SW_ALLOC(mail.from, ctx, S_FSM_FROM, size_t(n) * 4);
         SW_ALLOC(list, ctx, S_FSM_LIST, size_t(n) * 4);
         // per-workgroup sender segments of the sweep (grid-stride: each workgroup sees at most
         // seg_cap agents), then their counts
         seg_cap = (n + int64_t(grid) * kBlock - 1) / (int64_t(grid) * kBlock) * kBlock;
         SW_ALLOC(senders, ctx, S_FSM_SEND, size_t(seg_cap) * grid * 4 + size_t(grid) * 4);
         seg_count = senders + seg_cap * grid;
-        n_list = reinterpret_cast<unsigned *>(mail + n_words);
-        SW_HIP(hipMemsetAsync(mail, 0, size_t(n_words) * 8 + 64, s));
+        n_list = reinterpret_cast<unsigned *>(mw + 2 * n_words);
+        SW_HIP(hipMemsetAsync(mw, 0, size_t(n_words) * 16 + 64, s));
         hipLaunchKernelGGL(k_mail_from_outbox, dim3(grid), dim3(kBlock), 0, s, n,
                            fsm->outbox + size_t(t0 & 1) * size_t(n), hear_row_ptr, hear_col, mail);
         SW_LAUNCHED();
@@ -451,7 +494,7 @@ int swarm_protocol_run(swarm_ctx *ctx, int64_t n, const int32_t *ids, const doub
             hipLaunchKernelGGL(k_compact, dim3(grid_for(n_words, kBlock, 2048)), dim3(kBlock), 0, s, n_words, mail,
                                list, nl);
             SW_LAUNCHED();
-            hipLaunchKernelGGL(k_receive, dim3(2048), dim3(kBlock), 0, s, t, list, nl, nl_next, ids,
+            hipLaunchKernelGGL(k_receive, dim3(2048), dim3(kBlock), 0, s, t, list, mail.from, nl, nl_next, ids,
                                reinterpret_cast<const double2 *>(pos), row_ptr, col, tick_off, f, ob_in, ob_out, dt);
             SW_LAUNCHED();
             hipLaunchKernelGGL(k_sweep, dim3(grid), dim3(kBlock), 0, s, n, t, ids, tick_off, f, ob_out, senders,

@@ -47,6 +47,7 @@ enum Slot {
     S_AUC_LIST,       // auction: bidder lists, targets, keys, counters, per-round log
     S_FSM_MAIL,       // protocol: mail bitmap (1 bit per agent) + list counters
     S_FSM_LIST,       // protocol: receivers of the current tick
+    S_FSM_FROM,       // protocol: each receiver's sender when it has exactly one
     S_FSM_SEND,       // protocol: per-workgroup sender segments + counts
     S_NUM
 };
