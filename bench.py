@@ -56,14 +56,20 @@ def pmc_traffic(kernel_prefix):
     figure of the same command with its source, or None."""
     import glob
     best = None
-    for path in glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")):
+    paths = glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json"))
+    latest = os.path.join(ROOT, "profiles", "LATEST")  # names the round directory to prefer
+    if os.path.exists(latest):
+        pref = os.path.join(ROOT, "profiles", open(latest).read().strip(), "pmc_traffic.json")
+        paths = [pref] + [q for q in paths if q != pref] if os.path.exists(pref) else paths
+    for path in paths:
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
             continue
         for k, v in d.items():
             if k.startswith(kernel_prefix) and isinstance(v, dict):
-                m = path  # newest = last in name order (profiles/r1, r1_hybrid, r2, ...)
+                # profiles/LATEST's directory first, else the last in name order
+                m = (path == paths[0] and os.path.exists(latest), path)
                 if best is None or m > best[2]:
                     best = (v["hbm_bytes_per_dispatch"], os.path.relpath(path, ROOT), m)
     return None if best is None else (best[0], f"rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE, {best[1]}")
