@@ -1,5 +1,6 @@
 """Debug aid: per-wave phase timestamps of one sparse election round (libswarm_phases.so,
-built with -DSWARM_PHASES).  Usage: python tools/phase_probe.py N ROUND [ROUND ...]"""
+built with -DSWARM_PHASES: make -C distributed-swarm-algorithm_amd/csrc phases).
+Usage: python tools/phase_probe.py N ROUND [ROUND ...]"""
 import ctypes
 import os
 import sys
