@@ -25,9 +25,9 @@ namespace swarm {
 namespace {
 
 constexpr int kObsLds = 1024;  // obstacles staged in LDS per pass (3 doubles each)
-constexpr int kNb = 8;         // neighbour positions gathered in flight per thread
+constexpr int kNb = 4;         // neighbour positions gathered in flight per thread (8 waves/SIMD: 4 beats 8 at 4 waves)
 
-__global__ __launch_bounds__(kBlock) void k_physics(int64_t n, const int32_t *__restrict__ ids,
+__global__ __launch_bounds__(kBlock, 8) void k_physics(int64_t n, const int32_t *__restrict__ ids,
                                                    const uint8_t *__restrict__ state,
                                                    const int32_t *__restrict__ leader,
                                                    const double2 *__restrict__ pin, double2 *__restrict__ pout,

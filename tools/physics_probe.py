@@ -1,15 +1,17 @@
 """Time swarm_physics_step at bench scale (10M agents, deg-16 sensor graph, 16 obstacles).
-python tools/physics_probe.py [N]"""
+python tools/physics_probe.py [N] [LIBNAME]"""
 import sys
 import time
 
 sys.path.insert(0, "distributed-swarm-algorithm_amd")
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
-from swarm_amd import gen  # noqa: E402
+from swarm_amd import _lib, gen  # noqa: E402
 from swarm_amd.swarm import Swarm  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
+if len(sys.argv) > 2:  # an alternative build under swarm_amd/ (A/B)
+    _lib.load(__import__("os").path.join(_lib.HERE, sys.argv[2]))
 d = gen.swarm_inputs(n, 2026)
 s = Swarm(d["ids"], d["x"], d["y"], device="cuda:0").build_graph(1.0)
 s.elect()
