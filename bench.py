@@ -213,7 +213,13 @@ def main():
                        "elect_mode": args.elect_mode, "alloc_mode": a.stats.get("mode_used"),
                        "rounds_exec": r.rounds_exec, "parallelism": f"agents sharded x{world}"},
             "breakdown_ms": {"elect": t_elect_ms, "alloc": t_alloc_ms},
-            "hbm_frac_step": (r.rounds_exec * bytes_round + 24 * n + 36 * args.tasks)
+            # the step's algorithmic bytes (the frontier's per-round counters, DESIGN §4, + the
+            # allocation's compulsory 24 B/agent + 36 B/task) over its time
+            "hbm_frac_step": (r.bytes_total + 24 * n + 36 * args.tasks)
+            / ((t_elect_ms + t_alloc_ms) * 1e-3) / (HBM_PEAK_GBS * 1e9),
+            # SURVEY §8d's formula, which prices every executed round as a dense round
+            # (12N + 8E + 4 bytes): > 1 because the frontier reads only the changing neighbourhoods
+            "hbm_frac_step_dense_equivalent": (r.rounds_exec * bytes_round + 24 * n + 36 * args.tasks)
             / ((t_elect_ms + t_alloc_ms) * 1e-3) / (HBM_PEAK_GBS * 1e9),
             "roofline": ({"kernel": dom["kernel"], "bound": "hbm",
                           "achieved": dom["bytes_per_launch"] / (dom["avg_launch_ms"] * 1e-3) / 1e9,
