@@ -175,65 +175,98 @@ struct DecOut {
     uint8_t *has_pos;
 };
 
+// Parse one packet p[0, len) (the dispatch of on_message_received + the handlers' unpack).
+__device__ __forceinline__ void parse_packet(const uint8_t *p, int64_t len, bool inside, int wide, int64_t i,
+                                             const DecOut &o) {
+    const int hdr = wide ? 9 : 6;
+    int st = inside ? 1 : 4;
+    int64_t ty = 0, snd = 0, tick = 0, task = 0, win = 0;
+    float a = 0.f, b = 0.f;
+    uint8_t hp = 0;
+    if (inside && len >= hdr) {
+        ty = p[0];
+        snd = wide ? int64_t(get_u32(p + 1)) : int64_t(p[1]);
+        tick = int64_t(get_u32(p + (wide ? 5 : 2)));
+        const uint8_t *q = p + hdr;
+        const int64_t pl = len - hdr;
+        st = 0;
+        switch (int(ty)) {
+            case T_HB:
+                if (pl == 8) {
+                    a = __uint_as_float(get_u32(q));
+                    b = __uint_as_float(get_u32(q + 4));
+                    hp = 1;
+                }
+                break;
+            case T_ACCLAIM:
+            case T_COORD:
+                break;
+            case T_CLAIM:
+                if (pl == 8) {
+                    task = int64_t(get_u32(q));
+                    a = __uint_as_float(get_u32(q + 4));
+                } else {
+                    st = 3;
+                }
+                break;
+            case T_CONFLICT:
+                if (pl == (wide ? 8 : 5)) {
+                    task = int64_t(get_u32(q));
+                    win = wide ? int64_t(get_u32(q + 4)) : int64_t(q[4]);
+                } else {
+                    st = 3;
+                }
+                break;
+            default:
+                st = 2;
+        }
+    }
+    o.status[i] = int8_t(st);
+    o.type[i] = (inside && len >= hdr) ? ty : 0;
+    o.sender[i] = snd;
+    o.tick[i] = tick;
+    o.task[i] = task;
+    o.winner[i] = win;
+    o.a[i] = a;
+    o.b[i] = b;
+    o.has_pos[i] = hp;
+}
+
+// Packets [c0, c0 + kEncPer) per workgroup: when their offsets are in range and their bytes fit,
+// the workgroup's contiguous input range is loaded into LDS with 16-byte loads and parsed from
+// there; otherwise (malformed offsets, oversized packets) straight from global memory.
 __global__ __launch_bounds__(kBlock) void k_decode(int64_t m, const uint8_t *__restrict__ buf, int64_t buf_len,
                                                   const int64_t *__restrict__ off, int wide, DecOut o) {
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < m; i += int64_t(gridDim.x) * kBlock) {
-        const int64_t pb = off[i], pe = off[i + 1];
-        const bool inside = 0 <= pb && pb <= pe && pe <= buf_len;  // else status 4, nothing read
-        const uint8_t *p = buf + (inside ? pb : 0);
-        const int64_t len = inside ? pe - pb : 0;
-        const int hdr = wide ? 9 : 6;
-        int st = inside ? 1 : 4;
-        int64_t ty = 0, snd = 0, tick = 0, task = 0, win = 0;
-        float a = 0.f, b = 0.f;
-        uint8_t hp = 0;
-        if (inside && len >= hdr) {
-            ty = p[0];
-            snd = wide ? int64_t(get_u32(p + 1)) : int64_t(p[1]);
-            tick = int64_t(get_u32(p + (wide ? 5 : 2)));
-            const uint8_t *q = p + hdr;
-            const int64_t pl = len - hdr;
-            st = 0;
-            switch (int(ty)) {
-                case T_HB:
-                    if (pl == 8) {
-                        a = __uint_as_float(get_u32(q));
-                        b = __uint_as_float(get_u32(q + 4));
-                        hp = 1;
-                    }
-                    break;
-                case T_ACCLAIM:
-                case T_COORD:
-                    break;
-                case T_CLAIM:
-                    if (pl == 8) {
-                        task = int64_t(get_u32(q));
-                        a = __uint_as_float(get_u32(q + 4));
-                    } else {
-                        st = 3;
-                    }
-                    break;
-                case T_CONFLICT:
-                    if (pl == (wide ? 8 : 5)) {
-                        task = int64_t(get_u32(q));
-                        win = wide ? int64_t(get_u32(q + 4)) : int64_t(q[4]);
-                    } else {
-                        st = 3;
-                    }
-                    break;
-                default:
-                    st = 2;
+    __shared__ uint4 s_buf[kEncLds];
+    uint8_t *lb = reinterpret_cast<uint8_t *>(s_buf);
+    for (int64_t c0 = int64_t(blockIdx.x) * kEncPer; c0 < m; c0 += int64_t(gridDim.x) * kEncPer) {
+        const int64_t c1 = c0 + kEncPer < m ? c0 + kEncPer : m;
+        const int64_t lo = off[c0], hi = off[c1], alo = lo & ~int64_t(15);
+        const bool staged = 0 <= lo && lo <= hi && hi <= buf_len && hi - alo <= int64_t(kEncLds) * 16 &&
+                            (reinterpret_cast<uintptr_t>(buf) & 15) == 0;
+        if (staged) {  // [alo, A) and [B, hi) bytewise, [A, B) as 16-byte words
+            const int64_t A = (lo + 15) & ~int64_t(15), B = hi & ~int64_t(15);
+            if (A >= B) {
+                for (int64_t x = lo + threadIdx.x; x < hi; x += kBlock) lb[x - alo] = buf[x];
+            } else {
+                if (threadIdx.x < A - lo) lb[lo + threadIdx.x - alo] = buf[lo + threadIdx.x];
+                if (threadIdx.x < hi - B) lb[B + threadIdx.x - alo] = buf[B + threadIdx.x];
+                const uint4 *src = reinterpret_cast<const uint4 *>(buf + A);
+                for (int64_t q = threadIdx.x; q < (B - A) / 16; q += kBlock) s_buf[(A - alo) / 16 + q] = src[q];
             }
         }
-        o.status[i] = int8_t(st);
-        o.type[i] = len >= hdr ? ty : 0;
-        o.sender[i] = snd;
-        o.tick[i] = tick;
-        o.task[i] = task;
-        o.winner[i] = win;
-        o.a[i] = a;
-        o.b[i] = b;
-        o.has_pos[i] = hp;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kEncJ; ++j) {
+            const int64_t i = c0 + j * kBlock + threadIdx.x;
+            if (i >= c1) continue;
+            const int64_t pb = off[i], pe = off[i + 1];
+            const bool inside = 0 <= pb && pb <= pe && pe <= buf_len;  // else status 4, nothing read
+            const bool in_lds = staged && inside && pb >= lo && pe <= hi;
+            const uint8_t *p = in_lds ? lb + (pb - alo) : buf + (inside ? pb : 0);
+            parse_packet(p, inside ? pe - pb : 0, inside, wide, i, o);
+        }
+        __syncthreads();  // s_buf reused by the next chunk
     }
 }
 
@@ -294,7 +327,7 @@ int swarm_codec_decode(swarm_ctx *ctx, int64_t m, const uint8_t *buf, int64_t bu
     if (m == 0) return SWARM_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const DecOut o{status, type, sender, tick, task, winner, a, b, has_pos};
-    hipLaunchKernelGGL(k_decode, dim3(grid_for(m, kBlock, 4096)), dim3(kBlock), 0, s, m, buf, buf_len, offsets,
+    hipLaunchKernelGGL(k_decode, dim3(grid_for(m, kEncPer, 4096)), dim3(kBlock), 0, s, m, buf, buf_len, offsets,
                        int(wide != 0), o);
     SW_LAUNCHED();
     return SWARM_OK;
