@@ -22,8 +22,9 @@
 //   k_sparse_block             2048-agent chunk per workgroup (grid = resident workgroups,
 //                              next chunk's stamps loaded ahead): stamps -> LDS list -> gather,
 //                              4 lanes per marked agent with interleaved edges
-// Marks are plain byte stores, no atomics: stamp act[v] = t+1 (mod 256), double-buffered by
-// round parity and consumed (zeroed) by the sparse round that reads them.  Leaders alternate by
+// Marks are plain byte stores, no atomics: stamp act[v] = stamp_of(t+1) (1..255, never 0, so an
+// unmarked byte never matches), double-buffered by round parity and consumed (zeroed) by the
+// sparse round that reads them.  Leaders alternate by
 // parity: round t reads L[(t-1)&1] and writes L[t&1], which still holds the state after t-2; it
 // differs from the state after t-1 only on round t-1's risers, all marked (self-mark), so all
 // rewrite their entry.
@@ -100,6 +101,10 @@ __device__ unsigned long long g_phase[8192 * 8];
 #define PHASE(k) do {} while (0)
 #endif
 
+// Stamp byte of round t: 1, 2, ..., 255, 1, ...  (0 is "unmarked"; a round whose stamp were 0
+// would gather every agent).
+__host__ __device__ __forceinline__ uint8_t stamp_of(int t) { return uint8_t(1 + (t - 1) % 255); }
+
 // 4-bit mask of the bytes of w equal to the byte replicated in b4 (exact, no carry leakage).
 __device__ __forceinline__ unsigned bytes_eq4(unsigned w, unsigned b4) {
     const unsigned x = w ^ b4;
@@ -166,7 +171,7 @@ __global__ __launch_bounds__(kBlock) void k_elect_dense(
     if (guard && t > 1 && round_total(ring, t - 1, &s_bc) == 0) return;  // converged: no-op
     if (guard || tot) bookkeeping(ring, tot, t);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint8_t sw = uint8_t((t + 1) & 0xFF);
+    const uint8_t sw = stamp_of(t + 1);
     int *sc = s_col[wid];
     unsigned long long mine = 0;
     const int64_t ntask = (n + 63) / 64;
@@ -284,7 +289,7 @@ __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, const 
 }
 
 // Marked lanes of 8 stamps, consuming them (this parity is next written in round t+1, marks
-// for t+2; a stamp left behind would match again 256 rounds later: a spurious gather).
+// for t+2; a stamp left behind would match again 255 rounds later: a spurious gather).
 __device__ __forceinline__ unsigned take_stamps(uint8_t *ar, int64_t v0, int64_t n, uint2 wv, unsigned stamp4) {
     unsigned mask = bytes_eq4(wv.x, stamp4) | (bytes_eq4(wv.y, stamp4) << 4);
     if (v0 + kScan > n) mask &= (v0 >= n) ? 0u : ((1u << (n - v0)) - 1u);
@@ -328,8 +333,8 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
     const int32_t *__restrict__ P = f.L[(t - 1) & 1];
     int32_t *__restrict__ Q = f.L[t & 1];
     uint8_t *ar = f.act[t & 1], *aw = f.act[(t + 1) & 1];
-    const unsigned stamp4 = unsigned(t & 0xFF) * 0x01010101u;
-    const uint8_t sw = uint8_t((t + 1) & 0xFF);
+    const unsigned stamp4 = unsigned(stamp_of(t)) * 0x01010101u;
+    const uint8_t sw = stamp_of(t + 1);
     const int64_t n = f.n_rows;
     long long my_chg = 0, my_act = 0, my_edges = 0;
     const int64_t nchunks = (n + kChunk - 1) / kChunk;
@@ -384,7 +389,7 @@ __global__ __launch_bounds__(kBlock) void k_frontier_ghosts(const Off *__restric
                                                             const int32_t *__restrict__ in_lo, int64_t b_hi,
                                                             int64_t n_hi, const int32_t *__restrict__ in_hi, int t) {
     constexpr int G = 8;
-    const uint8_t sw = uint8_t((t + 1) & 0xFF);
+    const uint8_t sw = stamp_of(t + 1);
     uint8_t *aw = f.act[(t + 1) & 1];
     const int32_t *Lcur = f.L[t & 1];
     const int sub = threadIdx.x & (G - 1);
