@@ -457,7 +457,7 @@ def rows_bench(sw, dev, args):
 
 def sharded(args, rank, world, dev):
     """N > 1: one strip of a world-wide swarm per GPU (weak scaling: args.agents per GPU),
-    exact sharded election (RCCL halo per round + batched all-reduce) and allocation."""
+    exact sharded election (deep RCCL halo every k rounds + batched all-reduce) and allocation."""
     import torch
     import torch.distributed as dist
 
@@ -515,7 +515,9 @@ def sharded(args, rank, world, dev):
                                    "tasks/GPU allocation" % (args.agents, world, args.deg, args.tasks),
                        "agents_total": total_agents, "tasks_total": args.tasks * world,
                        "rounds_exec": r.rounds_exec,
-                       "parallelism": f"strip-sharded x{world}: RCCL halo P2P per round + all-reduce"},
+                       "halo_depth": sh.halo_depth,
+                       "parallelism": f"strip-sharded x{world}: RCCL halo P2P every {sh.halo_depth} rounds "
+                                      "(ghosts that deep, stepped locally) + one all-reduce per batch"},
             "alloc_stats": a[2],
             "roofline": None,
             "cpu_baseline": None,

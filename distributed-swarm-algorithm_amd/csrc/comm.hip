@@ -193,11 +193,13 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sh,
     unsigned long long *h = static_cast<unsigned long long *>(pinned(ctx, size_t(kC) * 8 * kMaxBatch));
     if (!h) return SWARM_ERR_OOM;
     const Rccl &R = rccl();
+    const int depth = sh->halo_depth > 1 ? sh->halo_depth : 1;
     int found = -1, t = 1, batch = 8;
     while (t <= max_rounds && found < 0) {
         const int tend = std::min(max_rounds, t + batch - 1);
         for (int r = t; r <= tend; ++r) {
             if ((rc = frontier_round_stepper(ctx, r, sh->row_ptr, sh->col, leader0, leader1, s))) return rc;
+            if (r % depth) continue;  // deep halo: ghosts are stepped locally between exchanges
             int32_t *Lcur = (r & 1) ? leader1 : leader0;
             const int64_t ns = sh->n_send_lo + sh->n_send_hi;
             if (ns) {

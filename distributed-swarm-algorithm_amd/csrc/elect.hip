@@ -164,7 +164,7 @@ __device__ __forceinline__ int row_max_from_lds(const int *s_col, Off w0, Off lo
 template <typename Off, bool MARK>
 __global__ __launch_bounds__(kBlock) void k_elect_dense(
     const Off *__restrict__ rp, const int32_t *__restrict__ col, const int32_t *__restrict__ lin,
-    int32_t *__restrict__ lout, int64_t n, unsigned long long *__restrict__ ring,
+    int32_t *__restrict__ lout, int64_t n, int64_t n_count, unsigned long long *__restrict__ ring,
     unsigned long long *__restrict__ tot, uint8_t *__restrict__ act_w, int t, int guard) {
     __shared__ int s_col[kWavesPerBlock][kWin];
     __shared__ unsigned long long s_bc, s_cnt[kWavesPerBlock];
@@ -208,7 +208,7 @@ __global__ __launch_bounds__(kBlock) void k_elect_dense(
         }
         const bool up = valid && m > own;
         if (valid) lout[v] = up ? m : own;
-        mine += __popcll(__ballot(up));
+        mine += __popcll(__ballot(up && v < n_count));  // sharded: ghost rows step, owners count
         if (MARK && up) {
             act_w[v] = sw;
             mark_row<Off>(act_w, col, b, e, Off(1), sw);
@@ -235,7 +235,8 @@ struct Frontier {
     int32_t *L[2];
     uint8_t *act[2];         // stamps, act_bytes(n_all) each (padded past n_all)
     unsigned long long *ring, *tot;
-    int64_t n_rows, n_all;
+    int64_t n_rows, n_all;   // rows stepped (owned + ghosts in sharded runs), all agents
+    int64_t n_count;         // rows [0, n_count) are owned: only their changes are counted
 };
 
 // Gather of the marked agents listed (chunk-relative) in lst[0, total), G lanes per agent,
@@ -246,8 +247,8 @@ template <typename Off, int G, int K>
 __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, const int32_t *__restrict__ col,
                                               const int32_t *__restrict__ P, int32_t *__restrict__ Q,
                                               uint8_t *__restrict__ aw, uint8_t sw, int64_t c0, const int *lst,
-                                              int total, int first, int step, long long &my_chg,
-                                              long long &my_act, long long &my_edges) {
+                                              int total, int first, int step, int64_t n_count,
+                                              long long &my_chg, long long &my_act, long long &my_edges) {
     const int lane = threadIdx.x & 63, sub = lane & (G - 1);
     for (int base = first; base < total; base += step) {
         const int i = base + lane / G;
@@ -280,7 +281,7 @@ __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, const 
                 mark_row<Off>(aw, col, b + sub, e, Off(G), sw);
             }
         }
-        my_chg += __popcll(__ballot(up && sub == 0));
+        my_chg += __popcll(__ballot(up && sub == 0 && v < n_count));
         if (valid && sub == 0) {
             my_act += 1;
             my_edges += (long long)(e - b);
@@ -371,8 +372,8 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
                 s_list[pos++] = threadIdx.x * kScan + j;
             }
             __syncthreads();
-            gather_listed<Off, G, K>(rp, col, P, Q, aw, sw, c0, s_list, total, wid * (64 / G), kBlock / G, my_chg,
-                                     my_act, my_edges);
+            gather_listed<Off, G, K>(rp, col, P, Q, aw, sw, c0, s_list, total, wid * (64 / G), kBlock / G,
+                                     f.n_count, my_chg, my_act, my_edges);
         }
         __syncthreads();  // LDS (s_wave, s_list) reused by the next chunk
     }
@@ -478,24 +479,27 @@ size_t act_bytes(int64_t n_all) {  // one parity, padded to whole chunks (+1 of 
 }
 
 template <typename Off>
-int launch_dense_round(const Off *rp, const int32_t *col, const int32_t *lin, int32_t *lout, int64_t n,
+int launch_dense_round(const Off *rp, const int32_t *col, const int32_t *lin, int32_t *lout, int64_t n, int64_t n_count,
                        unsigned long long *ring, unsigned long long *tot, uint8_t *act_w, int t, int guard,
                        hipStream_t s) {
     const unsigned grid = grid_for((n + 63) / 64, kWavesPerBlock, unsigned(tuning().dense_blocks));
     if (act_w)
-        hipLaunchKernelGGL((k_elect_dense<Off, true>), dim3(grid), dim3(kBlock), 0, s, rp, col, lin, lout, n, ring,
+        hipLaunchKernelGGL((k_elect_dense<Off, true>), dim3(grid), dim3(kBlock), 0, s, rp, col, lin, lout, n, n_count, ring,
                            tot, act_w, t, guard);
     else
-        hipLaunchKernelGGL((k_elect_dense<Off, false>), dim3(grid), dim3(kBlock), 0, s, rp, col, lin, lout, n, ring,
+        hipLaunchKernelGGL((k_elect_dense<Off, false>), dim3(grid), dim3(kBlock), 0, s, rp, col, lin, lout, n, n_count, ring,
                            tot, act_w, t, guard);
     SW_LAUNCHED();
     return SWARM_OK;
 }
 
-// Frontier view of the ctx slots for n_rows owned agents of n_all.
+// Frontier view of the ctx slots: every one of the n_all agents is stepped (ghost rows too: with a
+// halo deeper than one radius they are computed locally between exchanges), the first
+// step_rows (owned) are counted.
 int frontier_bind(swarm_ctx *ctx, int32_t *L0, int32_t *L1, Frontier *f) {
     SW_ARG(ctx->slot[S_ACT] != nullptr && ctx->slot[S_CHANGES] != nullptr, "swarm_frontier_begin first");
-    f->n_rows = ctx->step_rows;
+    f->n_rows = ctx->step_all;
+    f->n_count = ctx->step_rows;
     f->n_all = ctx->step_all;
     f->L[0] = L0;
     f->L[1] = L1;
@@ -541,7 +545,8 @@ template <typename Off>
 int launch_frontier_round(const Off *rp, const int32_t *col, const Frontier &f, int t, RoundKind k, int guard,
                           hipStream_t s) {
     if (k == RK_DENSE || k == RK_DENSE_MARK)
-        return launch_dense_round<Off>(rp, col, f.L[(t - 1) & 1], f.L[t & 1], f.n_rows, f.ring, f.tot,
+        return launch_dense_round<Off>(rp, col, f.L[(t - 1) & 1], f.L[t & 1], f.n_rows, f.n_count, f.ring,
+                                       f.tot,
                                        k == RK_DENSE_MARK ? f.act[(t + 1) & 1] : nullptr, t, guard, s);
     const int64_t nchunks = (f.n_rows + kChunk - 1) / kChunk;
     hipLaunchKernelGGL((k_sparse_block<Off>), dim3(grid_for(nchunks, 1, unsigned(tuning().sparse_blocks))), dim3(kBlock),
@@ -637,7 +642,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
             if (e2) SW_HIP(hipEventRecord(e2[0], s));
             if (mode == SWARM_ELECT_DENSE) {
                 kinds[r - t] = RK_DENSE;
-                rc = launch_dense_round<Off>(rp, col, bufs[(r - 1) & 1], bufs[r & 1], n, ring, nullptr, nullptr, r,
+                rc = launch_dense_round<Off>(rp, col, bufs[(r - 1) & 1], bufs[r & 1], n, n, ring, nullptr, nullptr, r,
                                              1, s);
             } else {
                 kinds[r - t] = plan_round(r);
@@ -734,7 +739,7 @@ int frontier_ghosts_both(swarm_ctx *ctx, int t, const int32_t *rp, const int32_t
     Frontier f{};
     int rc = frontier_bind(ctx, L0, L1, &f);
     if (rc) return rc;
-    SW_ARG(b_lo >= f.n_rows && b_lo + n_lo <= f.n_all && b_hi >= f.n_rows && b_hi + n_hi <= f.n_all,
+    SW_ARG(b_lo >= f.n_count && b_lo + n_lo <= f.n_all && b_hi >= f.n_count && b_hi + n_hi <= f.n_all,
            "ghost ranges must lie in [n_rows, n_all)");
     if (n_lo + n_hi == 0) return SWARM_OK;
     hipLaunchKernelGGL((k_frontier_ghosts<int32_t>), dim3(grid_for(n_lo + n_hi, kBlock / 8, 1024)), dim3(kBlock), 0,
@@ -793,7 +798,7 @@ int swarm_frontier_step(swarm_ctx *ctx, int32_t t, const int32_t *row_ptr, const
     using namespace swarm;
     SW_ARG(ctx != nullptr, "ctx is NULL");
     SW_ARG(t >= 1, "round must be >= 1");
-    if (ctx->step_rows == 0) return SWARM_OK;
+    if (ctx->step_all == 0) return SWARM_OK;
     SW_ARG(row_ptr && leader0 && leader1, "NULL array");
     return frontier_round_stepper(ctx, t, row_ptr, col, leader0, leader1, static_cast<hipStream_t>(stream));
 }
@@ -851,7 +856,8 @@ int swarm_elect_round(swarm_ctx *ctx, int64_t n_rows, const int32_t *row_ptr,
     unsigned long long *ring;
     SW_ALLOC(ring, ctx, S_TMP0, size_t(kCounters) * kRoundWords * 8);
     SW_HIP(hipMemsetAsync(ring, 0, size_t(kRoundWords) * 8, s));
-    int rc = launch_dense_round<int32_t>(row_ptr, col, leader_in, leader_out, n_rows, ring, nullptr, nullptr, 0, 0, s);
+    int rc = launch_dense_round<int32_t>(row_ptr, col, leader_in, leader_out, n_rows, n_rows, ring, nullptr, nullptr, 0,
+                                        0, s);
     if (rc) return rc;
     hipLaunchKernelGGL(k_sum_shards, dim3(1), dim3(kWave), 0, s, ring, 0,
                        reinterpret_cast<unsigned long long *>(changed));

@@ -71,7 +71,7 @@ class Shard(ctypes.Structure):
                 ("n_send_lo", ctypes.c_int64), ("send_hi", ctypes.c_void_p), ("n_send_hi", ctypes.c_int64),
                 ("ghost_lo_begin", ctypes.c_int64), ("n_ghost_lo", ctypes.c_int64),
                 ("ghost_hi_begin", ctypes.c_int64), ("n_ghost_hi", ctypes.c_int64),
-                ("peer_lo", ctypes.c_int32), ("peer_hi", ctypes.c_int32)]
+                ("peer_lo", ctypes.c_int32), ("peer_hi", ctypes.c_int32), ("halo_depth", ctypes.c_int32)]
 
 
 _lib = None

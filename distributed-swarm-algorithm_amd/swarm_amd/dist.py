@@ -2,17 +2,22 @@
 
 Partition.  The global square is cut into horizontal strips, one per rank (the agent storage
 order inside a shard is row-major cell order, so a strip is a contiguous ID-free range of the
-spatial order).  Each rank owns the agents inside its strip and keeps read-only *ghost* copies
-of the neighbouring ranks' agents within one radio radius of the shared border.
+spatial order).  Each rank owns the agents inside its strip and keeps *ghost* copies of the
+neighbouring ranks' agents within k radio radii of the shared border (k = halo depth).
 
 Election (exact, contract E2).  Rounds run on every rank in lockstep through the frontier
-stepper (include/swarm.h: swarm_frontier_*): round t gathers the owned agents, then the
-owned boundary agents' new leaders go to the neighbour ranks (torch.distributed P2P --
-RCCL over xGMI on GPUs, gloo in the CPU tests) and arrive as ghost updates that activate
-their local neighbours for round t + 1.  Per-round owned change counts are summed over ranks
-with one all-reduce every `check_every` rounds; the first globally zero round ends the run and
-is rounds_exec (rounds after it are no-ops everywhere).  Result: the same leaders, rounds and
-per-round change counts as a single-GPU run on the union graph.
+stepper (include/swarm.h: swarm_frontier_*): round t gathers owned AND ghost agents over the
+local graph; only owned changes are counted.  Every k-th round the owned agents within k radii
+of a border send their leaders to the neighbour rank (torch.distributed P2P -- RCCL over xGMI on
+GPUs, gloo in the CPU tests), where they overwrite the ghosts and activate their local
+neighbours for the next round.  Between exchanges a ghost near the halo's outer edge misses
+neighbours and may lag (a lower bound); that error starts one radius inside the outer edge and
+moves at most one radius per round, so after j <= k rounds it has not reached the border: owned
+agents are exact at every round, and so are the ghosts within one radius of the border.  Per-
+round owned change counts are summed over ranks with one all-reduce every `check_every` rounds;
+the first globally zero round ends the run and is rounds_exec (rounds after it are no-ops
+everywhere).  Result: the same leaders, rounds and per-round change counts as a single-GPU run
+on the union graph, with a halo exchange every k rounds instead of every round.
 
 Allocation (exact, contract A-H).  Each rank resolves the tasks inside its strip.  Every
 agent that can claim such a task lies within the claim radius Rp of it, so each rank first
@@ -25,8 +30,9 @@ every round, each rank's bidders bid into the task-key array, one MAX all-reduce
 (+ one bidder-count word per rank) makes them global, and every rank resolves every task the
 same way (owners as agent IDs).  Same rounds, prices and owners as one GPU over all agents.
 
-Exchanges per election round: 2 x (boundary agents x 4 B) per neighbour; ~20k agents per
-border at 10M agents per GPU, i.e. ~80 KB -- latency-bound, a few microseconds over xGMI.
+Exchanges: one per k election rounds, 2 x (k-radius band x 4 B) per neighbour (10k-20k agents
+per radius of border at 10M agents per GPU and N = 2-8) -- latency-bound; the deep halo trades k
+times fewer RCCL round trips for stepping k x 10k-20k ghost rows per border locally.
 """
 from __future__ import annotations
 
@@ -209,7 +215,7 @@ class GpuBackend:
                        L.ptr(sh.send_hi) if sh.send_hi.numel() else z, sh.send_hi.numel(),
                        sh.n_own, sh.n_glo, sh.n_own + sh.n_glo, sh.n_ghi,
                        sh.halo.lo if sh.halo.lo is not None else -1,
-                       sh.halo.hi if sh.halo.hi is not None else -1)
+                       sh.halo.hi if sh.halo.hi is not None else -1, sh.halo_depth)
         rounds = ctypes.c_int32(0)
         changes = np.zeros(max_rounds, np.int64)
         rc = L.check(L.lib().swarm_elect_sharded(L.ctx(), comm, ctypes.byref(desc), L.ptr(sh.leaders[0]),
@@ -291,7 +297,7 @@ class ShardedSwarm:
     """This rank's shard of a strip-partitioned swarm (see module docstring)."""
 
     def __init__(self, ids, x, y, caps, strip, *, radius: float = 1.0, group=None, device=None,
-                 backend=None, halo=None):
+                 backend=None, halo=None, halo_depth: int | None = None):
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.backend = backend if backend is not None else GpuBackend(self.device)
         self.halo = halo if halo is not None else Halo(group, self.device)
@@ -299,6 +305,7 @@ class ShardedSwarm:
         self.strip = (float(strip[0]), float(strip[1]))
         if self.halo.world > 1 and self.strip[1] - self.strip[0] <= self.radius:
             raise ValueError("strips must be taller than the radio radius")
+        self.halo_depth = self._agree_depth(halo_depth)
         dev = self.device
         pos = torch.stack([torch.as_tensor(np.ascontiguousarray(x), dtype=torch.float64),
                            torch.as_tensor(np.ascontiguousarray(y), dtype=torch.float64)], 1).to(dev)
@@ -310,17 +317,34 @@ class ShardedSwarm:
         self.pos, self.ids, self.caps = pos[perm].contiguous(), ids_t[perm].contiguous(), caps_t[perm].contiguous()
         self.perm = perm
         self.n_own = int(self.ids.numel())
-        # ghosts: neighbour ranks' agents within one radius of the shared borders
-        self.send_lo, self.send_hi = self._border(self.radius)
+        # ghosts: neighbour ranks' agents within halo_depth radii of the shared borders
+        self.send_lo, self.send_hi = self._border(self.radius * self.halo_depth)
         n_lo, n_hi = self.halo.exchange_counts(self.send_lo.numel(), self.send_hi.numel())
         gp_lo, gp_hi = self.halo.exchange(self.pos[self.send_lo], self.pos[self.send_hi], n_lo, n_hi, self.pos)
         gi_lo, gi_hi = self.halo.exchange(self.ids[self.send_lo], self.ids[self.send_hi], n_lo, n_hi, self.ids)
         self.n_glo, self.n_ghi = n_lo, n_hi
+        # ghosts within one radius of the border: exact at every round (the end-of-run check)
+        self.inner_lo = gp_lo[:, 1] >= self.strip[0] - self.radius - 1e-9
+        self.inner_hi = gp_hi[:, 1] <= self.strip[1] + self.radius + 1e-9
         self.all_pos = torch.cat([self.pos, gp_lo, gp_hi]).contiguous()
         self.all_ids = torch.cat([self.ids, gi_lo, gi_hi]).contiguous()
         self.row_ptr, self.col = self.backend.build_graph(self.all_pos, self.radius)
         self.leaders = (torch.empty(self.all_ids.numel(), dtype=torch.int32, device=dev),
                         torch.empty(self.all_ids.numel(), dtype=torch.int32, device=dev))
+
+    def _agree_depth(self, want):
+        """Halo depth k, the same on every rank: the requested depth (SWARM_HALO_DEPTH, default 16)
+        capped so that a k-radius band stays inside the neighbour's strip."""
+        import os
+        k = int(want if want is not None else os.environ.get("SWARM_HALO_DEPTH", "16"))
+        h = self.strip[1] - self.strip[0]
+        k = max(1, min(k, int(math.floor(h / self.radius)) - 1))
+        if self.halo.world > 1:
+            t = torch.tensor([-k], dtype=torch.int64)
+            if not getattr(self.halo, "host_staged", True):
+                t = t.to(self.device)
+            k = -int(self.halo.all_reduce_max_(t)[0])
+        return k
 
     def _border(self, width):
         y = self.pos[:, 1]
@@ -351,6 +375,8 @@ class ShardedSwarm:
             tend = min(max_rounds, t + check_every - 1)
             for r in range(t, tend + 1):
                 be.step(r, rp, col, lead)
+                if r % self.halo_depth:
+                    continue  # ghosts stepped locally between exchanges
                 cur = lead[r & 1]  # state after round r
                 in_lo, in_hi = h.exchange(cur[self.send_lo], cur[self.send_hi], self.n_glo, self.n_ghi, cur)
                 be.ghosts(r, g_lo, in_lo, rp, col, lead)
@@ -368,12 +394,14 @@ class ShardedSwarm:
         return ShardElectResult(rounds, np.array(changes[:rounds], np.int64), own, state, found > 0)
 
     def _check_ghosts(self, cur):
-        """Every ghost must hold its owner's final leader (cheap end-to-end halo check)."""
+        """Every ghost within one radius of the border must hold its owner's final leader (cheap
+        end-to-end halo check; the deeper ghosts may lag between exchanges by design)."""
         h = self.halo
         in_lo, in_hi = h.exchange(cur[self.send_lo], cur[self.send_hi], self.n_glo, self.n_ghi, cur)
         g_lo = cur[self.n_own:self.n_own + self.n_glo]
         g_hi = cur[self.n_own + self.n_glo:self.n_own + self.n_glo + self.n_ghi]
-        if not (torch.equal(in_lo, g_lo) and torch.equal(in_hi, g_hi)):
+        il, ih = self.inner_lo.to(cur.device), self.inner_hi.to(cur.device)
+        if not (torch.equal(in_lo[il], g_lo[il]) and torch.equal(in_hi[ih], g_hi[ih])):
             raise RuntimeError("sharded election: ghost leaders disagree with their owners")
 
     # ------------------------------------------------------------------ auction (C4 sharded)

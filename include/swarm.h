@@ -176,6 +176,10 @@ typedef struct swarm_shard {
     int64_t n_ghost_hi;
     int32_t peer_lo;         /* RCCL rank of the lower / upper neighbour, -1 = none */
     int32_t peer_hi;
+    int32_t halo_depth;      /* k >= 1 (0 = 1): the ghosts are every agent within k radii of the
+                                border; all n_all rows are stepped, the halo is exchanged after
+                                every k-th round only (owned rows stay exact: a wrong value
+                                starts at the halo's outer edge and moves one radius per round) */
 } swarm_shard;
 
 int swarm_comm_available(void);

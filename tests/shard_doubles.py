@@ -37,10 +37,11 @@ class NumpyBackend:
         self.counts = {}
 
     def step(self, t, rp, col, leaders):
+        # every row steps (ghost rows too: deep halos); only owned rows [0, n_rows) count
         Lr, Lw = leaders[(t - 1) & 1].numpy(), leaders[t & 1].numpy()
         rp_, col_ = rp.numpy(), col.numpy()
-        Lw[: self.n_rows] = Lr[: self.n_rows]
-        act = np.nonzero(self.act[: self.n_rows] == t)[0]
+        Lw[:] = Lr
+        act = np.nonzero(self.act == t)[0]
         changed = []
         for v in act:
             nb = col_[rp_[v]:rp_[v + 1]]
@@ -49,8 +50,9 @@ class NumpyBackend:
                 changed.append((v, m))
         for v, m in changed:
             Lw[v] = m
+            self.act[v] = t + 1
             self.act[col_[rp_[v]:rp_[v + 1]]] = t + 1
-        self.counts[t] = len(changed)
+        self.counts[t] = sum(1 for v, _ in changed if v < self.n_rows)
 
     def ghosts(self, t, begin, incoming, rp, col, leaders):
         cur = leaders[t & 1].numpy()

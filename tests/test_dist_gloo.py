@@ -24,7 +24,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_q, n_per, deg, check_every):
+def _worker(rank, world, port, out_q, n_per, deg, check_every, halo_depth):
     import sys
     for p in (PKG, ROOT, os.path.join(ROOT, "tests")):
         sys.path.insert(0, p)
@@ -35,24 +35,27 @@ def _worker(rank, world, port, out_q, n_per, deg, check_every):
         from swarm_amd import gen
         from swarm_amd.dist import ShardedSwarm
         d = gen.shard_inputs(n_per, SEED, world, rank, deg=deg, t=T_PER)
-        sh = ShardedSwarm(d["ids"], d["x"], d["y"], d["caps"], d["strip"], device="cpu", backend=NumpyBackend())
+        sh = ShardedSwarm(d["ids"], d["x"], d["y"], d["caps"], d["strip"], device="cpu", backend=NumpyBackend(),
+                          halo_depth=halo_depth)
         r = sh.elect(check_every=check_every)
+        sh._check_ghosts(sh.leaders[r.rounds_exec & 1])
         res, won, gst = sh.allocate(d["tx"], d["ty"], d["treq"])
         res0, won0, _ = sh.allocate(d["tx"], d["ty"], d["treq"], hysteresis=0.0)  # argmax (h = 0) mode
         out_q.put(dict(rank=rank, rounds=r.rounds_exec, changes=r.changes, ids=sh.ids.numpy(),
                        leader=r.leader.numpy(), state=r.state.numpy(), winner=res.winner.numpy(),
                        util=res.util.numpy(), won=won.numpy(), gstats=gst,
                        winner0=res0.winner.numpy(), won0=won0.numpy(),
-                       n_ghost=(sh.n_glo, sh.n_ghi)))
+                       n_ghost=(sh.n_glo, sh.n_ghi), depth=sh.halo_depth))
     finally:
         dist.destroy_process_group()
 
 
-def _run(world, n_per=N_PER, deg=16.0, check_every=7):
+def _run(world, n_per=N_PER, deg=16.0, check_every=7, halo_depth=1):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, n_per, deg, check_every)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, n_per, deg, check_every, halo_depth))
+             for r in range(world)]
     for p in procs:
         p.start()
     outs = [q.get(timeout=240) for _ in range(world)]
@@ -69,9 +72,11 @@ def _union(world, n_per=N_PER, deg=16.0):
     return ds, cat
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_election_and_allocation_match_single_graph(world, oracle_mod):
-    outs = _run(world)
+@pytest.mark.parametrize("world,depth", [(2, 1), (2, 4), (3, 16)])
+def test_sharded_election_and_allocation_match_single_graph(world, depth, oracle_mod):
+    """depth: halo depth k (ghosts k radii deep, exchanged every k rounds); 16 is capped by the
+    strip height (the same cap on every rank)."""
+    outs = _run(world, halo_depth=depth)
     ds, cat = _union(world)
     x, y, ids, caps = cat("x"), cat("y"), cat("ids"), cat("caps")
     rp, col = oracle_mod.rgg_csr(x, y, 1.0)
@@ -84,6 +89,7 @@ def test_sharded_election_and_allocation_match_single_graph(world, oracle_mod):
         assert all(got[k] == want[k] for k in got)
         assert ((o["state"] == 3) == (o["leader"] == o["ids"])).all()
         assert sum(o["n_ghost"]) > 0
+        assert o["depth"] == outs[0]["depth"] and 1 <= o["depth"] <= depth
     assert sum(len(o["ids"]) for o in outs) == len(ids)
     # allocation: every rank resolves its own tasks; the union resolver must agree
     wa = oracle_mod.allocate(ids, x, y, caps, cat("tx"), cat("ty"), cat("treq"))
