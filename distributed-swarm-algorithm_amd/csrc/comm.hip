@@ -195,6 +195,7 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sh,
     const Rccl &R = rccl();
     const int depth = sh->halo_depth > 1 ? sh->halo_depth : 1;
     int found = -1, t = 1, batch = 8;
+    std::vector<int64_t> hist;
     while (t <= max_rounds && found < 0) {
         const int tend = std::min(max_rounds, t + batch - 1);
         for (int r = t; r <= tend; ++r) {
@@ -228,6 +229,7 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sh,
         SW_HIP(hipStreamSynchronize(s));
         for (int r = t; r <= tend; ++r) {
             const unsigned long long c = h[size_t(r - t) * kC];  // C_CHG: owned changes
+            hist.push_back(int64_t(c));
             if (changes_host) changes_host[r - 1] = int64_t(c);
             if (c == 0) {
                 found = r;
@@ -235,7 +237,7 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sh,
             }
         }
         t = tend + 1;
-        batch = std::min(batch * 2, kMaxBatch);
+        batch = next_round_batch(hist.data(), hist.size(), batch, kMaxBatch);
     }
     *rounds_exec = found > 0 ? found : max_rounds;
     return found > 0 ? SWARM_OK : SWARM_NOT_CONVERGED;

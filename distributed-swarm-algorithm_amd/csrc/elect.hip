@@ -612,6 +612,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     SW_ALLOC(dtot, ctx, S_ESTATS, size_t(kCounters) * 8 * kMaxBatch);
 
     int found = -1, t = 1, batch = 8, launched = 0;
+    std::vector<int64_t> hist;  // per-round change counts read so far (batch sizing)
     int64_t act_sum = 0, edge_sum = 0, chg_sum = 0, dense_rounds = 0, sp_launches = 0;
     double bytes = 0.0, sp_bytes = 0.0, sp_ms = 0.0;
     std::vector<RoundKind> kinds(kMaxBatch);
@@ -672,6 +673,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         for (int r = t; r <= tend; ++r) {
             const unsigned long long *rb = hbuf + size_t(r - t) * kCounters;
             const int64_t c = int64_t(rb[C_CHG]);
+            hist.push_back(c);
             const bool dn = kinds[r - t] == RK_DENSE || kinds[r - t] == RK_DENSE_MARK;
             if (changes_host) changes_host[r - 1] = c;
             const int64_t act = dn ? n : int64_t(rb[C_ACT]);
@@ -692,7 +694,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
             }
         }
         t = tend + 1;
-        batch = batch < kMaxBatch ? batch * 2 : kMaxBatch;
+        batch = next_round_batch(hist.data(), hist.size(), batch, kMaxBatch);
     }
     const int last = found > 0 ? found : max_rounds;
     // after a zero-change round both buffers hold the final state (dense and frontier alike);
