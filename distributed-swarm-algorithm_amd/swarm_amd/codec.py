@@ -92,7 +92,7 @@ def decode(buf, offsets, *, wide=False, device=None) -> Decoded:
     raw = _to(buf, torch.uint8, dev)
     off = _to(offsets, torch.int64, dev)
     m = max(off.numel() - 1, 0)
-    e = lambda dt: torch.zeros(m, dtype=dt, device=dev)  # noqa: E731
+    e = lambda dt: torch.empty(m, dtype=dt, device=dev)  # noqa: E731  (k_decode writes every field)
     out = Decoded(e(torch.int8), e(torch.int64), e(torch.int64), e(torch.int64), e(torch.float32),
                   e(torch.float32), e(torch.int64), e(torch.int64), e(torch.uint8))
     if m:
