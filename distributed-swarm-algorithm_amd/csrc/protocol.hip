@@ -133,10 +133,10 @@ __device__ __forceinline__ void apply_heard(int64_t i, const Heard &h, double no
 // st; `heard`: it got a liveness proof this tick (its last_hb is now).  Returns the sends.
 __device__ __forceinline__ uint8_t timers(int64_t i, uint8_t &st, bool heard, int32_t &lead, bool &lead_set,
                                           int64_t t, double now, double timeout, double jitter, uint64_t seed,
-                                          const int32_t *__restrict__ ids, const int32_t *__restrict__ tick_off,
+                                          const int32_t *__restrict__ ids, int32_t toff, double last_hb,
                                           const Fsm &f) {
     uint8_t ob = 0;
-    if (st == ST_F && !heard && now - f.last_hb[i] > timeout) {
+    if (st == ST_F && !heard && now - last_hb > timeout) {
         st = ST_W;
         f.wait_start[i] = now;
         f.delay[i] = 0.0 + jitter * jitter_u(seed, ids[i], t);
@@ -151,7 +151,7 @@ __device__ __forceinline__ uint8_t timers(int64_t i, uint8_t &st, bool heard, in
         lead_set = true;
         ob |= kAcclaim;
     }
-    if (st == ST_L && ((t + tick_off[i]) % 10) == 0) ob |= kHeartbeat;
+    if (st == ST_L && ((t + toff) % 10) == 0) ob |= kHeartbeat;
     return ob;
 }
 
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(kBlock) void k_tick_pull(int64_t n, int64_t t, cons
         receive_row(rp[i], rp[i + 1], col, ob_in, ids, ids[i], ((t + tick_off[i]) % 10) == 0, h);
         apply_heard(i, h, now, pos, f);
         const uint8_t ob = h.ob | timers(i, h.st, h.live, h.lead, h.lead_set, t, now, timeout, jitter, seed, ids,
-                                         tick_off, f);
+                                         tick_off[i], f.last_hb[i], f);
         if (h.st != st0) f.state[i] = h.st;
         if (h.lead_set) f.leader[i] = h.lead;
         ob_out[i] = ob;
@@ -367,12 +367,17 @@ __global__ __launch_bounds__(kBlock) void k_receive(int64_t t, const int32_t *__
     }
 }
 
+// kSweepV consecutive agents per thread: their byte fields (alive, outbox, state) as one 32-bit
+// word each, their timers (last_hb, tick_off) loaded up front with the bytes, so a thread has
+// every load of a pass in flight at once instead of a dependent chain per agent.
+constexpr int kSweepV = 4;
+
 __global__ __launch_bounds__(kBlock) void k_sweep(int64_t n, int64_t t, const int32_t *__restrict__ ids,
                                                  const int32_t *__restrict__ tick_off, Fsm f,
                                                  uint8_t *__restrict__ ob_out, int32_t *__restrict__ senders,
                                                  int64_t seg_cap, int32_t *__restrict__ seg_count,
                                                  double dt, double timeout, double jitter, uint64_t seed,
-                                                 unsigned long long *__restrict__ counts) {
+                                                 unsigned long long *__restrict__ counts, int vec) {
     __shared__ unsigned s_cnt[4];
     __shared__ int s_ns;
     if (threadIdx.x < 4) s_cnt[threadIdx.x] = 0;
@@ -381,29 +386,64 @@ __global__ __launch_bounds__(kBlock) void k_sweep(int64_t n, int64_t t, const in
     int32_t *seg = senders + int64_t(blockIdx.x) * seg_cap;
     const double now = double(t) * dt;
     unsigned c_lead = 0, c_wait = 0, c_acc = 0, c_hb = 0;
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
-        const uint8_t alive = f.alive[i];
-        const uint8_t prev = ob_out[i];  // this tick's receive result, or a stale tick t-2 byte
-        uint8_t st = f.state[i];
-        if (!alive) {
-            if (prev) ob_out[i] = 0;
-            continue;
+    const int64_t ngroups = (n + kSweepV - 1) / kSweepV;
+    for (int64_t gi = int64_t(blockIdx.x) * kBlock + threadIdx.x; gi < ngroups; gi += int64_t(gridDim.x) * kBlock) {
+        const int64_t i0 = gi * kSweepV;
+        const bool full = vec && i0 + kSweepV <= n;
+        uint8_t al[kSweepV], pv[kSweepV], sv[kSweepV];
+        int32_t to[kSweepV];
+        double lh[kSweepV];
+        if (full) {  // vec: the host checked the alignments; i0 is a multiple of 4
+            const uint32_t wa = *reinterpret_cast<const uint32_t *>(f.alive + i0);
+            const uint32_t wp = *reinterpret_cast<const uint32_t *>(ob_out + i0);
+            const uint32_t ws = *reinterpret_cast<const uint32_t *>(f.state + i0);
+            const int4 tv = *reinterpret_cast<const int4 *>(tick_off + i0);
+            const double2 l0 = *reinterpret_cast<const double2 *>(f.last_hb + i0);
+            const double2 l1 = *reinterpret_cast<const double2 *>(f.last_hb + i0 + 2);
+#pragma unroll
+            for (int v = 0; v < kSweepV; ++v) {
+                al[v] = uint8_t(wa >> (8 * v));
+                pv[v] = uint8_t(wp >> (8 * v));
+                sv[v] = uint8_t(ws >> (8 * v));
+            }
+            to[0] = tv.x; to[1] = tv.y; to[2] = tv.z; to[3] = tv.w;
+            lh[0] = l0.x; lh[1] = l0.y; lh[2] = l1.x; lh[3] = l1.y;
+        } else {
+#pragma unroll
+            for (int v = 0; v < kSweepV; ++v) {
+                const int64_t i = i0 + v < n ? i0 + v : n - 1;
+                al[v] = i0 + v < n ? f.alive[i] : 0;
+                pv[v] = ob_out[i];
+                sv[v] = f.state[i];
+                to[v] = tick_off[i];
+                lh[v] = f.last_hb[i];
+            }
         }
-        const uint8_t rb = (prev & kFresh) ? prev : uint8_t(0);
-        const uint8_t st0 = st;
-        int32_t lead = 0;
-        bool lead_set = false;
-        const uint8_t ob = uint8_t((rb & (kAcclaim | kHeartbeat)) |
-                                   timers(i, st, (rb & kHeard) != 0, lead, lead_set, t, now, timeout, jitter, seed,
-                                          ids, tick_off, f));
-        if (st != st0) f.state[i] = st;
-        if (lead_set) f.leader[i] = lead;
-        if (ob != prev) ob_out[i] = ob;
-        if (ob) seg[atomicAdd(&s_ns, 1)] = int32_t(i);  // this workgroup's sender segment (LDS counter)
-        c_lead += st == ST_L;
-        c_wait += st == ST_W;
-        c_acc += (ob & kAcclaim) != 0;
-        c_hb += (ob & kHeartbeat) != 0;
+#pragma unroll
+        for (int v = 0; v < kSweepV; ++v) {
+            const int64_t i = i0 + v;
+            const uint8_t prev = pv[v];  // this tick's receive result, or a stale tick t-2 byte
+            if (!al[v]) {
+                if (i < n && prev) ob_out[i] = 0;
+                continue;
+            }
+            uint8_t st = sv[v];
+            const uint8_t rb = (prev & kFresh) ? prev : uint8_t(0);
+            const uint8_t st0 = st;
+            int32_t lead = 0;
+            bool lead_set = false;
+            const uint8_t ob = uint8_t((rb & (kAcclaim | kHeartbeat)) |
+                                       timers(i, st, (rb & kHeard) != 0, lead, lead_set, t, now, timeout, jitter,
+                                              seed, ids, to[v], lh[v], f));
+            if (st != st0) f.state[i] = st;
+            if (lead_set) f.leader[i] = lead;
+            if (ob != prev) ob_out[i] = ob;
+            if (ob) seg[atomicAdd(&s_ns, 1)] = int32_t(i);  // this workgroup's sender segment (LDS counter)
+            c_lead += st == ST_L;
+            c_wait += st == ST_W;
+            c_acc += (ob & kAcclaim) != 0;
+            c_hb += (ob & kHeartbeat) != 0;
+        }
     }
     add_counts(c_lead, c_wait, c_acc, c_hb, s_cnt, counts);  // (ends with a barrier: s_ns is final)
     if (threadIdx.x == 0) seg_count[blockIdx.x] = s_ns;
@@ -455,6 +495,9 @@ int swarm_protocol_run(swarm_ctx *ctx, int64_t n, const int32_t *ids, const doub
     const Fsm f{fsm->state, fsm->leader, fsm->last_hb, fsm->wait_start, fsm->delay,
                 reinterpret_cast<float2 *>(fsm->leader_pos), fsm->has_leader_pos, fsm->alive};
     const unsigned grid = grid_for(n, kBlock, 4096);
+    auto a16 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    // k_sweep's word loads: byte arrays 4-byte aligned (the tick's outbox half too), timers 16-byte
+    const int vec = a16(fsm->alive) && a16(fsm->outbox) && a16(fsm->state) && a16(tick_off) && a16(fsm->last_hb);
     const bool push = hear_row_ptr != nullptr;
     const int64_t n_words = (n + 63) / 64;
     Mail mail{};
@@ -470,7 +513,8 @@ int swarm_protocol_run(swarm_ctx *ctx, int64_t n, const int32_t *ids, const doub
         SW_ALLOC(list, ctx, S_FSM_LIST, size_t(n) * 4);
         // per-workgroup sender segments of the sweep (grid-stride: each workgroup sees at most
         // seg_cap agents), then their counts
-        seg_cap = (n + int64_t(grid) * kBlock - 1) / (int64_t(grid) * kBlock) * kBlock;
+        const int64_t ngroups = (n + kSweepV - 1) / kSweepV;  // k_sweep: kSweepV agents per thread
+        seg_cap = (ngroups + int64_t(grid) * kBlock - 1) / (int64_t(grid) * kBlock) * kBlock * kSweepV;
         SW_ALLOC(senders, ctx, S_FSM_SEND, size_t(seg_cap) * grid * 4 + size_t(grid) * 4);
         seg_count = senders + seg_cap * grid;
         n_list = reinterpret_cast<unsigned *>(mw + 2 * n_words);
@@ -498,7 +542,8 @@ int swarm_protocol_run(swarm_ctx *ctx, int64_t n, const int32_t *ids, const doub
                                reinterpret_cast<const double2 *>(pos), row_ptr, col, tick_off, f, ob_in, ob_out, dt);
             SW_LAUNCHED();
             hipLaunchKernelGGL(k_sweep, dim3(grid), dim3(kBlock), 0, s, n, t, ids, tick_off, f, ob_out, senders,
-                               seg_cap, seg_count, dt, timeout, jitter, seed, cnt);
+                               seg_cap, seg_count, dt, timeout, jitter, seed, cnt,
+                               int(vec && (reinterpret_cast<uintptr_t>(ob_out) & 3) == 0));
             SW_LAUNCHED();
             hipLaunchKernelGGL(k_mail, dim3(grid), dim3(kBlock), 0, s, senders, seg_cap, seg_count, hear_row_ptr,
                                hear_col, mail);
