@@ -328,6 +328,10 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
     __shared__ int s_wave[kWavesPerBlock];
     __shared__ long long s_red[3][kWavesPerBlock];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#ifdef SWARM_PHASES  // debug build: per-workgroup start/end clocks, marked agents (sum, max chunk)
+    const unsigned long long ph_t0 = wall_clock64();
+    long long ph_sum = 0, ph_max = 0;
+#endif
     bookkeeping(f.ring, f.tot, t);
     // single-GPU runs: round t-2 changed nothing => round t-1 had no marked agent => neither t
     if (guard && t > 2 && f.tot[(t - 2) % kRing] == 0) return;
@@ -364,6 +368,10 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
             off += (w < wid) ? s_wave[w] : 0;
             total += s_wave[w];
         }
+#ifdef SWARM_PHASES
+        ph_sum += total;
+        ph_max = total > ph_max ? total : ph_max;
+#endif
         if (total > 0) {
             int pos = off + incl - cnt;
             while (mask) {
@@ -378,6 +386,14 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
         __syncthreads();  // LDS (s_wave, s_list) reused by the next chunk
     }
     flush_counts(f.ring, t, my_chg, my_act, my_edges, s_red);
+#ifdef SWARM_PHASES
+    if (threadIdx.x == 0 && blockIdx.x < 8192) {
+        g_phase[blockIdx.x * 8 + 0] = ph_t0;
+        g_phase[blockIdx.x * 8 + 1] = wall_clock64();
+        g_phase[blockIdx.x * 8 + 2] = (unsigned long long)ph_sum;
+        g_phase[blockIdx.x * 8 + 3] = (unsigned long long)ph_max;
+    }
+#endif
 }
 
 // Sharded runs: halo values for ghosts [b_lo, b_lo + n_lo) and [b_hi, b_hi + n_hi) after round
