@@ -186,3 +186,31 @@ def test_gpu_large_ids_match_oracle(oracle_mod):
     for k in OUT:
         np.testing.assert_array_equal(got[k], want[k], err_msg=k)
     np.testing.assert_array_equal(c, want["counts"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [20001, 20000])
+def test_gpu_sweep_unaligned_arrays_match_oracle(oracle_mod, n):
+    """k_sweep reads 4 agents per thread with word loads when every per-agent array is aligned;
+    arrays one byte / one element off force its scalar path (and odd n the word path's tail):
+    both must give the oracle's states, timers and counts."""
+    import torch
+    g = _random_case(n, 9, 50.0)
+    g["ticks"], g["kill_ticks"] = np.int64(120), np.array([50, 90], np.int64)
+    want = _run_oracle(oracle_mod, g)
+    s = _gpu_swarm(g)
+
+    def shifted(t):  # same values, storage one element past an aligned allocation
+        buf = torch.empty(t.numel() + 1, dtype=t.dtype, device=t.device)
+        v = buf[1:].view(t.shape)
+        v.copy_(t)
+        return v
+
+    for k in ("alive", "outbox", "last_hb"):
+        s.fsm[k] = shifted(s.fsm[k])
+    s.tick_off = shifted(s.tick_off)
+    counts = s.protocol_run(120, kill_ticks=g["kill_ticks"], seed=9)
+    got = _gpu_state(s)
+    for k in OUT:
+        np.testing.assert_array_equal(got[k], want[k], err_msg=k)
+    np.testing.assert_array_equal(counts, want["counts"])
