@@ -289,12 +289,28 @@ __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, const 
     }
 }
 
-// Marked lanes of 8 stamps, consuming them (this parity is next written in round t+1, marks
+// S stamps per thread as one word: 8 (uint2, 2 048-agent chunks) or 2 (uint16, 512-agent chunks:
+// small swarms, whose 2 048-agent chunks would leave most CUs idle).
+template <int S> struct StampWord;
+template <> struct StampWord<8> { using T = uint2; };
+template <> struct StampWord<2> { using T = uint16_t; };
+
+__device__ __forceinline__ unsigned stamp_bits(uint2 w, unsigned stamp4) {
+    return bytes_eq4(w.x, stamp4) | (bytes_eq4(w.y, stamp4) << 4);
+}
+__device__ __forceinline__ unsigned stamp_bits(uint16_t w, unsigned stamp4) {
+    return bytes_eq4(unsigned(w), stamp4) & 3u;  // the two zero high bytes never match (stamps >= 1)
+}
+__device__ __forceinline__ bool any_stamp(uint2 w) { return (w.x | w.y) != 0; }
+__device__ __forceinline__ bool any_stamp(uint16_t w) { return w != 0; }
+
+// Marked lanes of S stamps, consuming them (this parity is next written in round t+1, marks
 // for t+2; a stamp left behind would match again 255 rounds later: a spurious gather).
-__device__ __forceinline__ unsigned take_stamps(uint8_t *ar, int64_t v0, int64_t n, uint2 wv, unsigned stamp4) {
-    unsigned mask = bytes_eq4(wv.x, stamp4) | (bytes_eq4(wv.y, stamp4) << 4);
-    if (v0 + kScan > n) mask &= (v0 >= n) ? 0u : ((1u << (n - v0)) - 1u);
-    if (wv.x | wv.y) *reinterpret_cast<uint2 *>(ar + v0) = make_uint2(0u, 0u);
+template <int S, typename W>
+__device__ __forceinline__ unsigned take_stamps(uint8_t *ar, int64_t v0, int64_t n, W wv, unsigned stamp4) {
+    unsigned mask = stamp_bits(wv, stamp4);
+    if (v0 + S > n) mask &= (v0 >= n) ? 0u : ((1u << (n - v0)) - 1u);
+    if (any_stamp(wv)) *reinterpret_cast<W *>(ar + v0) = W{};
     return mask;
 }
 
@@ -319,11 +335,13 @@ __device__ __forceinline__ void flush_counts(unsigned long long *ring, int t, lo
     }
 }
 
-// One workgroup per 2048-agent chunk: 8 stamps per thread, the chunk's marked agents compacted
-// in LDS and gathered by the whole workgroup.
-template <typename Off, int G = kG, int K = kKs>
+// One workgroup per chunk of kBlock * S agents: S stamps per thread, the chunk's marked agents
+// compacted in LDS and gathered by the whole workgroup.
+template <typename Off, int S = kScan, int G = kG, int K = kKs>
 __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_block(
     const Off *__restrict__ rp, const int32_t *__restrict__ col, Frontier f, int t, int guard) {
+    using W = typename StampWord<S>::T;
+    constexpr int kChunk = kBlock * S;
     __shared__ int s_list[kChunk];
     __shared__ int s_wave[kWavesPerBlock];
     __shared__ long long s_red[3][kWavesPerBlock];
@@ -344,15 +362,15 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
     long long my_chg = 0, my_act = 0, my_edges = 0;
     const int64_t nchunks = (n + kChunk - 1) / kChunk;
     const int64_t NG = gridDim.x;
-    uint2 nxt = make_uint2(0u, 0u);  // stamps are padded past n_all; the next chunk's are loaded ahead
+    W nxt{};  // stamps are padded past n_all; the next chunk's are loaded ahead
     if (int64_t(blockIdx.x) < nchunks)
-        nxt = *reinterpret_cast<const uint2 *>(ar + int64_t(blockIdx.x) * kChunk + int64_t(threadIdx.x) * kScan);
+        nxt = *reinterpret_cast<const W *>(ar + int64_t(blockIdx.x) * kChunk + int64_t(threadIdx.x) * S);
     for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += NG) {
         const int64_t c0 = chunk * kChunk;
-        const int64_t v0 = c0 + int64_t(threadIdx.x) * kScan;
-        const uint2 wv = nxt;
-        if (chunk + NG < nchunks) nxt = *reinterpret_cast<const uint2 *>(ar + v0 + NG * kChunk);
-        unsigned mask = take_stamps(ar, v0, n, wv, stamp4);
+        const int64_t v0 = c0 + int64_t(threadIdx.x) * S;
+        const W wv = nxt;
+        if (chunk + NG < nchunks) nxt = *reinterpret_cast<const W *>(ar + v0 + NG * kChunk);
+        unsigned mask = take_stamps<S>(ar, v0, n, wv, stamp4);
         const int cnt = __popc(mask);
         int incl = cnt;
 #pragma unroll
@@ -377,7 +395,7 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
             while (mask) {
                 const int j = __ffs(mask) - 1;
                 mask &= mask - 1;
-                s_list[pos++] = threadIdx.x * kScan + j;
+                s_list[pos++] = threadIdx.x * S + j;
             }
             __syncthreads();
             gather_listed<Off, G, K>(rp, col, P, Q, aw, sw, c0, s_list, total, wid * (64 / G), kBlock / G,
@@ -473,10 +491,12 @@ struct Tuning {
     int dense_blocks = 2048;  // grid cap of the dense round kernel
     int dense_rounds = 8;     // frontier: rounds 1..dense_rounds run dense (the last one marks)
     int sparse_blocks = 2048; // grid cap of k_sparse_block (8 resident workgroups per CU)
+    int small_chunks = 512;   // fewer 2048-agent chunks than this: 512-agent chunks instead
     Tuning() {
         dense_blocks = env_int("SWARM_DENSE_BLOCKS", 2048);
         dense_rounds = env_int("SWARM_DENSE_ROUNDS", 8);
         sparse_blocks = env_int("SWARM_SPARSE_BLOCKS", 2048);
+        small_chunks = env_int("SWARM_SMALL_CHUNKS", 512);
         if (dense_blocks < 1) dense_blocks = 1;
         if (dense_rounds < 0) dense_rounds = 0;
         if (sparse_blocks < 1) sparse_blocks = 1;
@@ -565,8 +585,14 @@ int launch_frontier_round(const Off *rp, const int32_t *col, const Frontier &f, 
                                        f.tot,
                                        k == RK_DENSE_MARK ? f.act[(t + 1) & 1] : nullptr, t, guard, s);
     const int64_t nchunks = (f.n_rows + kChunk - 1) / kChunk;
-    hipLaunchKernelGGL((k_sparse_block<Off>), dim3(grid_for(nchunks, 1, unsigned(tuning().sparse_blocks))), dim3(kBlock),
-                       0, s, rp, col, f, t, guard);
+    if (nchunks < tuning().small_chunks) {  // small swarm: 512-agent chunks, 4x the workgroups
+        const int64_t nc2 = (f.n_rows + kBlock * 2 - 1) / (kBlock * 2);
+        hipLaunchKernelGGL((k_sparse_block<Off, 2>), dim3(grid_for(nc2, 1, unsigned(tuning().sparse_blocks))),
+                           dim3(kBlock), 0, s, rp, col, f, t, guard);
+    } else {
+        hipLaunchKernelGGL((k_sparse_block<Off>), dim3(grid_for(nchunks, 1, unsigned(tuning().sparse_blocks))),
+                           dim3(kBlock), 0, s, rp, col, f, t, guard);
+    }
     SW_LAUNCHED();
     return SWARM_OK;
 }
