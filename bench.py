@@ -158,7 +158,7 @@ def main():
     # no-op rounds a batch issues after convergence.
     rt = sw.elect(mode=args.elect_mode, max_rounds=1 << 16, timed=True)
     if args.elect_mode == "frontier" and rt.sparse_launches:
-        pmc = pmc_traffic("k_sparse_block")
+        pmc = pmc_traffic("k_sparse_block<int, 8,")  # the 2 048-agent-chunk variant (10M agents)
         dom = {"kernel": "k_sparse_block (sparse E2 round: marked agents gather)",
                "bytes_per_launch": rt.sparse_bytes / rt.sparse_launches,
                "avg_launch_ms": rt.sparse_ms / rt.sparse_launches, "launches": rt.sparse_launches,
