@@ -1,12 +1,15 @@
 """Time the batch codec at 10M messages of every type: encode (fields -> packets) and decode.
-python tools/codec_probe.py [M] [wide]"""
+python tools/codec_probe.py [M] [wide|narrow] [LIBNAME]   (LIBNAME: an alternative build under swarm_amd/, A/B)"""
 import sys
 import time
 
 sys.path.insert(0, "distributed-swarm-algorithm_amd")
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
-from swarm_amd import codec  # noqa: E402
+from swarm_amd import _lib, codec  # noqa: E402
+
+if len(sys.argv) > 3:
+    _lib.load(__import__("os").path.join(_lib.HERE, sys.argv[3]))
 
 m = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
 wide = len(sys.argv) > 2 and sys.argv[2] == "wide"
