@@ -132,6 +132,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
+    # a non-converged election would report max_rounds rounds: refuse to print such a number
+    assert r.converged, f"election did not converge in {r.rounds_exec} rounds"
+    assert a.stats["mode_used"] in (_lib.ALLOC_BINNED, _lib.ALLOC_DENSE), a.stats
+    check = final_state_check(sw, r)
 
     agent_rounds = float(n) * rounds_total
     if world > 1:
@@ -236,6 +240,8 @@ def main():
                                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                                      "bytes_per_launch": bytes_round, "avg_launch_ms": dense_round_ms,
                                      "agent_rounds_per_s": n / (dense_round_ms * 1e-3)},
+            "build": _lib.provenance(),
+            "result_check": check,
             "elect_stats": {"rounds_launched": r.rounds_launched, "active_total": r.active_total,
                             "edges_total": r.edges_total,
                             "dense_rounds": r.dense_rounds, "changes_total": rt.changes_total},
@@ -244,43 +250,80 @@ def main():
     # ---- the other §8 rows, each timed once at its own scale (informational; not `value`)
     if rank == 0 and args.rows:
         out["rows"] = rows_bench(sw, dev, args)
-    # ---- CPU baseline: the oracle restatement on the host cores, bounded sample
+    # ---- CPU baseline: the oracle's restatement of the same algorithm (frontier election +
+    # binned allocation) on the host cores -- the whole C3 step on every thread, and a bounded
+    # sample on one thread
     if rank == 0 and args.cpu_baseline:
-        from oracle import oracle
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-        oracle.set_threads(threads)
-        rph = rp.cpu().numpy().astype(np.int64)
-        colh = col.cpu().numpy()
-        idsh = sw.ids.cpu().numpy()
-        k = 1
-        t1 = time.perf_counter()
-        oracle.elect(rph, colh, idsh, max_rounds=k)
-        per_round = time.perf_counter() - t1
-        k = max(1, min(200, int(args.cpu_seconds * 0.6 / max(per_round, 1e-6))))
-        t1 = time.perf_counter()
-        oracle.elect(rph, colh, idsh, max_rounds=k)
-        per_round = (time.perf_counter() - t1) / k
-        # allocation: dense reference algorithm over a task sample (probe, then scale)
-        def alloc_sample(ts):
-            t1 = time.perf_counter()
-            oracle.allocate(d["ids"], d["x"], d["y"], d["caps"], d["tx"][:ts], d["ty"][:ts], d["treq"][:ts])
-            return (time.perf_counter() - t1) / ts
-        ts = min(args.tasks, max(threads, 1))
-        per_task = alloc_sample(ts)
-        ts = max(1, min(args.tasks, int(args.cpu_seconds * 0.4 / max(per_task, 1e-9))))
-        per_task = alloc_sample(ts)
-        t_est = per_round * r.rounds_exec + per_task * args.tasks
-        out["cpu_baseline"] = {
-            "value": n * r.rounds_exec / t_est, "unit": "agent-rounds/s", "cores": threads,
-            "kind": "port",
-            "sample": f"C oracle (OpenMP x{threads}): {k} dense E2 rounds on the full {n}-agent graph "
-                      f"({per_round * 1e3:.1f} ms/round) + dense allocation of {ts} tasks "
-                      f"({per_task * 1e3:.2f} ms/task); step time extrapolated to {r.rounds_exec} rounds "
-                      f"+ {args.tasks} tasks = {t_est:.1f} s"}
+        out["cpu_baseline"] = cpu_baseline_step(sw, d, r, a, args)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def final_state_check(sw, r):
+    """Cheap end-to-end check of the timed election's output (the full comparison against the
+    oracle is tests/test_scale.py): one more E2 round over the final leaders changes nothing
+    (every agent's leader is at least each neighbour's), and state == LEADER iff leader == id."""
+    import torch
+    from swarm_amd import _lib
+    lout = torch.empty_like(sw.leader)
+    changed = torch.zeros(1, dtype=torch.int64, device=sw.leader.device)
+    _lib.check(_lib.lib().swarm_elect_round(_lib.ctx(), sw.n, _lib.ptr(sw.row_ptr), _lib.ptr(sw.col),
+                                            _lib.ptr(sw.leader), _lib.ptr(lout), _lib.ptr(changed), _lib.stream()))
+    fixed_point = int(changed.item()) == 0 and bool(torch.equal(lout, sw.leader))
+    state_ok = bool(torch.equal(sw.state == _lib.LEADER, sw.leader == sw.ids))
+    assert fixed_point and state_ok, ("final election state is not a fixed point", fixed_point, state_ok)
+    return {"fixed_point": fixed_point, "state_consistent": state_ok, "rounds_exec": r.rounds_exec,
+            "converged": r.converged, "leaders": int((sw.state == _lib.LEADER).sum())}
+
+
+def _threads():
+    return int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+
+
+def cpu_baseline_step(sw, d, r, a, args):
+    """The C3 step on the host: the oracle's frontier election (orc_elect_frontier) and binned
+    allocation (orc_allocate_binned) -- the same algorithms the GPU runs, restated in C with
+    OpenMP -- over the same swarm (storage order), all host threads, measured whole (no
+    extrapolation).  One thread: the first rounds of the election and a task sample, scaled by
+    the agents recomputed (per round, from the full run) and by the task count."""
+    from oracle import oracle
+    threads = _threads()
+    rp = sw.row_ptr.cpu().numpy().astype(np.int64)
+    col = sw.col.cpu().numpy()
+    ids = sw.ids.cpu().numpy()
+    x, y = sw.pos[:, 0].cpu().numpy(), sw.pos[:, 1].cpu().numpy()
+    caps = sw.caps.cpu().numpy().view(np.uint32)
+    n = len(ids)
+    oracle.set_threads(threads)
+    t1 = time.perf_counter()
+    lead, _, rounds, _, active = oracle.elect_frontier(rp, col, ids, with_active=True)
+    t_el = time.perf_counter() - t1
+    t1 = time.perf_counter()
+    al = oracle.allocate_binned(ids, x, y, caps, d["tx"], d["ty"], d["treq"], use_pow=False)
+    t_al = time.perf_counter() - t1
+    same = (rounds == r.rounds_exec and bool(np.array_equal(lead, sw.leader.cpu().numpy()))
+            and bool(np.array_equal(al["winner"], a.winner.cpu().numpy())))
+    # one thread: the first k rounds (the heaviest) and a task sample
+    oracle.set_threads(1)
+    k = min(rounds, 40)
+    t1 = time.perf_counter()
+    oracle.elect_frontier(rp, col, ids, max_rounds=k)
+    t_k = time.perf_counter() - t1
+    ts = min(len(d["tx"]), 1000)
+    t1 = time.perf_counter()
+    oracle.allocate_binned(ids, x, y, caps, d["tx"][:ts], d["ty"][:ts], d["treq"][:ts], use_pow=False)
+    t_ts = time.perf_counter() - t1
+    oracle.set_threads(threads)
+    t1_est = t_k * float(active.sum()) / float(active[:k].sum()) + t_ts * len(d["tx"]) / ts
+    return {"value": n * rounds / (t_el + t_al), "unit": "agent-rounds/s", "cores": threads, "kind": "port",
+            "value_1core": n * rounds / t1_est, "elect_s": t_el, "alloc_s": t_al, "same_result_as_gpu": same,
+            "sample": f"C oracle, the GPU's algorithms (orc_elect_frontier + orc_allocate_binned), the whole C3 step "
+                      f"on the same {n}-agent swarm: election {rounds} rounds {t_el:.2f} s + {len(d['tx'])}-task "
+                      f"allocation {t_al:.2f} s on {threads} threads (measured, not extrapolated); 1 thread: "
+                      f"rounds 1-{k} ({t_k:.1f} s) + {ts} tasks ({t_ts:.1f} s), scaled by recomputed agents and "
+                      f"tasks to {t1_est:.0f} s"}
 
 
 def _timed(fn, reps=1):

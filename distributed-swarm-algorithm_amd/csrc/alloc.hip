@@ -67,7 +67,7 @@ struct Params {
     int64_t id_span;
     int64_t *nclaim;
     int64_t *nmsg;
-    unsigned long long *stats;  // kStatShards x 16 u64: [claims, conflicts, flagged, candidates, overflow]
+    unsigned long long *stats;  // kStatShards x 16 u64: [claims, conflicts, flagged, candidates, overflow, bad treq]
 };
 
 constexpr int kStatShards = 64;   // each shard on its own 128-B line
@@ -76,13 +76,15 @@ constexpr int kStatStride = 16;
 // Per-workgroup totals, flushed once per workgroup into one of 64 shards (a single
 // contended counter costs ~12 ns per arrival: MI355X_MICROARCH.md 'fanin').
 struct BlockStats {
-    unsigned long long claims = 0, msgs = 0, overflow = 0;
+    unsigned long long claims = 0, msgs = 0, overflow = 0, bad = 0;
 };
+constexpr int kNumStats = 6;
 
 __device__ __forceinline__ void flush_stats(const Params &P, unsigned long long claims, unsigned long long msgs,
                                             unsigned long long flagged, unsigned long long cand,
-                                            unsigned long long overflow) {
+                                            unsigned long long overflow, unsigned long long bad = 0) {
     unsigned long long *sh = P.stats + size_t(blockIdx.x & (kStatShards - 1)) * kStatStride;
+    if (bad) atomicAdd(sh + 5, bad);
     if (claims) atomicAdd(sh + 0, claims);
     if (msgs) atomicAdd(sh + 1, msgs);
     if (flagged) atomicAdd(sh + 2, flagged);
@@ -91,7 +93,7 @@ __device__ __forceinline__ void flush_stats(const Params &P, unsigned long long 
 }
 
 __global__ void k_fold_stats(const unsigned long long *__restrict__ sh, unsigned long long *__restrict__ out) {
-    for (int c = 0; c < 5; ++c) {
+    for (int c = 0; c < kNumStats; ++c) {
         unsigned long long v = sh[size_t(threadIdx.x) * kStatStride + c];
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -207,12 +209,14 @@ __global__ __launch_bounds__(kBlock) void k_alloc_binned(
         if (threadIdx.x == 0) {
             finish_task(P, k, w0, u0, s_w0c != 0, accepted, first_id, cur_id, cur_u, cur_idx, nclaims, bs);
             bs.overflow += overflow ? 1 : 0;
+            bs.bad += bad_req(rq) ? 1 : 0;
         }
         __syncthreads();
     }
     const long long c = block_sum_ll(my_cand, s_red64);
     const long long f = block_sum_ll(my_flag, s_red64);
-    if (threadIdx.x == 0) flush_stats(P, bs.claims, bs.msgs, (unsigned long long)f, (unsigned long long)c, bs.overflow);
+    if (threadIdx.x == 0)
+        flush_stats(P, bs.claims, bs.msgs, (unsigned long long)f, (unsigned long long)c, bs.overflow, bs.bad);
 }
 
 // ------------------------------------------------------------------------------- dense
@@ -296,7 +300,7 @@ __global__ __launch_bounds__(kBlock) void k_alloc_dense_chain(
     const int64_t wave = (int64_t(blockIdx.x) * kBlock + threadIdx.x) >> 6;
     const int64_t nwaves = (int64_t(gridDim.x) * kBlock) >> 6;
     BlockStats bs;
-    __shared__ unsigned long long s_c[kBlock / kWave], s_m[kBlock / kWave];
+    __shared__ unsigned long long s_c[kBlock / kWave], s_m[kBlock / kWave], s_b[kBlock / kWave];
     for (int64_t k = wave; k < t_count; k += nwaves) {
         const double2 tp = tpos[k];
         const int rq = treq[k];
@@ -376,15 +380,17 @@ __global__ __launch_bounds__(kBlock) void k_alloc_dense_chain(
             has = true;
             if (++accepted == 1) first_id = cur_id;
         }
-        if (lane == 0)
+        if (lane == 0) {
             finish_task(P, k, w0, u0, w0_claimed, accepted, first_id, cur_id, cur_u, cur_idx, nclaims, bs);
+            bs.bad += bad_req(rq) ? 1 : 0;
+        }
     }
-    if (lane == 0) { s_c[threadIdx.x >> 6] = bs.claims; s_m[threadIdx.x >> 6] = bs.msgs; }
+    if (lane == 0) { s_c[threadIdx.x >> 6] = bs.claims; s_m[threadIdx.x >> 6] = bs.msgs; s_b[threadIdx.x >> 6] = bs.bad; }
     __syncthreads();
     if (threadIdx.x == 0) {
-        unsigned long long c = 0, m = 0;
-        for (int w = 0; w < kBlock / kWave; ++w) { c += s_c[w]; m += s_m[w]; }
-        flush_stats(P, c, m, 0, 0, 0);
+        unsigned long long c = 0, m = 0, b = 0;
+        for (int w = 0; w < kBlock / kWave; ++w) { c += s_c[w]; m += s_m[w]; b += s_b[w]; }
+        flush_stats(P, c, m, 0, 0, 0, b);
     }
 }
 
@@ -510,8 +516,12 @@ int swarm_allocate(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *
     unsigned long long *folded = dstats + size_t(kStatShards) * kStatStride;
     hipLaunchKernelGGL(k_fold_stats, dim3(1), dim3(kWave), 0, s, dstats, folded);
     SW_LAUNCHED();
-    SW_HIP(hipMemcpyAsync(hs, folded, 40, hipMemcpyDeviceToHost, s));
+    SW_HIP(hipMemcpyAsync(hs, folded, 8 * kNumStats, hipMemcpyDeviceToHost, s));
     SW_HIP(hipStreamSynchronize(s));
+    if (hs[5]) {  // outputs were computed treating those capability indices as absent
+        set_error("invalid argument: %llu task(s) with treq outside [-1, 31]", (unsigned long long)hs[5]);
+        return SWARM_ERR_ARG;
+    }
     if (stats) {
         stats->n_claims = int64_t(hs[0]);
         stats->n_conflicts = int64_t(hs[1]);

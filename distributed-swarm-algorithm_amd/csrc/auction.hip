@@ -438,6 +438,35 @@ int auc_tail_threshold() {
     return tail < 0 ? 0 : (tail > kTailCap ? kTailCap : tail);
 }
 
+__global__ __launch_bounds__(kBlock) void k_count_bad_req(const int8_t *__restrict__ treq, int64_t t,
+                                                         unsigned long long *__restrict__ out) {
+    unsigned long long c = 0;
+    for (int64_t k = int64_t(blockIdx.x) * kBlock + threadIdx.x; k < t; k += int64_t(gridDim.x) * kBlock)
+        c += bad_req(treq[k]) ? 1 : 0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
+}
+
+// SWARM_ERR_ARG if any treq lies outside [-1, 31] (a capability index beyond the 32-bit mask).
+int check_treq(swarm_ctx *ctx, int64_t t, const int8_t *treq, hipStream_t s) {
+    if (t == 0) return SWARM_OK;
+    unsigned long long *d;
+    SW_ALLOC(d, ctx, S_TMP0, 64);
+    SW_HIP(hipMemsetAsync(d, 0, 8, s));
+    hipLaunchKernelGGL(k_count_bad_req, dim3(grid_for(t, kBlock, 256)), dim3(kBlock), 0, s, treq, t, d);
+    SW_LAUNCHED();
+    unsigned long long *h = static_cast<unsigned long long *>(pinned(ctx, 64));
+    if (!h) return SWARM_ERR_OOM;
+    SW_HIP(hipMemcpyAsync(h, d, 8, hipMemcpyDeviceToHost, s));
+    SW_HIP(hipStreamSynchronize(s));
+    if (h[0]) {
+        set_error("invalid argument: %llu task(s) with treq outside [-1, 31]", h[0]);
+        return SWARM_ERR_ARG;
+    }
+    return SWARM_OK;
+}
+
 // Candidate lists, ascending-ID index, drop-out flags and round counters for n agents against t
 // tasks (n, t > 0): everything but the task keys and the price / owner / assigned arrays.
 int auc_prepare(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos, const uint32_t *acaps, int64_t t,
@@ -621,6 +650,7 @@ int swarm_auction(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *a
     SW_ARG(n == 0 || (ids && apos && acaps && assigned), "NULL agent array");
     SW_ARG(t == 0 || (tpos && treq && owner && price), "NULL task array");
     hipStream_t s = static_cast<hipStream_t>(stream);
+    if (int rc0 = check_treq(ctx, t, treq, s)) return rc0;
     if (stats) *stats = swarm_auction_stats{};
     if (n) SW_HIP(hipMemsetAsync(assigned, 0xFF, size_t(n) * 4, s));  // -1
     if (t) {
@@ -756,6 +786,7 @@ int swarm_auction_begin(swarm_ctx *ctx, int64_t n, const int32_t *ids, const dou
     SW_ARG(t == 0 || (tpos && treq && owner_id && price), "NULL task array");
     hipStream_t s = static_cast<hipStream_t>(stream);
     ctx->auc = AucPersist{};
+    if (int rc0 = check_treq(ctx, t, treq, s)) return rc0;
     if (stats) *stats = swarm_auction_stats{};
     if (n) SW_HIP(hipMemsetAsync(assigned, 0xFF, size_t(n) * 4, s));
     if (t) {

@@ -3,10 +3,12 @@
 #include <new>
 
 #include "swarm_common.h"
+#include "build/src_hash.h"  // SWARM_SRC_HASH (Makefile: sha256 of the library's sources)
 
 namespace swarm {
 
 static thread_local char g_err[1024] = "";
+static thread_local int g_scratch_code = SWARM_ERR_OOM;
 
 void set_error(const char *fmt, ...) {
     va_list ap;
@@ -15,7 +17,24 @@ void set_error(const char *fmt, ...) {
     va_end(ap);
 }
 
+int scratch_code() { return g_scratch_code; }
+
+// A ctx's scratch lives on the device it was created on: using it from another device would
+// hand that device's kernels foreign buffers.
+bool ctx_on_current_device(const swarm_ctx *ctx) {
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev != ctx->device) {
+        set_error("invalid argument: ctx was created on device %d but device %d is current (one ctx per device)",
+                  ctx->device, dev);
+        g_scratch_code = SWARM_ERR_ARG;
+        return false;
+    }
+    return true;
+}
+
 void *scratch(swarm_ctx *ctx, Slot s, size_t bytes) {
+    if (!ctx_on_current_device(ctx)) return nullptr;
+    g_scratch_code = SWARM_ERR_OOM;
     if (bytes == 0) bytes = 16;
     if (ctx->cap[s] >= bytes) return ctx->slot[s];
     if (ctx->slot[s]) {
@@ -57,7 +76,7 @@ extern "C" {
 
 const char *swarm_last_error(void) { return swarm::g_err; }
 
-const char *swarm_version(void) { return "swarm-mi355x 0.1.0 (gfx950)"; }
+const char *swarm_version(void) { return "swarm-mi355x 0.2.0 (gfx950) src=" SWARM_SRC_HASH; }
 
 int swarm_ctx_create(swarm_ctx **out) {
     SW_ARG(out != nullptr, "out is NULL");

@@ -161,11 +161,14 @@ __device__ __forceinline__ int row_max_from_lds(const int *s_col, Off w0, Off lo
 // ---------------------------------------------------------------- dense Jacobi round
 // MARK: also stamp every riser and its neighbours for round t+1 (act_w = t+1), so that round
 // t+1 can run sparse.
-template <typename Off, bool MARK>
+// DIR: directed graph -- a riser marks the agents that HEAR it (hrp/hcol, the transpose of
+// rp/col), not the agents it hears.
+template <typename Off, bool MARK, bool DIR = false>
 __global__ __launch_bounds__(kBlock) void k_elect_dense(
     const Off *__restrict__ rp, const int32_t *__restrict__ col, const int32_t *__restrict__ lin,
     int32_t *__restrict__ lout, int64_t n, int64_t n_count, unsigned long long *__restrict__ ring,
-    unsigned long long *__restrict__ tot, uint8_t *__restrict__ act_w, int t, int guard) {
+    unsigned long long *__restrict__ tot, uint8_t *__restrict__ act_w, int t, int guard,
+    const Off *__restrict__ hrp = nullptr, const int32_t *__restrict__ hcol = nullptr) {
     __shared__ int s_col[kWavesPerBlock][kWin];
     __shared__ unsigned long long s_bc, s_cnt[kWavesPerBlock];
     if (guard && t > 1 && round_total(ring, t - 1, &s_bc) == 0) return;  // converged: no-op
@@ -211,7 +214,10 @@ __global__ __launch_bounds__(kBlock) void k_elect_dense(
         mine += __popcll(__ballot(up && v < n_count));  // sharded: ghost rows step, owners count
         if (MARK && up) {
             act_w[v] = sw;
-            mark_row<Off>(act_w, col, b, e, Off(1), sw);
+            if (DIR)
+                mark_row<Off>(act_w, hcol, hrp[v], hrp[v + 1], Off(1), sw);
+            else
+                mark_row<Off>(act_w, col, b, e, Off(1), sw);
         }
         b = nb;
         e = ne;
@@ -243,8 +249,9 @@ struct Frontier {
 // `first`/`step` select this wave's share; risers mark themselves and their neighbours.  Lane
 // `sub` of an agent takes edges b + sub + G*j (interleaved: one load instruction covers G
 // consecutive edges of every agent it serves, so each touches one cache line per agent).
-template <typename Off, int G, int K>
+template <typename Off, int G, int K, bool DIR>
 __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, const int32_t *__restrict__ col,
+                                              const Off *__restrict__ hrp, const int32_t *__restrict__ hcol,
                                               const int32_t *__restrict__ P, int32_t *__restrict__ Q,
                                               uint8_t *__restrict__ aw, uint8_t sw, int64_t c0, const int *lst,
                                               int total, int first, int step, int64_t n_count,
@@ -273,7 +280,9 @@ __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, const 
         if (valid && sub == 0) Q[v] = m;
         if (up) {
             if (sub == 0) aw[v] = sw;
-            if (e - b <= G * K) {  // one pass: c[] still holds this lane's edges
+            if (DIR) {  // the agents that hear v
+                mark_row<Off>(aw, hcol, hrp[v] + sub, hrp[v + 1], Off(G), sw);
+            } else if (e - b <= G * K) {  // one pass: c[] still holds this lane's edges
 #pragma unroll
                 for (int j = 0; j < K; ++j)
                     if (b + sub + G * j < e) aw[c[j]] = sw;
@@ -337,9 +346,10 @@ __device__ __forceinline__ void flush_counts(unsigned long long *ring, int t, lo
 
 // One workgroup per chunk of kBlock * S agents: S stamps per thread, the chunk's marked agents
 // compacted in LDS and gathered by the whole workgroup.
-template <typename Off, int S = kScan, int G = kG, int K = kKs>
+template <typename Off, int S = kScan, bool DIR = false, int G = kG, int K = kKs>
 __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_block(
-    const Off *__restrict__ rp, const int32_t *__restrict__ col, Frontier f, int t, int guard) {
+    const Off *__restrict__ rp, const int32_t *__restrict__ col, Frontier f, int t, int guard,
+    const Off *__restrict__ hrp = nullptr, const int32_t *__restrict__ hcol = nullptr) {
     using W = typename StampWord<S>::T;
     constexpr int kChunk = kBlock * S;
     __shared__ int s_list[kChunk];
@@ -398,7 +408,7 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
                 s_list[pos++] = threadIdx.x * S + j;
             }
             __syncthreads();
-            gather_listed<Off, G, K>(rp, col, P, Q, aw, sw, c0, s_list, total, wid * (64 / G), kBlock / G,
+            gather_listed<Off, G, K, DIR>(rp, col, hrp, hcol, P, Q, aw, sw, c0, s_list, total, wid * (64 / G), kBlock / G,
                                      f.n_count, my_chg, my_act, my_edges);
         }
         __syncthreads();  // LDS (s_wave, s_list) reused by the next chunk
@@ -517,14 +527,17 @@ size_t act_bytes(int64_t n_all) {  // one parity, padded to whole chunks (+1 of 
 template <typename Off>
 int launch_dense_round(const Off *rp, const int32_t *col, const int32_t *lin, int32_t *lout, int64_t n, int64_t n_count,
                        unsigned long long *ring, unsigned long long *tot, uint8_t *act_w, int t, int guard,
-                       hipStream_t s) {
+                       hipStream_t s, const Off *hrp = nullptr, const int32_t *hcol = nullptr) {
     const unsigned grid = grid_for((n + 63) / 64, kWavesPerBlock, unsigned(tuning().dense_blocks));
-    if (act_w)
+    if (act_w && hrp)
+        hipLaunchKernelGGL((k_elect_dense<Off, true, true>), dim3(grid), dim3(kBlock), 0, s, rp, col, lin, lout, n,
+                           n_count, ring, tot, act_w, t, guard, hrp, hcol);
+    else if (act_w)
         hipLaunchKernelGGL((k_elect_dense<Off, true>), dim3(grid), dim3(kBlock), 0, s, rp, col, lin, lout, n, n_count, ring,
-                           tot, act_w, t, guard);
+                           tot, act_w, t, guard, nullptr, nullptr);
     else
         hipLaunchKernelGGL((k_elect_dense<Off, false>), dim3(grid), dim3(kBlock), 0, s, rp, col, lin, lout, n, n_count, ring,
-                           tot, act_w, t, guard);
+                           tot, act_w, t, guard, nullptr, nullptr);
     SW_LAUNCHED();
     return SWARM_OK;
 }
@@ -533,6 +546,7 @@ int launch_dense_round(const Off *rp, const int32_t *col, const int32_t *lin, in
 // halo deeper than one radius they are computed locally between exchanges), the first
 // step_rows (owned) are counted.
 int frontier_bind(swarm_ctx *ctx, int32_t *L0, int32_t *L1, Frontier *f) {
+    if (!ctx_on_current_device(ctx)) return SWARM_ERR_ARG;
     SW_ARG(ctx->slot[S_ACT] != nullptr && ctx->slot[S_CHANGES] != nullptr, "swarm_frontier_begin first");
     f->n_rows = ctx->step_all;
     f->n_count = ctx->step_rows;
@@ -577,22 +591,26 @@ RoundKind plan_round(int t) {
     return RK_SPARSE;
 }
 
+// hrp/hcol: the transpose CSR of a directed graph (who hears each agent), or NULL (symmetric).
 template <typename Off>
 int launch_frontier_round(const Off *rp, const int32_t *col, const Frontier &f, int t, RoundKind k, int guard,
-                          hipStream_t s) {
+                          hipStream_t s, const Off *hrp = nullptr, const int32_t *hcol = nullptr) {
     if (k == RK_DENSE || k == RK_DENSE_MARK)
         return launch_dense_round<Off>(rp, col, f.L[(t - 1) & 1], f.L[t & 1], f.n_rows, f.n_count, f.ring,
                                        f.tot,
-                                       k == RK_DENSE_MARK ? f.act[(t + 1) & 1] : nullptr, t, guard, s);
+                                       k == RK_DENSE_MARK ? f.act[(t + 1) & 1] : nullptr, t, guard, s, hrp, hcol);
     const int64_t nchunks = (f.n_rows + kChunk - 1) / kChunk;
-    if (nchunks < tuning().small_chunks) {  // small swarm: 512-agent chunks, 4x the workgroups
-        const int64_t nc2 = (f.n_rows + kBlock * 2 - 1) / (kBlock * 2);
-        hipLaunchKernelGGL((k_sparse_block<Off, 2>), dim3(grid_for(nc2, 1, unsigned(tuning().sparse_blocks))),
-                           dim3(kBlock), 0, s, rp, col, f, t, guard);
-    } else {
-        hipLaunchKernelGGL((k_sparse_block<Off>), dim3(grid_for(nchunks, 1, unsigned(tuning().sparse_blocks))),
-                           dim3(kBlock), 0, s, rp, col, f, t, guard);
-    }
+    const bool small = nchunks < tuning().small_chunks;  // small swarm: 512-agent chunks, 4x the workgroups
+    const int64_t nc = small ? (f.n_rows + kBlock * 2 - 1) / (kBlock * 2) : nchunks;
+    const dim3 grid(grid_for(nc, 1, unsigned(tuning().sparse_blocks)));
+    if (hrp && small)
+        hipLaunchKernelGGL((k_sparse_block<Off, 2, true>), grid, dim3(kBlock), 0, s, rp, col, f, t, guard, hrp, hcol);
+    else if (hrp)
+        hipLaunchKernelGGL((k_sparse_block<Off, kScan, true>), grid, dim3(kBlock), 0, s, rp, col, f, t, guard, hrp, hcol);
+    else if (small)
+        hipLaunchKernelGGL((k_sparse_block<Off, 2>), grid, dim3(kBlock), 0, s, rp, col, f, t, guard, nullptr, nullptr);
+    else
+        hipLaunchKernelGGL((k_sparse_block<Off>), grid, dim3(kBlock), 0, s, rp, col, f, t, guard, nullptr, nullptr);
     SW_LAUNCHED();
     return SWARM_OK;
 }
@@ -610,7 +628,7 @@ template <typename Off>
 int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, const int32_t *ids,
                int32_t *leader, uint8_t *state, int32_t max_rounds, int32_t mode,
                int32_t *rounds_exec, int64_t *changes_host, swarm_elect_stats *st,
-               void *stream) {
+               void *stream, const Off *hrp = nullptr, const int32_t *hcol = nullptr) {
     SW_ARG(ctx != nullptr, "ctx is NULL");
     SW_ARG(n >= 0, "n < 0");
     SW_ARG(n < (int64_t(1) << 31), "n must be < 2^31");
@@ -632,6 +650,13 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     SW_HIP(hipMemcpyAsync(&e_total, rp + n, sizeof(Off), hipMemcpyDeviceToHost, s));
     SW_HIP(hipStreamSynchronize(s));
     SW_ARG(e_total == 0 || col != nullptr, "col is NULL but the graph has edges");
+    if (hrp) {  // directed: the transpose must hold the same edges
+        Off h_total = 0;
+        SW_HIP(hipMemcpyAsync(&h_total, hrp + n, sizeof(Off), hipMemcpyDeviceToHost, s));
+        SW_HIP(hipStreamSynchronize(s));
+        SW_ARG(h_total == e_total, "hear_row_ptr[n] != row_ptr[n]: not the transpose of the graph");
+        SW_ARG(h_total == 0 || hcol != nullptr, "hear_col is NULL but the graph has edges");
+    }
     int32_t *bufs[2] = {leader, nullptr};
     SW_ALLOC(bufs[1], ctx, S_LEADER_B, size_t(n) * 4);
     SW_HIP(hipMemcpyAsync(leader, ids, size_t(n) * 4, hipMemcpyDeviceToDevice, s));
@@ -689,7 +714,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
                                              1, s);
             } else {
                 kinds[r - t] = plan_round(r);
-                rc = launch_frontier_round<Off>(rp, col, f, r, kinds[r - t], 1, s);
+                rc = launch_frontier_round<Off>(rp, col, f, r, kinds[r - t], 1, s, hrp, hcol);
             }
             if (rc) return rc;
             if (e2) SW_HIP(hipEventRecord(e2[1], s));
@@ -810,6 +835,16 @@ int swarm_elect(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t
                 swarm_elect_stats *stats, void *stream) {
     return swarm::elect_impl<int32_t>(ctx, n, row_ptr, col, ids, leader, state, max_rounds, mode,
                                       rounds_exec, changes_per_round, stats, stream);
+}
+
+int swarm_elect_directed(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col,
+                         const int32_t *hear_row_ptr, const int32_t *hear_col, const int32_t *ids,
+                         int32_t *leader, uint8_t *state, int32_t max_rounds, int32_t mode,
+                         int32_t *rounds_exec, int64_t *changes_per_round, swarm_elect_stats *stats,
+                         void *stream) {
+    SW_ARG(hear_row_ptr != nullptr || n == 0, "hear_row_ptr is NULL (use swarm_elect for a symmetric graph)");
+    return swarm::elect_impl<int32_t>(ctx, n, row_ptr, col, ids, leader, state, max_rounds, mode,
+                                      rounds_exec, changes_per_round, stats, stream, hear_row_ptr, hear_col);
 }
 
 int swarm_elect_i64(swarm_ctx *ctx, int64_t n, const int64_t *row_ptr, const int32_t *col,

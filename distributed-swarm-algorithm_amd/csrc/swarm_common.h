@@ -89,8 +89,11 @@ namespace swarm {
 int comm_allreduce_max_u64(swarm_comm *comm, unsigned long long *buf, size_t count, hipStream_t s);
 int comm_rank(const swarm_comm *comm, int *rank, int *nranks);
 
-// Returns a device buffer of at least `bytes` for `s` (nullptr + error on failure).
+// Returns a device buffer of at least `bytes` for `s` (nullptr + error on failure: the ctx
+// belongs to another device -> scratch_code() SWARM_ERR_ARG, else SWARM_ERR_OOM).
 void *scratch(swarm_ctx *ctx, Slot s, size_t bytes);
+int scratch_code();
+bool ctx_on_current_device(const swarm_ctx *ctx);
 void *pinned(swarm_ctx *ctx, size_t bytes);
 
 }  // namespace swarm
@@ -116,7 +119,7 @@ void *pinned(swarm_ctx *ctx, size_t bytes);
 #define SW_ALLOC(ptr, ctx, slot, bytes)                                                  \
     do {                                                                                 \
         (ptr) = static_cast<std::remove_reference_t<decltype(ptr)>>(swarm::scratch((ctx), (slot), (bytes)));      \
-        if (!(ptr)) return SWARM_ERR_OOM;                                                \
+        if (!(ptr)) return swarm::scratch_code();                                        \
     } while (0)
 
 // Launch-error check after a kernel launch.

@@ -16,9 +16,16 @@ __device__ __forceinline__ double utility(double ax, double ay, uint32_t caps, d
                                           int rq, double u_scale) {
     const double dx = ax - tx, dy = ay - ty;
     const double d = sqrt(dx * dx + dy * dy);
-    const double has = (rq >= 0 && !((caps >> rq) & 1u)) ? 0.0 : 1.0;
+    // agent.py:343-345: a required capability the agent lacks -> 0.  rq in [0, 31] is a bit of
+    // the mask; rq >= 32 names a capability no agent holds (never a shift by >= 32: the ISA
+    // would wrap it mod 32 and alias bit rq - 32).  The entry points reject treq outside
+    // [-1, 31] with SWARM_ERR_ARG; this keeps the arithmetic defined either way.
+    const double has = (rq < 0) ? 1.0 : (rq < 32 && ((caps >> rq) & 1u)) ? 1.0 : 0.0;
     return (u_scale / (1.0 + d)) * has;
 }
+
+// treq outside [-1, 31] (counted by the kernels, reported as SWARM_ERR_ARG by the entry points)
+__host__ __device__ __forceinline__ bool bad_req(int rq) { return rq < -1 || rq > 31; }
 
 // Could the reference (libm pow for the squares, <= 2 ulp away) decide or round differently?
 __device__ __forceinline__ bool guard_flag(double U, double thr) {

@@ -24,7 +24,7 @@ ALLOC_AUTO, ALLOC_BINNED, ALLOC_DENSE = 0, 1, 2
 
 # every symbol include/swarm.h declares (tests/test_capi.py checks the two agree)
 EXPORTS = ("swarm_last_error", "swarm_version", "swarm_ctx_create", "swarm_ctx_destroy",
-           "swarm_elect", "swarm_elect_i64", "swarm_elect_round", "swarm_allocate",
+           "swarm_elect", "swarm_elect_directed", "swarm_elect_i64", "swarm_elect_round", "swarm_allocate",
            "swarm_utility", "swarm_build_rgg", "swarm_cell_order", "swarm_frontier_begin",
            "swarm_frontier_step", "swarm_frontier_ghosts", "swarm_frontier_changes",
            "swarm_comm_available", "swarm_comm_unique_id", "swarm_comm_create", "swarm_comm_destroy",
@@ -97,6 +97,7 @@ def load(path: str = LIB_PATH):
         sig_elect = [P, i64, P, P, P, P, P, i32, i32, ctypes.POINTER(i32), P, P, P]
         L.swarm_elect.argtypes = sig_elect
         L.swarm_elect_i64.argtypes = sig_elect
+        L.swarm_elect_directed.argtypes = [P, i64, P, P, P, P, P, P, P, i32, i32, ctypes.POINTER(i32), P, P, P]
         L.swarm_elect_round.argtypes = [P, i64, P, P, P, P, P, P]
         L.swarm_allocate.argtypes = [P, i64, P, P, P, i64, P, P, d, d, d, i32, P, P, P, P, i64,
                                      P, P, P, P]
@@ -141,18 +142,70 @@ def check(rc: int):
     return rc
 
 
+class Ctx:
+    """An owned swarm_ctx (scratch + frontier-stepper state) on the device current at creation.
+    libswarm refuses a ctx on any other device (SWARM_ERR_ARG)."""
+
+    def __init__(self):
+        self.handle = ctypes.c_void_p()
+        check(lib().swarm_ctx_create(ctypes.byref(self.handle)))
+        self.device = torch.cuda.current_device() if torch.cuda.is_available() else -1
+
+    @property
+    def _as_parameter_(self):  # ctypes passes the raw handle
+        return self.handle
+
+    def __del__(self):
+        h, L = getattr(self, "handle", None), _lib
+        if h is not None and h.value and L is not None:
+            L.swarm_ctx_destroy(h)
+            self.handle = ctypes.c_void_p()
+
+
 def ctx():
-    """Per-thread scratch context (bound to the device current at first use)."""
-    c = getattr(_tls, "ctx", None)
+    """This thread's scratch context for the current device (one per (thread, device): scratch
+    buffers belong to the device they were allocated on)."""
+    per = getattr(_tls, "ctx", None)
+    if per is None:
+        per = _tls.ctx = {}
+    dev = torch.cuda.current_device() if torch.cuda.is_available() else -1
+    c = per.get(dev)
     if c is None:
-        c = ctypes.c_void_p()
-        check(lib().swarm_ctx_create(ctypes.byref(c)))
-        _tls.ctx = c
+        c = per[dev] = Ctx()
     return c
 
 
 def version() -> str:
     return lib().swarm_version().decode()
+
+
+CSRC = os.path.join(os.path.dirname(HERE), "csrc")
+INCLUDE_H = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "swarm.h")
+
+
+def source_hash() -> str:
+    """sha256 prefix of this tree's library sources, as csrc/Makefile computes it for the build:
+    *.hip and *.h of csrc/ sorted by name, then csrc/Makefile, then include/swarm.h."""
+    import hashlib
+    names = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".h")))
+    h = hashlib.sha256()
+    for p in [os.path.join(CSRC, f) for f in names] + [os.path.join(CSRC, "Makefile"), INCLUDE_H]:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def built_hash() -> str:
+    """The source hash libswarm.so was built from (parsed from swarm_version())."""
+    v = version()
+    return v.split("src=", 1)[1].strip() if "src=" in v else ""
+
+
+def provenance() -> dict:
+    """Which build is loaded, and whether it matches this tree's sources."""
+    b, t = built_hash(), source_hash()
+    return {"libswarm": LIB_PATH, "version": version(), "src_hash_built": b, "src_hash_tree": t,
+            "matches_tree": b == t}
 
 
 def ptr(t, dtype=None, numel=None, name="tensor"):

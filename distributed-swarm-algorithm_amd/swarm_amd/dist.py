@@ -145,12 +145,16 @@ class GpuBackend:
         self.L = _lib
         self.device = device
         _lib.load()
+        # the shard's own ctx: the frontier stepper state between swarm_frontier_begin and the
+        # last step lives in it, out of reach of other libswarm calls of this thread
+        with torch.cuda.device(device):
+            self.ctx = _lib.Ctx()
 
     def cell_order(self, pos):
         n = pos.shape[0]
         perm = torch.empty(n, dtype=torch.int32, device=self.device)
         if n:
-            self.L.check(self.L.lib().swarm_cell_order(self.L.ctx(), n, self.L.ptr(pos), 1.0,
+            self.L.check(self.L.lib().swarm_cell_order(self.ctx, n, self.L.ptr(pos), 1.0,
                                                        self.L.ptr(perm), self.L.stream()))
         return perm.long()
 
@@ -160,27 +164,27 @@ class GpuBackend:
         rp = torch.empty(n + 1, dtype=torch.int32, device=self.device)
         ne = ctypes.c_int64(0)
         L = self.L
-        L.check(L.lib().swarm_build_rgg(L.ctx(), n, L.ptr(pos) if n else None, float(radius), L.ptr(rp), None, 0,
+        L.check(L.lib().swarm_build_rgg(self.ctx, n, L.ptr(pos) if n else None, float(radius), L.ptr(rp), None, 0,
                                         ctypes.byref(ne), L.stream()))
         col = torch.empty(max(ne.value, 1), dtype=torch.int32, device=self.device)
-        L.check(L.lib().swarm_build_rgg(L.ctx(), n, L.ptr(pos) if n else None, float(radius), L.ptr(rp), L.ptr(col),
+        L.check(L.lib().swarm_build_rgg(self.ctx, n, L.ptr(pos) if n else None, float(radius), L.ptr(rp), L.ptr(col),
                                         col.numel(), ctypes.byref(ne), L.stream()))
         return rp, col
 
     def begin(self, n_rows, init, leaders):
         L = self.L
-        L.check(L.lib().swarm_frontier_begin(L.ctx(), n_rows, init.numel(), L.ptr(init), L.ptr(leaders[0]),
+        L.check(L.lib().swarm_frontier_begin(self.ctx, n_rows, init.numel(), L.ptr(init), L.ptr(leaders[0]),
                                              L.ptr(leaders[1]), L.stream()))
 
     def step(self, t, rp, col, leaders):
         L = self.L
-        L.check(L.lib().swarm_frontier_step(L.ctx(), t, L.ptr(rp), L.ptr(col), L.ptr(leaders[0]),
+        L.check(L.lib().swarm_frontier_step(self.ctx, t, L.ptr(rp), L.ptr(col), L.ptr(leaders[0]),
                                             L.ptr(leaders[1]), L.stream()))
 
     def ghosts(self, t, begin, incoming, rp, col, leaders):
         L = self.L
         if incoming.numel():
-            L.check(L.lib().swarm_frontier_ghosts(L.ctx(), t, begin, incoming.numel(), L.ptr(incoming),
+            L.check(L.lib().swarm_frontier_ghosts(self.ctx, t, begin, incoming.numel(), L.ptr(incoming),
                                                   L.ptr(rp), L.ptr(col), L.ptr(leaders[0]), L.ptr(leaders[1]),
                                                   L.stream()))
 
@@ -218,7 +222,7 @@ class GpuBackend:
                        sh.halo.hi if sh.halo.hi is not None else -1, sh.halo_depth)
         rounds = ctypes.c_int32(0)
         changes = np.zeros(max_rounds, np.int64)
-        rc = L.check(L.lib().swarm_elect_sharded(L.ctx(), comm, ctypes.byref(desc), L.ptr(sh.leaders[0]),
+        rc = L.check(L.lib().swarm_elect_sharded(self.ctx, comm, ctypes.byref(desc), L.ptr(sh.leaders[0]),
                                                  L.ptr(sh.leaders[1]), max_rounds, ctypes.byref(rounds),
                                                  changes.ctypes.data_as(ctypes.c_void_p), L.stream()))
         r = rounds.value
@@ -227,7 +231,7 @@ class GpuBackend:
     def changes(self, t0, t1):
         L = self.L
         out = np.zeros(t1 - t0 + 1, np.int64)
-        L.check(L.lib().swarm_frontier_changes(L.ctx(), t0, t1, out.ctypes.data_as(__import__("ctypes").c_void_p),
+        L.check(L.lib().swarm_frontier_changes(self.ctx, t0, t1, out.ctypes.data_as(__import__("ctypes").c_void_p),
                                                L.stream()))
         return out
 
@@ -242,7 +246,7 @@ class GpuBackend:
                   assigned=torch.empty(n, dtype=torch.int32, device=dev), tpos=tpos, treq=treq)
         stats = L.AuctionStats()
         L.check(L.lib().swarm_auction_begin(
-            L.ctx(), n, L.ptr(ids) if n else None, L.ptr(pos) if n else None, L.ptr(caps) if n else None, t,
+            self.ctx, n, L.ptr(ids) if n else None, L.ptr(pos) if n else None, L.ptr(caps) if n else None, t,
             L.ptr(tpos) if t else None, L.ptr(treq) if t else None, float(claim_thr), float(u_scale), float(eps),
             L.ptr(st["owner_id"]) if t else None, L.ptr(st["price"]) if t else None,
             L.ptr(st["assigned"]) if n else None, ctypes.byref(stats), L.stream()))
@@ -251,13 +255,13 @@ class GpuBackend:
 
     def auction_bid(self, r, rank, world, keys, st):
         L = self.L
-        L.check(L.lib().swarm_auction_bid(L.ctx(), r, rank, world, L.ptr(keys),
+        L.check(L.lib().swarm_auction_bid(self.ctx, r, rank, world, L.ptr(keys),
                                           L.ptr(st["price"]) if st["price"].numel() else None,
                                           L.ptr(st["assigned"]) if st["assigned"].numel() else None, L.stream()))
 
     def auction_resolve(self, r, world, keys, st, log):
         L = self.L
-        L.check(L.lib().swarm_auction_resolve(L.ctx(), r, world, L.ptr(keys),
+        L.check(L.lib().swarm_auction_resolve(self.ctx, r, world, L.ptr(keys),
                                               L.ptr(st["owner_id"]) if st["owner_id"].numel() else None,
                                               L.ptr(st["price"]) if st["price"].numel() else None,
                                               L.ptr(st["assigned"]) if st["assigned"].numel() else None,
@@ -275,7 +279,7 @@ class GpuBackend:
         bidders = np.zeros(max_rounds, np.int64)
         stats = L.AuctionStats()
         rc = L.check(L.lib().swarm_auction_sharded(
-            L.ctx(), comm, n, L.ptr(ids) if n else None, L.ptr(pos) if n else None, L.ptr(caps) if n else None, t,
+            self.ctx, comm, n, L.ptr(ids) if n else None, L.ptr(pos) if n else None, L.ptr(caps) if n else None, t,
             L.ptr(tpos) if t else None, L.ptr(treq) if t else None, float(claim_thr), float(u_scale), float(eps),
             int(max_rounds), L.ptr(owner) if t else None, L.ptr(price) if t else None,
             L.ptr(assigned) if n else None, ctypes.byref(rounds), bidders.ctypes.data_as(ctypes.c_void_p),

@@ -175,7 +175,8 @@ class Swarm:
 
     # ------------------------------------------------------------------ election
     def elect(self, mode: str = "frontier", max_rounds: int = 1 << 16, timed: bool = False) -> ElectResult:
-        """Contract E2 to convergence on the GPU (swarm_elect).  timed: per-kernel HIP events."""
+        """Contract E2 to convergence on the GPU (swarm_elect; swarm_elect_directed when the
+        neighbour lists are not symmetric).  timed: per-kernel HIP events."""
         if self.row_ptr is None:
             raise RuntimeError("no neighbour graph: call build_graph() or set_graph()")
         m = {"dense": _lib.ELECT_DENSE, "frontier": _lib.ELECT_FRONTIER}[mode] | (_lib.ELECT_TIMED if timed else 0)
@@ -184,12 +185,21 @@ class Swarm:
         cap = int(max_rounds)
         changes = np.zeros(cap, np.int64)
         st = _lib.ElectStats()
+        hear = getattr(self, "_hear", None)
         with torch.cuda.device(self.device):
-            rc = _lib.check(_lib.lib().swarm_elect(
-                _lib.ctx(), n, _lib.ptr(self.row_ptr, torch.int32), _lib.ptr(self.col, torch.int32),
-                _lib.ptr(self.ids, torch.int32), _lib.ptr(self.leader, torch.int32),
-                _lib.ptr(self.state, torch.uint8), cap, m, ctypes.byref(rounds),
-                changes.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st), _lib.stream()))
+            if hear is None:  # symmetric graph: risers mark through their own rows
+                rc = _lib.check(_lib.lib().swarm_elect(
+                    _lib.ctx(), n, _lib.ptr(self.row_ptr, torch.int32), _lib.ptr(self.col, torch.int32),
+                    _lib.ptr(self.ids, torch.int32), _lib.ptr(self.leader, torch.int32),
+                    _lib.ptr(self.state, torch.uint8), cap, m, ctypes.byref(rounds),
+                    changes.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st), _lib.stream()))
+            else:  # directed (from_agents / set_graph with asymmetric lists): mark the hearers
+                rc = _lib.check(_lib.lib().swarm_elect_directed(
+                    _lib.ctx(), n, _lib.ptr(self.row_ptr, torch.int32), _lib.ptr(self.col, torch.int32),
+                    _lib.ptr(hear[0], torch.int32), _lib.ptr(hear[1], torch.int32) if hear[1].numel() else None,
+                    _lib.ptr(self.ids, torch.int32), _lib.ptr(self.leader, torch.int32),
+                    _lib.ptr(self.state, torch.uint8), cap, m, ctypes.byref(rounds),
+                    changes.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st), _lib.stream()))
         r = rounds.value
         res = ElectResult(r, changes[:r].copy(), self.leader, self.state, rc == _lib.OK,
                           st.rounds_launched, st.active_total, st.edges_total, st.dense_rounds,

@@ -82,6 +82,8 @@ typedef struct swarm_elect_stats {
 } swarm_elect_stats;
 
 const char *swarm_last_error(void);
+/* "swarm-mi355x <version> (gfx950) src=<16 hex>": the hex digits are the sha256 prefix of the
+ * sources the library was built from (csrc/Makefile HASHED), so a stale build is detectable. */
 const char *swarm_version(void);
 
 int swarm_ctx_create(swarm_ctx **out);
@@ -97,7 +99,8 @@ int swarm_ctx_destroy(swarm_ctx *ctx);
  *   stop after the first round with zero changes; rounds_exec counts that round.
  *   state[v] = SWARM_LEADER iff leader[v] == ids[v], else SWARM_FOLLOWER.
  * row_ptr/col: CSR of N(v) (who v hears) over storage indices; FRONTIER mode requires it
- * symmetric.  leader (device, n): output.  changes_per_round (host, capacity max_rounds, may
+ * symmetric (a riser marks the agents in its own row) -- use swarm_elect_directed otherwise.
+ * leader (device, n): output.  changes_per_round (host, capacity max_rounds, may
  * be NULL): per-round change counts for rounds 1..rounds_exec.  stats (host) may be NULL.
  * Returns SWARM_NOT_CONVERGED if max_rounds rounds all changed something.
  */
@@ -105,6 +108,17 @@ int swarm_elect(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t
                 const int32_t *ids, int32_t *leader, uint8_t *state, int32_t max_rounds,
                 int32_t mode, int32_t *rounds_exec, int64_t *changes_per_round,
                 swarm_elect_stats *stats, void *stream);
+
+/* Same for a directed neighbour graph (agent.py:59-65: update_sensors' per-agent neighbour
+ * lists need not be symmetric).  hear_row_ptr/hear_col (device) is the transpose of
+ * row_ptr/col -- for each agent, the agents that hear it -- through which FRONTIER rounds mark
+ * the agents a riser can change next round.  hear_row_ptr[n] must equal row_ptr[n]
+ * (SWARM_ERR_ARG otherwise).  DENSE mode ignores it. */
+int swarm_elect_directed(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col,
+                         const int32_t *hear_row_ptr, const int32_t *hear_col, const int32_t *ids,
+                         int32_t *leader, uint8_t *state, int32_t max_rounds, int32_t mode,
+                         int32_t *rounds_exec, int64_t *changes_per_round, swarm_elect_stats *stats,
+                         void *stream);
 
 /* Same with int64 row offsets (graphs with >= 2^31 edges). */
 int swarm_elect_i64(swarm_ctx *ctx, int64_t n, const int64_t *row_ptr, const int32_t *col,

@@ -44,6 +44,10 @@ def lib():
         l, d, i = ctypes.c_long, ctypes.c_double, ctypes.c_int
         L.orc_elect.restype = l
         L.orc_elect.argtypes = [l, P, P, P, P, P, l, P]
+        L.orc_elect_frontier.restype = l
+        L.orc_elect_frontier.argtypes = [l, P, P, P, P, P, P, P, l, P, P]
+        L.orc_allocate_binned.restype = l
+        L.orc_allocate_binned.argtypes = [l, P, P, P, P, l, P, P, P, d, d, d, i, P, P, P, P, P]
         L.orc_utility.restype = None
         L.orc_utility.argtypes = [l, P, P, P, P, P, P, d, i, P]
         L.orc_allocate.restype = l
@@ -94,6 +98,39 @@ def elect(row_ptr, col, ids, max_rounds=1 << 20):
     return leader, state, int(r), changes[: max(r, 0)].copy()
 
 
+def elect_frontier(row_ptr, col, ids, hear=None, max_rounds=1 << 20, with_active=False):
+    """E2 election by the frontier restatement (orc_elect_frontier): same outputs as elect();
+    hear = (row_ptr, col) of the transpose graph (who hears each agent), None when symmetric.
+    with_active: also return the agents recomputed per round."""
+    ids = _c(ids, np.int32)
+    n = len(ids)
+    rp = _c(row_ptr, np.int64)
+    cl = _c(col, np.int32)
+    hp, hc = (None, None) if hear is None else (_c(hear[0], np.int64), _c(hear[1], np.int32))
+    leader = np.empty(n, np.int32)
+    state = np.empty(n, np.uint8)
+    cap = max(1, min(max_rounds, 1 << 20))
+    changes = np.zeros(cap, np.int64)
+    active = np.zeros(cap, np.int64)
+    r = lib().orc_elect_frontier(n, _p(rp), _p(cl), None if hp is None else _p(hp), None if hc is None else _p(hc),
+                                 _p(ids), _p(leader), _p(state), cap, _p(changes), _p(active))
+    k = r if r > 0 else cap
+    out = (leader, state, int(r), changes[:max(r, 0)].copy())
+    return out + (active[:k].copy(),) if with_active else out
+
+
+def transpose_csr(row_ptr, col, n=None):
+    """(row_ptr, col) of the transpose graph, rows ascending (who hears each agent)."""
+    rp = np.asarray(row_ptr, np.int64)
+    cl = np.asarray(col, np.int64)
+    n = len(rp) - 1 if n is None else n
+    src = np.repeat(np.arange(n, dtype=np.int64), np.diff(rp))
+    o = np.lexsort((src, cl))
+    trp = np.zeros(n + 1, np.int64)
+    trp[1:] = np.cumsum(np.bincount(cl, minlength=n))
+    return trp, src[o].astype(np.int32)
+
+
 def utility(ax, ay, caps, tx, ty, treq, use_pow=True, u_scale=100.0):
     """Elementwise utility of (agent_i, task_i) pairs (agent.py:338-347), fp64."""
     arrs = [_c(ax, np.float64), _c(ay, np.float64), _c(caps, np.uint32), _c(tx, np.float64),
@@ -118,6 +155,26 @@ def allocate(ids, ax, ay, caps, tx, ty, treq, winner=None, util=None, claim_thr=
     total = lib().orc_allocate(n, _p(ids), *[_p(a) for a in arrs], t, *[_p(a) for a in tarr],
                                claim_thr, hysteresis, u_scale, int(use_pow), _p(w), _p(u),
                                _p(nclaim), _p(nmsg), _p(won))
+    return dict(winner=w, util=u, nclaim=nclaim, nmsg=nmsg, won=won, n_claims=int(total),
+                n_conflicts=int(nmsg.sum()))
+
+
+def allocate_binned(ids, ax, ay, caps, tx, ty, treq, winner=None, util=None, claim_thr=20.0,
+                    hysteresis=5.0, u_scale=100.0, use_pow=True):
+    """allocate() evaluating only the agents inside the claim radius (orc_allocate_binned):
+    same outputs, the CPU counterpart of the GPU's binned strategy."""
+    ids = _c(ids, np.int32)
+    n, t = len(ids), len(tx)
+    w = np.full(t, -1, np.int32) if winner is None else _c(winner, np.int32).copy()
+    u = np.zeros(t, np.float64) if util is None else _c(util, np.float64).copy()
+    nclaim = np.zeros(t, np.int64)
+    nmsg = np.zeros(t, np.int64)
+    won = np.zeros(n, np.int32)
+    arrs = [_c(ax, np.float64), _c(ay, np.float64), _c(caps, np.uint32)]
+    tarr = [_c(tx, np.float64), _c(ty, np.float64), _c(treq, np.int8)]
+    total = lib().orc_allocate_binned(n, _p(ids), *[_p(a) for a in arrs], t, *[_p(a) for a in tarr],
+                                      claim_thr, hysteresis, u_scale, int(use_pow), _p(w), _p(u),
+                                      _p(nclaim), _p(nmsg), _p(won))
     return dict(winner=w, util=u, nclaim=nclaim, nmsg=nmsg, won=won, n_claims=int(total),
                 n_conflicts=int(nmsg.sum()))
 

@@ -84,6 +84,67 @@ long orc_elect(long n, const int64_t *row_ptr, const int32_t *col, const int32_t
     return done ? rounds : -1;
 }
 
+/* Election to convergence, frontier form: the same rounds, leaders, rounds_exec and per-round
+ * change counts as orc_elect, but round t+1 only recomputes the agents marked by round t's
+ * risers -- each riser itself and every agent that hears it.  Exact: an unmarked agent's value
+ * already dominates every neighbour value, none of which changed.  hear_ptr/hear_col is the
+ * transpose of row_ptr/col (who hears v); pass NULL when the graph is symmetric.  Leaders are
+ * double-buffered by round parity: the write buffer holds round t-2's state, which differs
+ * from round t-1's only on round t-1's risers, all self-marked.  active[] (capacity max_rounds,
+ * may be NULL) receives the agents recomputed per round.  Restates orc_elect (agent.py:243-275
+ * under E2); it is pinned against orc_elect in tests/test_oracle_golden.py. */
+long orc_elect_frontier(long n, const int64_t *row_ptr, const int32_t *col, const int64_t *hear_ptr,
+                        const int32_t *hear_col, const int32_t *ids, int32_t *leader, uint8_t *state,
+                        long max_rounds, int64_t *changes, int64_t *active) {
+    const size_t nn = (size_t)(n > 0 ? n : 1);
+    int32_t *buf[2];
+    buf[0] = (int32_t *)malloc(sizeof(int32_t) * nn);
+    buf[1] = (int32_t *)malloc(sizeof(int32_t) * nn);
+    uint8_t *mark[2];
+    mark[0] = (uint8_t *)calloc(nn, 1);
+    mark[1] = (uint8_t *)malloc(nn);
+    memset(mark[1], 1, nn); /* round 1 recomputes everyone */
+    if (!hear_ptr) { hear_ptr = row_ptr; hear_col = col; }
+    for (long v = 0; v < n; ++v) buf[0][v] = buf[1][v] = ids[v];
+    long rounds = 0, done = 0;
+    while (rounds < max_rounds) {
+        const long t = rounds + 1;
+        const int32_t *P = buf[(t - 1) & 1];
+        int32_t *Q = buf[t & 1];
+        uint8_t *cur = mark[t & 1], *nxt = mark[(t + 1) & 1];
+        long c = 0, act = 0;
+#pragma omp parallel for schedule(dynamic, 4096) reduction(+ : c, act)
+        for (long v = 0; v < n; ++v) {
+            if (!cur[v]) continue;
+            cur[v] = 0;
+            ++act;
+            int32_t m = P[v];
+            for (int64_t e = row_ptr[v]; e < row_ptr[v + 1]; ++e) {
+                const int32_t s = P[col[e]];
+                if (s > m) m = s;
+            }
+            Q[v] = m;
+            if (m > P[v]) {
+                ++c;
+                __atomic_store_n(&nxt[v], (uint8_t)1, __ATOMIC_RELAXED);
+                for (int64_t e = hear_ptr[v]; e < hear_ptr[v + 1]; ++e)
+                    __atomic_store_n(&nxt[hear_col[e]], (uint8_t)1, __ATOMIC_RELAXED);
+            }
+        }
+        changes[rounds] = c;
+        if (active) active[rounds] = act;
+        ++rounds;
+        if (c == 0) { done = 1; break; }
+    }
+    const int32_t *fin = buf[rounds & 1];
+    for (long v = 0; v < n; ++v) {
+        leader[v] = fin[v];
+        state[v] = (fin[v] == ids[v]) ? ST_LEADER : ST_FOLLOWER;
+    }
+    free(buf[0]); free(buf[1]); free(mark[0]); free(mark[1]);
+    return done ? rounds : -1;
+}
+
 /* One utility, reference arithmetic (libm pow) or GPU arithmetic (x*x) by `use_pow`. */
 static inline double util_one(double ax, double ay, uint32_t caps, double tx, double ty,
                               int8_t treq, double u_scale, int use_pow) {
@@ -91,7 +152,9 @@ static inline double util_one(double ax, double ay, uint32_t caps, double tx, do
     double sx = use_pow ? pow(dx, 2.0) : dx * dx;
     double sy = use_pow ? pow(dy, 2.0) : dy * dy;
     double d = sqrt(sx + sy);
-    double has = (treq >= 0 && !((caps >> treq) & 1u)) ? 0.0 : 1.0;
+    /* agent.py:343-345: a required capability the agent lacks -> 0.0.  Indices >= 32 name a
+     * capability outside the 32-bit mask, which no agent holds (no shift by >= 32: UB in C). */
+    double has = (treq < 0) ? 1.0 : (treq < 32 && ((caps >> treq) & 1u)) ? 1.0 : 0.0;
     return (u_scale / (1.0 + d)) * has;
 }
 
@@ -156,6 +219,121 @@ long orc_allocate(long n, const int32_t *ids, const double *ax, const double *ay
         }
     }
     free(order);
+    return total;
+}
+
+/* orc_allocate restricted to the agents that can claim: with claim_thr > 0 and u_scale > 0 a
+ * claim needs U > claim_thr, i.e. d < u_scale / claim_thr - 1, so only agents inside that radius
+ * (widened by a relative 1e-9 against rounding) are evaluated, found through a uniform grid.
+ * Same outputs as orc_allocate (pinned against it in tests/test_oracle_golden.py); falls back to
+ * it when the claim radius is not finite.  The CPU baseline of the GPU's binned allocation. */
+typedef struct { int32_t id; float x; long idx; } claim_t;
+static int cmp_claim(const void *a, const void *b) {
+    const claim_t *p = (const claim_t *)a, *q = (const claim_t *)b;
+    return (p->id > q->id) - (p->id < q->id);
+}
+
+long orc_allocate_binned(long n, const int32_t *ids, const double *ax, const double *ay,
+                         const uint32_t *caps, long t, const double *tx, const double *ty,
+                         const int8_t *treq, double claim_thr, double hyst, double u_scale, int use_pow,
+                         int32_t *winner, double *util, int64_t *nclaim, int64_t *nmsg, int32_t *won) {
+    if (!(claim_thr > 0 && u_scale > 0) || n == 0)
+        return orc_allocate(n, ids, ax, ay, caps, t, tx, ty, treq, claim_thr, hyst, u_scale, use_pow, winner,
+                            util, nclaim, nmsg, won);
+    /* rp <= 0: nobody can claim, every task keeps its current claim (the loop finds no claims) */
+    const double rp = (u_scale / claim_thr - 1.0) * (1.0 + 1e-9) + 1e-12;
+    double xmin = ax[0], xmax = ax[0], ymin = ay[0], ymax = ay[0];
+    for (long i = 1; i < n; ++i) {
+        if (ax[i] < xmin) xmin = ax[i];
+        if (ax[i] > xmax) xmax = ax[i];
+        if (ay[i] < ymin) ymin = ay[i];
+        if (ay[i] > ymax) ymax = ay[i];
+    }
+    double cell = rp > 0 ? rp : 1.0;
+    long ncx, ncy;
+    for (;;) {
+        ncx = (long)floor((xmax - xmin) / cell) + 1;
+        ncy = (long)floor((ymax - ymin) / cell) + 1;
+        if ((double)ncx * (double)ncy <= 2.0 * (double)n + 1024.0) break;
+        cell *= 1.4142135623730951;
+    }
+    long *start = (long *)calloc((size_t)(ncx * ncy + 1), sizeof(long));
+    long *cellof = (long *)malloc(sizeof(long) * (size_t)n);
+    for (long i = 0; i < n; ++i) {
+        long cx = (long)floor((ax[i] - xmin) / cell), cy = (long)floor((ay[i] - ymin) / cell);
+        cx = cx < 0 ? 0 : cx >= ncx ? ncx - 1 : cx;
+        cy = cy < 0 ? 0 : cy >= ncy ? ncy - 1 : cy;
+        cellof[i] = cy * ncx + cx;
+        start[cellof[i] + 1]++;
+    }
+    for (long c = 0; c < ncx * ncy; ++c) start[c + 1] += start[c];
+    long *fillp = (long *)malloc(sizeof(long) * (size_t)(ncx * ncy));
+    for (long c = 0; c < ncx * ncy; ++c) fillp[c] = start[c];
+    long *members = (long *)malloc(sizeof(long) * (size_t)n);
+    for (long i = 0; i < n; ++i) members[fillp[cellof[i]]++] = i;
+    /* id -> storage index (won credit for a pre-existing winner that keeps its task) */
+    long *order = (long *)malloc(sizeof(long) * (size_t)n);
+    for (long i = 0; i < n; ++i) order[i] = i;
+    g_ids = ids;
+    qsort(order, (size_t)n, sizeof(long), cmp_by_id_g);
+    long total = 0;
+#pragma omp parallel reduction(+ : total)
+    {
+        long cap = 1024;
+        claim_t *cl = (claim_t *)malloc(sizeof(claim_t) * (size_t)cap);
+#pragma omp for schedule(dynamic, 16)
+        for (long k = 0; k < t; ++k) {
+            long m = 0;
+            if (rp > 0) {
+                long x0 = (long)floor((tx[k] - rp - xmin) / cell), x1 = (long)floor((tx[k] + rp - xmin) / cell);
+                long y0 = (long)floor((ty[k] - rp - ymin) / cell), y1 = (long)floor((ty[k] + rp - ymin) / cell);
+                x0 = x0 < 0 ? 0 : x0; y0 = y0 < 0 ? 0 : y0;
+                x1 = x1 >= ncx ? ncx - 1 : x1; y1 = y1 >= ncy ? ncy - 1 : y1;
+                for (long cy = y0; cy <= y1; ++cy)
+                    for (long cx = x0; cx <= x1; ++cx)
+                        for (long p = start[cy * ncx + cx]; p < start[cy * ncx + cx + 1]; ++p) {
+                            const long i = members[p];
+                            const double U = util_one(ax[i], ay[i], caps[i], tx[k], ty[k], treq[k], u_scale, use_pow);
+                            if (!(U > claim_thr)) continue;
+                            if (m == cap) {
+                                cap *= 2;
+                                cl = (claim_t *)realloc(cl, sizeof(claim_t) * (size_t)cap);
+                            }
+                            cl[m].id = ids[i];
+                            cl[m].x = (float)U;
+                            cl[m].idx = i;
+                            ++m;
+                        }
+            }
+            qsort(cl, (size_t)m, sizeof(claim_t), cmp_claim);
+            int32_t w = winner[k];
+            double u = util[k];
+            int has = w >= 0;
+            int64_t ms = 0;
+            for (long j = 0; j < m; ++j) {
+                const double x = (double)cl[j].x;
+                if (!has || x > u + hyst) {
+                    w = cl[j].id; u = x; has = 1; ++ms;
+                } else if (w != cl[j].id) {
+                    ++ms;
+                }
+            }
+            winner[k] = w; util[k] = u; nclaim[k] = m; nmsg[k] = ms; total += m;
+        }
+        free(cl);
+    }
+    for (long i = 0; i < n; ++i) won[i] = 0;
+    for (long k = 0; k < t; ++k) {
+        if (winner[k] < 0) continue;
+        long lo = 0, hi = n - 1;
+        while (lo <= hi) {
+            long mid = (lo + hi) / 2;
+            int32_t v = ids[order[mid]];
+            if (v == winner[k]) { won[order[mid]] += 1; break; }
+            if (v < winner[k]) lo = mid + 1; else hi = mid - 1;
+        }
+    }
+    free(start); free(cellof); free(fillp); free(members); free(order);
     return total;
 }
 
@@ -270,16 +448,99 @@ static float bits_f32(uint32_t u) {
     return f;
 }
 
+/* Uniform grid over task positions (cells of side >= r, at most 2t + 1024 cells); members of a
+ * cell in ascending task index. */
+typedef struct { double xmin, ymin, cell, r; long ncx, ncy; long *start, *members; } task_grid_t;
+
+static void task_grid_build(task_grid_t *g, long t, const double *tx, const double *ty, double r) {
+    double xmin = tx[0], xmax = tx[0], ymin = ty[0], ymax = ty[0];
+    for (long k = 1; k < t; ++k) {
+        if (tx[k] < xmin) xmin = tx[k];
+        if (tx[k] > xmax) xmax = tx[k];
+        if (ty[k] < ymin) ymin = ty[k];
+        if (ty[k] > ymax) ymax = ty[k];
+    }
+    double cell = r > 0 ? r : 1.0;
+    for (;;) {
+        g->ncx = (long)floor((xmax - xmin) / cell) + 1;
+        g->ncy = (long)floor((ymax - ymin) / cell) + 1;
+        if ((double)g->ncx * (double)g->ncy <= 2.0 * (double)t + 1024.0) break;
+        cell *= 1.4142135623730951;
+    }
+    g->xmin = xmin; g->ymin = ymin; g->cell = cell; g->r = r;
+    const long nc = g->ncx * g->ncy;
+    g->start = (long *)calloc((size_t)nc + 1, sizeof(long));
+    g->members = (long *)malloc(sizeof(long) * (size_t)t);
+    long *cof = (long *)malloc(sizeof(long) * (size_t)t);
+    for (long k = 0; k < t; ++k) {
+        long cx = (long)floor((tx[k] - xmin) / cell), cy = (long)floor((ty[k] - ymin) / cell);
+        cx = cx < 0 ? 0 : cx >= g->ncx ? g->ncx - 1 : cx;
+        cy = cy < 0 ? 0 : cy >= g->ncy ? g->ncy - 1 : cy;
+        cof[k] = cy * g->ncx + cx;
+        g->start[cof[k] + 1]++;
+    }
+    for (long c = 0; c < nc; ++c) g->start[c + 1] += g->start[c];
+    long *fp = (long *)malloc(sizeof(long) * (size_t)(nc > 0 ? nc : 1));
+    for (long c = 0; c < nc; ++c) fp[c] = g->start[c];
+    for (long k = 0; k < t; ++k) g->members[fp[cof[k]]++] = k;  /* ascending k within a cell */
+    free(fp);
+    free(cof);
+}
+
+static void task_grid_free(task_grid_t *g) { free(g->start); free(g->members); }
+
+static int cmp_ck(const void *a, const void *b) {
+    const int32_t x = *(const int32_t *)a, y = *(const int32_t *)b;
+    return (x > y) - (x < y);
+}
+
+/* Admissible tasks (U > thr) of one agent; with out_k/out_v, written in ascending task index
+ * (values follow their tasks).  Returns the count. */
+static int64_t task_grid_claims(const task_grid_t *g, double px, double py, uint32_t cap, const double *tx,
+                                const double *ty, const int8_t *treq, double thr, double u_scale, int use_pow,
+                                int32_t *out_k, float *out_v) {
+    if (!(g->r > 0)) return 0;
+    long x0 = (long)floor((px - g->r - g->xmin) / g->cell), x1 = (long)floor((px + g->r - g->xmin) / g->cell);
+    long y0 = (long)floor((py - g->r - g->ymin) / g->cell), y1 = (long)floor((py + g->r - g->ymin) / g->cell);
+    x0 = x0 < 0 ? 0 : x0; y0 = y0 < 0 ? 0 : y0;
+    x1 = x1 >= g->ncx ? g->ncx - 1 : x1; y1 = y1 >= g->ncy ? g->ncy - 1 : y1;
+    int64_t c = 0;
+    for (long cy = y0; cy <= y1; ++cy)
+        for (long cx = x0; cx <= x1; ++cx)
+            for (long p = g->start[cy * g->ncx + cx]; p < g->start[cy * g->ncx + cx + 1]; ++p) {
+                const long k = g->members[p];
+                if (util_one(px, py, cap, tx[k], ty[k], treq[k], u_scale, use_pow) > thr) {
+                    if (out_k) out_k[c] = (int32_t)k;
+                    ++c;
+                }
+            }
+    if (out_k) {
+        qsort(out_k, (size_t)c, sizeof(int32_t), cmp_ck);
+        for (int64_t j = 0; j < c; ++j)
+            out_v[j] = (float)util_one(px, py, cap, tx[out_k[j]], ty[out_k[j]], treq[out_k[j]], u_scale, use_pow);
+    }
+    return c;
+}
+
 long orc_auction(long n, const int32_t *ids, const double *ax, const double *ay, const uint32_t *caps,
                  long t, const double *tx, const double *ty, const int8_t *treq, double claim_thr,
                  double u_scale, int use_pow, float eps, long max_rounds, int32_t *owner, float *price,
                  int32_t *assigned, int64_t *bidders, int64_t *n_pairs) {
     int64_t *off = (int64_t *)calloc((size_t)n + 1, sizeof(int64_t));
+    /* candidate tasks of each agent in ascending task index: through a uniform grid over the
+     * tasks when the claim radius is finite (U > thr needs d < u_scale/thr - 1), else all */
+    task_grid_t tg;
+    const int binned = claim_thr > 0 && u_scale > 0 && t > 0;
+    if (binned) task_grid_build(&tg, t, tx, ty, (u_scale / claim_thr - 1.0) * (1.0 + 1e-9) + 1e-12);
 #pragma omp parallel for schedule(dynamic, 64)
     for (long a = 0; a < n; ++a) {
         int64_t c = 0;
-        for (long k = 0; k < t; ++k)
-            if (util_one(ax[a], ay[a], caps[a], tx[k], ty[k], treq[k], u_scale, use_pow) > claim_thr) ++c;
+        if (binned) {
+            c = task_grid_claims(&tg, ax[a], ay[a], caps[a], tx, ty, treq, claim_thr, u_scale, use_pow, NULL, NULL);
+        } else {
+            for (long k = 0; k < t; ++k)
+                if (util_one(ax[a], ay[a], caps[a], tx[k], ty[k], treq[k], u_scale, use_pow) > claim_thr) ++c;
+        }
         off[a + 1] = c;
     }
     for (long a = 0; a < n; ++a) off[a + 1] += off[a];
@@ -289,11 +550,16 @@ long orc_auction(long n, const int32_t *ids, const double *ax, const double *ay,
 #pragma omp parallel for schedule(dynamic, 64)
     for (long a = 0; a < n; ++a) {
         int64_t p = off[a];
+        if (binned) {
+            task_grid_claims(&tg, ax[a], ay[a], caps[a], tx, ty, treq, claim_thr, u_scale, use_pow, ck + p, cv + p);
+            continue;
+        }
         for (long k = 0; k < t; ++k) {
             double U = util_one(ax[a], ay[a], caps[a], tx[k], ty[k], treq[k], u_scale, use_pow);
             if (U > claim_thr) { ck[p] = (int32_t)k; cv[p] = (float)U; ++p; }
         }
     }
+    if (binned) task_grid_free(&tg);
     if (n_pairs) *n_pairs = np;
     /* id -> storage index via the ascending-ID order */
     long *order = (long *)malloc(sizeof(long) * (size_t)(n > 0 ? n : 1));

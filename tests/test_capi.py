@@ -51,3 +51,33 @@ def test_gpu_code_object_targets_gfx950_only():
     data = open(LIB, "rb").read()
     targets = set(re.findall(rb"amdgcn-amd-amdhsa-[-a-z0-9]*?(gfx[0-9a-z]+)", data))
     assert targets == {b"gfx950"}, targets
+
+
+def test_library_is_this_trees_build():
+    """Build provenance: swarm_version() carries the sha256 prefix of the sources libswarm.so
+    was built from (csrc/Makefile); it must equal this tree's, so a stale .so fails here."""
+    from swarm_amd import _lib
+    p = _lib.provenance()
+    assert p["src_hash_built"] and len(p["src_hash_built"]) == 16, p
+    assert p["matches_tree"], f"stale libswarm.so: rebuild with make -C distributed-swarm-algorithm_amd/csrc ({p})"
+
+
+def test_source_hash_tracks_every_source(tmp_path, monkeypatch):
+    """The tree hash changes when any hashed file changes (a kernel, a header, the Makefile)."""
+    import shutil
+    from swarm_amd import _lib
+    csrc = tmp_path / "csrc"
+    shutil.copytree(_lib.CSRC, csrc, ignore=shutil.ignore_patterns("build*", "*.o"))
+    inc = tmp_path / "swarm.h"
+    shutil.copy(_lib.INCLUDE_H, inc)
+    monkeypatch.setattr(_lib, "CSRC", str(csrc))
+    monkeypatch.setattr(_lib, "INCLUDE_H", str(inc))
+    base = _lib.source_hash()
+    for f in ("elect.hip", "utility.h", "Makefile"):
+        p = csrc / f
+        old = p.read_bytes()
+        p.write_bytes(old + b"\n")
+        assert _lib.source_hash() != base, f
+        p.write_bytes(old)
+    inc.write_bytes(inc.read_bytes() + b"\n")
+    assert _lib.source_hash() != base
