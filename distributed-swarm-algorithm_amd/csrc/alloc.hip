@@ -78,7 +78,7 @@ constexpr int kStatStride = 16;
 struct BlockStats {
     unsigned long long claims = 0, msgs = 0, overflow = 0, bad = 0;
 };
-constexpr int kNumStats = 6;
+constexpr int kNumStats = 7;  // + [6]: agents with a non-finite position (binned mode)
 
 __device__ __forceinline__ void flush_stats(const Params &P, unsigned long long claims, unsigned long long msgs,
                                             unsigned long long flagged, unsigned long long cand,
@@ -120,12 +120,114 @@ __device__ __forceinline__ void finish_task(const Params &P, int64_t k, int w0, 
     bs.msgs += (unsigned long long)msgs;
 }
 
+// ------------------------------------------------------------------------ hashed cells
+// BINNED candidates: agents bucketed by grid cell of side Rp, cells hashed into 2^k buckets (no
+// bounding box, so no device -> host round trip before the launch).  A task's Rp-disc covers at
+// most 3 x 3 cells; an agent is visited under its own cell only (its cell is recomputed and
+// compared), so cells sharing a bucket are never double counted.  Bucket = counting sort: one
+// wave-aggregated atomic per (wave, bucket) for the counts and in-bucket ranks, a hipCUB scan,
+// one scatter.  Order inside a bucket is arbitrary: the claims are collected in LDS and the
+// record chain picks by ID.
+struct HashGrid {
+    double inv_cell;
+    uint32_t mask;  // buckets - 1 (power of two)
+};
+
+constexpr double kCellClamp = 1e15;  // cells beyond +-1e15 merge (the distance test still decides)
+
+__device__ __forceinline__ int64_t hcell(double v, double inv) {
+    double f = floor(v * inv);
+    if (!(f >= -kCellClamp)) f = -kCellClamp;  // also NaN
+    if (f > kCellClamp) f = kCellClamp;
+    return int64_t(f);
+}
+
+__device__ __forceinline__ uint32_t hbucket(int64_t cx, int64_t cy, uint32_t mask) {
+    uint64_t h = uint64_t(cx) * 0x9E3779B97F4A7C15ull ^ (uint64_t(cy) + 0x632BE59BD9B4E019ull) * 0xC2B2AE3D27D4EB4Full;
+    h ^= h >> 32;
+    h *= 0xD6E8FEB86659FD93ull;
+    return uint32_t(h >> 32) & mask;
+}
+
+// Counts per bucket and each agent's rank in its bucket.  Agents in spatial storage order put a
+// wave's 64 lanes in a few cells: one atomic per distinct bucket of the wave.
+__global__ __launch_bounds__(kBlock) void k_hash_count(const double2 *__restrict__ apos, int64_t n, HashGrid hg,
+                                                      uint32_t *__restrict__ cnt, uint32_t *__restrict__ key,
+                                                      uint32_t *__restrict__ rank,
+                                                      unsigned long long *__restrict__ nonfinite) {
+    const int lane = threadIdx.x & 63;
+    const int64_t stride = int64_t(gridDim.x) * kBlock;
+    unsigned long long bad = 0;
+    for (int64_t base = int64_t(blockIdx.x) * kBlock + (threadIdx.x & ~63); base < n; base += stride) {
+        const int64_t i = base + lane;
+        const bool valid = i < n;
+        uint32_t k = 0;
+        if (valid) {
+            const double2 p = apos[i];
+            bad += (isfinite(p.x) && isfinite(p.y)) ? 0 : 1;
+            k = hbucket(hcell(p.x, hg.inv_cell), hcell(p.y, hg.inv_cell), hg.mask);
+        }
+        uint32_t r = 0;
+        unsigned long long todo = __ballot(valid);
+        while (todo) {
+            const int lead = __ffsll((long long)todo) - 1;
+            const uint32_t lk = __shfl(k, lead, 64);
+            const unsigned long long same = __ballot(valid && k == lk) & todo;
+            uint32_t b = 0;
+            if (lane == lead) b = atomicAdd(&cnt[lk], uint32_t(__popcll(same)));
+            b = __shfl(b, lead, 64);
+            if ((same >> lane) & 1ull) r = b + uint32_t(__popcll(same & ((1ull << lane) - 1ull)));
+            todo &= ~same;
+        }
+        if (valid) {
+            key[i] = k;
+            rank[i] = r;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) bad += __shfl_xor(bad, off, 64);
+    if (lane == 0 && bad) atomicAdd(nonfinite, bad);
+}
+
+__global__ __launch_bounds__(kBlock) void k_hash_scatter(int64_t n, const uint32_t *__restrict__ key,
+                                                        const uint32_t *__restrict__ rank,
+                                                        const uint32_t *__restrict__ off,
+                                                        int32_t *__restrict__ sorted) {
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock)
+        sorted[off[key[i]] + rank[i]] = int32_t(i);
+}
+
+// Candidates of a task: every agent within its cell window, visited once (own cell only) --
+// fn(storage index, position).
+template <typename Fn>
+__device__ __forceinline__ void for_candidates(double2 tp, double rp, const HashGrid &hg,
+                                               const int32_t *__restrict__ sorted,
+                                               const uint32_t *__restrict__ off,
+                                               const double2 *__restrict__ apos, Fn fn) {
+    const int64_t x0 = hcell(tp.x - rp, hg.inv_cell), y0 = hcell(tp.y - rp, hg.inv_cell);
+    int64_t x1 = hcell(tp.x + rp, hg.inv_cell), y1 = hcell(tp.y + rp, hg.inv_cell);
+    // the window is 2 Rp wide with cells of side Rp: at most 3 cells per axis (4 with rounding)
+    if (x1 > x0 + 3) x1 = x0 + 3;
+    if (y1 > y0 + 3) y1 = y0 + 3;
+    for (int64_t cy = y0; cy <= y1; ++cy)
+        for (int64_t cx = x0; cx <= x1; ++cx) {
+            const uint32_t b = hbucket(cx, cy, hg.mask);
+            const uint32_t a = off[b], e = off[b + 1];
+            for (uint32_t q = a + threadIdx.x; q < e; q += kBlock) {
+                const int32_t i = sorted[q];
+                const double2 p = apos[i];
+                if (hcell(p.x, hg.inv_cell) != cx || hcell(p.y, hg.inv_cell) != cy) continue;  // another cell
+                fn(i, p);
+            }
+        }
+}
+
 // ------------------------------------------------------------------------------ binned
 __global__ __launch_bounds__(kBlock) void k_alloc_binned(
     int64_t t_count, const double2 *__restrict__ tpos, const int8_t *__restrict__ treq,
     const int32_t *__restrict__ ids, const double2 *__restrict__ apos,
     const uint32_t *__restrict__ caps, const int32_t *__restrict__ sorted_idx,
-    const uint32_t *__restrict__ cell_off, Grid g, double rp, Params P) {
+    const uint32_t *__restrict__ bucket_off, HashGrid hg, double rp, Params P) {
     __shared__ int s_id[kCap];
     __shared__ float s_x[kCap];
     __shared__ int s_ix[kCap];
@@ -141,20 +243,11 @@ __global__ __launch_bounds__(kBlock) void k_alloc_binned(
         const double u0 = P.util[k];
         if (threadIdx.x == 0) { s_n = 0; s_w0c = 0; }
         __syncthreads();
-        // task's Rp-disc in grid coordinates (empty if it misses the agents' bounding box)
-        const bool miss = tp.x + rp < g.xmin || tp.x - rp > g.xmax || tp.y + rp < g.ymin || tp.y - rp > g.ymax;
-        const int64_t x0 = miss ? 1 : cell_coord(tp.x - rp, g.xmin, g.inv_cell, g.ncx);
-        const int64_t x1 = miss ? 0 : cell_coord(tp.x + rp, g.xmin, g.inv_cell, g.ncx);
-        const int64_t y0 = miss ? 1 : cell_coord(tp.y - rp, g.ymin, g.inv_cell, g.ncy);
-        const int64_t y1 = miss ? 0 : cell_coord(tp.y + rp, g.ymin, g.inv_cell, g.ncy);
         // pass 1: evaluate candidates, keep claims in LDS
-        for (int64_t yy = y0; yy <= y1; ++yy) {
-            const uint32_t a = cell_off[yy * g.ncx + x0], b = cell_off[yy * g.ncx + x1 + 1];
-            for (uint32_t q = a + threadIdx.x; q < b; q += kBlock) {
-                const int32_t i = sorted_idx[q];
-                const double2 p = apos[i];
+        if (P.rp2 >= 0.0)
+            for_candidates(tp, rp, hg, sorted_idx, bucket_off, apos, [&](int32_t i, double2 p) {
                 const double dx = p.x - tp.x, dy = p.y - tp.y;
-                if (dx * dx + dy * dy > P.rp2) continue;
+                if (dx * dx + dy * dy > P.rp2) return;
                 ++my_cand;
                 const double U = utility(p.x, p.y, caps[i], tp.x, tp.y, rq, P.u_scale);
                 my_flag += guard_flag(U, P.thr);
@@ -164,8 +257,7 @@ __global__ __launch_bounds__(kBlock) void k_alloc_binned(
                     if (slot < kCap) { s_id[slot] = id; s_x[slot] = float(U); s_ix[slot] = i; }
                     if (id == w0) s_w0c = 1;
                 }
-            }
-        }
+            });
         __syncthreads();
         const int nclaims = s_n;
         const bool overflow = nclaims > kCap;
@@ -184,20 +276,15 @@ __global__ __launch_bounds__(kBlock) void k_alloc_binned(
                     }
                 }
             } else {  // exact recompute over the candidates (rare: > kCap claims on one task)
-                for (int64_t yy = y0; yy <= y1; ++yy) {
-                    const uint32_t a = cell_off[yy * g.ncx + x0], b = cell_off[yy * g.ncx + x1 + 1];
-                    for (uint32_t q = a + threadIdx.x; q < b; q += kBlock) {
-                        const int32_t i = sorted_idx[q];
-                        const double2 p = apos[i];
-                        const double dx = p.x - tp.x, dy = p.y - tp.y;
-                        if (dx * dx + dy * dy > P.rp2) continue;
-                        const double U = utility(p.x, p.y, caps[i], tp.x, tp.y, rq, P.u_scale);
-                        const int id = ids[i];
-                        if (U > P.thr && id > prev && id < best && (!has || double(float(U)) > cur_u + P.h)) {
-                            best = id; best_x = float(U); best_ix = i;
-                        }
+                for_candidates(tp, rp, hg, sorted_idx, bucket_off, apos, [&](int32_t i, double2 p) {
+                    const double dx = p.x - tp.x, dy = p.y - tp.y;
+                    if (dx * dx + dy * dy > P.rp2) return;
+                    const double U = utility(p.x, p.y, caps[i], tp.x, tp.y, rq, P.u_scale);
+                    const int id = ids[i];
+                    if (U > P.thr && id > prev && id < best && (!has || double(float(U)) > cur_u + P.h)) {
+                        best = id; best_x = float(U); best_ix = i;
                     }
-                }
+                });
             }
             const int win = block_min_int(best, s_red);
             if (win == INT_MAX) break;
@@ -456,29 +543,44 @@ int swarm_allocate(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *
     const bool nothing = (n == 0) || (used == SWARM_ALLOC_BINNED && rc <= 0.0);
     if (t > 0 && nothing) {
         // no agent can claim: every task keeps its current claim (won credited via id_to_index)
-        const double rp = 0.0;
-        Grid g{0, 0, -1, -1, 1, 1, 1, 1};
         uint32_t *off;
         SW_ALLOC(off, ctx, S_CELL_START, 16);
         SW_HIP(hipMemsetAsync(off, 0, 16, s));
         P.rp2 = -1.0;
         hipLaunchKernelGGL(k_alloc_binned, dim3(grid_for(t, 1, 4096)), dim3(kBlock), 0, s, t,
                            reinterpret_cast<const double2 *>(tpos), treq, ids,
-                           reinterpret_cast<const double2 *>(apos), acaps, (const int32_t *)nullptr,
-                           off, g, rp, P);
+                           reinterpret_cast<const double2 *>(apos), acaps, (const int32_t *)nullptr, off,
+                           HashGrid{1.0, 0}, 0.0, P);
         SW_LAUNCHED();
     } else if (t > 0 && used == SWARM_ALLOC_BINNED) {
+        // agents bucketed by hashed cell of side Rp (counting sort, no host round trip)
         const double rp = rc * (1.0 + 1e-9) + 1e-12;
         P.rp2 = rp * rp;
-        Grid g;
-        int rcode = make_grid(ctx, n, apos, rp, 2 * n + 1024, &g, s);
-        if (rcode) return rcode;
+        uint32_t nb = 1024;
+        while (nb < uint32_t(1) << 30 && int64_t(nb) * 8 < n) nb <<= 1;
+        const HashGrid hg{1.0 / rp, nb - 1};
+        uint32_t *cnt, *off, *key, *rank;
         int32_t *sorted;
-        uint32_t *off;
-        if ((rcode = bin_agents(ctx, n, apos, g, &sorted, &off, s))) return rcode;
+        SW_ALLOC(cnt, ctx, S_KEYS_IN, size_t(nb + 1) * 4);
+        SW_ALLOC(off, ctx, S_CELL_START, size_t(nb + 1) * 4);
+        SW_ALLOC(key, ctx, S_KEYS_OUT, size_t(n) * 4);
+        SW_ALLOC(rank, ctx, S_VALS_IN, size_t(n) * 4);
+        SW_ALLOC(sorted, ctx, S_VALS_OUT, size_t(n) * 4);
+        SW_HIP(hipMemsetAsync(cnt, 0, size_t(nb + 1) * 4, s));
+        hipLaunchKernelGGL(k_hash_count, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s,
+                           reinterpret_cast<const double2 *>(apos), n, hg, cnt, key, rank, dstats + 6);
+        SW_LAUNCHED();
+        size_t tmp_bytes = 0;
+        SW_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, off, int(nb + 1), s));
+        void *tmp;
+        SW_ALLOC(tmp, ctx, S_CUB_TMP, tmp_bytes);
+        SW_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, int(nb + 1), s));
+        hipLaunchKernelGGL(k_hash_scatter, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s, n, key, rank, off,
+                           sorted);
+        SW_LAUNCHED();
         hipLaunchKernelGGL(k_alloc_binned, dim3(grid_for(t, 1, 4096)), dim3(kBlock), 0, s, t,
                            reinterpret_cast<const double2 *>(tpos), treq, ids,
-                           reinterpret_cast<const double2 *>(apos), acaps, sorted, off, g, rp, P);
+                           reinterpret_cast<const double2 *>(apos), acaps, sorted, off, hg, rp, P);
         SW_LAUNCHED();
     } else if (t > 0) {
         P.rp2 = 0;
@@ -518,6 +620,10 @@ int swarm_allocate(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *
     SW_LAUNCHED();
     SW_HIP(hipMemcpyAsync(hs, folded, 8 * kNumStats, hipMemcpyDeviceToHost, s));
     SW_HIP(hipStreamSynchronize(s));
+    if (hs[6]) {
+        set_error("invalid argument: %llu agent position(s) are not finite", (unsigned long long)hs[6]);
+        return SWARM_ERR_ARG;
+    }
     if (hs[5]) {  // outputs were computed treating those capability indices as absent
         set_error("invalid argument: %llu task(s) with treq outside [-1, 31]", (unsigned long long)hs[5]);
         return SWARM_ERR_ARG;

@@ -112,12 +112,50 @@ __device__ __forceinline__ unsigned bytes_eq4(unsigned w, unsigned b4) {
     return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
 }
 
+// ------------------------------------------------------------------ stamp layout
+// Stamps are not stored in agent order.  Agents are grouped in blocks of B = 2^bshift consecutive
+// storage indices; block b lives in chunk b mod M, at block position b div M, so a chunk (the
+// sparse round's unit of work: C = 2^cshift = 2 048 or 512 stamps, one workgroup pass) holds
+// blocks spread evenly over the whole swarm.  A wave front that lies along a cell row marks a long
+// run of consecutive agents; in agent order that run lands in one or two chunks (hundreds of
+// marked agents, the slowest workgroup of the round), here it is dealt out B agents per chunk.
+// Within a block the agents stay consecutive: their rows are one contiguous slice of col.  B = C
+// is the identity (agent order).
+struct StampMap {
+    uint32_t M;   // chunks
+    float invM;   // 1 / M: the block's chunk and position from one float product, corrected by +-1
+    int cshift;   // log2(C)
+    int bshift;   // log2(B)
+};
+
+// 32-bit on the device (register pressure: the sparse kernel runs at the 64-VGPR cap of 8 waves
+// per SIMD).  b < 2^28 and the quotient is below C / B <= 256, so the float product is within
+// 2^-14 of b / M: one correction step makes it exact.
+__device__ __forceinline__ uint32_t stamp_slot(const StampMap &m, int32_t v) {
+    const uint32_t b = uint32_t(v) >> m.bshift;
+    uint32_t q = __float2uint_rz(__uint2float_rz(b) * m.invM);
+    int32_t r = int32_t(b - q * m.M);
+    if (r < 0) {
+        --q;
+        r += int32_t(m.M);
+    } else if (r >= int32_t(m.M)) {
+        ++q;
+        r -= int32_t(m.M);
+    }
+    return (uint32_t(r) << m.cshift) + (q << m.bshift) + (uint32_t(v) & ((1u << m.bshift) - 1));
+}
+
+// storage index of in-chunk stamp position j of chunk k
+__device__ __forceinline__ int64_t stamp_agent(const StampMap &m, int64_t k, int j) {
+    return ((int64_t(j >> m.bshift) * m.M + k) << m.bshift) | (j & ((1 << m.bshift) - 1));
+}
+
 constexpr int kKm = 8;  // marking re-walks: col loads in flight per lane
 
 // Mark col[k] for k = k0, k0 + step, ... < e with kKm loads in flight per batch.
 template <typename Off>
-__device__ __forceinline__ void mark_row(uint8_t *aw, const int32_t *__restrict__ col, Off k0, Off e, Off step,
-                                         uint8_t s) {
+__device__ __forceinline__ void mark_row(uint8_t *aw, const StampMap &sm, const int32_t *__restrict__ col, Off k0,
+                                         Off e, Off step, uint8_t s) {
     for (Off k = k0; k < e; k += step * kKm) {
         int c[kKm];
 #pragma unroll
@@ -127,7 +165,7 @@ __device__ __forceinline__ void mark_row(uint8_t *aw, const int32_t *__restrict_
         }
 #pragma unroll
         for (int j = 0; j < kKm; ++j)
-            if (k + step * j < e) aw[c[j]] = s;
+            if (k + step * j < e) aw[stamp_slot(sm, c[j])] = s;
     }
 }
 
@@ -167,7 +205,7 @@ template <typename Off, bool MARK, bool DIR = false>
 __global__ __launch_bounds__(kBlock) void k_elect_dense(
     const Off *__restrict__ rp, const int32_t *__restrict__ col, const int32_t *__restrict__ lin,
     int32_t *__restrict__ lout, int64_t n, int64_t n_count, unsigned long long *__restrict__ ring,
-    unsigned long long *__restrict__ tot, uint8_t *__restrict__ act_w, int t, int guard,
+    unsigned long long *__restrict__ tot, uint8_t *__restrict__ act_w, StampMap sm, int t, int guard,
     const Off *__restrict__ hrp = nullptr, const int32_t *__restrict__ hcol = nullptr) {
     __shared__ int s_col[kWavesPerBlock][kWin];
     __shared__ unsigned long long s_bc, s_cnt[kWavesPerBlock];
@@ -213,11 +251,11 @@ __global__ __launch_bounds__(kBlock) void k_elect_dense(
         if (valid) lout[v] = up ? m : own;
         mine += __popcll(__ballot(up && v < n_count));  // sharded: ghost rows step, owners count
         if (MARK && up) {
-            act_w[v] = sw;
+            act_w[stamp_slot(sm, v)] = sw;
             if (DIR)
-                mark_row<Off>(act_w, hcol, hrp[v], hrp[v + 1], Off(1), sw);
+                mark_row<Off>(act_w, sm, hcol, hrp[v], hrp[v + 1], Off(1), sw);
             else
-                mark_row<Off>(act_w, col, b, e, Off(1), sw);
+                mark_row<Off>(act_w, sm, col, b, e, Off(1), sw);
         }
         b = nb;
         e = ne;
@@ -236,13 +274,18 @@ constexpr int kScan = 8;                 // stamps per thread (one 8-B load)
 constexpr int kChunk = kBlock * kScan;   // k_sparse_block: agents per workgroup work unit
 constexpr int kG = 4;                    // lanes per marked agent
 constexpr int kKs = 8;                   // loads in flight per lane
+constexpr int kListCap = 4096;           // marked agents listed in LDS per workgroup (16 KiB)
 
 struct Frontier {
     int32_t *L[2];
-    uint8_t *act[2];         // stamps, act_bytes(n_all) each (padded past n_all)
+    uint8_t *act[2];         // stamps, sm.M << sm.cshift bytes each (stamp_slot layout)
+    // sm: the layout this round's stamps were written in (read and consumed); wsm: the layout of
+    // the marks it writes for the next round.  Same chunk size and count, so the host may switch
+    // the layout at any round boundary (stamp_map).
     unsigned long long *ring, *tot;
     int64_t n_rows, n_all;   // rows stepped (owned + ghosts in sharded runs), all agents
     int64_t n_count;         // rows [0, n_count) are owned: only their changes are counted
+    StampMap sm, wsm;
 };
 
 // Gather of the marked agents listed (chunk-relative) in lst[0, total), G lanes per agent,
@@ -253,14 +296,14 @@ template <typename Off, int G, int K, bool DIR>
 __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, const int32_t *__restrict__ col,
                                               const Off *__restrict__ hrp, const int32_t *__restrict__ hcol,
                                               const int32_t *__restrict__ P, int32_t *__restrict__ Q,
-                                              uint8_t *__restrict__ aw, uint8_t sw, int64_t c0, const int *lst,
-                                              int total, int first, int step, int64_t n_count,
+                                              uint8_t *__restrict__ aw, const StampMap &sm, uint8_t sw,
+                                              const int *lst, int total, int first, int step, int64_t n_count,
                                               long long &my_chg, long long &my_act, long long &my_edges) {
     const int lane = threadIdx.x & 63, sub = lane & (G - 1);
     for (int base = first; base < total; base += step) {
         const int i = base + lane / G;
         const bool valid = i < total;
-        const int64_t v = c0 + lst[valid ? i : total - 1];
+        const int64_t v = lst[valid ? i : total - 1];
         const Off b = rp[v], e = rp[v + 1];
         const int own = P[v];
         int m = own;
@@ -279,15 +322,15 @@ __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, const 
         const bool up = valid && m > own;
         if (valid && sub == 0) Q[v] = m;
         if (up) {
-            if (sub == 0) aw[v] = sw;
+            if (sub == 0) aw[stamp_slot(sm, v)] = sw;
             if (DIR) {  // the agents that hear v
-                mark_row<Off>(aw, hcol, hrp[v] + sub, hrp[v + 1], Off(G), sw);
+                mark_row<Off>(aw, sm, hcol, hrp[v] + sub, hrp[v + 1], Off(G), sw);
             } else if (e - b <= G * K) {  // one pass: c[] still holds this lane's edges
 #pragma unroll
                 for (int j = 0; j < K; ++j)
-                    if (b + sub + G * j < e) aw[c[j]] = sw;
+                    if (b + sub + G * j < e) aw[stamp_slot(sm, c[j])] = sw;
             } else {
-                mark_row<Off>(aw, col, b + sub, e, Off(G), sw);
+                mark_row<Off>(aw, sm, col, b + sub, e, Off(G), sw);
             }
         }
         my_chg += __popcll(__ballot(up && sub == 0 && v < n_count));
@@ -315,11 +358,13 @@ __device__ __forceinline__ bool any_stamp(uint16_t w) { return w != 0; }
 
 // Marked lanes of S stamps, consuming them (this parity is next written in round t+1, marks
 // for t+2; a stamp left behind would match again 255 rounds later: a spurious gather).
+// s0: first stamp slot of the word, v0: its first agent (the S slots are agents v0 .. v0+S-1).
 template <int S, typename W>
-__device__ __forceinline__ unsigned take_stamps(uint8_t *ar, int64_t v0, int64_t n, W wv, unsigned stamp4) {
+__device__ __forceinline__ unsigned take_stamps(uint8_t *ar, int64_t s0, int64_t v0, int64_t n, W wv,
+                                                unsigned stamp4) {
     unsigned mask = stamp_bits(wv, stamp4);
     if (v0 + S > n) mask &= (v0 >= n) ? 0u : ((1u << (n - v0)) - 1u);
-    if (any_stamp(wv)) *reinterpret_cast<W *>(ar + v0) = W{};
+    if (any_stamp(wv)) *reinterpret_cast<W *>(ar + s0) = W{};
     return mask;
 }
 
@@ -352,7 +397,7 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
     const Off *__restrict__ hrp = nullptr, const int32_t *__restrict__ hcol = nullptr) {
     using W = typename StampWord<S>::T;
     constexpr int kChunk = kBlock * S;
-    __shared__ int s_list[kChunk];
+    __shared__ int s_list[kListCap];
     __shared__ int s_wave[kWavesPerBlock];
     __shared__ long long s_red[3][kWavesPerBlock];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -370,49 +415,74 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
     const uint8_t sw = stamp_of(t + 1);
     const int64_t n = f.n_rows;
     long long my_chg = 0, my_act = 0, my_edges = 0;
-    const int64_t nchunks = (n + kChunk - 1) / kChunk;
+    const int64_t nchunks = f.sm.M;  // chunk k: stamp slots [k*kChunk, (k+1)*kChunk)
     const int64_t NG = gridDim.x;
-    W nxt{};  // stamps are padded past n_all; the next chunk's are loaded ahead
-    if (int64_t(blockIdx.x) < nchunks)
-        nxt = *reinterpret_cast<const W *>(ar + int64_t(blockIdx.x) * kChunk + int64_t(threadIdx.x) * S);
-    for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += NG) {
-        const int64_t c0 = chunk * kChunk;
-        const int64_t v0 = c0 + int64_t(threadIdx.x) * S;
-        const W wv = nxt;
-        if (chunk + NG < nchunks) nxt = *reinterpret_cast<const W *>(ar + v0 + NG * kChunk);
-        unsigned mask = take_stamps<S>(ar, v0, n, wv, stamp4);
-        const int cnt = __popc(mask);
-        int incl = cnt;
+    const int j0 = threadIdx.x * S;  // this thread's S slots: consecutive agents of one block
+    // The stamp words of all this workgroup's chunks (grid-stride, up to kPre at a time) are loaded
+    // at once, with clamped addresses so that no load waits on a branch; their marked lanes are
+    // kept as S bits per chunk.  The marked agents of all those chunks then go into ONE list in
+    // LDS, gathered together: a round costs one stamp load latency and one gather chain per
+    // workgroup, not one of each per chunk.  (List order is free: every listed agent is
+    // independent of the others within a round.)
+    constexpr int kPre = 32 / S < 4 ? 32 / S : 4;
+    constexpr int kLogS = S == 8 ? 3 : 1;
+    int listed = 0;  // workgroup-uniform
+    for (int64_t cg = blockIdx.x; cg < nchunks; cg += NG * kPre) {
+        W wv[kPre];
 #pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int x = __shfl_up(incl, off, 64);
-            if (lane >= off) incl += x;
+        for (int p = 0; p < kPre; ++p) {
+            const int64_t chunk = cg + p * NG < nchunks ? cg + p * NG : nchunks - 1;
+            wv[p] = *reinterpret_cast<const W *>(ar + chunk * kChunk + j0);
         }
-        if (lane == 63) s_wave[wid] = incl;
-        __syncthreads();
-        int off = 0, total = 0;
+        unsigned masks = 0;
 #pragma unroll
-        for (int w = 0; w < kWavesPerBlock; ++w) {
-            off += (w < wid) ? s_wave[w] : 0;
-            total += s_wave[w];
+        for (int p = 0; p < kPre; ++p) {
+            const int64_t chunk = cg + p * NG;
+            if (chunk < nchunks)
+                masks |= take_stamps<S>(ar, chunk * kChunk + j0, stamp_agent(f.sm, chunk, j0), n, wv[p], stamp4)
+                         << (p * S);
         }
-#ifdef SWARM_PHASES
-        ph_sum += total;
-        ph_max = total > ph_max ? total : ph_max;
-#endif
-        if (total > 0) {
-            int pos = off + incl - cnt;
-            while (mask) {
-                const int j = __ffs(mask) - 1;
-                mask &= mask - 1;
-                s_list[pos++] = threadIdx.x * S + j;
+        // append the group's marked agents, gathering whenever the list fills up
+        for (;;) {
+            const int cnt = __popc(masks);
+            int incl = cnt;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int x = __shfl_up(incl, off, 64);
+                if (lane >= off) incl += x;
             }
+            if (lane == 63) s_wave[wid] = incl;
             __syncthreads();
-            gather_listed<Off, G, K, DIR>(rp, col, hrp, hcol, P, Q, aw, sw, c0, s_list, total, wid * (64 / G), kBlock / G,
-                                     f.n_count, my_chg, my_act, my_edges);
+            int off = 0, total = 0;
+#pragma unroll
+            for (int w = 0; w < kWavesPerBlock; ++w) {
+                off += (w < wid) ? s_wave[w] : 0;
+                total += s_wave[w];
+            }
+            __syncthreads();  // s_wave read by all
+            if (total == 0) break;
+#ifdef SWARM_PHASES
+            ph_sum += total;
+            ph_max = total > ph_max ? total : ph_max;
+#endif
+            int pos = listed + off + incl - cnt;
+            while (masks && pos < kListCap) {
+                const int bit = __ffs(masks) - 1;
+                masks &= masks - 1;
+                s_list[pos++] = int(stamp_agent(f.sm, cg + (bit >> kLogS) * NG, j0)) + (bit & (S - 1));
+            }
+            listed = listed + total < kListCap ? listed + total : kListCap;
+            __syncthreads();  // list entries visible
+            if (listed < kListCap) break;  // everything fitted
+            gather_listed<Off, G, K, DIR>(rp, col, hrp, hcol, P, Q, aw, f.wsm, sw, s_list, listed, wid * (64 / G),
+                                          kBlock / G, f.n_count, my_chg, my_act, my_edges);
+            listed = 0;
+            __syncthreads();  // the list is reused
         }
-        __syncthreads();  // LDS (s_wave, s_list) reused by the next chunk
     }
+    if (listed > 0)
+        gather_listed<Off, G, K, DIR>(rp, col, hrp, hcol, P, Q, aw, f.wsm, sw, s_list, listed, wid * (64 / G),
+                                      kBlock / G, f.n_count, my_chg, my_act, my_edges);
     flush_counts(f.ring, t, my_chg, my_act, my_edges, s_red);
 #ifdef SWARM_PHASES
     if (threadIdx.x == 0 && blockIdx.x < 8192) {
@@ -453,7 +523,7 @@ __global__ __launch_bounds__(kBlock) void k_frontier_ghosts(const Off *__restric
                 }
                 for (Off k = rp[g] + sub; k < rp[g + 1]; k += G) {
                     const int32_t c = col[k];
-                    if (c < f.n_rows) aw[c] = sw;
+                    if (c < f.n_rows) aw[stamp_slot(f.wsm, c)] = sw;
                 }
             }
         }
@@ -502,7 +572,11 @@ struct Tuning {
     int dense_rounds = 8;     // frontier: rounds 1..dense_rounds run dense (the last one marks)
     int sparse_blocks = 2048; // grid cap of k_sparse_block (8 resident workgroups per CU)
     int small_chunks = 512;   // fewer 2048-agent chunks than this: 512-agent chunks instead
+    int stamp_bshift = 5;     // log2 of the stamp layout's block (stamp_slot)
+    int il_min_changes = 2000; // interleaved stamp layout while the last read round changed >= this
     Tuning() {
+        il_min_changes = env_int("SWARM_IL_MIN_CHANGES", 2000);
+        stamp_bshift = env_int("SWARM_STAMP_BSHIFT", 5);
         dense_blocks = env_int("SWARM_DENSE_BLOCKS", 2048);
         dense_rounds = env_int("SWARM_DENSE_ROUNDS", 8);
         sparse_blocks = env_int("SWARM_SPARSE_BLOCKS", 2048);
@@ -520,24 +594,41 @@ const Tuning &tuning() {
 
 size_t ring_bytes() { return size_t(kRing) * kCounters * kRoundWords * 8 + size_t(kRing) * 8; }
 
-size_t act_bytes(int64_t n_all) {  // one parity, padded to whole chunks (+1 of slack)
-    return size_t((n_all + 2 * kChunk - 1) / kChunk) * kChunk;
+// Stamp layout of an n_all-agent stepper (stamp_slot): 2 048-stamp chunks, or 512 when a swarm has
+// fewer than small_chunks of the large ones (more workgroups for small swarms).
+// interleaved: blocks of 2^bshift agents dealt over the chunks (default); otherwise agent order.
+StampMap stamp_map(int64_t n_all, bool interleaved = true) {
+    const bool small = (n_all + kChunk - 1) / kChunk < tuning().small_chunks;
+    StampMap m{};
+    m.cshift = small ? 9 : 11;  // kBlock * 2 or kBlock * kScan stamps
+    m.bshift = tuning().stamp_bshift < 3 ? 3 : tuning().stamp_bshift;  // a thread's 8 stamps: one block
+    if (m.bshift > m.cshift || !interleaved) m.bshift = m.cshift;
+    const int64_t per = int64_t(1) << (m.cshift - m.bshift);  // blocks per chunk
+    const int64_t nblocks = (n_all + (int64_t(1) << m.bshift) - 1) >> m.bshift;
+    m.M = uint32_t(nblocks > 0 ? (nblocks + per - 1) / per : 1);  // = ceil(n_all / C) for every bshift
+    m.invM = 1.0f / float(m.M);
+    return m;
+}
+
+size_t act_bytes(int64_t n_all) {  // one parity: every chunk of the stamp layout
+    const StampMap m = stamp_map(n_all);
+    return size_t(m.M) << m.cshift;
 }
 
 template <typename Off>
 int launch_dense_round(const Off *rp, const int32_t *col, const int32_t *lin, int32_t *lout, int64_t n, int64_t n_count,
-                       unsigned long long *ring, unsigned long long *tot, uint8_t *act_w, int t, int guard,
-                       hipStream_t s, const Off *hrp = nullptr, const int32_t *hcol = nullptr) {
+                       unsigned long long *ring, unsigned long long *tot, uint8_t *act_w, StampMap sm, int t,
+                       int guard, hipStream_t s, const Off *hrp = nullptr, const int32_t *hcol = nullptr) {
     const unsigned grid = grid_for((n + 63) / 64, kWavesPerBlock, unsigned(tuning().dense_blocks));
     if (act_w && hrp)
         hipLaunchKernelGGL((k_elect_dense<Off, true, true>), dim3(grid), dim3(kBlock), 0, s, rp, col, lin, lout, n,
-                           n_count, ring, tot, act_w, t, guard, hrp, hcol);
+                           n_count, ring, tot, act_w, sm, t, guard, hrp, hcol);
     else if (act_w)
         hipLaunchKernelGGL((k_elect_dense<Off, true>), dim3(grid), dim3(kBlock), 0, s, rp, col, lin, lout, n, n_count, ring,
-                           tot, act_w, t, guard, nullptr, nullptr);
+                           tot, act_w, sm, t, guard, nullptr, nullptr);
     else
         hipLaunchKernelGGL((k_elect_dense<Off, false>), dim3(grid), dim3(kBlock), 0, s, rp, col, lin, lout, n, n_count, ring,
-                           tot, act_w, t, guard, nullptr, nullptr);
+                           tot, act_w, sm, t, guard, nullptr, nullptr);
     SW_LAUNCHED();
     return SWARM_OK;
 }
@@ -556,6 +647,7 @@ int frontier_bind(swarm_ctx *ctx, int32_t *L0, int32_t *L1, Frontier *f) {
     uint8_t *a = static_cast<uint8_t *>(ctx->slot[S_ACT]);
     f->act[0] = a;
     f->act[1] = a + act_bytes(f->n_all);
+    f->sm = f->wsm = stamp_map(f->n_all);
     f->ring = static_cast<unsigned long long *>(ctx->slot[S_CHANGES]);
     f->tot = f->ring + size_t(kRing) * kCounters * kRoundWords;
     return SWARM_OK;
@@ -576,7 +668,8 @@ int frontier_alloc(swarm_ctx *ctx, int64_t n_rows, int64_t n_all, int32_t *L0, i
     if (rc) return rc;
     SW_HIP(hipMemsetAsync(f->ring, 0, ring_bytes(), s));
     SW_HIP(hipMemsetAsync(f->act[0], 0, sb, s));
-    if (tuning().dense_rounds == 0 && n_all) SW_HIP(hipMemsetAsync(f->act[1], 1, size_t(n_all), s));
+    // every slot, padding included: take_stamps drops slots past n_all
+    if (tuning().dense_rounds == 0 && n_all) SW_HIP(hipMemsetAsync(f->act[1], 1, sb / 2, s));
     return SWARM_OK;
 }
 
@@ -598,11 +691,10 @@ int launch_frontier_round(const Off *rp, const int32_t *col, const Frontier &f, 
     if (k == RK_DENSE || k == RK_DENSE_MARK)
         return launch_dense_round<Off>(rp, col, f.L[(t - 1) & 1], f.L[t & 1], f.n_rows, f.n_count, f.ring,
                                        f.tot,
-                                       k == RK_DENSE_MARK ? f.act[(t + 1) & 1] : nullptr, t, guard, s, hrp, hcol);
-    const int64_t nchunks = (f.n_rows + kChunk - 1) / kChunk;
-    const bool small = nchunks < tuning().small_chunks;  // small swarm: 512-agent chunks, 4x the workgroups
-    const int64_t nc = small ? (f.n_rows + kBlock * 2 - 1) / (kBlock * 2) : nchunks;
-    const dim3 grid(grid_for(nc, 1, unsigned(tuning().sparse_blocks)));
+                                       k == RK_DENSE_MARK ? f.act[(t + 1) & 1] : nullptr, f.wsm, t, guard, s, hrp,
+                                       hcol);
+    const bool small = f.sm.cshift == 9;  // small swarm: 512-agent chunks, 4x the workgroups
+    const dim3 grid(grid_for(f.sm.M, 1, unsigned(tuning().sparse_blocks)));
     if (hrp && small)
         hipLaunchKernelGGL((k_sparse_block<Off, 2, true>), grid, dim3(kBlock), 0, s, rp, col, f, t, guard, hrp, hcol);
     else if (hrp)
@@ -679,7 +771,9 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     SW_ALLOC(dtot, ctx, S_ESTATS, size_t(kCounters) * 8 * kMaxBatch);
 
     int found = -1, t = 1, batch = 8, launched = 0;
-    std::vector<int64_t> hist;  // per-round change counts read so far (batch sizing)
+    std::vector<int64_t> hist;  // per-round change counts read so far (batch sizing, layout)
+    const StampMap il_map = stamp_map(n, true), ag_map = stamp_map(n, false);
+    StampMap rd_map = il_map;
     int64_t act_sum = 0, edge_sum = 0, chg_sum = 0, dense_rounds = 0, sp_launches = 0;
     double bytes = 0.0, sp_bytes = 0.0, sp_ms = 0.0;
     std::vector<RoundKind> kinds(kMaxBatch);
@@ -710,11 +804,16 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
             if (e2) SW_HIP(hipEventRecord(e2[0], s));
             if (mode == SWARM_ELECT_DENSE) {
                 kinds[r - t] = RK_DENSE;
-                rc = launch_dense_round<Off>(rp, col, bufs[(r - 1) & 1], bufs[r & 1], n, n, ring, nullptr, nullptr, r,
-                                             1, s);
+                rc = launch_dense_round<Off>(rp, col, bufs[(r - 1) & 1], bufs[r & 1], n, n, ring, nullptr, nullptr,
+                                             StampMap{}, r, 1, s);
             } else {
                 kinds[r - t] = plan_round(r);
+                // marks for round r+1: interleaved layout while rounds are busy (balance), agent
+                // order once they are sparse (locality of the few gathers)
+                f.sm = rd_map;
+                f.wsm = (hist.empty() || hist.back() >= tuning().il_min_changes) ? il_map : ag_map;
                 rc = launch_frontier_round<Off>(rp, col, f, r, kinds[r - t], 1, s, hrp, hcol);
+                rd_map = f.wsm;
             }
             if (rc) return rc;
             if (e2) SW_HIP(hipEventRecord(e2[1], s));
@@ -935,8 +1034,8 @@ int swarm_elect_round(swarm_ctx *ctx, int64_t n_rows, const int32_t *row_ptr,
     unsigned long long *ring;
     SW_ALLOC(ring, ctx, S_TMP0, size_t(kCounters) * kRoundWords * 8);
     SW_HIP(hipMemsetAsync(ring, 0, size_t(kRoundWords) * 8, s));
-    int rc = launch_dense_round<int32_t>(row_ptr, col, leader_in, leader_out, n_rows, n_rows, ring, nullptr, nullptr, 0,
-                                        0, s);
+    int rc = launch_dense_round<int32_t>(row_ptr, col, leader_in, leader_out, n_rows, n_rows, ring, nullptr, nullptr,
+                                        StampMap{}, 0, 0, s);
     if (rc) return rc;
     hipLaunchKernelGGL(k_sum_shards, dim3(1), dim3(kWave), 0, s, ring, 0,
                        reinterpret_cast<unsigned long long *>(changed));
