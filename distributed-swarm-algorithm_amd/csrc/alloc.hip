@@ -32,20 +32,6 @@
 namespace swarm {
 namespace {
 
-constexpr int kCap = 2048;  // claims per task kept in LDS (beyond: exact recompute path)
-
-__device__ __forceinline__ int block_min_int(int v, int *s_red) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    int m = s_red[0];
-#pragma unroll
-    for (int w = 1; w < kBlock / kWave; ++w) m = min(m, s_red[w]);
-    return m;
-}
-
 __device__ __forceinline__ long long block_sum_ll(long long v, long long *s_red) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -167,18 +153,25 @@ __global__ __launch_bounds__(kBlock) void k_hash_count(const double2 *__restrict
             bad += (isfinite(p.x) && isfinite(p.y)) ? 0 : 1;
             k = hbucket(hcell(p.x, hg.inv_cell), hcell(p.y, hg.inv_cell), hg.mask);
         }
-        uint32_t r = 0;
+        // group the wave's lanes by bucket (no memory traffic), then ONE atomic instruction: every
+        // group's first lane adds its group size, and each lane's rank = group base + lanes of its
+        // group below it
+        uint32_t lead = 0, gsize = 0, below = 0;
         unsigned long long todo = __ballot(valid);
         while (todo) {
-            const int lead = __ffsll((long long)todo) - 1;
-            const uint32_t lk = __shfl(k, lead, 64);
+            const int l = __ffsll((long long)todo) - 1;
+            const uint32_t lk = __shfl(k, l, 64);
             const unsigned long long same = __ballot(valid && k == lk) & todo;
-            uint32_t b = 0;
-            if (lane == lead) b = atomicAdd(&cnt[lk], uint32_t(__popcll(same)));
-            b = __shfl(b, lead, 64);
-            if ((same >> lane) & 1ull) r = b + uint32_t(__popcll(same & ((1ull << lane) - 1ull)));
+            if ((same >> lane) & 1ull) {
+                lead = uint32_t(l);
+                gsize = uint32_t(__popcll(same));
+                below = uint32_t(__popcll(same & ((1ull << lane) - 1ull)));
+            }
             todo &= ~same;
         }
+        uint32_t b = 0;
+        if (valid && lead == uint32_t(lane)) b = atomicAdd(&cnt[k], gsize);
+        const uint32_t r = __shfl(b, int(lead), 64) + below;
         if (valid) {
             key[i] = k;
             rank[i] = r;
@@ -197,70 +190,143 @@ __global__ __launch_bounds__(kBlock) void k_hash_scatter(int64_t n, const uint32
         sorted[off[key[i]] + rank[i]] = int32_t(i);
 }
 
-// Candidates of a task: every agent within its cell window, visited once (own cell only) --
-// fn(storage index, position).
-template <typename Fn>
-__device__ __forceinline__ void for_candidates(double2 tp, double rp, const HashGrid &hg,
-                                               const int32_t *__restrict__ sorted,
-                                               const uint32_t *__restrict__ off,
-                                               const double2 *__restrict__ apos, Fn fn) {
+// A task's cell window (at most 4 x 4 cells; 3 x 3 in practice: the window is 2 Rp wide with
+// cells of side Rp) as one flat candidate range: cell j holds bucket entries
+// [a[j], a[j] + pre[j+1] - pre[j]), its coordinates are (cx[j], cy[j]).  Built by the task's wave.
+constexpr int kMaxCells = 16;
+struct CellWindow {
+    uint32_t a[kMaxCells], pre[kMaxCells + 1];
+    int64_t cx[kMaxCells], cy[kMaxCells];
+    int ncell;
+};
+
+__device__ __forceinline__ void window_setup(double2 tp, double rp, const HashGrid &hg,
+                                             const uint32_t *__restrict__ off, CellWindow &w, int lane) {
     const int64_t x0 = hcell(tp.x - rp, hg.inv_cell), y0 = hcell(tp.y - rp, hg.inv_cell);
     int64_t x1 = hcell(tp.x + rp, hg.inv_cell), y1 = hcell(tp.y + rp, hg.inv_cell);
-    // the window is 2 Rp wide with cells of side Rp: at most 3 cells per axis (4 with rounding)
-    if (x1 > x0 + 3) x1 = x0 + 3;
+    if (x1 > x0 + 3) x1 = x0 + 3;  // never taken (see above): a guard on the table size
     if (y1 > y0 + 3) y1 = y0 + 3;
-    for (int64_t cy = y0; cy <= y1; ++cy)
-        for (int64_t cx = x0; cx <= x1; ++cx) {
-            const uint32_t b = hbucket(cx, cy, hg.mask);
-            const uint32_t a = off[b], e = off[b + 1];
-            for (uint32_t q = a + threadIdx.x; q < e; q += kBlock) {
-                const int32_t i = sorted[q];
-                const double2 p = apos[i];
-                if (hcell(p.x, hg.inv_cell) != cx || hcell(p.y, hg.inv_cell) != cy) continue;  // another cell
-                fn(i, p);
-            }
-        }
+    const int wx = int(x1 - x0 + 1), nc = wx * int(y1 - y0 + 1);
+    uint32_t len = 0;
+    if (lane < nc) {
+        const int64_t cx = x0 + lane % wx, cy = y0 + lane / wx;
+        const uint32_t b = hbucket(cx, cy, hg.mask);
+        const uint32_t a = off[b];
+        len = off[b + 1] - a;
+        w.a[lane] = a;
+        w.cx[lane] = cx;
+        w.cy[lane] = cy;
+    }
+    uint32_t incl = len;  // inclusive prefix of the lengths
+#pragma unroll
+    for (int o = 1; o < kMaxCells; o <<= 1) {
+        const uint32_t x = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += x;
+    }
+    if (lane < kMaxCells) w.pre[lane + 1] = incl;
+    if (lane == 0) {
+        w.pre[0] = 0;
+        w.ncell = nc;
+    }
+    __builtin_amdgcn_wave_barrier();
 }
 
 // ------------------------------------------------------------------------------ binned
+// One WAVE per task (4 tasks per workgroup): pass 1 evaluates the window's candidates, kWU per
+// lane with all their loads in flight, and keeps the claims in the wave's LDS list (ballot
+// slots, no atomics); pass 2 walks the record chain with wave-wide min-ID reductions.  A task is
+// latency-bound (dependent loads, then the chain), so the point is tasks in flight: 32 per CU.
+constexpr int kWCap = 512;  // claims per task kept in LDS (beyond: exact recompute path; C3 max ~350)
+constexpr int kWU = 4;      // candidates in flight per lane
+
+__device__ __forceinline__ int wave_min_int(int v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
+    return v;
+}
+
 __global__ __launch_bounds__(kBlock) void k_alloc_binned(
     int64_t t_count, const double2 *__restrict__ tpos, const int8_t *__restrict__ treq,
     const int32_t *__restrict__ ids, const double2 *__restrict__ apos,
     const uint32_t *__restrict__ caps, const int32_t *__restrict__ sorted_idx,
     const uint32_t *__restrict__ bucket_off, HashGrid hg, double rp, Params P) {
-    __shared__ int s_id[kCap];
-    __shared__ float s_x[kCap];
-    __shared__ int s_ix[kCap];
-    __shared__ int s_n, s_w0c, s_red[kBlock / kWave], s_sel_ix;
-    __shared__ float s_sel_x;
-    __shared__ long long s_red64[kBlock / kWave];
+    constexpr int kW = kBlock / kWave;
+    __shared__ int s_id[kW][kWCap];
+    __shared__ float s_x[kW][kWCap];
+    __shared__ int s_ix[kW][kWCap];
+    __shared__ CellWindow s_win[kW];
+    __shared__ long long s_red64[kW];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int *cid = s_id[wid], *cix = s_ix[wid];
+    float *cxv = s_x[wid];
+    CellWindow &w = s_win[wid];
+    const unsigned long long below = (1ull << lane) - 1ull;
     long long my_cand = 0, my_flag = 0;
     BlockStats bs;
-    for (int64_t k = blockIdx.x; k < t_count; k += gridDim.x) {
+    const int64_t nw = int64_t(gridDim.x) * kW;
+    for (int64_t k = int64_t(blockIdx.x) * kW + wid; k < t_count; k += nw) {
         const double2 tp = tpos[k];
         const int rq = treq[k];
         const int w0 = P.winner[k];
         const double u0 = P.util[k];
-        if (threadIdx.x == 0) { s_n = 0; s_w0c = 0; }
-        __syncthreads();
+        int nclaims = 0;
+        bool w0c = false;
+        uint32_t total = 0;
+        if (P.rp2 >= 0.0) {
+            window_setup(tp, rp, hg, bucket_off, w, lane);
+            total = w.pre[w.ncell];
+        }
         // pass 1: evaluate candidates, keep claims in LDS
-        if (P.rp2 >= 0.0)
-            for_candidates(tp, rp, hg, sorted_idx, bucket_off, apos, [&](int32_t i, double2 p) {
-                const double dx = p.x - tp.x, dy = p.y - tp.y;
-                if (dx * dx + dy * dy > P.rp2) return;
-                ++my_cand;
-                const double U = utility(p.x, p.y, caps[i], tp.x, tp.y, rq, P.u_scale);
-                my_flag += guard_flag(U, P.thr);
-                if (U > P.thr) {
-                    const int id = ids[i];
-                    const int slot = atomicAdd(&s_n, 1);
-                    if (slot < kCap) { s_id[slot] = id; s_x[slot] = float(U); s_ix[slot] = i; }
-                    if (id == w0) s_w0c = 1;
+        for (uint32_t q0 = 0; q0 < total; q0 += 64 * kWU) {
+            int32_t ii[kWU];
+            int jj[kWU];
+#pragma unroll
+            for (int u = 0; u < kWU; ++u) {
+                const uint32_t q = q0 + u * 64 + lane;
+                int j = 0;
+                while (j + 1 < w.ncell && w.pre[j + 1] <= q) ++j;
+                jj[u] = q < total ? j : -1;
+                ii[u] = sorted_idx[q < total ? w.a[j] + (q - w.pre[j]) : 0];
+            }
+            double2 p[kWU];
+            uint32_t cp[kWU];
+            int32_t idv[kWU];
+#pragma unroll
+            for (int u = 0; u < kWU; ++u) {
+                p[u] = apos[ii[u]];
+                cp[u] = caps[ii[u]];
+                idv[u] = ids[ii[u]];
+            }
+#pragma unroll
+            for (int u = 0; u < kWU; ++u) {
+                bool claim = false;
+                float x = 0.f;
+                const int j = jj[u];
+                if (j >= 0 && hcell(p[u].x, hg.inv_cell) == w.cx[j] && hcell(p[u].y, hg.inv_cell) == w.cy[j]) {
+                    const double dx = p[u].x - tp.x, dy = p[u].y - tp.y;
+                    if (dx * dx + dy * dy <= P.rp2) {
+                        ++my_cand;
+                        const double U = utility(p[u].x, p[u].y, cp[u], tp.x, tp.y, rq, P.u_scale);
+                        my_flag += guard_flag(U, P.thr);
+                        claim = U > P.thr;
+                        x = float(U);
+                    }
                 }
-            });
-        __syncthreads();
-        const int nclaims = s_n;
-        const bool overflow = nclaims > kCap;
+                const unsigned long long bm = __ballot(claim);
+                if (claim) {
+                    const int slot = nclaims + __popcll(bm & below);
+                    if (slot < kWCap) {
+                        cid[slot] = idv[u];
+                        cxv[slot] = x;
+                        cix[slot] = ii[u];
+                    }
+                }
+                w0c = w0c || __ballot(claim && idv[u] == w0) != 0ull;
+                nclaims += __popcll(bm);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        const bool overflow = nclaims > kWCap;
         // pass 2: the record chain
         int prev = -1, cur_id = w0, cur_idx = -1, accepted = 0, first_id = -1;
         bool has = w0 >= 0;
@@ -269,41 +335,58 @@ __global__ __launch_bounds__(kBlock) void k_alloc_binned(
             int best = INT_MAX, best_ix = -1;
             float best_x = 0.f;
             if (!overflow) {
-                for (int j = threadIdx.x; j < nclaims; j += kBlock) {
-                    const int id = s_id[j];
-                    if (id > prev && id < best && (!has || double(s_x[j]) > cur_u + P.h)) {
-                        best = id; best_x = s_x[j]; best_ix = s_ix[j];
+                for (int j = lane; j < nclaims; j += 64) {
+                    const int id = cid[j];
+                    if (id > prev && id < best && (!has || double(cxv[j]) > cur_u + P.h)) {
+                        best = id;
+                        best_x = cxv[j];
+                        best_ix = cix[j];
                     }
                 }
-            } else {  // exact recompute over the candidates (rare: > kCap claims on one task)
-                for_candidates(tp, rp, hg, sorted_idx, bucket_off, apos, [&](int32_t i, double2 p) {
-                    const double dx = p.x - tp.x, dy = p.y - tp.y;
-                    if (dx * dx + dy * dy > P.rp2) return;
-                    const double U = utility(p.x, p.y, caps[i], tp.x, tp.y, rq, P.u_scale);
+            } else {  // exact recompute over the candidates (rare: > kWCap claims on one task)
+                for (uint32_t q = lane; q < total; q += 64) {
+                    int j = 0;
+                    while (j + 1 < w.ncell && w.pre[j + 1] <= q) ++j;
+                    const int32_t i = sorted_idx[w.a[j] + (q - w.pre[j])];
+                    const double2 pp = apos[i];
+                    if (hcell(pp.x, hg.inv_cell) != w.cx[j] || hcell(pp.y, hg.inv_cell) != w.cy[j]) continue;
+                    const double dx = pp.x - tp.x, dy = pp.y - tp.y;
+                    if (dx * dx + dy * dy > P.rp2) continue;
+                    const double U = utility(pp.x, pp.y, caps[i], tp.x, tp.y, rq, P.u_scale);
                     const int id = ids[i];
                     if (U > P.thr && id > prev && id < best && (!has || double(float(U)) > cur_u + P.h)) {
-                        best = id; best_x = float(U); best_ix = i;
+                        best = id;
+                        best_x = float(U);
+                        best_ix = i;
                     }
-                });
+                }
             }
-            const int win = block_min_int(best, s_red);
+            const int win = wave_min_int(best);
             if (win == INT_MAX) break;
-            if (best == win) { s_sel_x = best_x; s_sel_ix = best_ix; }
-            __syncthreads();
-            cur_id = win; cur_u = double(s_sel_x); cur_idx = s_sel_ix; has = true; prev = win;
+            const int src = __ffsll((long long)__ballot(best == win)) - 1;
+            cur_u = double(__shfl(best_x, src, 64));
+            cur_idx = __shfl(best_ix, src, 64);
+            cur_id = win;
+            has = true;
+            prev = win;
             if (++accepted == 1) first_id = win;
         }
-        if (threadIdx.x == 0) {
-            finish_task(P, k, w0, u0, s_w0c != 0, accepted, first_id, cur_id, cur_u, cur_idx, nclaims, bs);
+        if (lane == 0) {
+            finish_task(P, k, w0, u0, w0c, accepted, first_id, cur_id, cur_u, cur_idx, nclaims, bs);
             bs.overflow += overflow ? 1 : 0;
             bs.bad += bad_req(rq) ? 1 : 0;
         }
-        __syncthreads();
+        __builtin_amdgcn_wave_barrier();  // the wave's window and claim list are reused
     }
     const long long c = block_sum_ll(my_cand, s_red64);
     const long long f = block_sum_ll(my_flag, s_red64);
+    const long long cl = block_sum_ll((long long)bs.claims, s_red64);
+    const long long ms = block_sum_ll((long long)bs.msgs, s_red64);
+    const long long ov = block_sum_ll((long long)bs.overflow, s_red64);
+    const long long bd = block_sum_ll((long long)bs.bad, s_red64);
     if (threadIdx.x == 0)
-        flush_stats(P, bs.claims, bs.msgs, (unsigned long long)f, (unsigned long long)c, bs.overflow, bs.bad);
+        flush_stats(P, (unsigned long long)cl, (unsigned long long)ms, (unsigned long long)f, (unsigned long long)c,
+                    (unsigned long long)ov, (unsigned long long)bd);
 }
 
 // ------------------------------------------------------------------------------- dense
@@ -547,7 +630,7 @@ int swarm_allocate(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *
         SW_ALLOC(off, ctx, S_CELL_START, 16);
         SW_HIP(hipMemsetAsync(off, 0, 16, s));
         P.rp2 = -1.0;
-        hipLaunchKernelGGL(k_alloc_binned, dim3(grid_for(t, 1, 4096)), dim3(kBlock), 0, s, t,
+        hipLaunchKernelGGL(k_alloc_binned, dim3(grid_for(t, kBlock / kWave, 4096)), dim3(kBlock), 0, s, t,
                            reinterpret_cast<const double2 *>(tpos), treq, ids,
                            reinterpret_cast<const double2 *>(apos), acaps, (const int32_t *)nullptr, off,
                            HashGrid{1.0, 0}, 0.0, P);
@@ -578,7 +661,7 @@ int swarm_allocate(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *
         hipLaunchKernelGGL(k_hash_scatter, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s, n, key, rank, off,
                            sorted);
         SW_LAUNCHED();
-        hipLaunchKernelGGL(k_alloc_binned, dim3(grid_for(t, 1, 4096)), dim3(kBlock), 0, s, t,
+        hipLaunchKernelGGL(k_alloc_binned, dim3(grid_for(t, kBlock / kWave, 4096)), dim3(kBlock), 0, s, t,
                            reinterpret_cast<const double2 *>(tpos), treq, ids,
                            reinterpret_cast<const double2 *>(apos), acaps, sorted, off, hg, rp, P);
         SW_LAUNCHED();

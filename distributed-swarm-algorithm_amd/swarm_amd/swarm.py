@@ -183,7 +183,7 @@ class Swarm:
         n = self.n
         rounds = ctypes.c_int32(0)
         cap = int(max_rounds)
-        changes = np.zeros(cap, np.int64)
+        changes = np.empty(cap, np.int64)  # libswarm writes rounds 1..rounds_exec
         st = _lib.ElectStats()
         hear = getattr(self, "_hear", None)
         with torch.cuda.device(self.device):
@@ -231,9 +231,10 @@ class Swarm:
              else _to(winner, torch.int32, dev).clone())
         u = (torch.zeros(t, dtype=torch.float64, device=dev) if util is None
              else _to(util, torch.float64, dev).clone())
-        won = torch.zeros(self.n, dtype=torch.int32, device=dev)
-        nclaim = torch.zeros(t, dtype=torch.int64, device=dev)
-        nmsg = torch.zeros(t, dtype=torch.int64, device=dev)
+        # libswarm zeroes won and writes nclaim / nmsg for every task
+        won = torch.empty(self.n, dtype=torch.int32, device=dev)
+        nclaim = torch.empty(t, dtype=torch.int64, device=dev)
+        nmsg = torch.empty(t, dtype=torch.int64, device=dev)
         idx = self.id_index()
         st = _lib.AllocStats()
         m = {"auto": _lib.ALLOC_AUTO, "binned": _lib.ALLOC_BINNED, "dense": _lib.ALLOC_DENSE}[mode]
