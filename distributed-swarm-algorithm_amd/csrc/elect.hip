@@ -89,6 +89,24 @@ __device__ __forceinline__ void bookkeeping(unsigned long long *ring, unsigned l
         *slot(ring, t + kRing / 2, i / kShards, i % kShards) = 0;
 }
 
+// The same in two halves, so that block 0 does not put a dependent load in front of its own
+// work: the shard loads are issued at kernel start, the sum published at the end.
+__device__ __forceinline__ unsigned long long bookkeeping_load(unsigned long long *ring, unsigned long long *tot,
+                                                               int t) {
+    return (blockIdx.x == 0 && tot && t > 1 && threadIdx.x < kWave) ? *slot(ring, t - 1, C_CHG, threadIdx.x) : 0ull;
+}
+__device__ __forceinline__ void bookkeeping_finish(unsigned long long *ring, unsigned long long *tot, int t,
+                                                   unsigned long long v) {
+    if (blockIdx.x != 0) return;
+    if (tot && t > 1 && threadIdx.x < kWave) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        if (threadIdx.x == 0) tot[(t - 1) % kRing] = v;
+    }
+    for (int i = threadIdx.x; i < kCounters * kShards; i += kBlock)
+        *slot(ring, t + kRing / 2, i / kShards, i % kShards) = 0;
+}
+
 #ifdef SWARM_PHASES  // debug build only: per-wave phase timestamps of the last launched round
 __device__ unsigned long long g_phase[8192 * 8];
 #define PHASE(k)                                                                         \
@@ -404,10 +422,13 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
 #ifdef SWARM_PHASES  // debug build: per-workgroup start/end clocks, marked agents (sum, max chunk)
     const unsigned long long ph_t0 = wall_clock64();
     long long ph_sum = 0, ph_max = 0;
+    unsigned long long ph_stamps = 0, ph_listed = 0, ph_gathered = 0;
 #endif
-    bookkeeping(f.ring, f.tot, t);
-    // single-GPU runs: round t-2 changed nothing => round t-1 had no marked agent => neither t
-    if (guard && t > 2 && f.tot[(t - 2) % kRing] == 0) return;
+    const unsigned long long bk = bookkeeping_load(f.ring, f.tot, t);
+    // single-GPU runs: round t-2 changed nothing => round t-1 had no marked agent => neither t.
+    // Loaded here, tested only once the first stamp words are in flight (no dependent load in
+    // front of the round's own chain).
+    const unsigned long long prev2 = (guard && t > 2) ? f.tot[(t - 2) % kRing] : 1ull;
     const int32_t *__restrict__ P = f.L[(t - 1) & 1];
     int32_t *__restrict__ Q = f.L[t & 1];
     uint8_t *ar = f.act[t & 1], *aw = f.act[(t + 1) & 1];
@@ -431,9 +452,12 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
         W wv[kPre];
 #pragma unroll
         for (int p = 0; p < kPre; ++p) {
-            const int64_t chunk = cg + p * NG < nchunks ? cg + p * NG : nchunks - 1;
+            // past the end: this thread's own first word again (a shared fallback address would
+            // put every workgroup's redundant loads on one L2 channel)
+            const int64_t chunk = cg + p * NG < nchunks ? cg + p * NG : cg;
             wv[p] = *reinterpret_cast<const W *>(ar + chunk * kChunk + j0);
         }
+        if (prev2 == 0) break;  // converged: nothing is marked
         unsigned masks = 0;
 #pragma unroll
         for (int p = 0; p < kPre; ++p) {
@@ -442,6 +466,9 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
                 masks |= take_stamps<S>(ar, chunk * kChunk + j0, stamp_agent(f.sm, chunk, j0), n, wv[p], stamp4)
                          << (p * S);
         }
+#ifdef SWARM_PHASES
+        if (!ph_stamps) ph_stamps = wall_clock64() + (masks & 0);
+#endif
         // append the group's marked agents, gathering whenever the list fills up
         for (;;) {
             const int cnt = __popc(masks);
@@ -480,16 +507,26 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
             __syncthreads();  // the list is reused
         }
     }
+#ifdef SWARM_PHASES
+    ph_listed = wall_clock64();
+#endif
     if (listed > 0)
         gather_listed<Off, G, K, DIR>(rp, col, hrp, hcol, P, Q, aw, f.wsm, sw, s_list, listed, wid * (64 / G),
                                       kBlock / G, f.n_count, my_chg, my_act, my_edges);
+#ifdef SWARM_PHASES
+    ph_gathered = wall_clock64() + (my_chg & 0);
+#endif
     flush_counts(f.ring, t, my_chg, my_act, my_edges, s_red);
+    bookkeeping_finish(f.ring, f.tot, t, bk);
 #ifdef SWARM_PHASES
     if (threadIdx.x == 0 && blockIdx.x < 8192) {
         g_phase[blockIdx.x * 8 + 0] = ph_t0;
         g_phase[blockIdx.x * 8 + 1] = wall_clock64();
         g_phase[blockIdx.x * 8 + 2] = (unsigned long long)ph_sum;
         g_phase[blockIdx.x * 8 + 3] = (unsigned long long)ph_max;
+        g_phase[blockIdx.x * 8 + 4] = ph_stamps;
+        g_phase[blockIdx.x * 8 + 5] = ph_listed;
+        g_phase[blockIdx.x * 8 + 6] = ph_gathered;
     }
 #endif
 }

@@ -31,5 +31,14 @@ for R in map(int, sys.argv[2:]):
     print(f"round {R}: wg dur us med {np.median(dur):.1f} p90 {np.percentile(dur, 90):.1f} max {dur.max():.1f}; "
           f"start spread {start.max():.1f} us; marked sum med {np.median(ph[:, 2]):.0f} max {ph[:, 2].max()}; "
           f"max chunk {ph[:, 3].max()}")
+    t0 = ph[:, 0].min()
+    ok = ph[:, 4] > 0
+    if not ok.any():
+        continue
+    rel = lambda c: (ph[ok, c] - ph[ok, 0]) * 0.01  # noqa: E731
+    print(f"   phases (from each wg's start, median / max): stamps in {np.median(rel(4)):.1f} / {rel(4).max():.1f}, "
+          f"list done {np.median(rel(5)):.1f} / {rel(5).max():.1f}, gathered {np.median(rel(6)):.1f} / "
+          f"{rel(6).max():.1f}, end {np.median(rel(1)):.1f} / {rel(1).max():.1f}; kernel span (first start -> last "
+          f"end) {(ph[:, 1].max() - t0) * 0.01:.1f} us")
     for w in order[:5]:
         print(f"   wg {w}: dur {dur[w]:.1f} us start {start[w]:.1f} marked {ph[w, 2]} max chunk {ph[w, 3]}")
