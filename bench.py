@@ -536,10 +536,21 @@ def sharded(args, rank, world, dev):
     dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+    cdev = dev if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t[0])
     total_agents = args.agents * world
+    check = sharded_state_check(sh, r)
+    # dominant kernel on every rank: k_sparse_block timed with HIP events over one instrumented
+    # election of this rank's shard graph (owned + ghost rows) -- the kernel the sharded loop
+    # launches every round, on the same graph; rank 0 reports its own, and the spread over ranks
+    dom = shard_roofline(sh, dev)
+    fr = torch.tensor([dom["frac"], -dom["frac"]], dtype=torch.float64, device=cdev)
+    dist.all_reduce(fr, op=dist.ReduceOp.MAX)
+    path = ("native RCCL loop (swarm_elect_sharded: ncclSend/ncclRecv halo + ncclAllReduce per batch)"
+            if getattr(sh, "_native", None) is not None else
+            f"torch.distributed {dist.get_backend()} halo" + (" (host-staged)" if sh.halo.host_staged else ""))
     if rank == 0:
         out = {
             "metric": "agent-rounds/sec (election+allocation) at 10M agents; % of HBM roofline",
@@ -559,12 +570,17 @@ def sharded(args, rank, world, dev):
                        "agents_total": total_agents, "tasks_total": args.tasks * world,
                        "rounds_exec": r.rounds_exec,
                        "halo_depth": sh.halo_depth,
-                       "parallelism": f"strip-sharded x{world}: RCCL halo P2P every {sh.halo_depth} rounds "
-                                      "(ghosts that deep, stepped locally) + one all-reduce per batch"},
+                       "parallelism": f"strip-sharded x{world}: {path}; halo exchanged every {sh.halo_depth} "
+                                      "rounds (ghosts that deep, stepped locally)"},
             "alloc_stats": a[2],
-            "roofline": None,
+            "result_check": check,
+            "roofline": dict(dom, frac_max_over_ranks=float(fr[0]), frac_min_over_ranks=-float(fr[1]),
+                             note="rank 0's k_sparse_block over its shard graph (owned + ghost rows), HIP events "
+                                  "on libswarm's stream, one instrumented election of that graph"),
             "cpu_baseline": None,
         }
+        if args.cpu_baseline:
+            out["cpu_baseline"] = shard_cpu_baseline(sh, tx, ty, tq)
     # C4 on N GPUs beside the headline: 100k agents split over the ranks, 100k tasks replicated,
     # the native sharded auction (one RCCL MAX all-reduce of the task keys per round)
     if args.rows:
@@ -574,6 +590,85 @@ def sharded(args, rank, world, dev):
     if rank == 0:
         print(json.dumps(out), flush=True)
     dist.destroy_process_group()
+
+
+def sharded_state_check(sh, r):
+    """End-to-end check of a sharded election on this rank: one more E2 round over the owned rows
+    of the shard graph changes nothing (their neighbours are owned agents or ghosts within one
+    radius of the border, which hold their owners' final leaders: ShardedSwarm._check_ghosts),
+    and state == LEADER iff leader == id.  Raises on failure."""
+    import torch
+    import torch.distributed as dist
+    from swarm_amd import _lib
+    L = sh.leaders[r.rounds_exec & 1]
+    lout = torch.empty_like(L)
+    changed = torch.zeros(1, dtype=torch.int64, device=L.device)
+    with torch.cuda.device(L.device):
+        _lib.check(_lib.lib().swarm_elect_round(_lib.ctx(), sh.n_own, _lib.ptr(sh.row_ptr), _lib.ptr(sh.col),
+                                                _lib.ptr(L), _lib.ptr(lout), _lib.ptr(changed), _lib.stream()))
+    ok = torch.tensor([int(changed.item() == 0 and torch.equal(lout[: sh.n_own], L[: sh.n_own])),
+                       int(torch.equal(r.state == _lib.LEADER, r.leader == sh.ids))], dtype=torch.int64,
+                      device=L.device if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    fixed_point, state_ok = bool(ok[0]), bool(ok[1])
+    assert fixed_point and state_ok, ("sharded election state is not a fixed point", fixed_point, state_ok)
+    return {"fixed_point_all_ranks": fixed_point, "state_consistent_all_ranks": state_ok,
+            "rounds_exec": r.rounds_exec, "converged": r.converged}
+
+
+def shard_roofline(sh, dev):
+    """k_sparse_block's algorithmic bytes per launch over its HIP-event time, from one instrumented
+    single-GPU election of this rank's shard graph (ELECT_TIMED)."""
+    import ctypes
+
+    import torch
+    from swarm_amd import _lib
+    n = sh.all_ids.numel()
+    lead = torch.empty(n, dtype=torch.int32, device=dev)
+    state = torch.empty(n, dtype=torch.uint8, device=dev)
+    rounds = ctypes.c_int32(0)
+    st = _lib.ElectStats()
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().swarm_elect(_lib.ctx(), n, _lib.ptr(sh.row_ptr), _lib.ptr(sh.col),
+                                          _lib.ptr(sh.all_ids), _lib.ptr(lead), _lib.ptr(state), 1 << 16,
+                                          _lib.ELECT_FRONTIER | _lib.ELECT_TIMED, ctypes.byref(rounds), None,
+                                          ctypes.byref(st), _lib.stream()))
+    torch.cuda.synchronize()
+    bpl = st.sparse_bytes / max(st.sparse_launches, 1)
+    ms = st.sparse_ms / max(st.sparse_launches, 1)
+    pmc = pmc_traffic("k_sparse_block<int, 8,")
+    ach = bpl / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    return {"kernel": "k_sparse_block (sparse E2 round: marked agents gather)", "bound": "hbm", "achieved": ach,
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": pmc[0] if pmc else None,
+            "traffic_source": pmc[1] if pmc else None, "bytes_per_launch": bpl, "avg_launch_ms": ms,
+            "launches": int(st.sparse_launches), "shard_rows": int(n), "shard_rounds": int(rounds.value)}
+
+
+def shard_cpu_baseline(sh, tx, ty, tq):
+    """Rank 0's share on the host: the oracle's frontier election over its shard graph (owned +
+    ghost rows, as one graph) and the binned allocation of its tasks over its owned agents, all
+    host threads -- the same per-GPU work as the N = 1 line's CPU sample."""
+    from oracle import oracle
+    threads = _threads()
+    oracle.set_threads(threads)
+    rp = sh.row_ptr.cpu().numpy().astype(np.int64)
+    col = sh.col.cpu().numpy()
+    ids = sh.all_ids.cpu().numpy()
+    t1 = time.perf_counter()
+    _, _, rounds, _ = oracle.elect_frontier(rp, col, ids)
+    t_el = time.perf_counter() - t1
+    pos = sh.pos.cpu().numpy()
+    t1 = time.perf_counter()
+    oracle.allocate_binned(sh.ids.cpu().numpy(), pos[:, 0].copy(), pos[:, 1].copy(),
+                           sh.caps.cpu().numpy().view(np.uint32), tx.cpu().numpy(), ty.cpu().numpy(),
+                           tq.cpu().numpy(), use_pow=False)
+    t_al = time.perf_counter() - t1
+    n = len(ids)
+    return {"value": n * rounds / (t_el + t_al), "unit": "agent-rounds/s", "cores": threads, "kind": "port",
+            "elect_s": t_el, "alloc_s": t_al,
+            "sample": f"rank 0's share on the host: C oracle orc_elect_frontier over its {n}-row shard graph "
+                      f"({rounds} rounds, {t_el:.2f} s) + orc_allocate_binned of its {tx.numel()} tasks "
+                      f"({t_al:.2f} s), {threads} threads"}
 
 
 def sharded_auction_row(args, rank, world, dev):

@@ -44,6 +44,59 @@ import torch
 import torch.distributed as dist
 
 
+@dataclass
+class Part:
+    """One rank's share of a global swarm (partition()): indices into the global arrays."""
+    rank: int
+    world: int
+    strip: tuple             # (y_lo, y_hi) of this rank's strip
+    cuts: np.ndarray         # the world - 1 interior strip boundaries (the same on every rank)
+    agents: np.ndarray       # int64 indices of the owned agents, ascending
+    tasks: np.ndarray        # int64 indices of the tasks this rank resolves, ascending
+
+
+def strip_cuts(y, world: int) -> np.ndarray:
+    """world - 1 horizontal cuts at the y-quantiles k / world: strips of (nearly) equal agent
+    counts.  Agent i belongs to strip searchsorted(cuts, y[i], 'right'): ties at a cut go up."""
+    y = np.asarray(y, np.float64)
+    if world <= 1 or len(y) == 0:
+        return np.zeros(0, np.float64)
+    ks = [(k * len(y)) // world for k in range(1, world)]
+    return np.partition(y, ks)[ks].astype(np.float64)
+
+
+def partition(x, y, world: int, rank: int, *, ty=None, min_height: float = 0.0) -> Part:
+    """Split ONE global swarm (every rank passes the same arrays) into `world` horizontal strips
+    of equal agent count; rank `rank` owns the agents of strip `rank` and the tasks whose y falls
+    in it (tasks outside the agents' y-range go to the first / last strip).
+
+    Why the strips reproduce the single-swarm results: every agent is owned by
+    exactly one rank, every RGG edge joins agents of the same or of adjacent strips when strips
+    are taller than the radio radius (ShardedSwarm checks), and ShardedSwarm's deep halo and
+    claim-radius halo give each rank every neighbour / claimant of its owned agents and tasks --
+    so elect() and allocate() equal Swarm.elect() / Swarm.allocate() on the union, whatever the
+    cut positions (tests/test_dist_gloo.py: one global swarm through partition())."""
+    if not 0 <= rank < world:
+        raise ValueError("rank out of range")
+    x = np.asarray(x, np.float64)
+    y = np.asarray(y, np.float64)
+    cuts = strip_cuts(y, world)
+    who = np.searchsorted(cuts, y, side="right")
+    agents = np.nonzero(who == rank)[0].astype(np.int64)
+    lo = float(y.min()) if len(y) else 0.0
+    hi = float(y.max()) if len(y) else 0.0
+    edges = np.concatenate([[lo], cuts, [hi]])
+    strip = (float(edges[rank]), float(edges[rank + 1]))
+    if world > 1 and np.diff(edges).min() <= min_height:
+        raise ValueError(f"strips of {world} equal agent counts are not taller than {min_height}: "
+                         "too few agents per rank for this radius")
+    tasks = np.zeros(0, np.int64)
+    if ty is not None:
+        tw = np.searchsorted(cuts, np.asarray(ty, np.float64), side="right")
+        tasks = np.nonzero(tw == rank)[0].astype(np.int64)
+    return Part(rank, world, strip, cuts, agents, tasks)
+
+
 def _neighbors(rank, world):
     return (rank - 1 if rank > 0 else None), (rank + 1 if rank < world - 1 else None)
 
@@ -335,6 +388,30 @@ class ShardedSwarm:
         self.row_ptr, self.col = self.backend.build_graph(self.all_pos, self.radius)
         self.leaders = (torch.empty(self.all_ids.numel(), dtype=torch.int32, device=dev),
                         torch.empty(self.all_ids.numel(), dtype=torch.int32, device=dev))
+
+    @classmethod
+    def from_global(cls, ids, x, y, caps=None, *, ty=None, radius: float = 1.0, group=None, device=None,
+                    backend=None, halo=None, halo_depth: int | None = None):
+        """This rank's shard of ONE global swarm (every rank passes the same arrays): strips of
+        equal agent count (partition()).  self.part holds the global indices of the owned agents
+        and of the tasks this rank resolves (allocate_global)."""
+        if halo is not None:
+            rank, world = halo.rank, halo.world
+        else:
+            rank, world = dist.get_rank(group), dist.get_world_size(group)
+        part = partition(x, y, world, rank, ty=ty, min_height=radius)
+        a = part.agents
+        caps_a = None if caps is None else np.asarray(caps)[a]
+        sh = cls(np.asarray(ids)[a], np.asarray(x)[a], np.asarray(y)[a], caps_a, part.strip, radius=radius,
+                 group=group, device=device, backend=backend, halo=halo, halo_depth=halo_depth)
+        sh.part = part
+        return sh
+
+    def allocate_global(self, tx, ty, treq, **kw):
+        """allocate() over this rank's share (self.part.tasks) of a GLOBAL task list; the result
+        rows are those tasks, in ascending global index."""
+        k = self.part.tasks
+        return self.allocate(np.asarray(tx)[k], np.asarray(ty)[k], np.asarray(treq)[k], **kw)
 
     def _agree_depth(self, want):
         """Halo depth k, the same on every rank: the requested depth (SWARM_HALO_DEPTH, default 16)

@@ -80,6 +80,8 @@ class NumpyBackend:
         out.winner = torch.as_tensor(r["winner"])
         out.util = torch.as_tensor(r["util"])
         out.won = torch.as_tensor(r["won"])
+        out.nmsg = torch.as_tensor(r["nmsg"])
+        out.nclaim = torch.as_tensor(r["nclaim"])
         out.stats = dict(n_claims=r["n_claims"], n_conflicts=r["n_conflicts"], n_flagged=0,
                          n_candidates=len(ids) * len(tx), n_overflow=0)
         return out

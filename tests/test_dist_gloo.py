@@ -166,3 +166,87 @@ def test_sharded_auction_matches_single_auction(world, check_every, oracle_mod):
         np.testing.assert_array_equal(o["owner"], owner_id)
         np.testing.assert_array_equal(o["price"], want["price"])
         assert all(by_id[int(i)] == int(a) for i, a in zip(o["ids"], o["assigned"]))
+
+
+# ------------------------------------------------------------------ one global swarm, partitioned
+G_N, G_T = 4000, 150
+
+
+def _global_worker(rank, world, port, out_q, depth):
+    import sys
+    for p in (PKG, ROOT, os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from shard_doubles import NumpyBackend
+        from swarm_amd import gen
+        from swarm_amd.dist import ShardedSwarm
+        d = gen.swarm_inputs(G_N, SEED + 3, t=G_T)  # the same global arrays on every rank
+        sh = ShardedSwarm.from_global(d["ids"], d["x"], d["y"], d["caps"], ty=d["ty"], device="cpu",
+                                      backend=NumpyBackend(), halo_depth=depth)
+        r = sh.elect(check_every=5)
+        res, won, gst = sh.allocate_global(d["tx"], d["ty"], d["treq"])
+        out_q.put(dict(rank=rank, rounds=r.rounds_exec, changes=r.changes, ids=sh.ids.numpy(),
+                       leader=r.leader.numpy(), tasks=sh.part.tasks, agents=sh.part.agents,
+                       winner=res.winner.numpy(), util=res.util.numpy(), nmsg=res.nmsg.numpy(),
+                       won=won.numpy(), gstats=gst))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,depth", [(2, 4), (3, 16)])
+def test_partitioned_global_swarm_matches_single_swarm(world, depth, oracle_mod):
+    """ShardedSwarm.from_global: one global input (random IDs, tasks anywhere) cut into strips of
+    equal agent count on every rank; the union of the shards' results equals the single-swarm
+    oracle (leaders, rounds, per-round changes, winners, claim values, conflicts, won counts)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_global_worker, args=(r, world, port, q, depth)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=240) for _ in range(world)], key=lambda o: o["rank"])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from swarm_amd import gen
+    d = gen.swarm_inputs(G_N, SEED + 3, t=G_T)
+    # every agent and every task owned exactly once, strips of near-equal size
+    agents = np.concatenate([o["agents"] for o in outs])
+    assert np.array_equal(np.sort(agents), np.arange(G_N))
+    assert max(len(o["agents"]) for o in outs) - min(len(o["agents"]) for o in outs) <= 2
+    tasks = np.concatenate([o["tasks"] for o in outs])
+    assert np.array_equal(np.sort(tasks), np.arange(G_T))
+    rp, col = oracle_mod.rgg_csr(d["x"], d["y"], 1.0)
+    lead, _, rounds, changes = oracle_mod.elect(rp, col, d["ids"])
+    want = dict(zip(d["ids"].tolist(), lead.tolist()))
+    for o in outs:
+        assert o["rounds"] == rounds
+        np.testing.assert_array_equal(o["changes"], changes)
+        assert all(want[int(i)] == int(v) for i, v in zip(o["ids"], o["leader"]))
+    wa = oracle_mod.allocate(d["ids"], d["x"], d["y"], d["caps"], d["tx"], d["ty"], d["treq"])
+    for key in ("winner", "util", "nmsg"):
+        got = np.empty_like(wa[key])
+        for o in outs:
+            got[o["tasks"]] = o[key]
+        np.testing.assert_array_equal(got, wa[key])
+    won_want = dict(zip(d["ids"].tolist(), wa["won"].tolist()))
+    for o in outs:
+        assert all(won_want[int(i)] == int(w) for i, w in zip(o["ids"], o["won"]))
+        assert o["gstats"]["n_claims"] == wa["n_claims"]
+
+
+def test_partition_cuts():
+    from swarm_amd.dist import partition, strip_cuts
+    g = np.random.default_rng(0)
+    y = g.uniform(0, 100, 10_001)
+    cuts = strip_cuts(y, 4)
+    parts = [partition(np.zeros_like(y), y, 4, r, ty=y[:50]) for r in range(4)]
+    assert np.array_equal(np.sort(np.concatenate([p.agents for p in parts])), np.arange(len(y)))
+    assert [len(p.agents) for p in parts] == [2500, 2500, 2500, 2501]
+    assert all(np.array_equal(p.cuts, cuts) for p in parts)
+    for p in parts:  # owned agents lie inside the strip
+        assert (y[p.agents] >= p.strip[0]).all() and (y[p.agents] <= p.strip[1]).all()
+    with pytest.raises(ValueError):
+        partition(np.zeros(8), np.arange(8.0), 4, 0, min_height=5.0)
