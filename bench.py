@@ -145,16 +145,20 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         elapsed, agent_rounds = float(mx[0]), float(t[1])
 
-    # ---- split timing of one step (untimed replay): election vs allocation
-    torch.cuda.synchronize()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-    ev[0].record()
-    r = sw.elect(mode=args.elect_mode, max_rounds=1 << 16)
-    ev[1].record()
-    a = sw.allocate(tpos_x, tpos_y, treq)
-    ev[2].record()
-    torch.cuda.synchronize()
-    t_elect_ms, t_alloc_ms = ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])
+    # ---- split timing of a step (untimed replays, median of 3): election vs allocation
+    splits = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        ev[0].record()
+        r = sw.elect(mode=args.elect_mode, max_rounds=1 << 16)
+        ev[1].record()
+        a = sw.allocate(tpos_x, tpos_y, treq)
+        ev[2].record()
+        torch.cuda.synchronize()
+        splits.append((ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])))
+    t_elect_ms = float(np.median([x[0] for x in splits]))
+    t_alloc_ms = float(np.median([x[1] for x in splits]))
 
     # ---- per-kernel device time of the election (HIP events recorded by libswarm around every
     # launch on the stream it launches on), one instrumented replay.  The dominant kernel is the

@@ -28,6 +28,7 @@
 #include "utility.h"
 
 #include <climits>
+#include <cstring>
 
 namespace swarm {
 namespace {
@@ -64,7 +65,9 @@ constexpr int kStatStride = 16;
 struct BlockStats {
     unsigned long long claims = 0, msgs = 0, overflow = 0, bad = 0;
 };
-constexpr int kNumStats = 7;  // + [6]: agents with a non-finite position (binned mode)
+// + [6]: agents with a non-finite position (hashed binning), [7]: agents outside their cell's range
+// (swarm_allocate_indexed: the index is stale)
+constexpr int kNumStats = 8;
 
 __device__ __forceinline__ void flush_stats(const Params &P, unsigned long long claims, unsigned long long msgs,
                                             unsigned long long flagged, unsigned long long cand,
@@ -231,6 +234,54 @@ __device__ __forceinline__ void window_setup(double2 tp, double rp, const HashGr
     __builtin_amdgcn_wave_barrier();
 }
 
+// The same window over a caller's cell index (swarm_cell_index: agents stored in row-major cell
+// order, cell side <= the claim radius allows): one entry per grid ROW the window covers, the
+// contiguous storage range of its cells x0..x1 -- no binning pass, no per-candidate cell test.
+__device__ __forceinline__ void window_setup_rows(double2 tp, double rp, const Grid &g,
+                                                  const uint32_t *__restrict__ off, CellWindow &w, int lane) {
+    const bool miss = tp.x + rp < g.xmin || tp.x - rp > g.xmax || tp.y + rp < g.ymin || tp.y - rp > g.ymax;
+    const int64_t x0 = cell_coord(tp.x - rp, g.xmin, g.inv_cell, g.ncx);
+    const int64_t x1 = cell_coord(tp.x + rp, g.xmin, g.inv_cell, g.ncx);
+    const int64_t y0 = cell_coord(tp.y - rp, g.ymin, g.inv_cell, g.ncy);
+    int64_t y1 = cell_coord(tp.y + rp, g.ymin, g.inv_cell, g.ncy);
+    if (y1 > y0 + kMaxCells - 1) y1 = y0 + kMaxCells - 1;  // the host checks rows <= kMaxCells
+    const int nc = miss ? 0 : int(y1 - y0 + 1);
+    uint32_t len = 0;
+    if (lane < nc) {
+        const int64_t row = (y0 + lane) * g.ncx;
+        const uint32_t a = off[row + x0];
+        len = off[row + x1 + 1] - a;
+        w.a[lane] = a;
+    }
+    uint32_t incl = len;
+#pragma unroll
+    for (int o = 1; o < kMaxCells; o <<= 1) {
+        const uint32_t x = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += x;
+    }
+    if (lane < kMaxCells) w.pre[lane + 1] = incl;
+    if (lane == 0) {
+        w.pre[0] = 0;
+        w.ncell = nc;
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Staleness test of a cell index: every agent must lie in its cell's range.
+__global__ __launch_bounds__(kBlock) void k_check_index(const double2 *__restrict__ apos, int64_t n, Grid g,
+                                                       const uint32_t *__restrict__ off,
+                                                       unsigned long long *__restrict__ bad_out) {
+    unsigned long long bad = 0;
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+        const double2 p = apos[i];
+        const int64_t c = cell_coord(p.y, g.ymin, g.inv_cell, g.ncy) * g.ncx + cell_coord(p.x, g.xmin, g.inv_cell, g.ncx);
+        bad += (isfinite(p.x) && isfinite(p.y) && off[c] <= uint32_t(i) && uint32_t(i) < off[c + 1]) ? 0 : 1;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) bad += __shfl_xor(bad, o, 64);
+    if ((threadIdx.x & 63) == 0 && bad) atomicAdd(bad_out, bad);
+}
+
 // ------------------------------------------------------------------------------ binned
 // One WAVE per task (4 tasks per workgroup): pass 1 evaluates the window's candidates, kWU per
 // lane with all their loads in flight, and keeps the claims in the wave's LDS list (ballot
@@ -245,11 +296,14 @@ __device__ __forceinline__ int wave_min_int(int v) {
     return v;
 }
 
+// HASH: candidates from the hashed buckets (sorted_idx, bucket_off, hg); otherwise from a cell
+// index over the storage order (bucket_off = cell_off, grid g; sorted_idx unused).
+template <bool HASH>
 __global__ __launch_bounds__(kBlock) void k_alloc_binned(
     int64_t t_count, const double2 *__restrict__ tpos, const int8_t *__restrict__ treq,
     const int32_t *__restrict__ ids, const double2 *__restrict__ apos,
     const uint32_t *__restrict__ caps, const int32_t *__restrict__ sorted_idx,
-    const uint32_t *__restrict__ bucket_off, HashGrid hg, double rp, Params P) {
+    const uint32_t *__restrict__ bucket_off, HashGrid hg, Grid g, double rp, Params P) {
     constexpr int kW = kBlock / kWave;
     __shared__ int s_id[kW][kWCap];
     __shared__ float s_x[kW][kWCap];
@@ -273,7 +327,10 @@ __global__ __launch_bounds__(kBlock) void k_alloc_binned(
         bool w0c = false;
         uint32_t total = 0;
         if (P.rp2 >= 0.0) {
-            window_setup(tp, rp, hg, bucket_off, w, lane);
+            if (HASH)
+                window_setup(tp, rp, hg, bucket_off, w, lane);
+            else
+                window_setup_rows(tp, rp, g, bucket_off, w, lane);
             total = w.pre[w.ncell];
         }
         // pass 1: evaluate candidates, keep claims in LDS
@@ -286,7 +343,8 @@ __global__ __launch_bounds__(kBlock) void k_alloc_binned(
                 int j = 0;
                 while (j + 1 < w.ncell && w.pre[j + 1] <= q) ++j;
                 jj[u] = q < total ? j : -1;
-                ii[u] = sorted_idx[q < total ? w.a[j] + (q - w.pre[j]) : 0];
+                const uint32_t e = q < total ? w.a[j] + (q - w.pre[j]) : 0;
+                ii[u] = HASH ? sorted_idx[e] : int32_t(e);
             }
             double2 p[kWU];
             uint32_t cp[kWU];
@@ -302,7 +360,8 @@ __global__ __launch_bounds__(kBlock) void k_alloc_binned(
                 bool claim = false;
                 float x = 0.f;
                 const int j = jj[u];
-                if (j >= 0 && hcell(p[u].x, hg.inv_cell) == w.cx[j] && hcell(p[u].y, hg.inv_cell) == w.cy[j]) {
+                if (j >= 0 && (!HASH || (hcell(p[u].x, hg.inv_cell) == w.cx[j] &&
+                                         hcell(p[u].y, hg.inv_cell) == w.cy[j]))) {
                     const double dx = p[u].x - tp.x, dy = p[u].y - tp.y;
                     if (dx * dx + dy * dy <= P.rp2) {
                         ++my_cand;
@@ -347,9 +406,11 @@ __global__ __launch_bounds__(kBlock) void k_alloc_binned(
                 for (uint32_t q = lane; q < total; q += 64) {
                     int j = 0;
                     while (j + 1 < w.ncell && w.pre[j + 1] <= q) ++j;
-                    const int32_t i = sorted_idx[w.a[j] + (q - w.pre[j])];
+                    const uint32_t e = w.a[j] + (q - w.pre[j]);
+                    const int32_t i = HASH ? sorted_idx[e] : int32_t(e);
                     const double2 pp = apos[i];
-                    if (hcell(pp.x, hg.inv_cell) != w.cx[j] || hcell(pp.y, hg.inv_cell) != w.cy[j]) continue;
+                    if (HASH && (hcell(pp.x, hg.inv_cell) != w.cx[j] || hcell(pp.y, hg.inv_cell) != w.cy[j]))
+                        continue;
                     const double dx = pp.x - tp.x, dy = pp.y - tp.y;
                     if (dx * dx + dy * dy > P.rp2) continue;
                     const double U = utility(pp.x, pp.y, caps[i], tp.x, tp.y, rq, P.u_scale);
@@ -585,17 +646,14 @@ __global__ __launch_bounds__(kBlock) void k_utility(int64_t m, const double2 *__
 }
 
 }  // namespace
-}  // namespace swarm
+static_assert(sizeof(swarm_grid) == sizeof(Grid), "swarm_grid mirrors the internal Grid");
 
-extern "C" {
-
-int swarm_allocate(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos,
-                   const uint32_t *acaps, int64_t t, const double *tpos, const int8_t *treq,
-                   double claim_thr, double hysteresis, double u_scale, int32_t mode,
-                   int32_t *winner, double *util, int32_t *won, const int32_t *id_to_index,
-                   int64_t id_span, int64_t *nclaim, int64_t *nmsg, swarm_alloc_stats *stats,
-                   void *stream) {
-    using namespace swarm;
+// ix / ix_off: a cell index (swarm_cell_index) of the agents' storage order, or NULL.
+int alloc_impl(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos, const uint32_t *acaps,
+               int64_t t, const double *tpos, const int8_t *treq, double claim_thr, double hysteresis,
+               double u_scale, int32_t mode, int32_t *winner, double *util, int32_t *won,
+               const int32_t *id_to_index, int64_t id_span, int64_t *nclaim, int64_t *nmsg,
+               swarm_alloc_stats *stats, void *stream, const Grid *ix, const uint32_t *ix_off) {
     SW_ARG(ctx != nullptr, "ctx is NULL");
     SW_ARG(n >= 0 && n < (int64_t(1) << 31), "n out of range");
     SW_ARG(t >= 0 && t < (int64_t(1) << 31), "t out of range");
@@ -630,10 +688,24 @@ int swarm_allocate(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *
         SW_ALLOC(off, ctx, S_CELL_START, 16);
         SW_HIP(hipMemsetAsync(off, 0, 16, s));
         P.rp2 = -1.0;
-        hipLaunchKernelGGL(k_alloc_binned, dim3(grid_for(t, kBlock / kWave, 4096)), dim3(kBlock), 0, s, t,
+        hipLaunchKernelGGL(k_alloc_binned<true>, dim3(grid_for(t, kBlock / kWave, 4096)), dim3(kBlock), 0, s, t,
                            reinterpret_cast<const double2 *>(tpos), treq, ids,
                            reinterpret_cast<const double2 *>(apos), acaps, (const int32_t *)nullptr, off,
-                           HashGrid{1.0, 0}, 0.0, P);
+                           HashGrid{1.0, 0}, Grid{}, 0.0, P);
+        SW_LAUNCHED();
+    } else if (t > 0 && used == SWARM_ALLOC_BINNED && ix) {
+        // the caller's cell index: the window's grid rows are contiguous storage ranges
+        const double rp = rc * (1.0 + 1e-9) + 1e-12;
+        P.rp2 = rp * rp;
+        SW_ARG(std::floor(2.0 * rp * ix->inv_cell) + 2.0 <= double(kMaxCells),
+               "claim radius spans more than 16 rows of the index's cells (use swarm_allocate)");
+        hipLaunchKernelGGL(k_check_index, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s,
+                           reinterpret_cast<const double2 *>(apos), n, *ix, ix_off, dstats + 7);
+        SW_LAUNCHED();
+        hipLaunchKernelGGL(k_alloc_binned<false>, dim3(grid_for(t, kBlock / kWave, 4096)), dim3(kBlock), 0, s, t,
+                           reinterpret_cast<const double2 *>(tpos), treq, ids,
+                           reinterpret_cast<const double2 *>(apos), acaps, (const int32_t *)nullptr, ix_off,
+                           HashGrid{1.0, 0}, *ix, rp, P);
         SW_LAUNCHED();
     } else if (t > 0 && used == SWARM_ALLOC_BINNED) {
         // agents bucketed by hashed cell of side Rp (counting sort, no host round trip)
@@ -661,9 +733,9 @@ int swarm_allocate(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *
         hipLaunchKernelGGL(k_hash_scatter, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s, n, key, rank, off,
                            sorted);
         SW_LAUNCHED();
-        hipLaunchKernelGGL(k_alloc_binned, dim3(grid_for(t, kBlock / kWave, 4096)), dim3(kBlock), 0, s, t,
+        hipLaunchKernelGGL(k_alloc_binned<true>, dim3(grid_for(t, kBlock / kWave, 4096)), dim3(kBlock), 0, s, t,
                            reinterpret_cast<const double2 *>(tpos), treq, ids,
-                           reinterpret_cast<const double2 *>(apos), acaps, sorted, off, hg, rp, P);
+                           reinterpret_cast<const double2 *>(apos), acaps, sorted, off, hg, Grid{}, rp, P);
         SW_LAUNCHED();
     } else if (t > 0) {
         P.rp2 = 0;
@@ -703,6 +775,11 @@ int swarm_allocate(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *
     SW_LAUNCHED();
     SW_HIP(hipMemcpyAsync(hs, folded, 8 * kNumStats, hipMemcpyDeviceToHost, s));
     SW_HIP(hipStreamSynchronize(s));
+    if (hs[7]) {
+        set_error("stale cell index: %llu agent(s) outside their cell's range (positions moved since "
+                  "swarm_cell_index)", (unsigned long long)hs[7]);
+        return SWARM_ERR_STALE;
+    }
     if (hs[6]) {
         set_error("invalid argument: %llu agent position(s) are not finite", (unsigned long long)hs[6]);
         return SWARM_ERR_ARG;
@@ -720,6 +797,84 @@ int swarm_allocate(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *
         stats->mode_used = used;
     }
     return SWARM_OK;
+}
+
+// keys[i] < keys[i-1] anywhere -> *bad += 1 per such i
+__global__ __launch_bounds__(kBlock) void k_count_unsorted(const uint32_t *__restrict__ keys, int64_t n,
+                                                          unsigned long long *__restrict__ bad_out) {
+    unsigned long long bad = 0;
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x + 1; i < n; i += int64_t(gridDim.x) * kBlock)
+        bad += keys[i] < keys[i - 1] ? 1 : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) bad += __shfl_xor(bad, o, 64);
+    if ((threadIdx.x & 63) == 0 && bad) atomicAdd(bad_out, bad);
+}
+
+}  // namespace swarm
+
+extern "C" {
+
+int swarm_allocate(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos,
+                   const uint32_t *acaps, int64_t t, const double *tpos, const int8_t *treq,
+                   double claim_thr, double hysteresis, double u_scale, int32_t mode,
+                   int32_t *winner, double *util, int32_t *won, const int32_t *id_to_index,
+                   int64_t id_span, int64_t *nclaim, int64_t *nmsg, swarm_alloc_stats *stats,
+                   void *stream) {
+    return swarm::alloc_impl(ctx, n, ids, apos, acaps, t, tpos, treq, claim_thr, hysteresis, u_scale, mode, winner,
+                             util, won, id_to_index, id_span, nclaim, nmsg, stats, stream, nullptr, nullptr);
+}
+
+int swarm_cell_index(swarm_ctx *ctx, int64_t n, const double *pos, double cell, swarm_grid *grid,
+                     uint32_t *cell_off, int64_t cell_off_capacity, int64_t *ncells, void *stream) {
+    using namespace swarm;
+    SW_ARG(ctx != nullptr && grid != nullptr && ncells != nullptr, "NULL argument");
+    SW_ARG(n >= 1 && n < (int64_t(1) << 31), "n out of range (need at least one agent)");
+    SW_ARG(cell > 0 && std::isfinite(cell), "cell must be positive and finite");
+    SW_ARG(pos != nullptr, "NULL array");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    Grid g;
+    int rc = make_grid(ctx, n, pos, cell, 4 * n + 1024, &g, s);  // swarm_cell_order's grid
+    if (rc) return rc;
+    memcpy(grid, &g, sizeof(g));
+    *ncells = g.ncx * g.ncy;
+    if (cell_off == nullptr) return SWARM_OK;
+    SW_ARG(cell_off_capacity >= *ncells + 1, "cell_off capacity < ncells + 1");
+    uint32_t *keys;
+    int32_t *vals;
+    unsigned long long *bad;
+    SW_ALLOC(keys, ctx, S_KEYS_IN, size_t(n) * 4);
+    SW_ALLOC(vals, ctx, S_VALS_IN, size_t(n) * 4);
+    SW_ALLOC(bad, ctx, S_TMP0, 8);
+    SW_HIP(hipMemsetAsync(bad, 0, 8, s));
+    hipLaunchKernelGGL(k_cell_keys, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s,
+                       reinterpret_cast<const double2 *>(pos), n, g, keys, vals);
+    SW_LAUNCHED();
+    hipLaunchKernelGGL(k_count_unsorted, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s, keys, n, bad);
+    SW_LAUNCHED();
+    hipLaunchKernelGGL(k_cell_offsets, dim3(grid_for(n + 1, kBlock, 8192)), dim3(kBlock), 0, s, keys, n, *ncells,
+                       cell_off);
+    SW_LAUNCHED();
+    unsigned long long *hb = static_cast<unsigned long long *>(pinned(ctx, 64));
+    if (!hb) return SWARM_ERR_OOM;
+    SW_HIP(hipMemcpyAsync(hb, bad, 8, hipMemcpyDeviceToHost, s));
+    SW_HIP(hipStreamSynchronize(s));
+    SW_ARG(hb[0] == 0, "positions are not in cell order (swarm_cell_order's layout with this cell)");
+    return SWARM_OK;
+}
+
+int swarm_allocate_indexed(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos,
+                           const uint32_t *acaps, const swarm_grid *grid, const uint32_t *cell_off, int64_t t,
+                           const double *tpos, const int8_t *treq, double claim_thr, double hysteresis,
+                           double u_scale, int32_t *winner, double *util, int32_t *won,
+                           const int32_t *id_to_index, int64_t id_span, int64_t *nclaim, int64_t *nmsg,
+                           swarm_alloc_stats *stats, void *stream) {
+    using namespace swarm;
+    SW_ARG(grid != nullptr && cell_off != nullptr, "NULL index");
+    SW_ARG(grid->ncx >= 1 && grid->ncy >= 1 && grid->inv_cell > 0, "bad grid");
+    Grid g;
+    memcpy(&g, grid, sizeof(g));
+    return alloc_impl(ctx, n, ids, apos, acaps, t, tpos, treq, claim_thr, hysteresis, u_scale, SWARM_ALLOC_BINNED,
+                      winner, util, won, id_to_index, id_span, nclaim, nmsg, stats, stream, &g, cell_off);
 }
 
 int swarm_utility(swarm_ctx *ctx, int64_t m, const double *apos, const uint32_t *acaps,

@@ -141,9 +141,10 @@ inline int next_round_batch(const int64_t *hist, size_t nh, int batch, int max_b
     if (nh >= k && !doubling_only) {
         const double slope = double(hist[nh - k] - hist[nh - 1]) / double(k - 1);
         if (slope > 0) {
-            const double rem = 1.5 * double(hist[nh - 1]) / slope;
-            int p = 8;
-            while (p < rem && p < max_batch) p <<= 1;
+            // rounds left on the linear trend, + 25 % and 4 rounds of margin: an overshoot costs one
+            // no-op launch per round (~6 µs), an undershoot one more host round trip
+            const double rem = 1.25 * double(hist[nh - 1]) / slope + 4.0;
+            const int p = rem < 8.0 ? 8 : (rem > double(max_batch) ? max_batch : int(rem + 0.5));
             if (p < b) b = p;
         }
     }

@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libswarm.so")
 
 OK, NOT_CONVERGED = 0, 1
-ERR_ARG, ERR_HIP, ERR_OOM, ERR_RANGE = -1, -2, -3, -4
+ERR_ARG, ERR_HIP, ERR_OOM, ERR_RANGE, ERR_STALE = -1, -2, -3, -4, -5
 FOLLOWER, ELECTION_WAIT, LEADER = 1, 2, 3
 ELECT_DENSE, ELECT_FRONTIER, ELECT_TIMED = 0, 1, 0x100
 ALLOC_AUTO, ALLOC_BINNED, ALLOC_DENSE = 0, 1, 2
@@ -30,7 +30,8 @@ EXPORTS = ("swarm_last_error", "swarm_version", "swarm_ctx_create", "swarm_ctx_d
            "swarm_comm_available", "swarm_comm_unique_id", "swarm_comm_create", "swarm_comm_destroy",
            "swarm_elect_sharded", "swarm_auction", "swarm_physics_step", "swarm_codec_encode",
            "swarm_codec_decode", "swarm_protocol_run", "swarm_auction_begin",
-           "swarm_auction_bid", "swarm_auction_resolve", "swarm_auction_sharded")
+           "swarm_auction_bid", "swarm_auction_resolve", "swarm_auction_sharded", "swarm_cell_index",
+           "swarm_allocate_indexed")
 
 
 class SwarmError(RuntimeError):
@@ -63,6 +64,11 @@ class AuctionStats(ctypes.Structure):
     _fields_ = [("n_pairs", ctypes.c_int64), ("n_flagged", ctypes.c_int64),
                 ("rounds_launched", ctypes.c_int64), ("tail_rounds", ctypes.c_int64),
                 ("bids_total", ctypes.c_int64)]
+
+
+class Grid(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_double) for k in ("xmin", "ymin", "xmax", "ymax", "cell", "inv_cell")] + \
+               [("ncx", ctypes.c_int64), ("ncy", ctypes.c_int64)]
 
 
 class Shard(ctypes.Structure):
@@ -102,6 +108,9 @@ def load(path: str = LIB_PATH):
         L.swarm_allocate.argtypes = [P, i64, P, P, P, i64, P, P, d, d, d, i32, P, P, P, P, i64,
                                      P, P, P, P]
         L.swarm_utility.argtypes = [P, i64, P, P, P, P, d, P, P]
+        L.swarm_cell_index.argtypes = [P, i64, P, d, ctypes.POINTER(Grid), P, i64, ctypes.POINTER(i64), P]
+        L.swarm_allocate_indexed.argtypes = [P, i64, P, P, P, ctypes.POINTER(Grid), P, i64, P, P, d, d, d, P, P, P,
+                                             P, i64, P, P, P, P]
         L.swarm_build_rgg.argtypes = [P, i64, P, d, P, P, i64, ctypes.POINTER(i64), P]
         L.swarm_cell_order.argtypes = [P, i64, P, d, P, P]
         L.swarm_frontier_begin.argtypes = [P, i64, i64, P, P, P, P]

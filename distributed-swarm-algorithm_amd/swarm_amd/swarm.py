@@ -110,6 +110,8 @@ class Swarm:
         else:
             raise ValueError(f"unknown layout {layout!r}")
         self.layout = layout
+        self.cell = float(cell)
+        self._cindex = None  # (Grid, cell_off): cell index of the spatial storage order, built lazily
         self.ids, self.pos, self.caps = ids_t, pos, caps_t
         if n and int(ids_t.min()) < 0:
             raise ValueError("agent IDs must be non-negative")
@@ -220,6 +222,27 @@ class Swarm:
                 self._id_index = t
         return self._id_index
 
+    def _indexable(self, mode, claim_thr, u_scale) -> bool:
+        """The binned round can use the storage order's cell index: spatial layout, a finite claim
+        radius spanning <= 16 index rows (else swarm_allocate bins by hashed cells)."""
+        if self.layout != "spatial" or self.n < 2 or mode == "dense" or not (claim_thr > 0 and u_scale > 0):
+            return False
+        rp = (u_scale / claim_thr - 1.0) * (1 + 1e-9) + 1e-12
+        return rp > 0 and np.floor(2.0 * rp / self.cell) + 2 <= 16  # index cells are >= self.cell
+
+    def _cell_index(self):
+        """(Grid, cell_off) of the storage order (swarm_cell_index), built once; the allocation
+        verifies it on the device every call and drops it when positions have moved."""
+        if self._cindex is None:
+            L, g, nc = _lib.lib(), _lib.Grid(), ctypes.c_int64(0)
+            _lib.check(L.swarm_cell_index(_lib.ctx(), self.n, _lib.ptr(self.pos), self.cell, ctypes.byref(g), None, 0,
+                                          ctypes.byref(nc), _lib.stream()))
+            off = torch.empty(nc.value + 1, dtype=torch.int32, device=self.device)
+            _lib.check(L.swarm_cell_index(_lib.ctx(), self.n, _lib.ptr(self.pos), self.cell, ctypes.byref(g),
+                                          _lib.ptr(off), off.numel(), ctypes.byref(nc), _lib.stream()))
+            self._cindex = (g, off)
+        return self._cindex
+
     def allocate(self, tx, ty, treq, *, winner=None, util=None, claim_thr: float = 20.0,
                  hysteresis: float = 5.0, u_scale: float = 100.0, mode: str = "auto") -> AllocResult:
         """One allocation round over t tasks (swarm_allocate).  winner/util = existing claims."""
@@ -238,13 +261,33 @@ class Swarm:
         idx = self.id_index()
         st = _lib.AllocStats()
         m = {"auto": _lib.ALLOC_AUTO, "binned": _lib.ALLOC_BINNED, "dense": _lib.ALLOC_DENSE}[mode]
+        L = _lib.lib()
         with torch.cuda.device(dev):
-            _lib.check(_lib.lib().swarm_allocate(
-                _lib.ctx(), self.n, _lib.ptr(self.ids), _lib.ptr(self.pos), _lib.ptr(self.caps), t,
-                _lib.ptr(tpos), _lib.ptr(tq), float(claim_thr), float(hysteresis), float(u_scale), m,
-                _lib.ptr(w), _lib.ptr(u), _lib.ptr(won), _lib.ptr(idx),
-                0 if idx is None else idx.numel(), _lib.ptr(nclaim), _lib.ptr(nmsg),
-                ctypes.byref(st), _lib.stream()))
+            ci = self._cell_index() if self._indexable(mode, claim_thr, u_scale) else None
+            rc = _lib.ERR_STALE
+            if ci is not None:  # spatial storage order: no binning pass (swarm_allocate_indexed)
+                # the claim table is updated in place: keep the caller's for a stale-index retry
+                w0 = None if winner is None else w.clone()
+                u0 = None if util is None else u.clone()
+                rc = L.swarm_allocate_indexed(
+                    _lib.ctx(), self.n, _lib.ptr(self.ids), _lib.ptr(self.pos), _lib.ptr(self.caps),
+                    ctypes.byref(ci[0]), _lib.ptr(ci[1]), t, _lib.ptr(tpos), _lib.ptr(tq), float(claim_thr),
+                    float(hysteresis), float(u_scale), _lib.ptr(w), _lib.ptr(u), _lib.ptr(won), _lib.ptr(idx),
+                    0 if idx is None else idx.numel(), _lib.ptr(nclaim), _lib.ptr(nmsg), ctypes.byref(st),
+                    _lib.stream())
+                if rc == _lib.ERR_STALE:  # positions moved since the index: bin them this call
+                    self._cindex = None
+                    w.copy_(w0) if w0 is not None else w.fill_(-1)
+                    u.copy_(u0) if u0 is not None else u.zero_()
+                else:
+                    _lib.check(rc)
+            if rc == _lib.ERR_STALE:
+                _lib.check(L.swarm_allocate(
+                    _lib.ctx(), self.n, _lib.ptr(self.ids), _lib.ptr(self.pos), _lib.ptr(self.caps), t,
+                    _lib.ptr(tpos), _lib.ptr(tq), float(claim_thr), float(hysteresis), float(u_scale), m,
+                    _lib.ptr(w), _lib.ptr(u), _lib.ptr(won), _lib.ptr(idx),
+                    0 if idx is None else idx.numel(), _lib.ptr(nclaim), _lib.ptr(nmsg),
+                    ctypes.byref(st), _lib.stream()))
         stats = {k: getattr(st, k) for k, _ in _lib.AllocStats._fields_}
         return AllocResult(w, u, won, nclaim, nmsg, stats)
 
@@ -320,6 +363,7 @@ class Swarm:
                     float(dt), float(max_speed), ctypes.byref(sing), _lib.stream()))
                 total += sing.value
                 self.pos, other = other, self.pos
+                self._cindex = None  # agents moved: the storage order is no longer their cell order
         return {"singular": total}
 
     # ------------------------------------------------------------------ timer FSM (f2)

@@ -37,6 +37,7 @@ extern "C" {
 #define SWARM_ERR_HIP (-2)     /* HIP runtime error (message has the hipError string) */
 #define SWARM_ERR_OOM (-3)     /* scratch allocation failed */
 #define SWARM_ERR_RANGE (-4)   /* a size exceeds the index type (e.g. >= 2^31 edges) */
+#define SWARM_ERR_STALE (-5)   /* swarm_allocate_indexed: positions moved since swarm_cell_index */
 
 /* Agent states as stored in the uint8 state array (agent.py:19-22 AgentState values). */
 #define SWARM_FOLLOWER 1
@@ -229,6 +230,34 @@ int swarm_allocate(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *
                    int32_t *winner, double *util, int32_t *won, const int32_t *id_to_index,
                    int64_t id_span, int64_t *nclaim, int64_t *nmsg, swarm_alloc_stats *stats,
                    void *stream);
+
+/*
+ * The same round (BINNED) over agents stored in cell order -- swarm_cell_order's layout, the
+ * spatial layout of swarm_amd.Swarm -- without a binning pass: a task's claim window is the
+ * grid rows it covers, each a contiguous range of storage indices.  The index comes from
+ * swarm_cell_index over the same positions.  Every call verifies on the device that each agent
+ * still lies in its cell's range; if not (positions moved since the index was built) it returns
+ * SWARM_ERR_STALE and the outputs are undefined -- rebuild the index, or call swarm_allocate.
+ * Claim radius (u_scale / claim_thr - 1) must span at most 16 grid rows (SWARM_ERR_ARG).
+ */
+typedef struct swarm_grid {
+    double xmin, ymin, xmax, ymax;  /* bounding box of the indexed positions */
+    double cell, inv_cell;          /* cell side (>= the requested one if the grid was capped) */
+    int64_t ncx, ncy;               /* cells per row, rows */
+} swarm_grid;
+
+/* grid (host) and cell_off (device, ncells + 1): agents of cell c = cy * ncx + cx are storage
+ * indices [cell_off[c], cell_off[c + 1]).  cell_off == NULL: fill grid and *ncells only.
+ * SWARM_ERR_ARG if pos is not in cell order.  Synchronises the stream. */
+int swarm_cell_index(swarm_ctx *ctx, int64_t n, const double *pos, double cell, swarm_grid *grid,
+                     uint32_t *cell_off, int64_t cell_off_capacity, int64_t *ncells, void *stream);
+
+int swarm_allocate_indexed(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos,
+                           const uint32_t *acaps, const swarm_grid *grid, const uint32_t *cell_off,
+                           int64_t t, const double *tpos, const int8_t *treq, double claim_thr,
+                           double hysteresis, double u_scale, int32_t *winner, double *util,
+                           int32_t *won, const int32_t *id_to_index, int64_t id_span,
+                           int64_t *nclaim, int64_t *nmsg, swarm_alloc_stats *stats, void *stream);
 
 /*
  * Exact fp64 utility for m (agent, task) pairs (agent.py:338-347), GPU arithmetic.

@@ -1,0 +1,106 @@
+"""swarm_allocate_indexed (the binned allocation over the spatial storage order's cell index, no
+binning pass) against swarm_allocate's hashed binning and the oracle; staleness detection when
+positions move after the index was built (agent.py:292-325, contract A-H)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mods():
+    import swarm_amd.swarm as swm
+    from swarm_amd import _lib, gen
+    _lib.load()
+    return swm, _lib, gen
+
+
+def _both(s, d, **kw):
+    """Swarm.allocate through the index (default for the spatial layout) and through hashed
+    binning (the same swarm with the index path disabled)."""
+    a = s.allocate(d["tx"], d["ty"], d["treq"], **kw)
+    assert s._cindex is not None  # the indexed path ran
+    saved = s._indexable
+    s._indexable = lambda *a_, **k_: False
+    try:
+        b = s.allocate(d["tx"], d["ty"], d["treq"], **kw)
+    finally:
+        s._indexable = saved
+    return a, b
+
+
+@pytest.mark.parametrize("n,t,seed,h", [(300_000, 3_000, 1, 5.0), (60_000, 20_000, 2, 0.0), (5_000, 800, 3, 5.0)])
+def test_indexed_equals_hashed_and_oracle(mods, oracle_mod, n, t, seed, h):
+    swm, _lib, gen = mods
+    d = gen.swarm_inputs(n, seed, t=t)
+    s = swm.Swarm(d["ids"], d["x"], d["y"], d["caps"], device="cuda")
+    a, b = _both(s, d, hysteresis=h)
+    for k in ("winner", "nclaim", "nmsg", "won"):
+        np.testing.assert_array_equal(getattr(a, k).cpu().numpy(), getattr(b, k).cpu().numpy(), err_msg=k)
+    np.testing.assert_array_equal(a.util.cpu().numpy().view(np.uint64), b.util.cpu().numpy().view(np.uint64))
+    for k in ("n_claims", "n_conflicts", "n_flagged", "n_candidates", "n_overflow"):
+        assert a.stats[k] == b.stats[k], k
+    ids, x, y = s.ids.cpu().numpy(), s.pos[:, 0].cpu().numpy(), s.pos[:, 1].cpu().numpy()
+    want = oracle_mod.allocate_binned(ids, x, y, s.caps.cpu().numpy().view(np.uint32), d["tx"], d["ty"], d["treq"],
+                                      hysteresis=h, use_pow=False)
+    np.testing.assert_array_equal(a.winner.cpu().numpy(), want["winner"])
+    np.testing.assert_array_equal(a.won.cpu().numpy(), want["won"])
+
+
+def test_prior_claims_and_tasks_outside(mods, oracle_mod):
+    """Pre-loaded claim table and tasks far outside the agents' bounding box (empty windows)."""
+    swm, _lib, gen = mods
+    d = gen.swarm_inputs(20_000, 7, t=500)
+    d["tx"][:50] += 1e4  # no agent within reach
+    g = np.random.default_rng(7)
+    w = np.where(g.random(500) < 0.3, g.integers(0, 20_000, 500), -1).astype(np.int32)
+    u = np.where(w >= 0, g.uniform(20, 100, 500), 0.0)
+    s = swm.Swarm(d["ids"], d["x"], d["y"], d["caps"], device="cuda")
+    a, b = _both(s, d, winner=w, util=u)
+    np.testing.assert_array_equal(a.winner.cpu().numpy(), b.winner.cpu().numpy())
+    np.testing.assert_array_equal(a.util.cpu().numpy(), b.util.cpu().numpy())
+    np.testing.assert_array_equal(a.won.cpu().numpy(), b.won.cpu().numpy())
+    assert (a.nclaim.cpu().numpy()[:50] == 0).all()
+
+
+def test_stale_index_detected_and_recovered(mods, oracle_mod):
+    swm, _lib, gen = mods
+    d = gen.swarm_inputs(50_000, 9, t=2_000)
+    s = swm.Swarm(d["ids"], d["x"], d["y"], d["caps"], device="cuda")
+    s.allocate(d["tx"], d["ty"], d["treq"])
+    g, off = s._cindex
+    # move agents behind the Swarm's back: the next call must notice and rebin
+    s.pos[:, 0] = s.pos[:, 0].flip(0)
+    L = _lib.lib()
+    t = len(d["tx"])
+    tpos = torch.stack([torch.as_tensor(d["tx"]), torch.as_tensor(d["ty"])], 1).cuda().contiguous()
+    tq = torch.as_tensor(d["treq"]).cuda()
+    w = torch.full((t,), -1, dtype=torch.int32, device="cuda")
+    u = torch.zeros(t, dtype=torch.float64, device="cuda")
+    rc = L.swarm_allocate_indexed(_lib.ctx(), s.n, _lib.ptr(s.ids), _lib.ptr(s.pos), _lib.ptr(s.caps),
+                                  ctypes.byref(g), _lib.ptr(off), t, _lib.ptr(tpos), _lib.ptr(tq), 20.0, 5.0, 100.0,
+                                  _lib.ptr(w), _lib.ptr(u), None, None, 0, None, None, None, _lib.stream())
+    assert rc == _lib.ERR_STALE
+    a = s.allocate(d["tx"], d["ty"], d["treq"])  # falls back to hashed binning
+    ids, x, y = s.ids.cpu().numpy(), s.pos[:, 0].cpu().numpy(), s.pos[:, 1].cpu().numpy()
+    want = oracle_mod.allocate_binned(ids, x, y, s.caps.cpu().numpy().view(np.uint32), d["tx"], d["ty"], d["treq"],
+                                      use_pow=False)
+    np.testing.assert_array_equal(a.winner.cpu().numpy(), want["winner"])
+    np.testing.assert_array_equal(a.won.cpu().numpy(), want["won"])
+
+
+def test_cell_index_rejects_unsorted(mods):
+    swm, _lib, gen = mods
+    d = gen.swarm_inputs(10_000, 4)
+    pos = torch.stack([torch.as_tensor(d["x"]), torch.as_tensor(d["y"])], 1).cuda().contiguous()  # input order
+    g, nc = _lib.Grid(), ctypes.c_int64(0)
+    L = _lib.lib()
+    _lib.check(L.swarm_cell_index(_lib.ctx(), 10_000, _lib.ptr(pos), 1.0, ctypes.byref(g), None, 0, ctypes.byref(nc),
+                                  _lib.stream()))
+    off = torch.empty(nc.value + 1, dtype=torch.int32, device="cuda")
+    with pytest.raises(_lib.SwarmError, match="not in cell order"):
+        _lib.check(L.swarm_cell_index(_lib.ctx(), 10_000, _lib.ptr(pos), 1.0, ctypes.byref(g), _lib.ptr(off),
+                                      off.numel(), ctypes.byref(nc), _lib.stream()))
