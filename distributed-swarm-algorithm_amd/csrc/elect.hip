@@ -89,16 +89,14 @@ __device__ __forceinline__ void bookkeeping(unsigned long long *ring, unsigned l
         *slot(ring, t + kRing / 2, i / kShards, i % kShards) = 0;
 }
 
-// The same in two halves, so that block 0 does not put a dependent load in front of its own
-// work: the shard loads are issued at kernel start, the sum published at the end.
-__device__ __forceinline__ unsigned long long bookkeeping_load(unsigned long long *ring, unsigned long long *tot,
-                                                               int t) {
-    return (blockIdx.x == 0 && tot && t > 1 && threadIdx.x < kWave) ? *slot(ring, t - 1, C_CHG, threadIdx.x) : 0ull;
-}
-__device__ __forceinline__ void bookkeeping_finish(unsigned long long *ring, unsigned long long *tot, int t,
-                                                   unsigned long long v) {
-    if (blockIdx.x != 0) return;
+// The same, done by the LAST workgroup of a sparse round: grid-stride over M chunks gives the last
+// workgroups one chunk fewer than the first ones, so the dependent load is off the round's
+// critical path.  (Done synchronously: a shard sum held in registers through the gather was
+// spilled to scratch by every thread of every workgroup -- 4 MB written per round.)
+__device__ __forceinline__ void bookkeeping_last(unsigned long long *ring, unsigned long long *tot, int t) {
+    if (blockIdx.x != gridDim.x - 1) return;
     if (tot && t > 1 && threadIdx.x < kWave) {
+        unsigned long long v = *slot(ring, t - 1, C_CHG, threadIdx.x);
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
         if (threadIdx.x == 0) tot[(t - 1) % kRing] = v;
@@ -316,7 +314,7 @@ __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, const 
                                               const int32_t *__restrict__ P, int32_t *__restrict__ Q,
                                               uint8_t *__restrict__ aw, const StampMap &sm, uint8_t sw,
                                               const int *lst, int total, int first, int step, int64_t n_count,
-                                              long long &my_chg, long long &my_act, long long &my_edges) {
+                                              long long &my_chg, int &my_act, int &my_edges) {
     const int lane = threadIdx.x & 63, sub = lane & (G - 1);
     for (int base = first; base < total; base += step) {
         const int i = base + lane / G;
@@ -354,7 +352,7 @@ __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, const 
         my_chg += __popcll(__ballot(up && sub == 0 && v < n_count));
         if (valid && sub == 0) {
             my_act += 1;
-            my_edges += (long long)(e - b);
+            my_edges += int(e - b);
         }
     }
 }
@@ -386,8 +384,10 @@ __device__ __forceinline__ unsigned take_stamps(uint8_t *ar, int64_t s0, int64_t
     return mask;
 }
 
-__device__ __forceinline__ void flush_counts(unsigned long long *ring, int t, long long my_chg, long long my_act,
-                                             long long my_edges, long long (*s_red)[kWavesPerBlock]) {
+// my_act / my_edges: this lane's marked agents and edges of the round (32-bit per lane: VGPRs are
+// at the 8-waves-per-SIMD cap in the sparse kernel)
+__device__ __forceinline__ void flush_counts(unsigned long long *ring, int t, long long my_chg, int my_act,
+                                             int my_edges, long long (*s_red)[kWavesPerBlock]) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
     for (int o2 = 32; o2 > 0; o2 >>= 1) {
@@ -424,7 +424,7 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
     long long ph_sum = 0, ph_max = 0;
     unsigned long long ph_stamps = 0, ph_listed = 0, ph_gathered = 0;
 #endif
-    const unsigned long long bk = bookkeeping_load(f.ring, f.tot, t);
+    bookkeeping_last(f.ring, f.tot, t);
     // single-GPU runs: round t-2 changed nothing => round t-1 had no marked agent => neither t.
     // Loaded here, tested only once the first stamp words are in flight (no dependent load in
     // front of the round's own chain).
@@ -435,7 +435,8 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
     const unsigned stamp4 = unsigned(stamp_of(t)) * 0x01010101u;
     const uint8_t sw = stamp_of(t + 1);
     const int64_t n = f.n_rows;
-    long long my_chg = 0, my_act = 0, my_edges = 0;
+    long long my_chg = 0;
+    int my_act = 0, my_edges = 0;
     const int64_t nchunks = f.sm.M;  // chunk k: stamp slots [k*kChunk, (k+1)*kChunk)
     const int64_t NG = gridDim.x;
     const int j0 = threadIdx.x * S;  // this thread's S slots: consecutive agents of one block
@@ -517,7 +518,6 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
     ph_gathered = wall_clock64() + (my_chg & 0);
 #endif
     flush_counts(f.ring, t, my_chg, my_act, my_edges, s_red);
-    bookkeeping_finish(f.ring, f.tot, t, bk);
 #ifdef SWARM_PHASES
     if (threadIdx.x == 0 && blockIdx.x < 8192) {
         g_phase[blockIdx.x * 8 + 0] = ph_t0;
