@@ -161,9 +161,10 @@ __device__ __forceinline__ uint32_t stamp_slot(const StampMap &m, int32_t v) {
     return (uint32_t(r) << m.cshift) + (q << m.bshift) + (uint32_t(v) & ((1u << m.bshift) - 1));
 }
 
-// storage index of in-chunk stamp position j of chunk k
+// storage index of in-chunk stamp position j of chunk k (32-bit: every slot's agent is < 2^31, and
+// a 64-bit per-lane product hoisted out of the scan loop is a VGPR pair the sparse kernel spills)
 __device__ __forceinline__ int64_t stamp_agent(const StampMap &m, int64_t k, int j) {
-    return ((int64_t(j >> m.bshift) * m.M + k) << m.bshift) | (j & ((1 << m.bshift) - 1));
+    return int64_t(((uint32_t(j >> m.bshift) * m.M + uint32_t(k)) << m.bshift) | uint32_t(j & ((1 << m.bshift) - 1)));
 }
 
 constexpr int kKm = 8;  // marking re-walks: col loads in flight per lane
@@ -374,13 +375,13 @@ __device__ __forceinline__ bool any_stamp(uint16_t w) { return w != 0; }
 
 // Marked lanes of S stamps, consuming them (this parity is next written in round t+1, marks
 // for t+2; a stamp left behind would match again 255 rounds later: a spurious gather).
-// s0: first stamp slot of the word, v0: its first agent (the S slots are agents v0 .. v0+S-1).
+// cbase: the chunk's first stamp (this thread's word is cbase[threadIdx.x]), v0: the word's first
+// agent (its S slots are agents v0 .. v0+S-1).
 template <int S, typename W>
-__device__ __forceinline__ unsigned take_stamps(uint8_t *ar, int64_t s0, int64_t v0, int64_t n, W wv,
-                                                unsigned stamp4) {
+__device__ __forceinline__ unsigned take_stamps(uint8_t *cbase, int64_t v0, int64_t n, W wv, unsigned stamp4) {
     unsigned mask = stamp_bits(wv, stamp4);
     if (v0 + S > n) mask &= (v0 >= n) ? 0u : ((1u << (n - v0)) - 1u);
-    if (any_stamp(wv)) *reinterpret_cast<W *>(ar + s0) = W{};
+    if (any_stamp(wv)) reinterpret_cast<W *>(cbase)[threadIdx.x] = W{};
     return mask;
 }
 
@@ -456,7 +457,8 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
             // past the end: this thread's own first word again (a shared fallback address would
             // put every workgroup's redundant loads on one L2 channel)
             const int64_t chunk = cg + p * NG < nchunks ? cg + p * NG : cg;
-            wv[p] = *reinterpret_cast<const W *>(ar + chunk * kChunk + j0);
+            // chunk base uniform (SGPRs), 32-bit lane offset: no 64-bit per-lane address kept live
+            wv[p] = reinterpret_cast<const W *>(ar + chunk * kChunk)[threadIdx.x];
         }
         if (prev2 == 0) break;  // converged: nothing is marked
         unsigned masks = 0;
@@ -464,8 +466,7 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
         for (int p = 0; p < kPre; ++p) {
             const int64_t chunk = cg + p * NG;
             if (chunk < nchunks)
-                masks |= take_stamps<S>(ar, chunk * kChunk + j0, stamp_agent(f.sm, chunk, j0), n, wv[p], stamp4)
-                         << (p * S);
+                masks |= take_stamps<S>(ar + chunk * kChunk, stamp_agent(f.sm, chunk, j0), n, wv[p], stamp4) << (p * S);
         }
 #ifdef SWARM_PHASES
         if (!ph_stamps) ph_stamps = wall_clock64() + (masks & 0);
