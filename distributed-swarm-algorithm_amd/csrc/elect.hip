@@ -40,6 +40,7 @@
 // one kernel (register pressure: 6 instead of 8 waves per SIMD, +10 %), per-wave chunks with no
 // workgroup barrier (+6..30 %), 1 / 8 / 16 lanes per marked agent (+33..65 %), contiguous
 // instead of interleaved edge slices per lane (+14 %).
+#include <algorithm>
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
@@ -611,9 +612,10 @@ struct Tuning {
     int sparse_blocks = 2048; // grid cap of k_sparse_block (8 resident workgroups per CU)
     int small_chunks = 512;   // fewer 2048-agent chunks than this: 512-agent chunks instead
     int stamp_bshift = 5;     // log2 of the stamp layout's block (stamp_slot)
-    int il_min_changes = 2000; // interleaved stamp layout while the last read round changed >= this
+    int il_min_changes = -1;   // interleaved stamp layout while the last read round changed >= this
+                               // (-1: 8e-4 x agents, measured best at 100k, 1M and 10M agents)
     Tuning() {
-        il_min_changes = env_int("SWARM_IL_MIN_CHANGES", 2000);
+        il_min_changes = env_int("SWARM_IL_MIN_CHANGES", -1);
         stamp_bshift = env_int("SWARM_STAMP_BSHIFT", 5);
         dense_blocks = env_int("SWARM_DENSE_BLOCKS", 2048);
         dense_rounds = env_int("SWARM_DENSE_ROUNDS", 8);
@@ -811,6 +813,8 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     int found = -1, t = 1, batch = 8, launched = 0;
     std::vector<int64_t> hist;  // per-round change counts read so far (batch sizing, layout)
     const StampMap il_map = stamp_map(n, true), ag_map = stamp_map(n, false);
+    const int64_t il_min = tuning().il_min_changes >= 0 ? tuning().il_min_changes
+                                                        : std::max<int64_t>(1, int64_t(8e-4 * double(n)));
     StampMap rd_map = il_map;
     int64_t act_sum = 0, edge_sum = 0, chg_sum = 0, dense_rounds = 0, sp_launches = 0;
     double bytes = 0.0, sp_bytes = 0.0, sp_ms = 0.0;
@@ -849,7 +853,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
                 // marks for round r+1: interleaved layout while rounds are busy (balance), agent
                 // order once they are sparse (locality of the few gathers)
                 f.sm = rd_map;
-                f.wsm = (hist.empty() || hist.back() >= tuning().il_min_changes) ? il_map : ag_map;
+                f.wsm = (hist.empty() || hist.back() >= il_min) ? il_map : ag_map;
                 rc = launch_frontier_round<Off>(rp, col, f, r, kinds[r - t], 1, s, hrp, hcol);
                 rd_map = f.wsm;
             }
