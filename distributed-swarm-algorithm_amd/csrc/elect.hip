@@ -825,7 +825,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     double k_ms = 0;
     int64_t timed_rounds = 0;
     if (timed) {
-        ev.resize(2 * kMaxBatch);
+        ev.resize(2 * kMaxBatch + 2);
         for (auto &x : ev) SW_HIP(hipEventCreate(&x));
     }
     struct EvFree {
@@ -841,8 +841,16 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     while (t <= max_rounds && found < 0) {
         const int tend = (max_rounds - t + 1 < batch) ? max_rounds : t + batch - 1;
         int rc = 0;
+        // timing: dense rounds (and every round when a per-round log is written) get an event pair
+        // each; a batch's run of back-to-back sparse rounds gets ONE pair around it -- events
+        // between every launch would add their own cost to each round (rocprof's per-dispatch
+        // durations are the reference for this figure)
+        int seg_n = 0;  // sparse launches inside this batch's segment
         for (int r = t; r <= tend; ++r) {
-            hipEvent_t *e2 = timed ? &ev[2 * (r - t)] : nullptr;
+            const bool sparse = mode == SWARM_ELECT_FRONTIER && plan_round(r) == RK_SPARSE;
+            const bool seg = timed && sparse && !rlog;
+            if (seg && seg_n++ == 0) SW_HIP(hipEventRecord(ev[2 * kMaxBatch], s));
+            hipEvent_t *e2 = (timed && !seg) ? &ev[2 * (r - t)] : nullptr;
             if (e2) SW_HIP(hipEventRecord(e2[0], s));
             if (mode == SWARM_ELECT_DENSE) {
                 kinds[r - t] = RK_DENSE;
@@ -860,6 +868,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
             if (rc) return rc;
             if (e2) SW_HIP(hipEventRecord(e2[1], s));
         }
+        if (seg_n) SW_HIP(hipEventRecord(ev[2 * kMaxBatch + 1], s));
         launched = tend;
         // per-round totals of rounds [t, tend], reduced on device, then one small copy
         hipLaunchKernelGGL(k_batch_totals, dim3(tend - t + 1), dim3(kWave), 0, s, ring, t, dtot);
@@ -868,6 +877,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         SW_HIP(hipStreamSynchronize(s));
         for (int r = t; r <= tend; ++r) {  // every launched round's kernel time (rocprof's view)
             if (!timed) break;
+            if (seg_n && kinds[r - t] == RK_SPARSE) continue;  // in the segment
             float x = 0;
             SW_HIP(hipEventElapsedTime(&x, ev[2 * (r - t)], ev[2 * (r - t) + 1]));
             k_ms += x;
@@ -877,6 +887,14 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
                 ++sp_launches;
             }
             ktime[r - t] = x;
+        }
+        if (seg_n) {
+            float x = 0;
+            SW_HIP(hipEventElapsedTime(&x, ev[2 * kMaxBatch], ev[2 * kMaxBatch + 1]));
+            k_ms += x;
+            sp_ms += x;
+            timed_rounds += seg_n;
+            sp_launches += seg_n;
         }
         for (int r = t; r <= tend; ++r) {
             const unsigned long long *rb = hbuf + size_t(r - t) * kCounters;
