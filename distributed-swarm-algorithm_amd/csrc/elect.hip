@@ -306,6 +306,25 @@ struct Frontier {
     StampMap sm, wsm;
 };
 
+// 4-byte element idx of base with a 32-bit byte offset (idx < 2^30): the load takes the uniform
+// base in SGPRs and one offset VGPR, where a 64-bit index costs an address pair per load in flight
+// (the sparse kernel runs at the 64-VGPR cap).  Int64 offsets (graphs >= 2^30 edges or agents) use
+// plain indexing.
+template <typename T, typename I>
+__device__ __forceinline__ T ld4(const T *__restrict__ base, I idx) {
+    if constexpr (sizeof(I) == 4 && sizeof(T) == 4)
+        return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + (uint32_t(idx) << 2));
+    else
+        return base[idx];
+}
+template <typename T, typename I>
+__device__ __forceinline__ void st4(T *__restrict__ base, I idx, T v) {
+    if constexpr (sizeof(I) == 4 && sizeof(T) == 4)
+        *reinterpret_cast<T *>(reinterpret_cast<char *>(base) + (uint32_t(idx) << 2)) = v;
+    else
+        base[idx] = v;
+}
+
 // Gather of the marked agents listed (chunk-relative) in lst[0, total), G lanes per agent,
 // `first`/`step` select this wave's share; risers mark themselves and their neighbours.  Lane
 // `sub` of an agent takes edges b + sub + G*j (interleaved: one load instruction covers G
@@ -318,27 +337,28 @@ __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, const 
                                               const int *lst, int total, int first, int step, int64_t n_count,
                                               long long &my_chg, int &my_act, int &my_edges) {
     const int lane = threadIdx.x & 63, sub = lane & (G - 1);
+    using Ix = Off;  // 32-bit offsets in the int32-CSR instantiation (host: < 2^30 agents and edges)
     for (int base = first; base < total; base += step) {
         const int i = base + lane / G;
         const bool valid = i < total;
-        const int64_t v = lst[valid ? i : total - 1];
-        const Off b = rp[v], e = rp[v + 1];
-        const int own = P[v];
+        const int32_t v = lst[valid ? i : total - 1];
+        const Off b = ld4(rp, Ix(v)), e = ld4(rp, Ix(v + 1));
+        const int own = ld4(P, Ix(v));
         int m = own;
         int c[K];
         for (Off k = b + sub; k < e; k += G * K) {
 #pragma unroll
-            for (int j = 0; j < K; ++j) c[j] = col[(k + G * j < e) ? k + G * j : e - 1];
+            for (int j = 0; j < K; ++j) c[j] = ld4(col, (k + G * j < e) ? k + G * j : e - 1);
             int val[K];
 #pragma unroll
-            for (int j = 0; j < K; ++j) val[j] = P[c[j]];
+            for (int j = 0; j < K; ++j) val[j] = ld4(P, Ix(c[j]));
 #pragma unroll
             for (int j = 0; j < K; ++j) m = max(m, val[j]);
         }
 #pragma unroll
         for (int o2 = 1; o2 < G; o2 <<= 1) m = max(m, __shfl_xor(m, o2, 64));
         const bool up = valid && m > own;
-        if (valid && sub == 0) Q[v] = m;
+        if (valid && sub == 0) st4(Q, Ix(v), m);
         if (up) {
             if (sub == 0) aw[stamp_slot(sm, v)] = sw;
             if (DIR) {  // the agents that hear v
@@ -382,7 +402,7 @@ template <int S, typename W>
 __device__ __forceinline__ unsigned take_stamps(uint8_t *cbase, int64_t v0, int64_t n, W wv, unsigned stamp4) {
     unsigned mask = stamp_bits(wv, stamp4);
     if (v0 + S > n) mask &= (v0 >= n) ? 0u : ((1u << (n - v0)) - 1u);
-    if (any_stamp(wv)) reinterpret_cast<W *>(cbase)[threadIdx.x] = W{};
+    if (any_stamp(wv)) *reinterpret_cast<W *>(cbase + uint32_t(threadIdx.x * sizeof(W))) = W{};
     return mask;
 }
 
@@ -459,7 +479,7 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
             // put every workgroup's redundant loads on one L2 channel)
             const int64_t chunk = cg + p * NG < nchunks ? cg + p * NG : cg;
             // chunk base uniform (SGPRs), 32-bit lane offset: no 64-bit per-lane address kept live
-            wv[p] = reinterpret_cast<const W *>(ar + chunk * kChunk)[threadIdx.x];
+            wv[p] = *reinterpret_cast<const W *>(ar + chunk * kChunk + uint32_t(threadIdx.x * sizeof(W)));
         }
         if (prev2 == 0) break;  // converged: nothing is marked
         unsigned masks = 0;
@@ -782,6 +802,9 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     SW_HIP(hipMemcpyAsync(&e_total, rp + n, sizeof(Off), hipMemcpyDeviceToHost, s));
     SW_HIP(hipStreamSynchronize(s));
     SW_ARG(e_total == 0 || col != nullptr, "col is NULL but the graph has edges");
+    // the int32-CSR kernels address with 32-bit byte offsets (gather_listed's ld4)
+    SW_ARG(sizeof(Off) == 8 || (n < (int64_t(1) << 30) && int64_t(e_total) < (int64_t(1) << 30)),
+           "int32 CSR supports < 2^30 agents and edges: use swarm_elect_i64");
     if (hrp) {  // directed: the transpose must hold the same edges
         Off h_total = 0;
         SW_HIP(hipMemcpyAsync(&h_total, hrp + n, sizeof(Off), hipMemcpyDeviceToHost, s));
@@ -1018,7 +1041,7 @@ int swarm_frontier_begin(swarm_ctx *ctx, int64_t n_rows, int64_t n_all, const in
                          int32_t *leader0, int32_t *leader1, void *stream) {
     using namespace swarm;
     SW_ARG(ctx != nullptr, "ctx is NULL");
-    SW_ARG(n_rows >= 0 && n_all >= n_rows && n_all < (int64_t(1) << 31), "sizes out of range");
+    SW_ARG(n_rows >= 0 && n_all >= n_rows && n_all < (int64_t(1) << 30), "sizes out of range (n_all < 2^30)");
     SW_ARG(n_all == 0 || (init && leader0 && leader1), "NULL array");
     hipStream_t s = static_cast<hipStream_t>(stream);
     Frontier f{};

@@ -121,7 +121,8 @@ int swarm_elect_directed(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, cons
                          int32_t *rounds_exec, int64_t *changes_per_round, swarm_elect_stats *stats,
                          void *stream);
 
-/* Same with int64 row offsets (graphs with >= 2^31 edges). */
+/* Same with int64 row offsets: graphs with >= 2^30 edges or agents (the int32-CSR entry points
+ * address with 32-bit byte offsets and reject them with SWARM_ERR_ARG). */
 int swarm_elect_i64(swarm_ctx *ctx, int64_t n, const int64_t *row_ptr, const int32_t *col,
                     const int32_t *ids, int32_t *leader, uint8_t *state, int32_t max_rounds,
                     int32_t mode, int32_t *rounds_exec, int64_t *changes_per_round,
