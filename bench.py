@@ -251,14 +251,14 @@ def main():
                             "dense_rounds": r.dense_rounds, "changes_total": rt.changes_total},
             "alloc_stats": a.stats,
         }
+    # ---- CPU baseline: the oracle's restatement of the same algorithm (frontier election +
+    # binned allocation) on the host cores -- the whole C3 step on every thread, and a bounded
+    # sample on one thread.  Before the rows: some of them step this swarm (physics, timers).
+    if rank == 0 and args.cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_step(sw, d, r, a, args)
     # ---- the other §8 rows, each timed once at its own scale (informational; not `value`)
     if rank == 0 and args.rows:
         out["rows"] = rows_bench(sw, dev, args)
-    # ---- CPU baseline: the oracle's restatement of the same algorithm (frontier election +
-    # binned allocation) on the host cores -- the whole C3 step on every thread, and a bounded
-    # sample on one thread
-    if rank == 0 and args.cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline_step(sw, d, r, a, args)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
