@@ -1,0 +1,56 @@
+"""Election at swarm sizes on the sparse round's layout boundaries, against the oracle's frontier
+restatement (agent.py:263-275): leaders, states, rounds_exec and every per-round change count.
+
+The sparse round's stamps are dealt in 32-agent blocks over chunks of 2 048 stamps (512 below
+small_chunks = 512 chunks, i.e. swarms under 1 048 576 agents take the 512-stamp variant), the
+last block and the last chunk may be partial, and the host switches the stamp layout from
+interleaved to agent order once a round changes fewer than 8e-4 x N agents.  These sizes put the
+swarm's end inside a block, at a block / chunk edge and on both sides of the small / large
+variant switch, with dense (deg 16) and sparse (deg 3, many isolated agents and long chains)
+graphs.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def sw():
+    import swarm_amd.swarm as swm
+    from swarm_amd import _lib
+    _lib.load()
+    return swm
+
+
+@pytest.mark.parametrize("n,deg", [(2, 16.0), (31, 16.0), (33, 3.0), (2047, 16.0), (2049, 3.0), (65_537, 16.0),
+                                   (1_048_575, 16.0), (1_048_577, 16.0), (1_050_000, 3.0)])
+def test_elect_layout_boundaries(sw, oracle_mod, n, deg):
+    from swarm_amd import gen
+    d = gen.swarm_inputs(n, 977 + n, deg=deg)
+    s = sw.Swarm(d["ids"], d["x"], d["y"], d["caps"], device="cuda").build_graph(1.0)
+    rp = s.row_ptr.cpu().numpy().astype(np.int64)
+    lead, state, rounds, changes = oracle_mod.elect_frontier(rp, s.col.cpu().numpy(), s.ids.cpu().numpy())
+    for mode in ("frontier", "dense"):
+        r = s.elect(mode=mode, max_rounds=1 << 16)
+        assert r.converged and r.rounds_exec == rounds, (mode, r.rounds_exec, rounds)
+        np.testing.assert_array_equal(r.changes, changes)
+        np.testing.assert_array_equal(r.leader.cpu().numpy(), lead)
+        np.testing.assert_array_equal(r.state.cpu().numpy(), state)
+
+
+def test_elect_repeat_is_stable(sw, oracle_mod):
+    """Back-to-back elections on one swarm reuse the stamp buffers and counter ring: every call
+    must start clean (no stamp or count left over from the previous call's last rounds)."""
+    from swarm_amd import gen
+    d = gen.swarm_inputs(300_000, 5, deg=16.0)
+    s = sw.Swarm(d["ids"], d["x"], d["y"], d["caps"], device="cuda").build_graph(1.0)
+    rp = s.row_ptr.cpu().numpy().astype(np.int64)
+    lead, _, rounds, changes = oracle_mod.elect_frontier(rp, s.col.cpu().numpy(), s.ids.cpu().numpy())
+    for max_rounds in (rounds // 2, 1 << 16, 7, 1 << 16, 1 << 16):  # cut runs leave marks behind
+        r = s.elect(max_rounds=max_rounds)
+        k = min(max_rounds, rounds)
+        np.testing.assert_array_equal(r.changes[:k], changes[:k])
+        if max_rounds >= rounds:
+            assert r.converged and r.rounds_exec == rounds
+            np.testing.assert_array_equal(r.leader.cpu().numpy(), lead)
