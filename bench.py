@@ -427,7 +427,7 @@ def rows_bench(sw, dev, args):
     rows["f1_physics_step"] = {"agents": n, "ms_per_step": ms / steps,
                                "agent_steps_per_s": n * steps / (ms * 1e-3),
                                "roofline": _roof(82.0 * n + 20.0 * e + 16.0 * n_fol, ms / steps,
-                                                 "k_physics + k_physics_copy", "k_physics",
+                                                 "k_physics", "k_physics",
                                                  note="82 B/agent + 20 B/edge + 16 B per follower's leader gather")}
     if cpu:
         dp = gen.swarm_inputs(1_000_000, args.seed + 6)

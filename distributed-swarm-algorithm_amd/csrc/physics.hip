@@ -85,7 +85,10 @@ __global__ __launch_bounds__(kBlock, 8) void k_physics(int64_t n, const int32_t 
                     }
                 }
         }
-        if (!moving) continue;
+        if (!moving) {  // keeps its position (in the output buffer too: synchronous step)
+            if (valid) pout[i] = make_double2(px, py);
+            continue;
+        }
         double fax = 0.0, fay = 0.0;
         const double gx = t.x - px, gy = t.y - py;
         if (sqrt(gx * gx + gy * gy) > 0.5) {
@@ -134,15 +137,6 @@ __global__ __launch_bounds__(kBlock, 8) void k_physics(int64_t n, const int32_t 
     if ((threadIdx.x & 63) == 0 && sing) atomicAdd(singular, sing);
 }
 
-// Agents that do not move keep their position in the output buffer.
-__global__ __launch_bounds__(kBlock) void k_physics_copy(int64_t n, const uint8_t *__restrict__ has_t,
-                                                        const uint8_t *__restrict__ state,
-                                                        const int32_t *__restrict__ leader,
-                                                        const double2 *__restrict__ pin, double2 *__restrict__ pout) {
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock)
-        if (!has_t[i] && !(state[i] == SWARM_FOLLOWER && leader[i] >= 0)) pout[i] = pin[i];
-}
-
 }  // namespace
 }  // namespace swarm
 
@@ -167,10 +161,6 @@ int swarm_physics_step(swarm_ctx *ctx, int64_t n, const int32_t *ids, const uint
     unsigned long long *d_sing;
     SW_ALLOC(d_sing, ctx, S_TMP0, 64);
     SW_HIP(hipMemsetAsync(d_sing, 0, 8, s));
-    // order matters: k_physics_copy reads has_target before k_physics may set it (followers)
-    hipLaunchKernelGGL(k_physics_copy, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s, n, has_target, state,
-                       leader_index, reinterpret_cast<const double2 *>(pos_in), reinterpret_cast<double2 *>(pos_out));
-    SW_LAUNCHED();
     hipLaunchKernelGGL(k_physics, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, n, ids, state, leader_index,
                        reinterpret_cast<const double2 *>(pos_in), reinterpret_cast<double2 *>(pos_out),
                        reinterpret_cast<double2 *>(vel), reinterpret_cast<double2 *>(target), has_target, m, obstacles,
