@@ -19,9 +19,11 @@
 // (every batch of rounds):
 //   k_elect_dense<MARK=false>  the first dense_rounds-1 rounds (nearly every agent changes)
 //   k_elect_dense<MARK=true>   the last dense round: also marks the risers' neighbourhoods
-//   k_sparse_block             2048-agent chunk per workgroup (grid = resident workgroups,
-//                              next chunk's stamps loaded ahead): stamps -> LDS list -> gather,
-//                              4 lanes per marked agent with interleaved edges
+//   k_sparse_block             2 048 resident workgroups; each loads the stamp words of all its
+//                              2048-stamp chunks at once, lists their marked agents in LDS and
+//                              gathers them, 4 lanes per marked agent with interleaved edges.
+//                              Stamps are dealt in 32-agent blocks over the chunks while rounds
+//                              are busy (balance), in agent order in the tail (stamp_slot)
 // Marks are plain byte stores, no atomics: stamp act[v] = stamp_of(t+1) (1..255, never 0, so an
 // unmarked byte never matches), double-buffered by round parity and consumed (zeroed) by the
 // sparse round that reads them.  Leaders alternate by
@@ -32,14 +34,16 @@
 // Counters: every per-round count (changes, marked agents, edges, ghost rises) is a 64-way
 // sharded 64-bit counter on its own 128-byte line, added once per workgroup: one contended
 // counter per round costs ~12 ns per arrival (MI355X_MICROARCH.md, 'fanin').  The shards live
-// in a ring of kRing rounds; block 0 of round t recycles the slots of round t + kRing/2 and
-// publishes the total changes of round t-1 (tot[]), which sparse rounds use as their guard.
+// in a ring of kRing rounds; one workgroup of round t (block 0 of a dense round, the last block
+// of a sparse one) recycles the slots of round t + kRing/2 and publishes the total changes of
+// round t-1 (tot[]), which sparse rounds use as their guard.
 //
 // Measured and rejected: a push variant (risers atomicMax their value into the
 // neighbours: scattered device-scope atomics run at ~20 G/s), dense and sparse paths fused in
 // one kernel (register pressure: 6 instead of 8 waves per SIMD, +10 %), per-wave chunks with no
-// workgroup barrier (+6..30 %), 1 / 8 / 16 lanes per marked agent (+33..65 %), contiguous
-// instead of interleaved edge slices per lane (+14 %).
+// workgroup barrier (+6..30 %), 1 / 2 / 8 / 16 lanes per marked agent (+28..65 %), contiguous
+// instead of interleaved edge slices per lane (+14 %), paired / edge-flat / wave-flat / run-unit
+// gathers (+16..66 %).
 #include <algorithm>
 #include <climits>
 #include <cstdio>
