@@ -329,6 +329,35 @@ __device__ __forceinline__ void st4(T *__restrict__ base, I idx, T v) {
         base[idx] = v;
 }
 
+// Max over the G lanes of an agent's group (G = 4: a quad) through DPP quad permutes -- register
+// moves inside the wave, where __shfl_xor would be two LDS round trips (ds_bpermute).
+template <int G>
+__device__ __forceinline__ int group_max(int m) {
+    if constexpr (G == 4) {
+        m = max(m, __builtin_amdgcn_update_dpp(m, m, 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
+        m = max(m, __builtin_amdgcn_update_dpp(m, m, 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
+    } else {
+#pragma unroll
+        for (int o2 = 1; o2 < G; o2 <<= 1) m = max(m, __shfl_xor(m, o2, 64));
+    }
+    return m;
+}
+
+// Exclusive prefix over the wave of c (0 <= c < 2^B) and the wave total, from B ballots and
+// mbcnt (no LDS round trip: a __shfl_up scan is six ds_bpermute waits).
+template <int B>
+__device__ __forceinline__ int wave_excl_scan(int c, int &total) {
+    int ex = 0, tot = 0;
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        const unsigned long long m = __ballot((c >> b) & 1);
+        ex += int(__builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u))) << b;
+        tot += __popcll(m) << b;
+    }
+    total = tot;
+    return ex;
+}
+
 // Gather of the marked agents listed (chunk-relative) in lst[0, total), G lanes per agent,
 // `first`/`step` select this wave's share; risers mark themselves and their neighbours.  Lane
 // `sub` of an agent takes edges b + sub + G*j (interleaved: one load instruction covers G
@@ -359,8 +388,7 @@ __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, const 
 #pragma unroll
             for (int j = 0; j < K; ++j) m = max(m, val[j]);
         }
-#pragma unroll
-        for (int o2 = 1; o2 < G; o2 <<= 1) m = max(m, __shfl_xor(m, o2, 64));
+        m = group_max<G>(m);
         const bool up = valid && m > own;
         if (valid && sub == 0) st4(Q, Ix(v), m);
         if (up) {
@@ -498,14 +526,10 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
 #endif
         // append the group's marked agents, gathering whenever the list fills up
         for (;;) {
-            const int cnt = __popc(masks);
-            int incl = cnt;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const int x = __shfl_up(incl, off, 64);
-                if (lane >= off) incl += x;
-            }
-            if (lane == 63) s_wave[wid] = incl;
+            const int cnt = __popc(masks);  // <= kPre * S <= 32
+            int wtot;
+            const int excl = wave_excl_scan<6>(cnt, wtot);
+            if (lane == 0) s_wave[wid] = wtot;
             __syncthreads();
             int off = 0, total = 0;
 #pragma unroll
@@ -519,7 +543,7 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
             ph_sum += total;
             ph_max = total > ph_max ? total : ph_max;
 #endif
-            int pos = listed + off + incl - cnt;
+            int pos = listed + off + excl;
             while (masks && pos < kListCap) {
                 const int bit = __ffs(masks) - 1;
                 masks &= masks - 1;
