@@ -371,12 +371,25 @@ __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, const 
                                               long long &my_chg, int &my_act, int &my_edges) {
     const int lane = threadIdx.x & 63, sub = lane & (G - 1);
     using Ix = Off;  // 32-bit offsets in the int32-CSR instantiation (host: < 2^30 agents and edges)
+    if (first >= total) return;
+    // software pipeline: a pass's agent, row bounds and own leader are loaded during the previous
+    // pass, so a pass's chain is columns -> leaders only
+    int32_t nv = lst[first + lane / G < total ? first + lane / G : total - 1];
+    Off nb = ld4(rp, Ix(nv)), ne = ld4(rp, Ix(nv + 1));
+    int nown = ld4(P, Ix(nv));
     for (int base = first; base < total; base += step) {
         const int i = base + lane / G;
         const bool valid = i < total;
-        const int32_t v = lst[valid ? i : total - 1];
-        const Off b = ld4(rp, Ix(v)), e = ld4(rp, Ix(v + 1));
-        const int own = ld4(P, Ix(v));
+        const int32_t v = nv;
+        const Off b = nb, e = ne;
+        const int own = nown;
+        {  // unconditional (clamped past the end): a load behind a branch is waited for at the join
+            const int i2 = base + step + lane / G;
+            nv = lst[i2 < total ? i2 : total - 1];
+            nb = ld4(rp, Ix(nv));
+            ne = ld4(rp, Ix(nv + 1));
+            nown = ld4(P, Ix(nv));
+        }
         int m = own;
         int c[K];
         for (Off k = b + sub; k < e; k += G * K) {
