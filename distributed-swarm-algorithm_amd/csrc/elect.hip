@@ -343,6 +343,17 @@ __device__ __forceinline__ int group_max(int m) {
     return m;
 }
 
+// Wave sum (full exec): DPP within rows of 16 (quad xor 1, xor 2, half-row mirror, row mirror),
+// then the four row sums read into scalars -- no ds_bpermute round trips.
+__device__ __forceinline__ int wave_sum(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    x += __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    x += __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    x += __builtin_amdgcn_update_dpp(0, x, 0x140, 0xF, 0xF, false);  // row_mirror
+    return __builtin_amdgcn_readlane(x, 0) + __builtin_amdgcn_readlane(x, 16) + __builtin_amdgcn_readlane(x, 32) +
+           __builtin_amdgcn_readlane(x, 48);
+}
+
 // Exclusive prefix over the wave of c (0 <= c < 2^B) and the wave total, from B ballots and
 // mbcnt (no LDS round trip: a __shfl_up scan is six ds_bpermute waits).
 template <int B>
@@ -456,11 +467,8 @@ __device__ __forceinline__ unsigned take_stamps(uint8_t *cbase, int64_t v0, int6
 __device__ __forceinline__ void flush_counts(unsigned long long *ring, int t, long long my_chg, int my_act,
                                              int my_edges, long long (*s_red)[kWavesPerBlock]) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-    for (int o2 = 32; o2 > 0; o2 >>= 1) {
-        my_act += __shfl_xor(my_act, o2, 64);
-        my_edges += __shfl_xor(my_edges, o2, 64);
-    }
+    my_act = wave_sum(my_act);
+    my_edges = wave_sum(my_edges);
     if (lane == 0) {
         s_red[0][wid] = my_chg;  // wave-uniform (ballot counts)
         s_red[1][wid] = my_act;
