@@ -450,15 +450,16 @@ __device__ __forceinline__ unsigned stamp_bits(uint16_t w, unsigned stamp4) {
 __device__ __forceinline__ bool any_stamp(uint2 w) { return (w.x | w.y) != 0; }
 __device__ __forceinline__ bool any_stamp(uint16_t w) { return w != 0; }
 
-// Marked lanes of S stamps, consuming them (this parity is next written in round t+1, marks
-// for t+2; a stamp left behind would match again 255 rounds later: a spurious gather).
-// cbase: the chunk's first stamp (this thread's word is cbase[threadIdx.x]), v0: the word's first
-// agent (its S slots are agents v0 .. v0+S-1).
+// Marked lanes of S stamps (v0: the word's first agent; its S slots are agents v0 .. v0+S-1).
+// Stamps are not consumed here: a stamp left behind holds an older round's value and matches
+// only a round 510 rounds later (same parity, same stamp_of), and launch_frontier_round clears
+// each parity's buffer every 256 rounds (a bulk memset instead of a store per marked word).
+// (A stale match would only cost work: an agent none of whose neighbours changed recomputes its
+// own value and counts no change.)
 template <int S, typename W>
-__device__ __forceinline__ unsigned take_stamps(uint8_t *cbase, int64_t v0, int64_t n, W wv, unsigned stamp4) {
+__device__ __forceinline__ unsigned take_stamps(int64_t v0, int64_t n, W wv, unsigned stamp4) {
     unsigned mask = stamp_bits(wv, stamp4);
     if (v0 + S > n) mask &= (v0 >= n) ? 0u : ((1u << (n - v0)) - 1u);
-    if (any_stamp(wv)) *reinterpret_cast<W *>(cbase + uint32_t(threadIdx.x * sizeof(W))) = W{};
     return mask;
 }
 
@@ -540,7 +541,7 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
         for (int p = 0; p < kPre; ++p) {
             const int64_t chunk = cg + p * NG;
             if (chunk < nchunks)
-                masks |= take_stamps<S>(ar + chunk * kChunk, stamp_agent(f.sm, chunk, j0), n, wv[p], stamp4) << (p * S);
+                masks |= take_stamps<S>(stamp_agent(f.sm, chunk, j0), n, wv[p], stamp4) << (p * S);
         }
 #ifdef SWARM_PHASES
         if (!ph_stamps) ph_stamps = wall_clock64() + (masks & 0);
@@ -802,6 +803,10 @@ int launch_frontier_round(const Off *rp, const int32_t *col, const Frontier &f, 
                                        f.tot,
                                        k == RK_DENSE_MARK ? f.act[(t + 1) & 1] : nullptr, f.wsm, t, guard, s, hrp,
                                        hcol);
+    // the buffer this round marks into (parity t+1) was read by round t-1; every 256 rounds, per
+    // parity, it is cleared first, so no stamp outlives the 510 rounds after which its value
+    // recurs (take_stamps)
+    if (t > 2 && ((t - 1) & 255) < 2) SW_HIP(hipMemsetAsync(f.act[(t + 1) & 1], 0, act_bytes(f.n_all), s));
     const bool small = f.sm.cshift == 9;  // small swarm: 512-agent chunks, 4x the workgroups
     const dim3 grid(grid_for(f.sm.M, 1, unsigned(tuning().sparse_blocks)));
     if (hrp && small)
