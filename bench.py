@@ -251,14 +251,18 @@ def main():
                             "dense_rounds": r.dense_rounds, "changes_total": rt.changes_total},
             "alloc_stats": a.stats,
         }
-    # ---- CPU baseline: the oracle's restatement of the same algorithm (frontier election +
-    # binned allocation) on the host cores -- the whole C3 step on every thread, and a bounded
-    # sample on one thread.  Before the rows: some of them step this swarm (physics, timers).
-    if rank == 0 and args.cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline_step(sw, d, r, a, args)
-    # ---- the other §8 rows, each timed once at its own scale (informational; not `value`)
+    # ---- the other §8 rows, each timed once at its own scale (informational; not `value`);
+    # some of them step this swarm (physics, timers): the CPU baseline below compares against a
+    # host snapshot of the timed step, and runs last (its OpenMP threads would share the host
+    # with the rows' launches)
+    snap = host_snapshot(sw, a) if rank == 0 and args.cpu_baseline else None
     if rank == 0 and args.rows:
         out["rows"] = rows_bench(sw, dev, args)
+    # ---- CPU baseline: the oracle's restatement of the same algorithm (frontier election +
+    # binned allocation) on the host cores -- the whole C3 step on every thread, and a bounded
+    # sample on one thread
+    if rank == 0 and args.cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_step(snap, d, r, args)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -286,7 +290,16 @@ def _threads():
     return int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
 
 
-def cpu_baseline_step(sw, d, r, a, args):
+def host_snapshot(sw, a):
+    """Host copies of what cpu_baseline_step needs from the timed step: the graph, the swarm and
+    the GPU's results (taken before the rows step the same swarm)."""
+    return {"rp": sw.row_ptr.cpu().numpy().astype(np.int64), "col": sw.col.cpu().numpy(),
+            "ids": sw.ids.cpu().numpy(), "x": sw.pos[:, 0].cpu().numpy(), "y": sw.pos[:, 1].cpu().numpy(),
+            "caps": sw.caps.cpu().numpy().view(np.uint32), "leader": sw.leader.cpu().numpy(),
+            "winner": a.winner.cpu().numpy()}
+
+
+def cpu_baseline_step(h, d, r, args):
     """The C3 step on the host: the oracle's frontier election (orc_elect_frontier) and binned
     allocation (orc_allocate_binned) -- the same algorithms the GPU runs, restated in C with
     OpenMP -- over the same swarm (storage order), all host threads, measured whole (no
@@ -294,11 +307,7 @@ def cpu_baseline_step(sw, d, r, a, args):
     the agents recomputed (per round, from the full run) and by the task count."""
     from oracle import oracle
     threads = _threads()
-    rp = sw.row_ptr.cpu().numpy().astype(np.int64)
-    col = sw.col.cpu().numpy()
-    ids = sw.ids.cpu().numpy()
-    x, y = sw.pos[:, 0].cpu().numpy(), sw.pos[:, 1].cpu().numpy()
-    caps = sw.caps.cpu().numpy().view(np.uint32)
+    rp, col, ids, x, y, caps = h["rp"], h["col"], h["ids"], h["x"], h["y"], h["caps"]
     n = len(ids)
     oracle.set_threads(threads)
     t1 = time.perf_counter()
@@ -307,8 +316,8 @@ def cpu_baseline_step(sw, d, r, a, args):
     t1 = time.perf_counter()
     al = oracle.allocate_binned(ids, x, y, caps, d["tx"], d["ty"], d["treq"], use_pow=False)
     t_al = time.perf_counter() - t1
-    same = (rounds == r.rounds_exec and bool(np.array_equal(lead, sw.leader.cpu().numpy()))
-            and bool(np.array_equal(al["winner"], a.winner.cpu().numpy())))
+    same = (rounds == r.rounds_exec and bool(np.array_equal(lead, h["leader"]))
+            and bool(np.array_equal(al["winner"], h["winner"])))
     # one thread: the first k rounds (the heaviest) and a task sample
     oracle.set_threads(1)
     k = min(rounds, 40)
