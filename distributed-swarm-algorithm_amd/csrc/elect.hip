@@ -223,7 +223,7 @@ __device__ __forceinline__ int row_max_from_lds(const int *s_col, Off w0, Off lo
 // t+1 can run sparse.
 // DIR: directed graph -- a riser marks the agents that HEAR it (hrp/hcol, the transpose of
 // rp/col), not the agents it hears.
-template <typename Off, bool MARK, bool DIR = false>
+template <typename Off, bool MARK, bool DIR = false, bool FLAT = false>
 __global__ __launch_bounds__(kBlock) void k_elect_dense(
     const Off *__restrict__ rp, const int32_t *__restrict__ col, const int32_t *__restrict__ lin,
     int32_t *__restrict__ lout, int64_t n, int64_t n_count, unsigned long long *__restrict__ ring,
@@ -259,14 +259,35 @@ __global__ __launch_bounds__(kBlock) void k_elect_dense(
         int m = INT_MIN;
         for (Off w0 = W0; w0 < W1; w0 += kWin) {
             const Off wend = (W1 - w0 < kWin) ? W1 : w0 + kWin;
+            if constexpr (FLAT) {
+                // flat: the window's columns AND their leaders, 64 consecutive edges per load (the
+                // neighbours of ~4 consecutive agents: few cache lines per instruction), leaders
+                // into LDS, each lane then maxes its own row from LDS
+                constexpr int kH = kWin / 128;  // two halves: 8 columns + 8 leaders in flight per lane
+#pragma unroll 1
+                for (int h = 0; h < 2; ++h) {
+                    int c[kH];
 #pragma unroll
-            for (int j = 0; j < kWin / 64; ++j) {
-                const Off k = w0 + j * 64 + lane;
-                sc[j * 64 + lane] = col[k < wend ? k : wend - 1];
+                    for (int j = 0; j < kH; ++j) {
+                        const Off k = w0 + (h * kH + j) * 64 + lane;
+                        c[j] = col[k < wend ? k : wend - 1];
+                    }
+#pragma unroll
+                    for (int j = 0; j < kH; ++j) sc[(h * kH + j) * 64 + lane] = lin[c[j]];
+                }
+                __builtin_amdgcn_wave_barrier();
+                const Off lo = b > w0 ? b : w0, hi = e < wend ? e : wend;
+                for (Off k = lo; k < hi; ++k) m = max(m, sc[k - w0]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < kWin / 64; ++j) {
+                    const Off k = w0 + j * 64 + lane;
+                    sc[j * 64 + lane] = col[k < wend ? k : wend - 1];
+                }
+                __builtin_amdgcn_wave_barrier();
+                const Off lo = b > w0 ? b : w0, hi = e < wend ? e : wend;
+                m = row_max_from_lds<Off>(sc, w0, lo, hi, lin, m);
             }
-            __builtin_amdgcn_wave_barrier();
-            const Off lo = b > w0 ? b : w0, hi = e < wend ? e : wend;
-            m = row_max_from_lds<Off>(sc, w0, lo, hi, lin, m);
             __builtin_amdgcn_wave_barrier();
         }
         const bool up = valid && m > own;
@@ -682,10 +703,12 @@ struct Tuning {
     int sparse_blocks = 2048; // grid cap of k_sparse_block (8 resident workgroups per CU)
     int small_chunks = 512;   // fewer 2048-agent chunks than this: 512-agent chunks instead
     int stamp_bshift = 5;     // log2 of the stamp layout's block (stamp_slot)
+    int dense_flat = 1;       // dense rounds gather leaders 64 consecutive edges per load (FLAT)
     int il_min_changes = -1;   // interleaved stamp layout while the last read round changed >= this
                                // (-1: 8e-4 x agents, measured best at 100k, 1M and 10M agents)
     Tuning() {
         il_min_changes = env_int("SWARM_IL_MIN_CHANGES", -1);
+        dense_flat = env_int("SWARM_DENSE_FLAT", 1);
         stamp_bshift = env_int("SWARM_STAMP_BSHIFT", 5);
         dense_blocks = env_int("SWARM_DENSE_BLOCKS", 2048);
         dense_rounds = env_int("SWARM_DENSE_ROUNDS", 8);
@@ -730,7 +753,14 @@ int launch_dense_round(const Off *rp, const int32_t *col, const int32_t *lin, in
                        unsigned long long *ring, unsigned long long *tot, uint8_t *act_w, StampMap sm, int t,
                        int guard, hipStream_t s, const Off *hrp = nullptr, const int32_t *hcol = nullptr) {
     const unsigned grid = grid_for((n + 63) / 64, kWavesPerBlock, unsigned(tuning().dense_blocks));
-    if (act_w && hrp)
+    if (!hrp && sizeof(Off) == 4 && tuning().dense_flat) {
+        if (act_w)
+            hipLaunchKernelGGL((k_elect_dense<Off, true, false, true>), dim3(grid), dim3(kBlock), 0, s, rp, col, lin, lout,
+                               n, n_count, ring, tot, act_w, sm, t, guard, nullptr, nullptr);
+        else
+            hipLaunchKernelGGL((k_elect_dense<Off, false, false, true>), dim3(grid), dim3(kBlock), 0, s, rp, col, lin,
+                               lout, n, n_count, ring, tot, act_w, sm, t, guard, nullptr, nullptr);
+    } else if (act_w && hrp)
         hipLaunchKernelGGL((k_elect_dense<Off, true, true>), dim3(grid), dim3(kBlock), 0, s, rp, col, lin, lout, n,
                            n_count, ring, tot, act_w, sm, t, guard, hrp, hcol);
     else if (act_w)
