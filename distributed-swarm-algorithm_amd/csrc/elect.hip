@@ -297,8 +297,37 @@ __global__ __launch_bounds__(kBlock) void k_elect_dense(
             act_w[stamp_slot(sm, v)] = sw;
             if (DIR)
                 mark_row<Off>(act_w, sm, hcol, hrp[v], hrp[v + 1], Off(1), sw);
-            else
+            else if (!FLAT)
                 mark_row<Off>(act_w, sm, col, b, e, Off(1), sw);
+        }
+        if constexpr (MARK && FLAT && !DIR) {
+            // risers' neighbours marked by a flat re-walk of the wave's col slice: every lane flags
+            // its own row's slots in LDS (1 = riser), then 64 consecutive columns per load (L2-hot,
+            // two cache lines per instruction, where a lane walking its own row touches 64)
+            if (__ballot(up)) {
+                for (Off w0 = W0; w0 < W1; w0 += kWin) {
+                    const Off wend = (W1 - w0 < kWin) ? W1 : w0 + kWin;
+                    const Off lo = b > w0 ? b : w0, hi = e < wend ? e : wend;
+                    for (Off k = lo; k < hi; ++k) sc[k - w0] = up ? 1 : 0;
+                    __builtin_amdgcn_wave_barrier();
+                    constexpr int kH = kWin / 128;
+#pragma unroll 1
+                    for (int h = 0; h < 2; ++h) {
+                        int c[kH];
+                        bool fl[kH];
+#pragma unroll
+                        for (int j = 0; j < kH; ++j) {
+                            const Off k = w0 + (h * kH + j) * 64 + lane;
+                            c[j] = col[k < wend ? k : wend - 1];
+                            fl[j] = k < wend && sc[(h * kH + j) * 64 + lane] != 0;
+                        }
+#pragma unroll
+                        for (int j = 0; j < kH; ++j)
+                            if (fl[j]) act_w[stamp_slot(sm, c[j])] = sw;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
+            }
         }
         b = nb;
         e = ne;
