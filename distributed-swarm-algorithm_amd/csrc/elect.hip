@@ -172,18 +172,61 @@ __device__ __forceinline__ int64_t stamp_agent(const StampMap &m, int64_t k, int
     return int64_t(((uint32_t(j >> m.bshift) * m.M + uint32_t(k)) << m.bshift) | uint32_t(j & ((1 << m.bshift) - 1)));
 }
 
+// 4-byte element idx of base with a 32-bit byte offset (idx < 2^30): the load takes the uniform
+// base in SGPRs and one offset VGPR, where a 64-bit index costs an address pair per load in flight
+// (the sparse kernel runs at the 64-VGPR cap).  Int64 offsets (graphs >= 2^30 edges or agents) use
+// plain indexing.
+template <typename T, typename I>
+__device__ __forceinline__ T ld4(const T *__restrict__ base, I idx) {
+    if constexpr (sizeof(I) == 4 && sizeof(T) == 4)
+        return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + (uint32_t(idx) << 2));
+    else
+        return base[idx];
+}
+template <typename T, typename I>
+__device__ __forceinline__ void st4(T *__restrict__ base, I idx, T v) {
+    if constexpr (sizeof(I) == 4 && sizeof(T) == 4)
+        *reinterpret_cast<T *>(reinterpret_cast<char *>(base) + (uint32_t(idx) << 2)) = v;
+    else
+        base[idx] = v;
+}
+
+// Neighbour columns.  Col32: the CSR's int32 storage indices.  Col16: the same graph with each column
+// stored as a 16-bit delta from its row's 64-agent task base (v & ~63): col16[k] = col[k] - (v & ~63)
+// (swarm_graph_compact; only when every delta fits).  In the spatial storage order a neighbour lies
+// within about one cell row of its agent (7 000 agents at 10M), so the deltas fit, and every column
+// read -- the dense sweep streams all of them -- moves half the bytes.  The base is known wherever a
+// column is read: the dense wave's task, the sparse lane's agent.
+struct Col32 {
+    const int32_t *p;
+    template <typename I>
+    __device__ __forceinline__ int32_t at(I k, int32_t) const { return p[k]; }
+    // 32-bit byte offsets (k < 2^30: the int32-CSR elections)
+    template <typename I>
+    __device__ __forceinline__ int32_t at32(I k, int32_t) const { return ld4(p, k); }
+};
+struct Col16 {
+    const int16_t *p;
+    template <typename I>
+    __device__ __forceinline__ int32_t at(I k, int32_t base) const { return base + int32_t(p[k]); }
+    template <typename I>
+    __device__ __forceinline__ int32_t at32(I k, int32_t base) const {
+        return base + int32_t(*reinterpret_cast<const int16_t *>(reinterpret_cast<const char *>(p) + (uint32_t(k) << 1)));
+    }
+};
+
 constexpr int kKm = 8;  // marking re-walks: col loads in flight per lane
 
 // Mark col[k] for k = k0, k0 + step, ... < e with kKm loads in flight per batch.
-template <typename Off>
-__device__ __forceinline__ void mark_row(uint8_t *aw, const StampMap &sm, const int32_t *__restrict__ col, Off k0,
-                                         Off e, Off step, uint8_t s) {
+template <typename Off, typename CT>
+__device__ __forceinline__ void mark_row(uint8_t *aw, const StampMap &sm, CT cols, int32_t base, Off k0, Off e,
+                                         Off step, uint8_t s) {
     for (Off k = k0; k < e; k += step * kKm) {
         int c[kKm];
 #pragma unroll
         for (int j = 0; j < kKm; ++j) {
             const Off kk = k + step * j;
-            c[j] = col[kk < e ? kk : e - 1];
+            c[j] = cols.at(kk < e ? kk : e - 1, base);
         }
 #pragma unroll
         for (int j = 0; j < kKm; ++j)
@@ -223,9 +266,9 @@ __device__ __forceinline__ int row_max_from_lds(const int *s_col, Off w0, Off lo
 // t+1 can run sparse.
 // DIR: directed graph -- a riser marks the agents that HEAR it (hrp/hcol, the transpose of
 // rp/col), not the agents it hears.
-template <typename Off, bool MARK, bool DIR = false, bool FLAT = false>
+template <typename Off, bool MARK, bool DIR = false, bool FLAT = false, typename CT = Col32>
 __global__ __launch_bounds__(kBlock) void k_elect_dense(
-    const Off *__restrict__ rp, const int32_t *__restrict__ col, const int32_t *__restrict__ lin,
+    const Off *__restrict__ rp, CT cols, const int32_t *__restrict__ lin,
     int32_t *__restrict__ lout, int64_t n, int64_t n_count, unsigned long long *__restrict__ ring,
     unsigned long long *__restrict__ tot, uint8_t *__restrict__ act_w, StampMap sm, int t, int guard,
     const Off *__restrict__ hrp = nullptr, const int32_t *__restrict__ hcol = nullptr) {
@@ -251,6 +294,7 @@ __global__ __launch_bounds__(kBlock) void k_elect_dense(
     if (task < ntask) bounds(task, b, e);
     for (; task < ntask; task += stride) {
         const int64_t v = task * 64 + lane;
+        const int32_t tbase = int32_t(task * 64);  // Col16 deltas are relative to the task's first agent
         const bool valid = v < n;
         const Off W0 = __shfl(b, 0, 64), W1 = __shfl(e, 63, 64);
         const int own = lin[valid ? v : n - 1];
@@ -270,7 +314,7 @@ __global__ __launch_bounds__(kBlock) void k_elect_dense(
 #pragma unroll
                     for (int j = 0; j < kH; ++j) {
                         const Off k = w0 + (h * kH + j) * 64 + lane;
-                        c[j] = col[k < wend ? k : wend - 1];
+                        c[j] = cols.at(k < wend ? k : wend - 1, tbase);
                     }
 #pragma unroll
                     for (int j = 0; j < kH; ++j) sc[(h * kH + j) * 64 + lane] = lin[c[j]];
@@ -282,7 +326,7 @@ __global__ __launch_bounds__(kBlock) void k_elect_dense(
 #pragma unroll
                 for (int j = 0; j < kWin / 64; ++j) {
                     const Off k = w0 + j * 64 + lane;
-                    sc[j * 64 + lane] = col[k < wend ? k : wend - 1];
+                    sc[j * 64 + lane] = cols.at(k < wend ? k : wend - 1, tbase);
                 }
                 __builtin_amdgcn_wave_barrier();
                 const Off lo = b > w0 ? b : w0, hi = e < wend ? e : wend;
@@ -296,9 +340,9 @@ __global__ __launch_bounds__(kBlock) void k_elect_dense(
         if (MARK && up) {
             act_w[stamp_slot(sm, v)] = sw;
             if (DIR)
-                mark_row<Off>(act_w, sm, hcol, hrp[v], hrp[v + 1], Off(1), sw);
+                mark_row<Off>(act_w, sm, Col32{hcol}, 0, hrp[v], hrp[v + 1], Off(1), sw);
             else if (!FLAT)
-                mark_row<Off>(act_w, sm, col, b, e, Off(1), sw);
+                mark_row<Off>(act_w, sm, cols, tbase, b, e, Off(1), sw);
         }
         if constexpr (MARK && FLAT && !DIR) {
             // risers' neighbours marked by a flat re-walk of the wave's col slice: every lane flags
@@ -318,7 +362,7 @@ __global__ __launch_bounds__(kBlock) void k_elect_dense(
 #pragma unroll
                         for (int j = 0; j < kH; ++j) {
                             const Off k = w0 + (h * kH + j) * 64 + lane;
-                            c[j] = col[k < wend ? k : wend - 1];
+                            c[j] = cols.at(k < wend ? k : wend - 1, tbase);
                             fl[j] = k < wend && sc[(h * kH + j) * 64 + lane] != 0;
                         }
 #pragma unroll
@@ -358,26 +402,8 @@ struct Frontier {
     int64_t n_rows, n_all;   // rows stepped (owned + ghosts in sharded runs), all agents
     int64_t n_count;         // rows [0, n_count) are owned: only their changes are counted
     StampMap sm, wsm;
+    const int16_t *c16;      // Col16 columns of the same graph (swarm_graph_compact), or nullptr
 };
-
-// 4-byte element idx of base with a 32-bit byte offset (idx < 2^30): the load takes the uniform
-// base in SGPRs and one offset VGPR, where a 64-bit index costs an address pair per load in flight
-// (the sparse kernel runs at the 64-VGPR cap).  Int64 offsets (graphs >= 2^30 edges or agents) use
-// plain indexing.
-template <typename T, typename I>
-__device__ __forceinline__ T ld4(const T *__restrict__ base, I idx) {
-    if constexpr (sizeof(I) == 4 && sizeof(T) == 4)
-        return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + (uint32_t(idx) << 2));
-    else
-        return base[idx];
-}
-template <typename T, typename I>
-__device__ __forceinline__ void st4(T *__restrict__ base, I idx, T v) {
-    if constexpr (sizeof(I) == 4 && sizeof(T) == 4)
-        *reinterpret_cast<T *>(reinterpret_cast<char *>(base) + (uint32_t(idx) << 2)) = v;
-    else
-        base[idx] = v;
-}
 
 // Max over the G lanes of an agent's group (G = 4: a quad) through DPP quad permutes -- register
 // moves inside the wave, where __shfl_xor would be two LDS round trips (ds_bpermute).
@@ -423,8 +449,8 @@ __device__ __forceinline__ int wave_excl_scan(int c, int &total) {
 // `first`/`step` select this wave's share; risers mark themselves and their neighbours.  Lane
 // `sub` of an agent takes edges b + sub + G*j (interleaved: one load instruction covers G
 // consecutive edges of every agent it serves, so each touches one cache line per agent).
-template <typename Off, int G, int K, bool DIR>
-__device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, const int32_t *__restrict__ col,
+template <typename Off, int G, int K, bool DIR, typename CT>
+__device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, CT cols,
                                               const Off *__restrict__ hrp, const int32_t *__restrict__ hcol,
                                               const int32_t *__restrict__ P, int32_t *__restrict__ Q,
                                               uint8_t *__restrict__ aw, const StampMap &sm, uint8_t sw,
@@ -455,7 +481,7 @@ __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, const 
         int c[K];
         for (Off k = b + sub; k < e; k += G * K) {
 #pragma unroll
-            for (int j = 0; j < K; ++j) c[j] = ld4(col, (k + G * j < e) ? k + G * j : e - 1);
+            for (int j = 0; j < K; ++j) c[j] = cols.at32((k + G * j < e) ? k + G * j : e - 1, v & ~63);
             int val[K];
 #pragma unroll
             for (int j = 0; j < K; ++j) val[j] = ld4(P, Ix(c[j]));
@@ -468,13 +494,13 @@ __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, const 
         if (up) {
             if (sub == 0) aw[stamp_slot(sm, v)] = sw;
             if (DIR) {  // the agents that hear v
-                mark_row<Off>(aw, sm, hcol, hrp[v] + sub, hrp[v + 1], Off(G), sw);
+                mark_row<Off>(aw, sm, Col32{hcol}, 0, hrp[v] + sub, hrp[v + 1], Off(G), sw);
             } else if (e - b <= G * K) {  // one pass: c[] still holds this lane's edges
 #pragma unroll
                 for (int j = 0; j < K; ++j)
                     if (b + sub + G * j < e) aw[stamp_slot(sm, c[j])] = sw;
             } else {
-                mark_row<Off>(aw, sm, col, b + sub, e, Off(G), sw);
+                mark_row<Off>(aw, sm, cols, v & ~63, b + sub, e, Off(G), sw);
             }
         }
         my_chg += __popcll(__ballot(up && sub == 0 && v < n_count));
@@ -535,9 +561,9 @@ __device__ __forceinline__ void flush_counts(unsigned long long *ring, int t, lo
 
 // One workgroup per chunk of kBlock * S agents: S stamps per thread, the chunk's marked agents
 // compacted in LDS and gathered by the whole workgroup.
-template <typename Off, int S = kScan, bool DIR = false, int G = kG, int K = kKs>
+template <typename Off, int S = kScan, bool DIR = false, typename CT = Col32, int G = kG, int K = kKs>
 __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_block(
-    const Off *__restrict__ rp, const int32_t *__restrict__ col, Frontier f, int t, int guard,
+    const Off *__restrict__ rp, CT cols, Frontier f, int t, int guard,
     const Off *__restrict__ hrp = nullptr, const int32_t *__restrict__ hcol = nullptr) {
     using W = typename StampWord<S>::T;
     constexpr int kChunk = kBlock * S;
@@ -624,7 +650,7 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
             listed = listed + total < kListCap ? listed + total : kListCap;
             __syncthreads();  // list entries visible
             if (listed < kListCap) break;  // everything fitted
-            gather_listed<Off, G, K, DIR>(rp, col, hrp, hcol, P, Q, aw, f.wsm, sw, s_list, listed, wid * (64 / G),
+            gather_listed<Off, G, K, DIR>(rp, cols, hrp, hcol, P, Q, aw, f.wsm, sw, s_list, listed, wid * (64 / G),
                                           kBlock / G, f.n_count, my_chg, my_act, my_edges);
             listed = 0;
             __syncthreads();  // the list is reused
@@ -634,7 +660,7 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
     ph_listed = wall_clock64();
 #endif
     if (listed > 0)
-        gather_listed<Off, G, K, DIR>(rp, col, hrp, hcol, P, Q, aw, f.wsm, sw, s_list, listed, wid * (64 / G),
+        gather_listed<Off, G, K, DIR>(rp, cols, hrp, hcol, P, Q, aw, f.wsm, sw, s_list, listed, wid * (64 / G),
                                       kBlock / G, f.n_count, my_chg, my_act, my_edges);
 #ifdef SWARM_PHASES
     ph_gathered = wall_clock64() + (my_chg & 0);
@@ -693,6 +719,22 @@ __global__ __launch_bounds__(kBlock) void k_frontier_ghosts(const Off *__restric
         atomicAdd(slot(f.ring, t, C_GHOST, blockIdx.x & (kShards - 1)), (unsigned long long)rises);
 }
 
+// Col16 copy of an int32 CSR: col16[k] = col[k] - (v & ~63) for every edge k of row v; *bad is set
+// when a delta does not fit 16 bits (the caller then keeps the int32 columns).
+__global__ __launch_bounds__(kBlock) void k_build_col16(const int32_t *__restrict__ rp, const int32_t *__restrict__ col,
+                                                        int64_t n, int16_t *__restrict__ col16, int *__restrict__ bad) {
+    int out = 0;
+    for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < n; v += int64_t(gridDim.x) * kBlock) {
+        const int32_t base = int32_t(v) & ~63;
+        for (int32_t k = rp[v]; k < rp[v + 1]; ++k) {
+            const int32_t d = col[k] - base;
+            out |= (d < -32768 || d > 32767) ? 1 : 0;
+            col16[k] = int16_t(d);
+        }
+    }
+    if (__ballot(out) && (threadIdx.x & 63) == 0) atomicOr(bad, 1);
+}
+
 __global__ __launch_bounds__(kBlock) void k_state(const int32_t *__restrict__ leader,
                                                  const int32_t *__restrict__ ids,
                                                  uint8_t *__restrict__ state, int64_t n) {
@@ -733,10 +775,12 @@ struct Tuning {
     int small_chunks = 512;   // fewer 2048-agent chunks than this: 512-agent chunks instead
     int stamp_bshift = 5;     // log2 of the stamp layout's block (stamp_slot)
     int dense_flat = 1;       // dense rounds gather leaders 64 consecutive edges per load (FLAT)
+    int use_c16 = 1;          // swarm_elect_compact reads the 16-bit columns (0: its int32 ones; A/B aid)
     int il_min_changes = -1;   // interleaved stamp layout while the last read round changed >= this
                                // (-1: 8e-4 x agents, measured best at 100k, 1M and 10M agents)
     Tuning() {
         il_min_changes = env_int("SWARM_IL_MIN_CHANGES", -1);
+        use_c16 = env_int("SWARM_C16", 1);
         dense_flat = env_int("SWARM_DENSE_FLAT", 1);
         stamp_bshift = env_int("SWARM_STAMP_BSHIFT", 5);
         dense_blocks = env_int("SWARM_DENSE_BLOCKS", 2048);
@@ -780,23 +824,33 @@ size_t act_bytes(int64_t n_all) {  // one parity: every chunk of the stamp layou
 template <typename Off>
 int launch_dense_round(const Off *rp, const int32_t *col, const int32_t *lin, int32_t *lout, int64_t n, int64_t n_count,
                        unsigned long long *ring, unsigned long long *tot, uint8_t *act_w, StampMap sm, int t,
-                       int guard, hipStream_t s, const Off *hrp = nullptr, const int32_t *hcol = nullptr) {
+                       int guard, hipStream_t s, const Off *hrp = nullptr, const int32_t *hcol = nullptr,
+                       const int16_t *c16 = nullptr) {
     const unsigned grid = grid_for((n + 63) / 64, kWavesPerBlock, unsigned(tuning().dense_blocks));
-    if (!hrp && sizeof(Off) == 4 && tuning().dense_flat) {
+    const Col32 c32{col};
+    if (!hrp && sizeof(Off) == 4 && tuning().dense_flat && c16) {
+        const Col16 cc{c16};
         if (act_w)
-            hipLaunchKernelGGL((k_elect_dense<Off, true, false, true>), dim3(grid), dim3(kBlock), 0, s, rp, col, lin, lout,
-                               n, n_count, ring, tot, act_w, sm, t, guard, nullptr, nullptr);
+            hipLaunchKernelGGL((k_elect_dense<Off, true, false, true, Col16>), dim3(grid), dim3(kBlock), 0, s, rp, cc,
+                               lin, lout, n, n_count, ring, tot, act_w, sm, t, guard, nullptr, nullptr);
         else
-            hipLaunchKernelGGL((k_elect_dense<Off, false, false, true>), dim3(grid), dim3(kBlock), 0, s, rp, col, lin,
+            hipLaunchKernelGGL((k_elect_dense<Off, false, false, true, Col16>), dim3(grid), dim3(kBlock), 0, s, rp, cc,
+                               lin, lout, n, n_count, ring, tot, act_w, sm, t, guard, nullptr, nullptr);
+    } else if (!hrp && sizeof(Off) == 4 && tuning().dense_flat) {
+        if (act_w)
+            hipLaunchKernelGGL((k_elect_dense<Off, true, false, true>), dim3(grid), dim3(kBlock), 0, s, rp, c32, lin,
+                               lout, n, n_count, ring, tot, act_w, sm, t, guard, nullptr, nullptr);
+        else
+            hipLaunchKernelGGL((k_elect_dense<Off, false, false, true>), dim3(grid), dim3(kBlock), 0, s, rp, c32, lin,
                                lout, n, n_count, ring, tot, act_w, sm, t, guard, nullptr, nullptr);
     } else if (act_w && hrp)
-        hipLaunchKernelGGL((k_elect_dense<Off, true, true>), dim3(grid), dim3(kBlock), 0, s, rp, col, lin, lout, n,
+        hipLaunchKernelGGL((k_elect_dense<Off, true, true>), dim3(grid), dim3(kBlock), 0, s, rp, c32, lin, lout, n,
                            n_count, ring, tot, act_w, sm, t, guard, hrp, hcol);
     else if (act_w)
-        hipLaunchKernelGGL((k_elect_dense<Off, true>), dim3(grid), dim3(kBlock), 0, s, rp, col, lin, lout, n, n_count, ring,
+        hipLaunchKernelGGL((k_elect_dense<Off, true>), dim3(grid), dim3(kBlock), 0, s, rp, c32, lin, lout, n, n_count, ring,
                            tot, act_w, sm, t, guard, nullptr, nullptr);
     else
-        hipLaunchKernelGGL((k_elect_dense<Off, false>), dim3(grid), dim3(kBlock), 0, s, rp, col, lin, lout, n, n_count, ring,
+        hipLaunchKernelGGL((k_elect_dense<Off, false>), dim3(grid), dim3(kBlock), 0, s, rp, c32, lin, lout, n, n_count, ring,
                            tot, act_w, sm, t, guard, nullptr, nullptr);
     SW_LAUNCHED();
     return SWARM_OK;
@@ -861,21 +915,28 @@ int launch_frontier_round(const Off *rp, const int32_t *col, const Frontier &f, 
         return launch_dense_round<Off>(rp, col, f.L[(t - 1) & 1], f.L[t & 1], f.n_rows, f.n_count, f.ring,
                                        f.tot,
                                        k == RK_DENSE_MARK ? f.act[(t + 1) & 1] : nullptr, f.wsm, t, guard, s, hrp,
-                                       hcol);
+                                       hcol, f.c16);
     // the buffer this round marks into (parity t+1) was read by round t-1; every 256 rounds, per
     // parity, it is cleared first, so no stamp outlives the 510 rounds after which its value
     // recurs (take_stamps)
     if (t > 2 && ((t - 1) & 255) < 2) SW_HIP(hipMemsetAsync(f.act[(t + 1) & 1], 0, act_bytes(f.n_all), s));
     const bool small = f.sm.cshift == 9;  // small swarm: 512-agent chunks, 4x the workgroups
     const dim3 grid(grid_for(f.sm.M, 1, unsigned(tuning().sparse_blocks)));
+    const Col32 c32{col};
     if (hrp && small)
-        hipLaunchKernelGGL((k_sparse_block<Off, 2, true>), grid, dim3(kBlock), 0, s, rp, col, f, t, guard, hrp, hcol);
+        hipLaunchKernelGGL((k_sparse_block<Off, 2, true>), grid, dim3(kBlock), 0, s, rp, c32, f, t, guard, hrp, hcol);
     else if (hrp)
-        hipLaunchKernelGGL((k_sparse_block<Off, kScan, true>), grid, dim3(kBlock), 0, s, rp, col, f, t, guard, hrp, hcol);
+        hipLaunchKernelGGL((k_sparse_block<Off, kScan, true>), grid, dim3(kBlock), 0, s, rp, c32, f, t, guard, hrp, hcol);
+    else if (f.c16 && sizeof(Off) == 4 && small)
+        hipLaunchKernelGGL((k_sparse_block<Off, 2, false, Col16>), grid, dim3(kBlock), 0, s, rp, Col16{f.c16}, f, t,
+                           guard, nullptr, nullptr);
+    else if (f.c16 && sizeof(Off) == 4)
+        hipLaunchKernelGGL((k_sparse_block<Off, kScan, false, Col16>), grid, dim3(kBlock), 0, s, rp, Col16{f.c16}, f, t,
+                           guard, nullptr, nullptr);
     else if (small)
-        hipLaunchKernelGGL((k_sparse_block<Off, 2>), grid, dim3(kBlock), 0, s, rp, col, f, t, guard, nullptr, nullptr);
+        hipLaunchKernelGGL((k_sparse_block<Off, 2>), grid, dim3(kBlock), 0, s, rp, c32, f, t, guard, nullptr, nullptr);
     else
-        hipLaunchKernelGGL((k_sparse_block<Off>), grid, dim3(kBlock), 0, s, rp, col, f, t, guard, nullptr, nullptr);
+        hipLaunchKernelGGL((k_sparse_block<Off>), grid, dim3(kBlock), 0, s, rp, c32, f, t, guard, nullptr, nullptr);
     SW_LAUNCHED();
     return SWARM_OK;
 }
@@ -893,7 +954,8 @@ template <typename Off>
 int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, const int32_t *ids,
                int32_t *leader, uint8_t *state, int32_t max_rounds, int32_t mode,
                int32_t *rounds_exec, int64_t *changes_host, swarm_elect_stats *st,
-               void *stream, const Off *hrp = nullptr, const int32_t *hcol = nullptr) {
+               void *stream, const Off *hrp = nullptr, const int32_t *hcol = nullptr,
+               const int16_t *c16 = nullptr) {
     SW_ARG(ctx != nullptr, "ctx is NULL");
     SW_ARG(n >= 0, "n < 0");
     SW_ARG(n < (int64_t(1) << 31), "n must be < 2^31");
@@ -935,6 +997,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         int rc0 = frontier_alloc(ctx, n, n, bufs[0], bufs[1], &f, s);
         if (rc0) return rc0;
         ring = f.ring;
+        f.c16 = c16;
     } else {
         SW_ALLOC(ring, ctx, S_CHANGES, ring_bytes());
         SW_HIP(hipMemsetAsync(ring, 0, ring_bytes(), s));
@@ -991,7 +1054,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
             if (mode == SWARM_ELECT_DENSE) {
                 kinds[r - t] = RK_DENSE;
                 rc = launch_dense_round<Off>(rp, col, bufs[(r - 1) & 1], bufs[r & 1], n, n, ring, nullptr, nullptr,
-                                             StampMap{}, r, 1, s);
+                                             StampMap{}, r, 1, s, nullptr, nullptr, c16);
             } else {
                 kinds[r - t] = plan_round(r);
                 // marks for round r+1: interleaved layout while rounds are busy (balance), agent
@@ -1130,6 +1193,44 @@ int swarm_elect(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t
                 swarm_elect_stats *stats, void *stream) {
     return swarm::elect_impl<int32_t>(ctx, n, row_ptr, col, ids, leader, state, max_rounds, mode,
                                       rounds_exec, changes_per_round, stats, stream);
+}
+
+int swarm_graph_compact(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col, int16_t *col16,
+                        void *stream) {
+    using namespace swarm;
+    SW_ARG(ctx != nullptr, "ctx is NULL");
+    if (!ctx_on_current_device(ctx)) return SWARM_ERR_ARG;
+    SW_ARG(n >= 0 && n < (int64_t(1) << 30), "n out of range (< 2^30)");
+    if (n == 0) return SWARM_OK;
+    SW_ARG(row_ptr != nullptr, "row_ptr is NULL");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int32_t e_total = 0;
+    SW_HIP(hipMemcpyAsync(&e_total, row_ptr + n, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    SW_HIP(hipStreamSynchronize(s));
+    SW_ARG(e_total >= 0 && e_total < (int32_t(1) << 30), "int32 CSR supports < 2^30 edges");
+    if (e_total == 0) return SWARM_OK;
+    SW_ARG(col && col16, "NULL array");
+    int *bad;
+    SW_ALLOC(bad, ctx, S_TMP1, sizeof(int));
+    SW_HIP(hipMemsetAsync(bad, 0, sizeof(int), s));
+    hipLaunchKernelGGL(k_build_col16, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, row_ptr, col, n, col16, bad);
+    SW_LAUNCHED();
+    int hbad = 0;
+    SW_HIP(hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, s));
+    SW_HIP(hipStreamSynchronize(s));
+    if (hbad) {
+        set_error("a neighbour lies more than 32767 storage slots from its row's 64-agent base: keep the int32 columns");
+        return SWARM_ERR_RANGE;
+    }
+    return SWARM_OK;
+}
+
+int swarm_elect_compact(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col, const int16_t *col16,
+                        const int32_t *ids, int32_t *leader, uint8_t *state, int32_t max_rounds, int32_t mode,
+                        int32_t *rounds_exec, int64_t *changes_per_round, swarm_elect_stats *stats, void *stream) {
+    return swarm::elect_impl<int32_t>(ctx, n, row_ptr, col, ids, leader, state, max_rounds, mode, rounds_exec,
+                                      changes_per_round, stats, stream, nullptr, nullptr,
+                                      swarm::tuning().use_c16 ? col16 : nullptr);
 }
 
 int swarm_elect_directed(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col,

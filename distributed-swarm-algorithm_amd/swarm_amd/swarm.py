@@ -176,9 +176,35 @@ class Swarm:
         return self
 
     # ------------------------------------------------------------------ election
-    def elect(self, mode: str = "frontier", max_rounds: int = 1 << 16, timed: bool = False) -> ElectResult:
-        """Contract E2 to convergence on the GPU (swarm_elect; swarm_elect_directed when the
-        neighbour lists are not symmetric).  timed: per-kernel HIP events."""
+    def graph_compact(self) -> torch.Tensor | None:
+        """16-bit columns of the (symmetric) neighbour graph (swarm_graph_compact: each neighbour as
+        a delta from its row's 64-agent base), built on first use and rebuilt whenever row_ptr / col
+        are replaced or modified in place; None when a delta does not fit (the int32 columns are
+        used then) or the graph is directed."""
+        if self.row_ptr is None or getattr(self, "_hear", None) is not None or not 0 < self.n < (1 << 30):
+            return None
+        key = (self.row_ptr.data_ptr(), self.col.data_ptr(), self.row_ptr._version, self.col._version,
+               self.n, self.col.numel())
+        cached = getattr(self, "_c16", None)
+        if cached is None or cached[0] != key:
+            c16 = torch.empty(max(self.col.numel(), 1), dtype=torch.int16, device=self.device)
+            with torch.cuda.device(self.device):
+                rc = _lib.lib().swarm_graph_compact(_lib.ctx(), self.n, _lib.ptr(self.row_ptr, torch.int32),
+                                                    _lib.ptr(self.col, torch.int32) if self.col.numel() else None,
+                                                    _lib.ptr(c16), _lib.stream())
+            if rc == _lib.ERR_RANGE:
+                c16 = None
+            else:
+                _lib.check(rc)
+            self._c16 = cached = (key, c16)
+        return cached[1]
+
+    def elect(self, mode: str = "frontier", max_rounds: int = 1 << 16, timed: bool = False,
+              compact: bool = True) -> ElectResult:
+        """Contract E2 to convergence on the GPU (swarm_elect_compact with the graph's 16-bit
+        columns when they fit; swarm_elect_directed when the neighbour lists are not symmetric).
+        timed: per-kernel HIP events.  compact=False: the int32-column entry point swarm_elect
+        (same results)."""
         if self.row_ptr is None:
             raise RuntimeError("no neighbour graph: call build_graph() or set_graph()")
         m = {"dense": _lib.ELECT_DENSE, "frontier": _lib.ELECT_FRONTIER}[mode] | (_lib.ELECT_TIMED if timed else 0)
@@ -189,7 +215,14 @@ class Swarm:
         st = _lib.ElectStats()
         hear = getattr(self, "_hear", None)
         with torch.cuda.device(self.device):
-            if hear is None:  # symmetric graph: risers mark through their own rows
+            c16 = self.graph_compact() if (compact and hear is None) else None
+            if c16 is not None:  # symmetric graph, 16-bit columns
+                rc = _lib.check(_lib.lib().swarm_elect_compact(
+                    _lib.ctx(), n, _lib.ptr(self.row_ptr, torch.int32), _lib.ptr(self.col, torch.int32),
+                    _lib.ptr(c16), _lib.ptr(self.ids, torch.int32), _lib.ptr(self.leader, torch.int32),
+                    _lib.ptr(self.state, torch.uint8), cap, m, ctypes.byref(rounds),
+                    changes.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st), _lib.stream()))
+            elif hear is None:  # symmetric graph: risers mark through their own rows
                 rc = _lib.check(_lib.lib().swarm_elect(
                     _lib.ctx(), n, _lib.ptr(self.row_ptr, torch.int32), _lib.ptr(self.col, torch.int32),
                     _lib.ptr(self.ids, torch.int32), _lib.ptr(self.leader, torch.int32),

@@ -121,6 +121,21 @@ int swarm_elect_directed(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, cons
                          int32_t *rounds_exec, int64_t *changes_per_round, swarm_elect_stats *stats,
                          void *stream);
 
+/* Compact (16-bit) columns of a symmetric int32 CSR for the elections (an MI355X layout, no reference
+ * counterpart): col16[k] = col[k] - (v & ~63) for every edge k of row v, i.e. each neighbour as a
+ * delta from its row's 64-agent base.  In a spatial storage order (swarm_cell_order) a neighbour lies
+ * within about one grid row of its agent, so the deltas fit and every column read moves half the
+ * bytes.  col16 (device, row_ptr[n] int16, caller-allocated).  Returns SWARM_ERR_RANGE (col16
+ * unusable) when a delta does not fit in 16 bits.  Rebuild it whenever the graph changes. */
+int swarm_graph_compact(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col, int16_t *col16,
+                        void *stream);
+
+/* swarm_elect reading the graph's compact columns (swarm_graph_compact of the same row_ptr/col;
+ * col16 NULL: same as swarm_elect).  Same results, same stats. */
+int swarm_elect_compact(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col, const int16_t *col16,
+                        const int32_t *ids, int32_t *leader, uint8_t *state, int32_t max_rounds, int32_t mode,
+                        int32_t *rounds_exec, int64_t *changes_per_round, swarm_elect_stats *stats, void *stream);
+
 /* Same with int64 row offsets: graphs with >= 2^30 edges or agents (the int32-CSR entry points
  * address with 32-bit byte offsets and reject them with SWARM_ERR_ARG). */
 int swarm_elect_i64(swarm_ctx *ctx, int64_t n, const int64_t *row_ptr, const int32_t *col,

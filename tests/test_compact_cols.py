@@ -1,0 +1,108 @@
+"""16-bit column deltas for the election (swarm_graph_compact / swarm_elect_compact).
+
+The compact columns are an MI355X layout with no reference counterpart: the bar is that the
+election through them returns exactly what the int32-column path and the oracle return (leaders,
+states, rounds, every per-round change count; reference semantics agent.py:263-275), in both
+modes and at both sparse chunk sizes, and that a graph whose deltas do not fit is refused
+(SWARM_ERR_RANGE) and elected through the int32 columns instead.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def sw():
+    import swarm_amd.swarm as swm
+    from swarm_amd import _lib
+    _lib.load()
+    return swm
+
+
+def c16_np(rp, col):
+    """numpy restatement of the documented layout (include/swarm.h, swarm_graph_compact)."""
+    src = np.repeat(np.arange(len(rp) - 1, dtype=np.int64), np.diff(rp))
+    return (np.asarray(col, np.int64) - (src & ~63)).astype(np.int16)
+
+
+def test_graph_compact_layout(sw):
+    from swarm_amd import gen
+    d = gen.swarm_inputs(200000, 31)
+    s = sw.Swarm(d["ids"], d["x"], d["y"], device="cuda").build_graph(1.0)
+    c = s.graph_compact()
+    assert c is not None
+    np.testing.assert_array_equal(c.cpu().numpy(), c16_np(s.row_ptr.cpu().numpy(), s.col.cpu().numpy()))
+
+
+@pytest.mark.parametrize("n,seed", [(120000, 51), (1_200_000, 52)])
+def test_elect_compact_vs_int32_vs_oracle(sw, oracle_mod, n, seed):
+    # 120k agents: 512-stamp chunks; 1.2M: 2 048-stamp chunks
+    from swarm_amd import gen
+    d = gen.swarm_inputs(n, seed)
+    s = sw.Swarm(d["ids"], d["x"], d["y"], device="cuda").build_graph(1.0)
+    assert s.graph_compact() is not None
+    lead, state, rounds, changes = oracle_mod.elect(s.row_ptr.cpu().numpy(), s.col.cpu().numpy(),
+                                                    s.ids.cpu().numpy())
+    for mode in ("frontier", "dense"):
+        for compact in (True, False):
+            r = s.elect(mode=mode, compact=compact)
+            assert r.converged and r.rounds_exec == rounds, (mode, compact)
+            np.testing.assert_array_equal(r.changes, changes)
+            np.testing.assert_array_equal(r.leader.cpu().numpy(), lead)
+            np.testing.assert_array_equal(r.state.cpu().numpy(), state)
+
+
+def test_far_neighbours_refused_and_elected_with_int32(sw, oracle_mod):
+    """Input storage order of a random swarm: neighbours lie anywhere, deltas overflow int16."""
+    from swarm_amd import _lib, gen
+    d = gen.swarm_inputs(100000, 61)
+    s = sw.Swarm(d["ids"], d["x"], d["y"], layout="input", device="cuda").build_graph(1.0)
+    c16 = torch.empty(s.n_edges, dtype=torch.int16, device="cuda")
+    rc = _lib.lib().swarm_graph_compact(_lib.ctx(), s.n, _lib.ptr(s.row_ptr), _lib.ptr(s.col), _lib.ptr(c16),
+                                        _lib.stream())
+    assert rc == _lib.ERR_RANGE
+    assert s.graph_compact() is None
+    r = s.elect()
+    lead, state, rounds, changes = oracle_mod.elect(s.row_ptr.cpu().numpy(), s.col.cpu().numpy(),
+                                                    s.ids.cpu().numpy())
+    assert r.rounds_exec == rounds
+    np.testing.assert_array_equal(r.changes, changes)
+    np.testing.assert_array_equal(r.leader.cpu().numpy(), lead)
+
+
+def test_compact_rebuilt_after_graph_change(sw, oracle_mod):
+    from swarm_amd import gen
+    d = gen.swarm_inputs(50000, 12)
+    s = sw.Swarm(d["ids"], d["x"], d["y"], device="cuda").build_graph(1.0)
+    r1 = s.elect()
+    c1 = s.graph_compact()
+    assert s.graph_compact() is c1  # cached while the graph is unchanged
+    # in place: every edge now points at its own agent (no propagation at all)
+    s.col.copy_(torch.repeat_interleave(torch.arange(s.n, dtype=torch.int32, device="cuda"),
+                                        s.row_ptr.diff().long()))
+    r2 = s.elect()
+    assert s.graph_compact() is not c1
+    assert r1.rounds_exec > 1 and r2.rounds_exec == 1
+    np.testing.assert_array_equal(r2.leader.cpu().numpy(), s.ids.cpu().numpy())
+
+
+def test_elect_compact_null_is_int32_path(sw, oracle_mod):
+    """swarm_elect_compact with col16 = NULL is swarm_elect."""
+    from swarm_amd import _lib, gen
+    d = gen.swarm_inputs(30000, 21)
+    s = sw.Swarm(d["ids"], d["x"], d["y"], device="cuda").build_graph(1.0)
+    lead = torch.empty(s.n, dtype=torch.int32, device="cuda")
+    state = torch.empty(s.n, dtype=torch.uint8, device="cuda")
+    rounds = ctypes.c_int32(0)
+    _lib.check(_lib.lib().swarm_elect_compact(_lib.ctx(), s.n, _lib.ptr(s.row_ptr), _lib.ptr(s.col), None,
+                                              _lib.ptr(s.ids), _lib.ptr(lead), _lib.ptr(state), 1 << 16,
+                                              _lib.ELECT_FRONTIER, ctypes.byref(rounds), None, None, _lib.stream()))
+    o_lead, o_state, o_rounds, _ = oracle_mod.elect(s.row_ptr.cpu().numpy(), s.col.cpu().numpy(),
+                                                    s.ids.cpu().numpy())
+    assert rounds.value == o_rounds
+    np.testing.assert_array_equal(lead.cpu().numpy(), o_lead)
+    np.testing.assert_array_equal(state.cpu().numpy(), o_state)
