@@ -171,6 +171,10 @@ def main():
                "bytes_per_launch": rt.sparse_bytes / rt.sparse_launches,
                "avg_launch_ms": rt.sparse_ms / rt.sparse_launches, "launches": rt.sparse_launches,
                "traffic": pmc[0] if pmc else None, "traffic_source": pmc[1] if pmc else None,
+               # the per-unit figure counts 4 B per column; the compact columns read 2
+               "columns": "int16 deltas (swarm_elect_compact)" if getattr(rt, "compact", False) else "int32",
+               "bytes_per_launch_columns_as_read": (rt.sparse_bytes - (2.0 if getattr(rt, "compact", False) else 0.0)
+                                                    * (rt.edges_total - rt.dense_rounds * e)) / rt.sparse_launches,
                "all_rounds": {"bytes_per_launch": rt.bytes_total / max(rt.timed_launches, 1),
                               "avg_launch_ms": rt.gather_ms / max(rt.timed_launches, 1),
                               "launches": rt.timed_launches, "dense_rounds": rt.dense_rounds}}

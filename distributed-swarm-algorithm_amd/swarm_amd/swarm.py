@@ -242,6 +242,7 @@ class Swarm:
         res.changes_total = st.changes_total
         res.gather_ms, res.apply_ms, res.timed_launches = st.gather_ms, st.apply_ms, st.gather_launches
         res.sparse_ms, res.sparse_launches, res.sparse_bytes = st.sparse_ms, st.sparse_launches, st.sparse_bytes
+        res.compact = c16 is not None  # the rounds read the 16-bit columns (2 of the 4 column bytes)
         return res
 
     # ------------------------------------------------------------------ allocation
