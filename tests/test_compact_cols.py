@@ -34,7 +34,7 @@ def test_graph_compact_layout(sw):
     d = gen.swarm_inputs(200000, 31)
     s = sw.Swarm(d["ids"], d["x"], d["y"], device="cuda").build_graph(1.0)
     c = s.graph_compact()
-    assert c is not None
+    assert c is not None and c.numel() == s.n_edges
     np.testing.assert_array_equal(c.cpu().numpy(), c16_np(s.row_ptr.cpu().numpy(), s.col.cpu().numpy()))
 
 
