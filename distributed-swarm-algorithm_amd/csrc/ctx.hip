@@ -70,6 +70,34 @@ void *pinned(swarm_ctx *ctx, size_t bytes) {
     return p;
 }
 
+// Host memory the device writes directly (coherent, mapped): the election's per-batch counter
+// read-back lands here from the totals kernel itself, with no copy in the stream.
+void *mapped(swarm_ctx *ctx, size_t bytes, void **dev) {
+    if (ctx->mapped_cap < bytes) {
+        if (ctx->host_mapped) (void)hipHostFree(ctx->host_mapped);
+        ctx->host_mapped = ctx->mapped_dev = nullptr;
+        ctx->mapped_cap = 0;
+        void *p = nullptr;
+        hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocCoherent | hipHostMallocMapped);
+        if (e != hipSuccess) {
+            set_error("hipHostMalloc(%zu, coherent|mapped) -> %s", bytes, hipGetErrorString(e));
+            return nullptr;
+        }
+        void *d = nullptr;
+        e = hipHostGetDevicePointer(&d, p, 0);
+        if (e != hipSuccess) {
+            (void)hipHostFree(p);
+            set_error("hipHostGetDevicePointer -> %s", hipGetErrorString(e));
+            return nullptr;
+        }
+        ctx->host_mapped = p;
+        ctx->mapped_dev = d;
+        ctx->mapped_cap = bytes;
+    }
+    *dev = ctx->mapped_dev;
+    return ctx->host_mapped;
+}
+
 }  // namespace swarm
 
 extern "C" {
@@ -95,6 +123,7 @@ int swarm_ctx_destroy(swarm_ctx *ctx) {
     for (int s = 0; s < swarm::S_NUM; ++s)
         if (ctx->slot[s]) (void)hipFree(ctx->slot[s]);
     if (ctx->host_pinned) (void)hipHostFree(ctx->host_pinned);
+    if (ctx->host_mapped) (void)hipHostFree(ctx->host_mapped);
     delete ctx;
     return SWARM_OK;
 }

@@ -1005,10 +1005,12 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         ctx->step_rows = ctx->step_all = 0;  // the stepper state is gone
     }
     constexpr int kMaxBatch = 256;
-    unsigned long long *hbuf = static_cast<unsigned long long *>(pinned(ctx, size_t(kCounters) * 8 * kMaxBatch));
+    // the per-round totals land in mapped host memory, written by k_batch_totals itself
+    void *dmap = nullptr;
+    unsigned long long *hbuf =
+        static_cast<unsigned long long *>(mapped(ctx, size_t(kCounters) * 8 * kMaxBatch, &dmap));
     if (!hbuf) return SWARM_ERR_OOM;
-    unsigned long long *dtot;
-    SW_ALLOC(dtot, ctx, S_ESTATS, size_t(kCounters) * 8 * kMaxBatch);
+    unsigned long long *dtot = static_cast<unsigned long long *>(dmap);
 
     int found = -1, t = 1, batch = 8, launched = 0;
     std::vector<int64_t> hist;  // per-round change counts read so far (batch sizing, layout)
@@ -1038,9 +1040,32 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         FILE *&f;
         ~LogClose() { if (f) fclose(f); }
     } log_close{rlog};
-    while (t <= max_rounds && found < 0) {
-        const int tend = (max_rounds - t + 1 < batch) ? max_rounds : t + batch - 1;
+    // Look-ahead: each batch's counters are read back from a point kLook rounds before its end, so
+    // the GPU is still running the batch's last rounds while the host reads, decides the next batch
+    // and enqueues it (no idle gap at a batch boundary).  Rounds launched past convergence are
+    // guarded no-ops.  Per-round timing and the round log keep the plain read-at-the-end batches.
+    const int kLook = (timed || rlog) ? 0 : 8;
+    hipEvent_t ev_read;
+    SW_HIP(hipEventCreateWithFlags(&ev_read, hipEventDisableTiming));
+    struct EvReadFree {
+        hipEvent_t e;
+        ~EvReadFree() { (void)hipEventDestroy(e); }
+    } ev_read_free{ev_read};
+    int read_upto = 0;  // rounds whose counters the host has read
+    while (read_upto < max_rounds && found < 0) {
+        t = launched + 1;  // first round launched in this batch (> tend when only a read is left)
+        const int tend = std::min(max_rounds, launched + batch);
+        // read rounds (read_upto, tread]: at least one (the first batches are shorter than kLook)
+        const int tread = (tend == max_rounds) ? max_rounds : std::max(read_upto + 1, tend - kLook);
         int rc = 0;
+        // per-round totals of rounds (read_upto, tread], reduced on device into mapped host memory, an event
+        auto enqueue_read = [&]() -> int {
+            hipLaunchKernelGGL(k_batch_totals, dim3(tread - read_upto), dim3(kWave), 0, s, ring, read_upto + 1, dtot);
+            SW_LAUNCHED();
+            SW_HIP(hipEventRecord(ev_read, s));
+            return SWARM_OK;
+        };
+        if (tread <= launched && (rc = enqueue_read())) return rc;
         // timing: dense rounds (and every round when a per-round log is written) get an event pair
         // each; a batch's run of back-to-back sparse rounds gets ONE pair around it -- events
         // between every launch would add their own cost to each round (rocprof's per-dispatch
@@ -1067,40 +1092,40 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
             }
             if (rc) return rc;
             if (e2) SW_HIP(hipEventRecord(e2[1], s));
+            if (r == tread && (rc = enqueue_read())) return rc;
         }
         if (seg_n) SW_HIP(hipEventRecord(ev[2 * kMaxBatch + 1], s));
-        launched = tend;
-        // per-round totals of rounds [t, tend], reduced on device, then one small copy
-        hipLaunchKernelGGL(k_batch_totals, dim3(tend - t + 1), dim3(kWave), 0, s, ring, t, dtot);
-        SW_LAUNCHED();
-        SW_HIP(hipMemcpyAsync(hbuf, dtot, size_t(tend - t + 1) * kCounters * 8, hipMemcpyDeviceToHost, s));
-        SW_HIP(hipStreamSynchronize(s));
-        for (int r = t; r <= tend; ++r) {  // every launched round's kernel time (rocprof's view)
-            if (!timed) break;
-            if (seg_n && kinds[r - t] == RK_SPARSE) continue;  // in the segment
-            float x = 0;
-            SW_HIP(hipEventElapsedTime(&x, ev[2 * (r - t)], ev[2 * (r - t) + 1]));
-            k_ms += x;
-            ++timed_rounds;
-            if (kinds[r - t] == RK_SPARSE) {
-                sp_ms += x;
-                ++sp_launches;
+        launched = std::max(launched, tend);
+        SW_HIP(hipEventSynchronize(ev_read));
+        if (timed) {  // kLook == 0: this batch's rounds are exactly the rounds read
+            SW_HIP(hipStreamSynchronize(s));
+            for (int r = t; r <= tend; ++r) {  // every launched round's kernel time (rocprof's view)
+                if (seg_n && kinds[r - t] == RK_SPARSE) continue;  // in the segment
+                float x = 0;
+                SW_HIP(hipEventElapsedTime(&x, ev[2 * (r - t)], ev[2 * (r - t) + 1]));
+                k_ms += x;
+                ++timed_rounds;
+                if (kinds[r - t] == RK_SPARSE) {
+                    sp_ms += x;
+                    ++sp_launches;
+                }
+                ktime[r - t] = x;
             }
-            ktime[r - t] = x;
+            if (seg_n) {
+                float x = 0;
+                SW_HIP(hipEventElapsedTime(&x, ev[2 * kMaxBatch], ev[2 * kMaxBatch + 1]));
+                k_ms += x;
+                sp_ms += x;
+                timed_rounds += seg_n;
+                sp_launches += seg_n;
+            }
         }
-        if (seg_n) {
-            float x = 0;
-            SW_HIP(hipEventElapsedTime(&x, ev[2 * kMaxBatch], ev[2 * kMaxBatch + 1]));
-            k_ms += x;
-            sp_ms += x;
-            timed_rounds += seg_n;
-            sp_launches += seg_n;
-        }
-        for (int r = t; r <= tend; ++r) {
-            const unsigned long long *rb = hbuf + size_t(r - t) * kCounters;
+        for (int r = read_upto + 1; r <= tread; ++r) {
+            const unsigned long long *rb = hbuf + size_t(r - read_upto - 1) * kCounters;
             const int64_t c = int64_t(rb[C_CHG]);
             hist.push_back(c);
-            const bool dn = kinds[r - t] == RK_DENSE || kinds[r - t] == RK_DENSE_MARK;
+            const RoundKind kind = mode == SWARM_ELECT_DENSE ? RK_DENSE : plan_round(r);
+            const bool dn = kind == RK_DENSE || kind == RK_DENSE_MARK;
             if (changes_host) changes_host[r - 1] = c;
             const int64_t act = dn ? n : int64_t(rb[C_ACT]);
             const int64_t ed = dn ? int64_t(e_total) : int64_t(rb[C_EDGE]);
@@ -1110,17 +1135,19 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
             dense_rounds += dn ? 1 : 0;
             const double rbytes = round_bytes(dn, n, int64_t(e_total), act, ed);
             bytes += rbytes;
-            if (kinds[r - t] == RK_SPARSE) sp_bytes += rbytes;
+            if (kind == RK_SPARSE) sp_bytes += rbytes;
             if (rlog)
-                fprintf(rlog, "%d %lld %lld %lld %d %.2f\n", r, (long long)c, (long long)act, (long long)ed,
-                        int(kinds[r - t]), timed ? ktime[r - t] * 1e3 : 0.0);
+                fprintf(rlog, "%d %lld %lld %lld %d %.2f\n", r, (long long)c, (long long)act, (long long)ed, int(kind),
+                        timed ? ktime[r - t] * 1e3 : 0.0);
             if (c == 0) {
                 found = r;
                 break;
             }
         }
-        t = tend + 1;
-        batch = next_round_batch(hist.data(), hist.size(), batch, kMaxBatch);
+        read_upto = tread;
+        // a batch spans at most kRing/2 rounds of counter slots, look-ahead included (bookkeeping
+        // recycles the slot of round t - kRing/2 in round t)
+        batch = next_round_batch(hist.data(), hist.size(), batch, kMaxBatch - kLook);
     }
     const int last = found > 0 ? found : max_rounds;
     // after a zero-change round both buffers hold the final state (dense and frontier alike);

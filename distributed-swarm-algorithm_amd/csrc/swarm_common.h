@@ -80,6 +80,9 @@ struct swarm_ctx {
     size_t cap[swarm::S_NUM] = {};
     void *host_pinned = nullptr;   // small pinned staging buffer for scalar/array readback
     size_t host_cap = 0;
+    void *host_mapped = nullptr;   // coherent mapped host buffer the device writes (election read-back)
+    void *mapped_dev = nullptr;
+    size_t mapped_cap = 0;
     int64_t step_rows = 0;         // frontier stepper: owned rows / agents (rows + ghosts)
     int64_t step_all = 0;
 };
@@ -95,6 +98,7 @@ void *scratch(swarm_ctx *ctx, Slot s, size_t bytes);
 int scratch_code();
 bool ctx_on_current_device(const swarm_ctx *ctx);
 void *pinned(swarm_ctx *ctx, size_t bytes);
+void *mapped(swarm_ctx *ctx, size_t bytes, void **dev);
 
 }  // namespace swarm
 
