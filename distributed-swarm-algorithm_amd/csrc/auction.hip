@@ -160,7 +160,8 @@ __device__ __forceinline__ Best combine(Best x, Best y) {
 // W lanes (a power of two <= 64, aligned within the wave) evaluate agent a together, U list
 // entries per lane per pass.
 template <int W, int U>
-__device__ __forceinline__ unsigned long long group_bid(const AucState &s, int64_t a, int32_t *bk_out) {
+__device__ __forceinline__ unsigned long long group_bid(const AucState &s, int64_t a, int32_t *bk_out,
+                                                        const unsigned long long *kprev = nullptr) {
     const int lane = threadIdx.x & (W - 1);
     Best m{-INFINITY, -INFINITY, 0.0f, INT_MAX};
     const int64_t b = s.off[a], e = s.off[a + 1];
@@ -178,6 +179,13 @@ __device__ __forceinline__ unsigned long long group_bid(const AucState &s, int64
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) pr[u] = kk[u] >= 0 ? s.price[kk[u]] : 0.0f;
+        if (kprev) {  // fused rounds: the price after the previous round = max(price, its winning bid)
+            unsigned long long kp[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) kp[u] = kk[u] >= 0 ? kprev[kk[u]] : 0ull;
+#pragma unroll
+            for (int u = 0; u < U; ++u) pr[u] = fmaxf(pr[u], __uint_as_float(static_cast<uint32_t>(kp[u] >> 32)));
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u)
             if (kk[u] >= 0) m = combine(m, Best{vv[u] - pr[u], -INFINITY, pr[u], kk[u]});
@@ -335,6 +343,118 @@ __global__ __launch_bounds__(kBlock) void k_auc_clear_keys(AucState s, AucList l
         if (tgt[i] >= 0) key[tgt[i]] = 0;
 }
 
+// ---------------------------------------------------------------- fused rounds
+// Once the bidders are few enough that a round is launch- and latency-bound (<= fused_max), round q
+// is ONE kernel: list entry i (one wave) first resolves entry i's bid of round q-1 -- it won iff its
+// key still stands on its task -- and the agent that entry yields for round q (the loser itself, or
+// the owner the winner displaced; at most one) bids right away in the same wave.  Its prices are
+// those after round q-1: max(price, the task's winning bid of q-1), consistent whether or not that
+// task's resolver has written the price yet (a bid always exceeds the price it was made at).  Task
+// keys rotate over three buffers: round q bids into buf(q), resolves against buf(q-1) and clears
+// what round q-2 left in buf(q-2) = buf(q+1).  Entries keep their index from round to round (holes
+// where an entry yields no bidder); every batch starts from a fresh compact list (k_auc_rebuild).
+struct AucFused {
+    int32_t *L;                  // per entry: the agent bidding this round (-1: none)
+    int32_t *tgt;                // per entry: the task it bid on (-1: none / dropped out)
+    int32_t *tclr;               // per entry: the task its bid of the round before landed on
+    unsigned long long *mykey;   // per entry: its bid key
+    unsigned *cnt;               // list length (device)
+};
+enum AucFusedMode { AF_FIRST = 0, AF_NORMAL = 1, AF_RESOLVE_ONLY = 2 };
+
+__device__ __forceinline__ unsigned long long *auc_kbuf(const AucState &s, int64_t q) {
+    return s.key + size_t(q % 3) * size_t(s.t);
+}
+
+__global__ __launch_bounds__(kBlock) void k_auc_fused(AucState s, AucFused f, int64_t q, int mode) {
+    const unsigned m = *f.cnt;
+    if (blockIdx.x == 0)  // recycle the counter slot round q + kARing/2 will use
+        for (int i = threadIdx.x; i < kAShards; i += kBlock) *aslot(s.ring, q + kARing / 2, i) = 0;
+    const int lane = threadIdx.x & 63;
+    unsigned long long *kcur = auc_kbuf(s, q), *kprev = auc_kbuf(s, q - 1), *kold = auc_kbuf(s, q + 1);
+    const int64_t nw = int64_t(gridDim.x) * (kBlock / kWave);
+    unsigned long long nb = 0;
+    for (int64_t i = int64_t(blockIdx.x) * (kBlock / kWave) + (threadIdx.x >> 6); i < m; i += nw) {
+        int32_t app = -1;
+        if (lane == 0) {
+            const int32_t a = f.L[i];
+            if (mode == AF_FIRST) {
+                app = a;
+            } else {
+                const int32_t c2 = f.tclr[i], k1 = f.tgt[i];
+                if (c2 >= 0) kold[c2] = 0ull;  // round q-2's bid: nobody reads buf(q-2) this round
+                if (a >= 0 && k1 >= 0) {
+                    const unsigned long long top = kprev[k1];
+                    const int32_t prev = s.owner[k1];
+                    if (top == f.mykey[i]) {
+                        s.owner[k1] = a;
+                        s.assigned[a] = k1;
+                        s.price[k1] = __uint_as_float(static_cast<uint32_t>(top >> 32));
+                        if (prev >= 0) s.assigned[prev] = -1;
+                        app = prev;
+                    } else {
+                        app = a;
+                    }
+                }
+                f.tclr[i] = k1;
+            }
+        }
+        app = __shfl(app, 0, 64);
+        if (mode == AF_RESOLVE_ONLY || app < 0) {
+            if (lane == 0) {
+                f.L[i] = -1;
+                f.tgt[i] = -1;
+            }
+            continue;
+        }
+        ++nb;
+        int32_t bk;
+        const unsigned long long kk = group_bid<64, kBidU>(s, app, &bk, mode == AF_FIRST ? nullptr : kprev);
+        if (lane == 0) {
+            f.L[i] = app;
+            f.tgt[i] = kk ? bk : -1;
+            f.mykey[i] = kk;
+            if (kk) atomicMax(&kcur[bk], kk);
+            else s.out[app] = 1;
+        }
+    }
+    __shared__ unsigned long long s_nb[kBlock / kWave];
+    if (lane == 0) s_nb[threadIdx.x >> 6] = nb;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long v = 0;
+        for (int w = 0; w < kBlock / kWave; ++w) v += s_nb[w];
+        if (v) atomicAdd(aslot(s.ring, q, blockIdx.x & (kAShards - 1)), v);
+    }
+}
+
+// A fresh, compact list of the unassigned, active agents (every resolution done, keys zeroed).
+__global__ __launch_bounds__(kBlock) void k_auc_rebuild(AucState s, AucFused f) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t base = int64_t(blockIdx.x) * kBlock; base < s.n; base += int64_t(gridDim.x) * kBlock) {
+        const int64_t a = base + threadIdx.x;
+        const bool want = a < s.n && s.assigned[a] < 0 && !s.out[a];
+        const unsigned long long bal = __ballot(want);
+        unsigned pos0 = 0;
+        if (lane == 0 && bal) pos0 = atomicAdd(f.cnt, unsigned(__popcll(bal)));
+        pos0 = __shfl(pos0, 0, 64);
+        if (want) {
+            const unsigned p = pos0 + unsigned(__popcll(bal & ((1ull << lane) - 1)));
+            f.L[p] = int32_t(a);
+            f.tgt[p] = -1;
+            f.tclr[p] = -1;
+        }
+    }
+}
+
+// Per-round bidder totals of rounds q0 .. q0 + gridDim.x - 1 (the ring's shards) -> out.
+__global__ void k_auc_round_totals(unsigned long long *ring, int64_t q0, unsigned long long *out) {
+    unsigned long long v = *aslot(ring, q0 + blockIdx.x, threadIdx.x);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (threadIdx.x == 0) out[blockIdx.x] = v;
+}
+
 // ---------------------------------------------------------------- the long tail, one workgroup
 // Rounds r0, r0+1, ... until no agent bids or max_rounds: bidder list in LDS (the unassigned,
 // active agents; it never grows: a round removes its winners and drop-outs and adds at most one
@@ -428,6 +548,14 @@ __global__ __launch_bounds__(kTailBlock) void k_auc_tail(AucState s, int64_t r0,
         if (k >= 0) key_last[k] = 0;
     }
     if (threadIdx.x == 0) *done = r - r0;  // rounds this kernel ran (all had bidders)
+}
+
+// Fused rounds (one kernel per round) once a round had <= this many bidders (SWARM_AUCTION_FUSED,
+// read per call; 0 = never, tests use it to exercise both paths).
+int64_t auc_fused_threshold() {
+    int64_t f = 16384;
+    if (const char *e = getenv("SWARM_AUCTION_FUSED")) f = atoll(e);
+    return f < 0 ? 0 : f;
 }
 
 // Hand the rounds to k_auc_tail once a round had <= this many bidders (SWARM_AUCTION_TAIL,
@@ -675,8 +803,9 @@ int swarm_auction(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *a
     st.price = price;
     st.owner = owner;
     st.assigned = assigned;
-    SW_ALLOC(st.key, ctx, S_AUC_KEY, size_t(t) * 16);  // two halves: k_auc_tail double-buffers by round
-    SW_HIP(hipMemsetAsync(st.key, 0, size_t(t) * 16, s));
+    // three buffers: the fused rounds rotate over all of them, k_auc_tail double-buffers the first two
+    SW_ALLOC(st.key, ctx, S_AUC_KEY, size_t(t) * 24);
+    SW_HIP(hipMemsetAsync(st.key, 0, size_t(t) * 24, s));
     constexpr int kMaxBatch = 256;
     int64_t *dlog;
     SW_ALLOC(dlog, ctx, S_TMP1, (size_t(max_rounds) + 2) * 8);
@@ -685,10 +814,20 @@ int swarm_auction(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *a
 
     // bidder lists (round parity), per-entry targets and keys, list counters, per-round log
     AucList al{};
+    AucFused af{};
     {
         char *p;
         const size_t nb = size_t(n) * 4;
-        SW_ALLOC(p, ctx, S_AUC_LIST, 4 * nb + size_t(n) * 8 + 64 + (size_t(max_rounds) + 2) * 8);
+        const size_t lsz = 4 * nb + size_t(n) * 8 + 64 + (size_t(max_rounds) + 2) * 8;
+        SW_ALLOC(p, ctx, S_AUC_LIST, ((lsz + 63) & ~size_t(63)) + 3 * nb + size_t(n) * 8 + 64);
+        {  // the fused rounds' entry arrays, behind the list-driven rounds' ones
+            char *q = p + ((lsz + 63) & ~size_t(63));
+            af.mykey = reinterpret_cast<unsigned long long *>(q);
+            af.L = reinterpret_cast<int32_t *>(q + size_t(n) * 8);
+            af.tgt = af.L + n;
+            af.tclr = af.tgt + n;
+            af.cnt = reinterpret_cast<unsigned *>(af.tclr + n);
+        }
         al.L[0] = reinterpret_cast<int32_t *>(p);
         al.L[1] = reinterpret_cast<int32_t *>(p + nb);
         al.tgt[0] = reinterpret_cast<int32_t *>(p + 2 * nb);
@@ -704,11 +843,27 @@ int swarm_auction(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *a
         SW_HIP(hipStreamSynchronize(s));  // c0 leaves scope
     }
     const int64_t tail_thr = auc_tail_threshold();
+    const int64_t fused_max = auc_fused_threshold();
     int64_t r = 1, found = -1, last_nb = n, launched = 0, tail_rounds = 0, total_bids = 0;
     int batch = 8;
+    bool fused_mode = false;  // fused rounds have run (keys in three buffers, entries in af)
+    bool pending = false;     // the last fused round's bids are not resolved yet
+    // resolve what the last fused round left (a resolve-only round q) and zero every key buffer
+    auto fused_flush = [&](int64_t q) -> int {
+        if (pending) {
+            hipLaunchKernelGGL(k_auc_fused, dim3(grid_for(last_nb, kBlock / kWave, 8192)), dim3(kBlock), 0, s, st, af, q,
+                               int(AF_RESOLVE_ONLY));
+            SW_LAUNCHED();
+            pending = false;
+        }
+        SW_HIP(hipMemsetAsync(st.key, 0, size_t(t) * 24, s));
+        return SWARM_OK;
+    };
     while (r <= max_rounds && found < 0) {
         if (last_nb <= tail_thr) {  // the long tail: one workgroup runs every remaining round
-            if (r > 1) {
+            if (fused_mode) {
+                if (int rc = fused_flush(r)) return rc;
+            } else if (r > 1) {
                 hipLaunchKernelGGL(k_auc_clear_keys, dim3(grid_for(last_nb, kBlock, 1024)), dim3(kBlock), 0, s, st, al,
                                    r);
                 SW_LAUNCHED();
@@ -732,6 +887,44 @@ int swarm_auction(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *a
             break;
         }
         const int64_t rend = (max_rounds - r + 1 < batch) ? max_rounds : r + batch - 1;
+        if (r > 1 && last_nb <= fused_max) {  // fused rounds: one kernel per round
+            if (fused_mode) {
+                if (int rc = fused_flush(r)) return rc;
+            } else {
+                SW_HIP(hipMemsetAsync(st.key, 0, size_t(t) * 24, s));  // the list-driven rounds' keys
+                fused_mode = true;
+            }
+            SW_HIP(hipMemsetAsync(af.cnt, 0, sizeof(unsigned), s));
+            hipLaunchKernelGGL(k_auc_rebuild, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s, st, af);
+            SW_LAUNCHED();
+            const unsigned fgrid = grid_for(last_nb, kBlock / kWave, 8192);  // an upper bound: lists never grow
+            for (int64_t q = r; q <= rend; ++q) {
+                hipLaunchKernelGGL(k_auc_fused, dim3(fgrid), dim3(kBlock), 0, s, st, af, q,
+                                   int(q == r ? AF_FIRST : AF_NORMAL));
+                SW_LAUNCHED();
+            }
+            pending = true;
+            launched = rend;
+            hipLaunchKernelGGL(k_auc_round_totals, dim3(rend - r + 1), dim3(kWave), 0, s, st.ring, r,
+                               reinterpret_cast<unsigned long long *>(dlog));
+            SW_LAUNCHED();
+            SW_HIP(hipMemcpyAsync(h, dlog, size_t(rend - r + 1) * 8, hipMemcpyDeviceToHost, s));
+            SW_HIP(hipStreamSynchronize(s));
+            for (int64_t q = r; q <= rend; ++q) {
+                const int64_t nb = int64_t(h[q - r]);
+                if (nb == 0) {
+                    found = q;
+                    pending = false;  // round q resolved round q-1 and placed no bid
+                    break;
+                }
+                if (bidders_per_round) bidders_per_round[q - 1] = nb;
+                total_bids += nb;
+                last_nb = nb;
+            }
+            r = rend + 1;
+            batch = batch < kMaxBatch ? batch * 2 : kMaxBatch;
+            continue;
+        }
         // grids sized by the last known bidder count: an upper bound (lists never grow)
         const unsigned bgrid = grid_for(last_nb, kBlock / kWave, 8192), rgrid = grid_for(last_nb, kBlock, 4096);
         for (int64_t q = r; q <= rend; ++q) {
@@ -756,6 +949,7 @@ int swarm_auction(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *a
         r = rend + 1;
         batch = batch < kMaxBatch ? batch * 2 : kMaxBatch;
     }
+    if (pending && (fused_flush(r) != SWARM_OK)) return SWARM_ERR_HIP;  // max_rounds ended on a fused round
     *rounds_exec = int32_t(found > 0 ? found - 1 : max_rounds);
     if (stats) {
         unsigned long long fl[kAShards * kAStride];

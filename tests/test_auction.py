@@ -242,3 +242,37 @@ def test_gpu_auction_large_ids(oracle_mod):
     assert r.rounds_exec == want["rounds"]
     np.testing.assert_array_equal(r.price.cpu().numpy(), want["price"])
     np.testing.assert_array_equal(s.to_input_order(r.assigned), want["assigned"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fused,tail", [("1000000000", "0"), ("1000000000", "128"), ("0", "128"), ("4096", "0")])
+@pytest.mark.parametrize("n,seed", [(2000, 14), (20000, 15)])
+def test_gpu_auction_fused_rounds_match_oracle(oracle_mod, n, seed, fused, tail):
+    """Fused rounds (resolve round q-1 and bid round q in one kernel, keys over three buffers,
+    a fresh list per batch) against the oracle, alone, beside the list-driven rounds and before
+    the one-workgroup tail."""
+    from swarm_amd.swarm import Swarm
+    d = _inputs(n, seed)
+    want = oracle_mod.auction(d["ids"], d["x"], d["y"], d["caps"], d["tx"], d["ty"], d["treq"])
+    os.environ["SWARM_AUCTION_TAIL"] = tail
+    os.environ["SWARM_AUCTION_FUSED"] = fused
+    try:
+        s = Swarm(d["ids"], d["x"], d["y"], d["caps"], device="cuda")
+        r = s.auction(d["tx"], d["ty"], d["treq"])
+        cut = {}
+        for m in (1, 2, 9, 10, 25, 57, want["rounds"] - 1):
+            if 1 <= m < want["rounds"]:
+                cut[m] = s.auction(d["tx"], d["ty"], d["treq"], max_rounds=m)
+    finally:
+        del os.environ["SWARM_AUCTION_TAIL"]
+        del os.environ["SWARM_AUCTION_FUSED"]
+    assert r.converged and r.rounds_exec == want["rounds"]
+    np.testing.assert_array_equal(r.bidders, want["bidders"])
+    np.testing.assert_array_equal(r.price.cpu().numpy(), want["price"])
+    np.testing.assert_array_equal(s.to_input_order(r.assigned), want["assigned"])
+    for m, rc in cut.items():  # the state after exactly m rounds (every bid of round m resolved)
+        w = oracle_mod.auction(d["ids"], d["x"], d["y"], d["caps"], d["tx"], d["ty"], d["treq"], max_rounds=m)
+        assert not rc.converged and rc.rounds_exec == m, m
+        np.testing.assert_array_equal(rc.bidders, want["bidders"][:m])
+        np.testing.assert_array_equal(rc.price.cpu().numpy(), w["price"])
+        np.testing.assert_array_equal(s.to_input_order(rc.assigned), w["assigned"])

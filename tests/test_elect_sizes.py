@@ -54,3 +54,27 @@ def test_elect_repeat_is_stable(sw, oracle_mod):
         if max_rounds >= rounds:
             assert r.converged and r.rounds_exec == rounds
             np.testing.assert_array_equal(r.leader.cpu().numpy(), lead)
+
+
+@pytest.mark.parametrize("mode", ["frontier", "dense"])
+def test_cut_elections_around_batch_boundaries(sw, mode):
+    """max_rounds cuts at and around the host's batch and read-back points (batches double from 8,
+    counters are read 8 rounds before a batch ends): the state after exactly m rounds, every
+    per-round count up to m, and SWARM_NOT_CONVERGED.  Path graph, random IDs: after m rounds
+    agent i holds the max ID within m hops."""
+    n = 1500
+    rng = np.random.default_rng(12)
+    ids = rng.permutation(n).astype(np.int32)
+    rp = np.concatenate([[0], np.cumsum([1] + [2] * (n - 2) + [1])]).astype(np.int64)
+    col = np.concatenate([[1]] + [[i - 1, i + 1] for i in range(1, n - 1)] + [[n - 2]]).astype(np.int32)
+    s = sw.Swarm(ids, np.arange(float(n)), np.zeros(n), layout="input", device="cuda").set_graph(rp, col)
+    full = s.elect(mode=mode)
+    assert full.converged
+    for m in (1, 2, 7, 8, 9, 10, 15, 16, 17, 23, 24, 25, 31, 56, 57, 120, 121, 248, 249, 600):
+        if m >= full.rounds_exec:
+            continue
+        r = s.elect(mode=mode, max_rounds=m)
+        assert not r.converged and r.rounds_exec == m, (m, r.rounds_exec)
+        np.testing.assert_array_equal(r.changes, full.changes[:m])
+        want = np.array([ids[max(0, i - m):i + m + 1].max() for i in range(n)])
+        np.testing.assert_array_equal(r.leader.cpu().numpy(), want)
