@@ -553,7 +553,7 @@ __global__ __launch_bounds__(kTailBlock) void k_auc_tail(AucState s, int64_t r0,
 // Fused rounds (one kernel per round) once a round had <= this many bidders (SWARM_AUCTION_FUSED,
 // read per call; 0 = never, tests use it to exercise both paths).
 int64_t auc_fused_threshold() {
-    int64_t f = 16384;
+    int64_t f = 8192;  // C4 sweep (tail 32): 2048..32768 all within 0.3 ms
     if (const char *e = getenv("SWARM_AUCTION_FUSED")) f = atoll(e);
     return f < 0 ? 0 : f;
 }
@@ -561,7 +561,7 @@ int64_t auc_fused_threshold() {
 // Hand the rounds to k_auc_tail once a round had <= this many bidders (SWARM_AUCTION_TAIL,
 // read per call; 0 = never, tests use it to exercise both paths).
 int auc_tail_threshold() {
-    int tail = 128;  // C4 sweep: 16..512 -> best at 96..128
+    int tail = 32;  // C4 sweep after the fused rounds: 24..48 best
     if (const char *e = getenv("SWARM_AUCTION_TAIL")) tail = atoi(e);
     return tail < 0 ? 0 : (tail > kTailCap ? kTailCap : tail);
 }

@@ -1,6 +1,6 @@
 """A/B timing of the C4 auction (100k agents x 100k tasks, bench.py's seed) under different
 SWARM_AUCTION_FUSED / SWARM_AUCTION_TAIL settings, read per call.
-Usage: python tools/auction_ab.py FUSED[:TAIL] [FUSED[:TAIL] ...]"""
+Usage: python tools/auction_ab.py FUSED[:TAIL] ..."""
 import os
 import sys
 import time
@@ -16,7 +16,7 @@ s = Swarm(d["ids"], d["x"], d["y"], d["caps"], device="cuda:0")
 tx, ty, tr = (torch.as_tensor(d[k]).cuda() for k in ("tx", "ty", "treq"))
 ref = None
 for spec in sys.argv[1:]:
-    fused, _, tail = spec.partition(":")
+    fused, tail = (spec.split(":") + [""])[:2]
     os.environ["SWARM_AUCTION_FUSED"] = fused
     if tail:
         os.environ["SWARM_AUCTION_TAIL"] = tail
