@@ -129,6 +129,11 @@ class Swarm:
     def build_graph(self, radius: float = 1.0):
         """Radius graph over the current storage order, built on the GPU (swarm_build_rgg)."""
         n, dev = self.n, self.device
+        if self.layout == "spatial" and n > (1 << 26):
+            # seen on MI355X: 66M agents build in 0.1 s, 68M in spatial order never return (68M in
+            # input order do); cause not found yet (DESIGN.md §8) -- refuse instead of hanging
+            raise NotImplementedError("build_graph: more than 2^26 agents in spatial order is not supported yet; "
+                                      "shard the swarm (swarm_amd.dist) or use layout='input'")
         L = _lib.lib()
         row_ptr = torch.empty(n + 1, dtype=torch.int32, device=dev)
         ne = ctypes.c_int64(0)
@@ -200,13 +205,18 @@ class Swarm:
         return cached[1]
 
     def elect(self, mode: str = "frontier", max_rounds: int = 1 << 16, timed: bool = False,
-              compact: bool = True) -> ElectResult:
+              compact: bool = True, wide: bool | None = None) -> ElectResult:
         """Contract E2 to convergence on the GPU (swarm_elect_compact with the graph's 16-bit
         columns when they fit; swarm_elect_directed when the neighbour lists are not symmetric).
         timed: per-kernel HIP events.  compact=False: the int32-column entry point swarm_elect
-        (same results)."""
+        (same results).  wide: int64 row offsets (swarm_elect_i64) -- chosen by itself for
+        graphs of >= 2^30 edges (C5's 100M agents on one GPU: ~1.6e9), True forces it."""
         if self.row_ptr is None:
             raise RuntimeError("no neighbour graph: call build_graph() or set_graph()")
+        if wide is None:
+            wide = self.n_edges >= (1 << 30)
+        if wide:
+            return self._elect_wide(mode, max_rounds, timed)
         m = {"dense": _lib.ELECT_DENSE, "frontier": _lib.ELECT_FRONTIER}[mode] | (_lib.ELECT_TIMED if timed else 0)
         n = self.n
         rounds = ctypes.c_int32(0)
@@ -243,6 +253,36 @@ class Swarm:
         res.gather_ms, res.apply_ms, res.timed_launches = st.gather_ms, st.apply_ms, st.gather_launches
         res.sparse_ms, res.sparse_launches, res.sparse_bytes = st.sparse_ms, st.sparse_launches, st.sparse_bytes
         res.compact = c16 is not None  # the rounds read the 16-bit columns (2 of the 4 column bytes)
+        return res
+
+    def _elect_wide(self, mode: str, max_rounds: int, timed: bool) -> ElectResult:
+        """swarm_elect_i64 over an int64 copy of row_ptr (kept while row_ptr is unchanged)."""
+        if getattr(self, "_hear", None) is not None:
+            raise ValueError("int64 row offsets: symmetric neighbour graphs only (swarm_elect_i64)")
+        key = (self.row_ptr.data_ptr(), self.row_ptr._version, self.n)
+        cached = getattr(self, "_rp64", None)
+        if cached is None or cached[0] != key:
+            self._rp64 = cached = (key, self.row_ptr.to(torch.int64))
+        rp64 = cached[1]
+        m = {"dense": _lib.ELECT_DENSE, "frontier": _lib.ELECT_FRONTIER}[mode] | (_lib.ELECT_TIMED if timed else 0)
+        rounds = ctypes.c_int32(0)
+        cap = int(max_rounds)
+        changes = np.empty(cap, np.int64)
+        st = _lib.ElectStats()
+        with torch.cuda.device(self.device):
+            rc = _lib.check(_lib.lib().swarm_elect_i64(
+                _lib.ctx(), self.n, _lib.ptr(rp64, torch.int64), _lib.ptr(self.col, torch.int32),
+                _lib.ptr(self.ids, torch.int32), _lib.ptr(self.leader, torch.int32),
+                _lib.ptr(self.state, torch.uint8), cap, m, ctypes.byref(rounds),
+                changes.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st), _lib.stream()))
+        r = rounds.value
+        res = ElectResult(r, changes[:r].copy(), self.leader, self.state, rc == _lib.OK,
+                          st.rounds_launched, st.active_total, st.edges_total, st.dense_rounds,
+                          st.bytes_total)
+        res.changes_total = st.changes_total
+        res.gather_ms, res.apply_ms, res.timed_launches = st.gather_ms, st.apply_ms, st.gather_launches
+        res.sparse_ms, res.sparse_launches, res.sparse_bytes = st.sparse_ms, st.sparse_launches, st.sparse_bytes
+        res.compact = False
         return res
 
     # ------------------------------------------------------------------ allocation

@@ -78,3 +78,27 @@ def test_cut_elections_around_batch_boundaries(sw, mode):
         np.testing.assert_array_equal(r.changes, full.changes[:m])
         want = np.array([ids[max(0, i - m):i + m + 1].max() for i in range(n)])
         np.testing.assert_array_equal(r.leader.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("n,deg", [(2049, 3.0), (65_537, 16.0), (1_048_577, 16.0)])
+def test_elect_int64_offsets(sw, oracle_mod, n, deg):
+    """swarm_elect_i64 (int64 row offsets: graphs of >= 2^30 edges), forced on small swarms: the
+    same leaders, states, rounds and changes as the oracle, both strategies, and a cut run."""
+    from swarm_amd import gen
+    d = gen.swarm_inputs(n, 31 + n, deg=deg)
+    s = sw.Swarm(d["ids"], d["x"], d["y"], d["caps"], device="cuda").build_graph(1.0)
+    rp = s.row_ptr.cpu().numpy().astype(np.int64)
+    lead, state, rounds, changes = oracle_mod.elect_frontier(rp, s.col.cpu().numpy(), s.ids.cpu().numpy())
+    for mode in ("frontier", "dense"):
+        r = s.elect(mode=mode, wide=True)
+        assert r.converged and r.rounds_exec == rounds, (mode, r.rounds_exec, rounds)
+        np.testing.assert_array_equal(r.changes, changes)
+        np.testing.assert_array_equal(r.leader.cpu().numpy(), lead)
+        np.testing.assert_array_equal(r.state.cpu().numpy(), state)
+    if rounds > 3:
+        m = rounds // 2
+        r = s.elect(max_rounds=m, wide=True)
+        want = oracle_mod.elect_frontier(rp, s.col.cpu().numpy(), s.ids.cpu().numpy(), max_rounds=m)
+        assert not r.converged and r.rounds_exec == m
+        np.testing.assert_array_equal(r.leader.cpu().numpy(), want[0])
+        np.testing.assert_array_equal(r.changes, changes[:m])

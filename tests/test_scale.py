@@ -42,9 +42,15 @@ def c3(sw):
     torch.cuda.empty_cache()
 
 
-def test_c3_election_full_scale(c3, oracle_mod):
+@pytest.fixture(scope="module")
+def c3_elect(c3, oracle_mod):
+    _, _, h = c3
+    return oracle_mod.elect_frontier(h["rp"], h["col"], h["ids"])
+
+
+def test_c3_election_full_scale(c3, c3_elect):
     d, s, h = c3
-    lead, state, rounds, changes = oracle_mod.elect_frontier(h["rp"], h["col"], h["ids"])
+    lead, state, rounds, changes = c3_elect
     assert rounds > 1024  # the headline election wraps the 512-round counter ring
     for mode in ("frontier", "dense"):
         r = s.elect(mode=mode, max_rounds=1 << 16)
@@ -52,6 +58,18 @@ def test_c3_election_full_scale(c3, oracle_mod):
         np.testing.assert_array_equal(r.changes, changes)
         np.testing.assert_array_equal(r.leader.cpu().numpy(), lead)
         np.testing.assert_array_equal(r.state.cpu().numpy(), state)
+
+
+def test_c3_election_int64_offsets(c3, c3_elect):
+    """The int64-row-offset instantiation (swarm_elect_i64, what a >= 2^30-edge graph such as C5's
+    100M agents on one GPU runs) on the headline swarm."""
+    d, s, h = c3
+    lead, state, rounds, changes = c3_elect
+    r = s.elect(wide=True)
+    assert r.converged and r.rounds_exec == rounds and not r.compact
+    np.testing.assert_array_equal(r.changes, changes)
+    np.testing.assert_array_equal(r.leader.cpu().numpy(), lead)
+    np.testing.assert_array_equal(r.state.cpu().numpy(), state)
 
 
 def test_c3_allocation_full_scale(c3, oracle_mod):

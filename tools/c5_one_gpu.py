@@ -1,0 +1,85 @@
+"""Toward C5's swarm size on ONE MI355X: the bench's step (election to convergence + one
+allocation round) on 64M agents (deg 16, 10k tasks; build_graph takes at most 2^26 agents in
+spatial order), timed, with the election checked against the C oracle's frontier
+restatement (leaders, states, rounds, every per-round change count) and the allocation against
+the binned oracle.  Prints progress every 30 s while the oracle runs (one C call).
+Usage: python tools/c5_one_gpu.py [N] [--no-oracle]"""
+import json
+import sys
+import threading
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, "distributed-swarm-algorithm_amd")
+sys.path.insert(0, ".")
+from swarm_amd import gen  # noqa: E402
+from swarm_amd.swarm import Swarm  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 64_000_000
+t0 = time.time()
+d = gen.swarm_inputs(n, 2026 + 5, deg=16.0, t=10_000)
+print(f"inputs {time.time() - t0:.0f}s", flush=True)
+s = Swarm(d["ids"], d["x"], d["y"], d["caps"], device="cuda:0")
+torch.cuda.synchronize()
+print(f"swarm (cell order) {time.time() - t0:.0f}s", flush=True)
+s.build_graph(1.0)
+tx, ty, tq = (torch.as_tensor(d[k], device="cuda:0") for k in ("tx", "ty", "treq"))
+torch.cuda.synchronize()
+print(f"swarm + graph {time.time() - t0:.0f}s: n={s.n} E={s.n_edges} (>= 2^30: {s.n_edges >= 1 << 30}); "
+      f"HBM allocated {torch.cuda.memory_allocated() / 2**30:.1f} GiB", flush=True)
+
+r = s.elect()
+a = s.allocate(tx, ty, tq)
+torch.cuda.synchronize()
+steps = []
+for _ in range(3):
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    r = s.elect()
+    t2 = time.perf_counter()
+    a = s.allocate(tx, ty, tq)
+    torch.cuda.synchronize()
+    t3 = time.perf_counter()
+    steps.append((t3 - t1, t2 - t1, t3 - t2))
+best = min(steps)
+out = {"agents": s.n, "edges": s.n_edges, "int64_offsets": s.n_edges >= 1 << 30, "rounds": r.rounds_exec,
+       "converged": r.converged, "ms_per_step": best[0] * 1e3, "elect_ms": best[1] * 1e3, "alloc_ms": best[2] * 1e3,
+       "agent_rounds_per_s": s.n * r.rounds_exec / best[0],
+       "hbm_peak_gib": torch.cuda.max_memory_allocated() / 2**30}
+print(json.dumps(out), flush=True)
+if "--no-oracle" in sys.argv:
+    sys.exit(0)
+
+from oracle import oracle as orc  # noqa: E402  (the checker, never the measured path)
+
+rp = s.row_ptr.cpu().numpy().astype(np.int64)
+col = s.col.cpu().numpy()
+ids = s.ids.cpu().numpy()
+lead_gpu, state_gpu = s.leader.cpu().numpy(), s.state.cpu().numpy()
+res = {}
+
+
+def run():
+    res["elect"] = orc.elect_frontier(rp, col, ids)
+    res["alloc"] = orc.allocate_binned(ids, s.pos[:, 0].cpu().numpy(), s.pos[:, 1].cpu().numpy(),
+                                       s.caps.cpu().numpy().view(np.uint32), d["tx"], d["ty"], d["treq"],
+                                       use_pow=False)
+
+
+th = threading.Thread(target=run)
+t4 = time.time()
+th.start()
+while th.is_alive():
+    th.join(30)
+    print(f"oracle running {time.time() - t4:.0f}s", flush=True)
+lead, state, rounds, changes = res["elect"]
+al = res["alloc"]
+ok = {"rounds": rounds == r.rounds_exec, "changes": bool(np.array_equal(changes, r.changes)),
+      "leader": bool(np.array_equal(lead, lead_gpu)), "state": bool(np.array_equal(state, state_gpu)),
+      "alloc_winner": bool(np.array_equal(al["winner"], a.winner.cpu().numpy())),
+      "alloc_nclaim": bool(np.array_equal(al["nclaim"], a.nclaim.cpu().numpy())),
+      "alloc_won": bool(np.array_equal(al["won"], a.won.cpu().numpy()))}
+print(json.dumps({"oracle_s": time.time() - t4, "parity": ok, "all_equal": all(ok.values())}), flush=True)
+sys.exit(0 if all(ok.values()) else 1)
