@@ -370,8 +370,9 @@ class ShardedSwarm:
         caps_np = np.ascontiguousarray(caps if caps is not None else np.zeros(len(ids), np.uint32),
                                        dtype=np.uint32).view(np.int32)
         caps_t = torch.as_tensor(caps_np).to(dev)
+        from .swarm import take_rows
         perm = self.backend.cell_order(pos) if pos.shape[0] > 1 else torch.arange(pos.shape[0], device=dev)
-        self.pos, self.ids, self.caps = pos[perm].contiguous(), ids_t[perm].contiguous(), caps_t[perm].contiguous()
+        self.pos, self.ids, self.caps = take_rows(pos, perm), ids_t[perm].contiguous(), caps_t[perm].contiguous()
         self.perm = perm
         self.n_own = int(self.ids.numel())
         # ghosts: neighbour ranks' agents within halo_depth radii of the shared borders

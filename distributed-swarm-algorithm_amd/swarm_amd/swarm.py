@@ -80,6 +80,16 @@ class AllocResult:
     stats: dict = field(default_factory=dict)
 
 
+def take_rows(t: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """t[idx] for a 2-D tensor, gathered one column at a time.  On this PyTorch-ROCm build the
+    row gathers of an (N, 2) float64 tensor (t[idx], index_select, gather) return wrong rows
+    above 2^26 rows, while 1-D gathers are right (checked on MI355X at 68M and 140M rows); the
+    wrong positions piled 67M agents into one grid cell, and the graph build then never ended."""
+    if t.dim() != 2:
+        return t[idx].contiguous()
+    return torch.stack([t[:, j].contiguous()[idx] for j in range(t.shape[1])], 1).contiguous()
+
+
 class Swarm:
     """Structure-of-arrays swarm resident on one GPU."""
 
@@ -103,7 +113,7 @@ class Swarm:
                 _lib.check(_lib.lib().swarm_cell_order(_lib.ctx(), n, _lib.ptr(pos, torch.float64),
                                                        float(cell), _lib.ptr(perm), _lib.stream()))
             p = perm.long()
-            ids_t, pos, caps_t = ids_t[p].contiguous(), pos[p].contiguous(), caps_t[p].contiguous()
+            ids_t, pos, caps_t = ids_t[p].contiguous(), take_rows(pos, p), caps_t[p].contiguous()
             self.perm = perm
         elif layout in ("spatial", "input"):
             self.perm = torch.arange(n, dtype=torch.int32, device=dev)
@@ -129,11 +139,6 @@ class Swarm:
     def build_graph(self, radius: float = 1.0):
         """Radius graph over the current storage order, built on the GPU (swarm_build_rgg)."""
         n, dev = self.n, self.device
-        if self.layout == "spatial" and n > (1 << 26):
-            # seen on MI355X: 66M agents build in 0.1 s, 68M in spatial order never return (68M in
-            # input order do); cause not found yet (DESIGN.md §8) -- refuse instead of hanging
-            raise NotImplementedError("build_graph: more than 2^26 agents in spatial order is not supported yet; "
-                                      "shard the swarm (swarm_amd.dist) or use layout='input'")
         L = _lib.lib()
         row_ptr = torch.empty(n + 1, dtype=torch.int32, device=dev)
         ne = ctypes.c_int64(0)

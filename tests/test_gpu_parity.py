@@ -60,6 +60,23 @@ def test_gpu_rgg_builder_matches_oracle(sw, oracle_mod):
         np.testing.assert_array_equal(s.col.cpu().numpy(), col)
 
 
+def test_take_rows_above_2_26_rows(sw):
+    """The Swarm's position permutation (swarm.take_rows) above 2^26 rows, where this PyTorch-ROCm
+    build's row gathers of an (N, 2) float64 tensor return wrong rows (seen at 68M: the graph
+    build then never ended).  Checked against the CPU gather of the same rows."""
+    import torch
+    n = (1 << 26) + 4099
+    g = torch.Generator(device="cuda").manual_seed(3)
+    t = torch.rand(n, 2, dtype=torch.float64, device="cuda", generator=g)
+    p = torch.randperm(n, device="cuda", generator=g)
+    out = sw.take_rows(t, p)
+    k = torch.randint(0, n, (4096,), generator=torch.Generator().manual_seed(4))
+    k = torch.cat([k, torch.arange(n - 64, n)])
+    want = t.cpu()[p.cpu()[k]]
+    assert torch.equal(out.cpu()[k], want)
+    assert out.is_contiguous() and out.shape == (n, 2)
+
+
 @pytest.mark.parametrize("n,seed,deg", [(300000, 41, 16.0), (200000, 42, 6.0)])
 def test_elect_large_vs_oracle(sw, oracle_mod, n, seed, deg):
     from swarm_amd import gen

@@ -1,8 +1,8 @@
-"""Toward C5's swarm size on ONE MI355X: the bench's step (election to convergence + one
-allocation round) on 64M agents (deg 16, 10k tasks; build_graph takes at most 2^26 agents in
-spatial order), timed, with the election checked against the C oracle's frontier
-restatement (leaders, states, rounds, every per-round change count) and the allocation against
-the binned oracle.  Prints progress every 30 s while the oracle runs (one C call).
+"""C5's swarm size (100M agents, deg 16, 10k tasks) on ONE MI355X: the bench's step (election to
+convergence + one allocation round) timed, with the election checked against the C oracle's
+frontier restatement (leaders, states, rounds, every per-round change count) and the allocation
+against the binned oracle.  The graph has ~1.6e9 edges (>= 2^30), so Swarm.elect takes the
+int64-offset entry point (swarm_elect_i64).  Prints progress every 30 s while the oracle runs (one C call).
 Usage: python tools/c5_one_gpu.py [N] [--no-oracle]"""
 import json
 import sys
@@ -17,7 +17,7 @@ sys.path.insert(0, ".")
 from swarm_amd import gen  # noqa: E402
 from swarm_amd.swarm import Swarm  # noqa: E402
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 64_000_000
+n = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 100_000_000
 t0 = time.time()
 d = gen.swarm_inputs(n, 2026 + 5, deg=16.0, t=10_000)
 print(f"inputs {time.time() - t0:.0f}s", flush=True)
