@@ -210,9 +210,13 @@ struct Col16 {
     const int16_t *p;
     template <typename I>
     __device__ __forceinline__ int32_t at(I k, int32_t base) const { return base + int32_t(p[k]); }
+    // 32-bit byte offsets for the int32-CSR elections; plain indexing for int64 offsets
     template <typename I>
     __device__ __forceinline__ int32_t at32(I k, int32_t base) const {
-        return base + int32_t(*reinterpret_cast<const int16_t *>(reinterpret_cast<const char *>(p) + (uint32_t(k) << 1)));
+        if constexpr (sizeof(I) == 4)
+            return base + int32_t(*reinterpret_cast<const int16_t *>(reinterpret_cast<const char *>(p) + (uint32_t(k) << 1)));
+        else
+            return base + int32_t(p[k]);
     }
 };
 
@@ -929,10 +933,10 @@ int launch_frontier_round(const Off *rp, const int32_t *col, const Frontier &f, 
         hipLaunchKernelGGL((k_sparse_block<Off, 2, true>), grid, dim3(kBlock), 0, s, rp, c32, f, t, guard, hrp, hcol);
     else if (hrp)
         hipLaunchKernelGGL((k_sparse_block<Off, kScan, true>), grid, dim3(kBlock), 0, s, rp, c32, f, t, guard, hrp, hcol);
-    else if (f.c16 && sizeof(Off) == 4 && small)
+    else if (f.c16 && small)
         hipLaunchKernelGGL((k_sparse_block<Off, 2, false, Col16>), grid, dim3(kBlock), 0, s, rp, Col16{f.c16}, f, t,
                            guard, nullptr, nullptr);
-    else if (f.c16 && sizeof(Off) == 4)
+    else if (f.c16)
         hipLaunchKernelGGL((k_sparse_block<Off, kScan, false, Col16>), grid, dim3(kBlock), 0, s, rp, Col16{f.c16}, f, t,
                            guard, nullptr, nullptr);
     else if (small)
@@ -1236,7 +1240,7 @@ int swarm_graph_compact(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const
     int32_t e_total = 0;
     SW_HIP(hipMemcpyAsync(&e_total, row_ptr + n, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     SW_HIP(hipStreamSynchronize(s));
-    SW_ARG(e_total >= 0 && e_total < (int32_t(1) << 30), "int32 CSR supports < 2^30 edges");
+    SW_ARG(e_total >= 0, "row_ptr[n] < 0");  // >= 2^30 edges: for swarm_elect_compact_i64
     if (e_total == 0) return SWARM_OK;
     SW_ARG(col && col16, "NULL array");
     int *bad;
@@ -1278,6 +1282,15 @@ int swarm_elect_i64(swarm_ctx *ctx, int64_t n, const int64_t *row_ptr, const int
                     swarm_elect_stats *stats, void *stream) {
     return swarm::elect_impl<int64_t>(ctx, n, row_ptr, col, ids, leader, state, max_rounds, mode,
                                       rounds_exec, changes_per_round, stats, stream);
+}
+
+int swarm_elect_compact_i64(swarm_ctx *ctx, int64_t n, const int64_t *row_ptr, const int32_t *col,
+                            const int16_t *col16, const int32_t *ids, int32_t *leader, uint8_t *state,
+                            int32_t max_rounds, int32_t mode, int32_t *rounds_exec, int64_t *changes_per_round,
+                            swarm_elect_stats *stats, void *stream) {
+    return swarm::elect_impl<int64_t>(ctx, n, row_ptr, col, ids, leader, state, max_rounds, mode, rounds_exec,
+                                      changes_per_round, stats, stream, nullptr, nullptr,
+                                      swarm::tuning().use_c16 ? col16 : nullptr);
 }
 
 int swarm_frontier_begin(swarm_ctx *ctx, int64_t n_rows, int64_t n_all, const int32_t *init,

@@ -31,7 +31,8 @@ EXPORTS = ("swarm_last_error", "swarm_version", "swarm_ctx_create", "swarm_ctx_d
            "swarm_elect_sharded", "swarm_auction", "swarm_physics_step", "swarm_codec_encode",
            "swarm_codec_decode", "swarm_protocol_run", "swarm_auction_begin",
            "swarm_auction_bid", "swarm_auction_resolve", "swarm_auction_sharded", "swarm_cell_index",
-           "swarm_allocate_indexed", "swarm_graph_compact", "swarm_elect_compact")
+           "swarm_allocate_indexed", "swarm_graph_compact", "swarm_elect_compact",
+           "swarm_elect_compact_i64")
 
 
 class SwarmError(RuntimeError):
@@ -107,6 +108,7 @@ def load(path: str = LIB_PATH):
         L.swarm_elect_round.argtypes = [P, i64, P, P, P, P, P, P]
         L.swarm_graph_compact.argtypes = [P, i64, P, P, P, P]
         L.swarm_elect_compact.argtypes = [P, i64, P, P, P, P, P, P, i32, i32, ctypes.POINTER(i32), P, P, P]
+        L.swarm_elect_compact_i64.argtypes = [P, i64, P, P, P, P, P, P, i32, i32, ctypes.POINTER(i32), P, P, P]
         L.swarm_allocate.argtypes = [P, i64, P, P, P, i64, P, P, d, d, d, i32, P, P, P, P, i64,
                                      P, P, P, P]
         L.swarm_utility.argtypes = [P, i64, P, P, P, P, d, P, P]

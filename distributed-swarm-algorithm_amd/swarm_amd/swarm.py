@@ -221,7 +221,7 @@ class Swarm:
         if wide is None:
             wide = self.n_edges >= (1 << 30)
         if wide:
-            return self._elect_wide(mode, max_rounds, timed)
+            return self._elect_wide(mode, max_rounds, timed, compact)
         m = {"dense": _lib.ELECT_DENSE, "frontier": _lib.ELECT_FRONTIER}[mode] | (_lib.ELECT_TIMED if timed else 0)
         n = self.n
         rounds = ctypes.c_int32(0)
@@ -260,8 +260,9 @@ class Swarm:
         res.compact = c16 is not None  # the rounds read the 16-bit columns (2 of the 4 column bytes)
         return res
 
-    def _elect_wide(self, mode: str, max_rounds: int, timed: bool) -> ElectResult:
-        """swarm_elect_i64 over an int64 copy of row_ptr (kept while row_ptr is unchanged)."""
+    def _elect_wide(self, mode: str, max_rounds: int, timed: bool, compact: bool = True) -> ElectResult:
+        """swarm_elect_compact_i64 (16-bit columns when they fit) or swarm_elect_i64 over an int64
+        copy of row_ptr (kept while row_ptr is unchanged)."""
         if getattr(self, "_hear", None) is not None:
             raise ValueError("int64 row offsets: symmetric neighbour graphs only (swarm_elect_i64)")
         key = (self.row_ptr.data_ptr(), self.row_ptr._version, self.n)
@@ -275,8 +276,10 @@ class Swarm:
         changes = np.empty(cap, np.int64)
         st = _lib.ElectStats()
         with torch.cuda.device(self.device):
-            rc = _lib.check(_lib.lib().swarm_elect_i64(
+            c16 = self.graph_compact() if compact else None
+            rc = _lib.check(_lib.lib().swarm_elect_compact_i64(
                 _lib.ctx(), self.n, _lib.ptr(rp64, torch.int64), _lib.ptr(self.col, torch.int32),
+                _lib.ptr(c16) if c16 is not None else None,
                 _lib.ptr(self.ids, torch.int32), _lib.ptr(self.leader, torch.int32),
                 _lib.ptr(self.state, torch.uint8), cap, m, ctypes.byref(rounds),
                 changes.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st), _lib.stream()))
@@ -287,7 +290,7 @@ class Swarm:
         res.changes_total = st.changes_total
         res.gather_ms, res.apply_ms, res.timed_launches = st.gather_ms, st.apply_ms, st.gather_launches
         res.sparse_ms, res.sparse_launches, res.sparse_bytes = st.sparse_ms, st.sparse_launches, st.sparse_bytes
-        res.compact = False
+        res.compact = c16 is not None
         return res
 
     # ------------------------------------------------------------------ allocation

@@ -143,6 +143,14 @@ int swarm_elect_i64(swarm_ctx *ctx, int64_t n, const int64_t *row_ptr, const int
                     int32_t mode, int32_t *rounds_exec, int64_t *changes_per_round,
                     swarm_elect_stats *stats, void *stream);
 
+/* swarm_elect_compact with int64 row offsets (graphs of >= 2^30 edges; the 16-bit columns are
+ * built by swarm_graph_compact from the int32 row offsets, which hold up to 2^31 - 1 edges).
+ * Replaces the same election as swarm_elect_i64 (agent.py:263-275); col16 = NULL is swarm_elect_i64. */
+int swarm_elect_compact_i64(swarm_ctx *ctx, int64_t n, const int64_t *row_ptr, const int32_t *col,
+                            const int16_t *col16, const int32_t *ids, int32_t *leader, uint8_t *state,
+                            int32_t max_rounds, int32_t mode, int32_t *rounds_exec, int64_t *changes_per_round,
+                            swarm_elect_stats *stats, void *stream);
+
 /* One synchronous E2 round, dense, no convergence loop (building block for sharded runs):
  * leader_out[v] = max(leader_in[v], max_{u in N(v)} leader_in[u]) for v in [0, n_rows);
  * leader_in may hold n_rows + ghosts entries (col indexes it).  *changed (device int64) is

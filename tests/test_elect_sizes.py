@@ -89,9 +89,10 @@ def test_elect_int64_offsets(sw, oracle_mod, n, deg):
     s = sw.Swarm(d["ids"], d["x"], d["y"], d["caps"], device="cuda").build_graph(1.0)
     rp = s.row_ptr.cpu().numpy().astype(np.int64)
     lead, state, rounds, changes = oracle_mod.elect_frontier(rp, s.col.cpu().numpy(), s.ids.cpu().numpy())
-    for mode in ("frontier", "dense"):
-        r = s.elect(mode=mode, wide=True)
+    for mode, compact in (("frontier", True), ("frontier", False), ("dense", True)):
+        r = s.elect(mode=mode, wide=True, compact=compact)
         assert r.converged and r.rounds_exec == rounds, (mode, r.rounds_exec, rounds)
+        assert r.compact == (compact and s.graph_compact() is not None)
         np.testing.assert_array_equal(r.changes, changes)
         np.testing.assert_array_equal(r.leader.cpu().numpy(), lead)
         np.testing.assert_array_equal(r.state.cpu().numpy(), state)

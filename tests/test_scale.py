@@ -65,11 +65,12 @@ def test_c3_election_int64_offsets(c3, c3_elect):
     100M agents on one GPU runs) on the headline swarm."""
     d, s, h = c3
     lead, state, rounds, changes = c3_elect
-    r = s.elect(wide=True)
-    assert r.converged and r.rounds_exec == rounds and not r.compact
-    np.testing.assert_array_equal(r.changes, changes)
-    np.testing.assert_array_equal(r.leader.cpu().numpy(), lead)
-    np.testing.assert_array_equal(r.state.cpu().numpy(), state)
+    for compact in (True, False):
+        r = s.elect(wide=True, compact=compact)
+        assert r.converged and r.rounds_exec == rounds and r.compact == compact
+        np.testing.assert_array_equal(r.changes, changes)
+        np.testing.assert_array_equal(r.leader.cpu().numpy(), lead)
+        np.testing.assert_array_equal(r.state.cpu().numpy(), state)
 
 
 def test_c3_allocation_full_scale(c3, oracle_mod):
