@@ -31,7 +31,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--agents", type=int, default=10_000_000)
+    ap.add_argument("--agents", type=int, default=None,
+                    help="agents per GPU (default: 10M for C3; C5 splits 100M over the GPUs)")
+    ap.add_argument("--config", choices=["C3", "C5"], default="C3",
+                    help="C3: 10M agents per GPU (weak scaling); C5: 100M agents in all, split over the GPUs "
+                         "by contiguous ID range (12.5M per GPU at N = 8; strong scaling)")
     ap.add_argument("--tasks", type=int, default=10_000)
     ap.add_argument("--deg", type=float, default=16.0)
     ap.add_argument("--seed", type=int, default=2026)
@@ -41,7 +45,13 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--rows", type=int, default=1,
                     help="0 to skip the other SURVEY §8 rows (C2, C4 auction, physics, protocol, codec)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    a.world_hint = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.agents is None:
+        a.agents = 100_000_000 // a.world_hint if a.config == "C5" else 10_000_000
+    if a.config == "C5":
+        a.rows = 0  # the other §8 rows keep their own (C2 / C3-sized) workloads: not re-run at C5
+    return a
 
 
 def log(*a):
@@ -168,13 +178,10 @@ def main():
     if args.elect_mode == "frontier" and rt.sparse_launches:
         pmc = pmc_traffic("k_sparse_block<int, 8,")  # the 2 048-agent-chunk variant (10M agents)
         dom = {"kernel": "k_sparse_block (sparse E2 round: marked agents gather)",
-               "bytes_per_launch": rt.sparse_bytes / rt.sparse_launches,
+               **sparse_round_bytes(rt.active_total, rt.edges_total, rt.dense_rounds, rt.rounds_exec, n, e,
+                                    rt.sparse_launches, getattr(rt, "compact", False)),
                "avg_launch_ms": rt.sparse_ms / rt.sparse_launches, "launches": rt.sparse_launches,
                "traffic": pmc[0] if pmc else None, "traffic_source": pmc[1] if pmc else None,
-               # the per-unit figure counts 4 B per column; the compact columns read 2
-               "columns": "int16 deltas (swarm_elect_compact)" if getattr(rt, "compact", False) else "int32",
-               "bytes_per_launch_columns_as_read": (rt.sparse_bytes - (2.0 if getattr(rt, "compact", False) else 0.0)
-                                                    * (rt.edges_total - rt.dense_rounds * e)) / rt.sparse_launches,
                "all_rounds": {"bytes_per_launch": rt.bytes_total / max(rt.timed_launches, 1),
                               "avg_launch_ms": rt.gather_ms / max(rt.timed_launches, 1),
                               "launches": rt.timed_launches, "dense_rounds": rt.dense_rounds}}
@@ -215,12 +222,12 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.config == "C5" else "weak",
             "vs_baseline": None,
             "dtype": "int32+f64",
             "data": "synthetic (seeded RGG, SplitMix64)",
-            "config": {"workload": "C3: %d agents/GPU, deg %g RGG, election to convergence + %d-task allocation"
-                       % (n, args.deg, args.tasks),
+            "config": {"workload": "%s: %d agents/GPU, deg %g RGG, election to convergence + %d-task allocation"
+                       % (args.config, n, args.deg, args.tasks),
                        "agents_per_gpu": n, "edges_per_gpu": e, "tasks": args.tasks,
                        "elect_mode": args.elect_mode, "alloc_mode": a.stats.get("mode_used"),
                        "rounds_exec": r.rounds_exec, "parallelism": f"agents sharded x{world}"},
@@ -516,7 +523,9 @@ def rows_bench(sw, dev, args):
 
 
 def sharded(args, rank, world, dev):
-    """N > 1: one strip of a world-wide swarm per GPU (weak scaling: args.agents per GPU),
+    """N > 1: one strip of a world-wide swarm per GPU -- rank k owns the contiguous ID range
+    [k n, (k+1) n) (north_star: agents partitioned by ID range) -- (C3: args.agents per GPU, weak
+    scaling; C5: 100M in all),
     exact sharded election (deep RCCL halo every k rounds + batched all-reduce) and allocation."""
     import torch
     import torch.distributed as dist
@@ -578,13 +587,17 @@ def sharded(args, rank, world, dev):
             "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.config == "C5" else "weak",
             "vs_baseline": None,
             "dtype": "int32+f64",
-            "data": "synthetic (seeded RGG strips, SplitMix64 + Feistel IDs)",
-            "config": {"workload": "C5-style: %d agents/GPU x %d GPUs, deg %g, election to convergence + %d "
-                                   "tasks/GPU allocation" % (args.agents, world, args.deg, args.tasks),
+            "data": "synthetic (seeded RGG strips, SplitMix64; rank k owns the contiguous ID range "
+                    "[k n, (k+1) n), random order inside its strip)",
+            "config": {"workload": ("C5: %d agents sharded by ID range over %d GPUs (%d per GPU)"
+                                    % (total_agents, world, args.agents) if args.config == "C5" else
+                                    "C3 per GPU x %d GPUs (weak scaling): %d agents/GPU" % (world, args.agents))
+                       + ", deg %g, election to convergence + %d tasks/GPU allocation" % (args.deg, args.tasks),
                        "agents_total": total_agents, "tasks_total": args.tasks * world,
+                       "partition": "contiguous ID ranges = horizontal strips (gen.shard_inputs ids='range')",
                        "rounds_exec": r.rounds_exec,
                        "halo_depth": sh.halo_depth,
                        "parallelism": f"strip-sharded x{world}: {path}; halo exchanged every {sh.halo_depth} "
@@ -633,6 +646,27 @@ def sharded_state_check(sh, r):
             "rounds_exec": r.rounds_exec, "converged": r.converged}
 
 
+def sparse_round_bytes(active_total, edges_total, dense_rounds, rounds_exec, n, e, launches, compact):
+    """Algorithmic bytes per sparse-round launch on SURVEY §8(d)'s per-unit figure -- 12 B per
+    gathered agent (row offset, own leader, leader write) + 8 B per edge (column, neighbour
+    leader) -- over the executed sparse rounds, spread over every launched sparse round (as
+    rocprof's per-dispatch average is).  The frontier's own bookkeeping (the n-byte stamp scan of
+    every sparse round and the second row offset a lone agent reads) is reported beside it, not in
+    it; so are the bytes as read with 16-bit columns (2 of the 4 column bytes)."""
+    sp_active = active_total - dense_rounds * n
+    sp_edges = edges_total - dense_rounds * e
+    sp_rounds = rounds_exec - dense_rounds
+    b8d = 12.0 * sp_active + 8.0 * sp_edges
+    keep = float(n) * sp_rounds + 4.0 * sp_active
+    return {"bytes_per_launch": b8d / launches,
+            "bytes_source": "SURVEY 8(d): 12 B per gathered agent + 8 B per edge, sparse rounds",
+            "bookkeeping_bytes_per_launch": keep / launches,
+            "bookkeeping": "n-byte stamp scan per sparse round + 4 B second row offset per gathered agent",
+            "columns": "int16 deltas (swarm_elect_compact)" if compact else "int32",
+            "bytes_per_launch_columns_as_read": (b8d - (2.0 if compact else 0.0) * sp_edges) / launches,
+            "sparse_rounds_exec": int(sp_rounds), "gathered_agents": int(sp_active), "gathered_edges": int(sp_edges)}
+
+
 def shard_roofline(sh, dev):
     """k_sparse_block's algorithmic bytes per launch over its HIP-event time, from one instrumented
     single-GPU election of this rank's shard graph (ELECT_TIMED)."""
@@ -651,7 +685,9 @@ def shard_roofline(sh, dev):
                                           _lib.ELECT_FRONTIER | _lib.ELECT_TIMED, ctypes.byref(rounds), None,
                                           ctypes.byref(st), _lib.stream()))
     torch.cuda.synchronize()
-    bpl = st.sparse_bytes / max(st.sparse_launches, 1)
+    sb = sparse_round_bytes(st.active_total, st.edges_total, st.dense_rounds, rounds.value, n, int(sh.col.numel()),
+                            max(st.sparse_launches, 1), False)
+    bpl = sb["bytes_per_launch"]
     ms = st.sparse_ms / max(st.sparse_launches, 1)
     # the committed PMC figure is the N = 1 C3 bench's (10M agents): it stands for shards of about
     # that size only
@@ -659,7 +695,7 @@ def shard_roofline(sh, dev):
     ach = bpl / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
     return {"kernel": "k_sparse_block (sparse E2 round: marked agents gather)", "bound": "hbm", "achieved": ach,
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": pmc[0] if pmc else None,
-            "traffic_source": pmc[1] if pmc else None, "bytes_per_launch": bpl, "avg_launch_ms": ms,
+            "traffic_source": pmc[1] if pmc else None, **sb, "avg_launch_ms": ms,
             "launches": int(st.sparse_launches), "shard_rows": int(n), "shard_rounds": int(rounds.value)}
 
 

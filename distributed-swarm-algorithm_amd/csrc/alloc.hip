@@ -27,8 +27,10 @@
 #include "binning.h"
 #include "utility.h"
 
+#include <algorithm>
 #include <climits>
 #include <cstring>
+#include <vector>
 
 namespace swarm {
 namespace {
@@ -45,6 +47,35 @@ __device__ __forceinline__ long long block_sum_ll(long long v, long long *s_red)
     return m;
 }
 
+// Guard-band resolution.  The reference squares with libm pow (agent.py:340);
+// the device squares with x*x.  A task with ANY candidate pair inside the guard band (guard_flag)
+// is not finished by the main pass: it is appended to a deferred list, its guard-band pairs are
+// collected (PASS_COLLECT) and handed to the host, which decides them with the host's libm pow
+// exactly as agent.py:340/297/302 do, and the deferred tasks are then resolved once (PASS_RESOLVE)
+// with those decisions in place of the device's for exactly those pairs.
+struct FlagPair {            // device -> host
+    double ax, ay, tx, ty;
+    int32_t j;               // position of the task in the deferred list
+    int32_t agent;           // storage index
+    int32_t has;             // has_cap (agent.py:343-345)
+    int32_t pad;
+};
+struct Override {            // host -> device, sorted by (j, agent)
+    int32_t agent;
+    float x;                 // f32(U_ref): the claim payload (agent.py:302)
+    int32_t claim;           // U_ref > claim_thr (agent.py:297)
+    int32_t pad;
+};
+struct Defer {
+    int32_t *list = nullptr;               // deferred task indices
+    unsigned long long *count = nullptr;   // [0] deferred tasks, [1] guard-band pairs collected
+    uint8_t *tflag = nullptr;              // dense strategy: tasks with a guard-band pair
+    FlagPair *pairs = nullptr;
+    int64_t pair_cap = 0;
+    const uint32_t *ov_off = nullptr;      // deferred task j: overrides [ov_off[j], ov_off[j + 1])
+    const Override *ov = nullptr;
+};
+
 struct Params {
     double thr, h, u_scale, rp2;
     int32_t *winner;
@@ -55,7 +86,30 @@ struct Params {
     int64_t *nclaim;
     int64_t *nmsg;
     unsigned long long *stats;  // kStatShards x 16 u64: [claims, conflicts, flagged, candidates, overflow, bad treq]
+    Defer D;
+    int64_t check_blocks = 0;   // SRC_ROWS main pass: the last check_blocks workgroups verify the index
 };
+
+// candidate sources of the per-task wave kernel
+constexpr int SRC_HASH = 0;  // hashed cell buckets (swarm_allocate, BINNED)
+constexpr int SRC_ROWS = 1;  // the caller's cell index over the storage order (swarm_allocate_indexed)
+constexpr int SRC_ALL = 2;   // every agent (the dense strategy's deferred tasks)
+// passes
+constexpr int PASS_MAIN = 0;     // every task; guard-band tasks deferred when P.D.list is set
+constexpr int PASS_COLLECT = 1;  // deferred tasks: append their guard-band pairs
+constexpr int PASS_RESOLVE = 2;  // deferred tasks: claims with the host's decisions, chain, finish
+
+__device__ __forceinline__ void apply_override(const Params &P, uint32_t a, uint32_t b, int32_t agent, bool &claim,
+                                               float &x) {
+    for (uint32_t q = a; q < b; ++q) {
+        const Override o = P.D.ov[q];
+        if (o.agent == agent) {
+            claim = o.claim != 0;
+            x = o.x;
+            return;
+        }
+    }
+}
 
 constexpr int kStatShards = 64;   // each shard on its own 128-B line
 constexpr int kStatStride = 16;
@@ -267,15 +321,33 @@ __device__ __forceinline__ void window_setup_rows(double2 tp, double rp, const G
     __builtin_amdgcn_wave_barrier();
 }
 
-// Staleness test of a cell index: every agent must lie in its cell's range.
-__global__ __launch_bounds__(kBlock) void k_check_index(const double2 *__restrict__ apos, int64_t n, Grid g,
-                                                       const uint32_t *__restrict__ off,
-                                                       unsigned long long *__restrict__ bad_out) {
+// Every agent as one candidate range (the dense strategy's deferred tasks).
+__device__ __forceinline__ void window_setup_all(int64_t n, CellWindow &w, int lane) {
+    if (lane == 0) {
+        w.a[0] = 0;
+        w.pre[0] = 0;
+        w.pre[1] = uint32_t(n);
+        w.ncell = 1;
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Staleness test of a cell index: every agent must lie in its cell's range AND inside the indexed
+// bounding box.  cell_coord clamps, so an edge-cell agent that moved past [xmin, xmax] x [ymin,
+// ymax] still maps to its old cell; window_setup_rows skips every task whose disc misses that box,
+// so such an agent would lose its claims silently.  Run by `nb` extra workgroups of the indexed
+// allocation's own launch (b = 0..nb-1): the check streams the positions while the task waves
+// wait on their dependent loads; the host reads the count after the launch and reports
+// SWARM_ERR_STALE (outputs undefined) instead of the results.
+__device__ __forceinline__ void check_index_part(const double2 *__restrict__ apos, int64_t n, const Grid &g,
+                                                 const uint32_t *__restrict__ off,
+                                                 unsigned long long *__restrict__ bad_out, int64_t b, int64_t nb) {
     unsigned long long bad = 0;
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+    for (int64_t i = b * kBlock + threadIdx.x; i < n; i += nb * kBlock) {
         const double2 p = apos[i];
         const int64_t c = cell_coord(p.y, g.ymin, g.inv_cell, g.ncy) * g.ncx + cell_coord(p.x, g.xmin, g.inv_cell, g.ncx);
-        bad += (isfinite(p.x) && isfinite(p.y) && off[c] <= uint32_t(i) && uint32_t(i) < off[c + 1]) ? 0 : 1;
+        const bool inside = p.x >= g.xmin && p.x <= g.xmax && p.y >= g.ymin && p.y <= g.ymax;  // false for NaN
+        bad += (inside && off[c] <= uint32_t(i) && uint32_t(i) < off[c + 1]) ? 0 : 1;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) bad += __shfl_xor(bad, o, 64);
@@ -296,15 +368,18 @@ __device__ __forceinline__ int wave_min_int(int v) {
     return v;
 }
 
-// HASH: candidates from the hashed buckets (sorted_idx, bucket_off, hg); otherwise from a cell
-// index over the storage order (bucket_off = cell_off, grid g; sorted_idx unused).
-template <bool HASH>
+// SRC: where a task's candidates come from (SRC_HASH: the hashed buckets sorted_idx / bucket_off /
+// hg; SRC_ROWS: a cell index over the storage order, bucket_off = cell_off over grid g; SRC_ALL:
+// every agent).  PASS: see PASS_MAIN / PASS_COLLECT / PASS_RESOLVE.  In the COLLECT and RESOLVE
+// passes the wave's task is P.D.list[kk] (kk < t_count = the deferred count).
+template <int SRC, int PASS>
 __global__ __launch_bounds__(kBlock) void k_alloc_binned(
     int64_t t_count, const double2 *__restrict__ tpos, const int8_t *__restrict__ treq,
     const int32_t *__restrict__ ids, const double2 *__restrict__ apos,
     const uint32_t *__restrict__ caps, const int32_t *__restrict__ sorted_idx,
-    const uint32_t *__restrict__ bucket_off, HashGrid hg, Grid g, double rp, Params P) {
+    const uint32_t *__restrict__ bucket_off, HashGrid hg, Grid g, double rp, int64_t n_all, Params P) {
     constexpr int kW = kBlock / kWave;
+    constexpr bool HASH = SRC == SRC_HASH;
     __shared__ int s_id[kW][kWCap];
     __shared__ float s_x[kW][kWCap];
     __shared__ int s_ix[kW][kWCap];
@@ -317,20 +392,37 @@ __global__ __launch_bounds__(kBlock) void k_alloc_binned(
     const unsigned long long below = (1ull << lane) - 1ull;
     long long my_cand = 0, my_flag = 0;
     BlockStats bs;
-    const int64_t nw = int64_t(gridDim.x) * kW;
-    for (int64_t k = int64_t(blockIdx.x) * kW + wid; k < t_count; k += nw) {
+    int64_t task_blocks = gridDim.x;
+    if (SRC == SRC_ROWS && PASS == PASS_MAIN && P.check_blocks > 0) {
+        task_blocks -= P.check_blocks;
+        if (int64_t(blockIdx.x) >= task_blocks) {  // whole workgroup: no barrier below is reached
+            check_index_part(apos, n_all, g, bucket_off, P.stats + 7,  // shard 0, slot 7: folded into hs[7]
+                             int64_t(blockIdx.x) - task_blocks, P.check_blocks);
+            return;
+        }
+    }
+    const int64_t nw = task_blocks * kW;
+    for (int64_t kk = int64_t(blockIdx.x) * kW + wid; kk < t_count; kk += nw) {
+        const int64_t k = PASS == PASS_MAIN ? kk : int64_t(P.D.list[kk]);
         const double2 tp = tpos[k];
         const int rq = treq[k];
         const int w0 = P.winner[k];
         const double u0 = P.util[k];
+        uint32_t ov_a = 0, ov_b = 0;
+        if (PASS == PASS_RESOLVE) {
+            ov_a = P.D.ov_off[kk];
+            ov_b = P.D.ov_off[kk + 1];
+        }
         int nclaims = 0;
-        bool w0c = false;
+        bool w0c = false, tflag = false;
         uint32_t total = 0;
         if (P.rp2 >= 0.0) {
-            if (HASH)
+            if (SRC == SRC_HASH)
                 window_setup(tp, rp, hg, bucket_off, w, lane);
-            else
+            else if (SRC == SRC_ROWS)
                 window_setup_rows(tp, rp, g, bucket_off, w, lane);
+            else
+                window_setup_all(n_all, w, lane);
             total = w.pre[w.ncell];
         }
         // pass 1: evaluate candidates, keep claims in LDS
@@ -357,20 +449,32 @@ __global__ __launch_bounds__(kBlock) void k_alloc_binned(
             }
 #pragma unroll
             for (int u = 0; u < kWU; ++u) {
-                bool claim = false;
+                bool claim = false, fl = false;
                 float x = 0.f;
                 const int j = jj[u];
                 if (j >= 0 && (!HASH || (hcell(p[u].x, hg.inv_cell) == w.cx[j] &&
                                          hcell(p[u].y, hg.inv_cell) == w.cy[j]))) {
                     const double dx = p[u].x - tp.x, dy = p[u].y - tp.y;
                     if (dx * dx + dy * dy <= P.rp2) {
-                        ++my_cand;
+                        if (PASS == PASS_MAIN) ++my_cand;
                         const double U = utility(p[u].x, p[u].y, cp[u], tp.x, tp.y, rq, P.u_scale);
-                        my_flag += guard_flag(U, P.thr);
+                        fl = guard_flag(U, P.thr);
+                        if (PASS == PASS_MAIN) my_flag += fl;
                         claim = U > P.thr;
                         x = float(U);
+                        if (PASS == PASS_RESOLVE && fl) apply_override(P, ov_a, ov_b, ii[u], claim, x);
+                        if (PASS == PASS_COLLECT && fl) {
+                            const unsigned long long slot = atomicAdd(P.D.count + 1, 1ull);
+                            if (slot < (unsigned long long)P.D.pair_cap) {
+                                const bool has = rq < 0 || (rq < 32 && ((cp[u] >> rq) & 1u));
+                                P.D.pairs[slot] = FlagPair{p[u].x, p[u].y, tp.x, tp.y, int32_t(kk), ii[u],
+                                                           has ? 1 : 0, 0};
+                            }
+                        }
                     }
                 }
+                if (PASS == PASS_COLLECT) continue;
+                if (PASS == PASS_MAIN) tflag = tflag || __ballot(fl) != 0ull;
                 const unsigned long long bm = __ballot(claim);
                 if (claim) {
                     const int slot = nclaims + __popcll(bm & below);
@@ -385,6 +489,16 @@ __global__ __launch_bounds__(kBlock) void k_alloc_binned(
             }
         }
         __builtin_amdgcn_wave_barrier();
+        if (PASS == PASS_COLLECT) continue;
+        if (PASS == PASS_MAIN && tflag && P.D.list) {  // the libm pass decides this task
+            if (lane == 0) {
+                const unsigned long long slot = atomicAdd(P.D.count, 1ull);
+                P.D.list[slot] = int32_t(k);
+                bs.bad += bad_req(rq) ? 1 : 0;
+            }
+            __builtin_amdgcn_wave_barrier();
+            continue;
+        }
         const bool overflow = nclaims > kWCap;
         // pass 2: the record chain
         int prev = -1, cur_id = w0, cur_idx = -1, accepted = 0, first_id = -1;
@@ -414,10 +528,13 @@ __global__ __launch_bounds__(kBlock) void k_alloc_binned(
                     const double dx = pp.x - tp.x, dy = pp.y - tp.y;
                     if (dx * dx + dy * dy > P.rp2) continue;
                     const double U = utility(pp.x, pp.y, caps[i], tp.x, tp.y, rq, P.u_scale);
+                    bool claim = U > P.thr;
+                    float x = float(U);
+                    if (PASS == PASS_RESOLVE && guard_flag(U, P.thr)) apply_override(P, ov_a, ov_b, i, claim, x);
                     const int id = ids[i];
-                    if (U > P.thr && id > prev && id < best && (!has || double(float(U)) > cur_u + P.h)) {
+                    if (claim && id > prev && id < best && (!has || double(x) > cur_u + P.h)) {
                         best = id;
-                        best_x = float(U);
+                        best_x = x;
                         best_ix = i;
                     }
                 }
@@ -435,7 +552,7 @@ __global__ __launch_bounds__(kBlock) void k_alloc_binned(
         if (lane == 0) {
             finish_task(P, k, w0, u0, w0c, accepted, first_id, cur_id, cur_u, cur_idx, nclaims, bs);
             bs.overflow += overflow ? 1 : 0;
-            bs.bad += bad_req(rq) ? 1 : 0;
+            if (PASS == PASS_MAIN) bs.bad += bad_req(rq) ? 1 : 0;
         }
         __builtin_amdgcn_wave_barrier();  // the wave's window and claim list are reused
     }
@@ -492,11 +609,15 @@ __global__ __launch_bounds__(kBlock) void k_alloc_dense_tiles(
         for (int q = 0; q < kTileT; ++q) {
             float x = -INFINITY;
             int claim = 0;
+            bool fl = false;
             if (valid) {
                 const double U = utility(ax, ay, c, s_tx[q], s_ty[q], s_rq[q], P.u_scale);
-                my_flag += guard_flag(U, P.thr);
+                fl = guard_flag(U, P.thr);
+                my_flag += fl;
                 if (U > P.thr) { x = float(U); claim = 1; }
             }
+            // the task has a guard-band pair: the libm pass decides it (idempotent byte store)
+            if (P.D.tflag && __ballot(fl) != 0ull && (threadIdx.x & 63) == 0) P.D.tflag[tt * kTileT + q] = 1;
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) {
                 x = fmaxf(x, __shfl_xor(x, off, 64));
@@ -533,8 +654,15 @@ __global__ __launch_bounds__(kBlock) void k_alloc_dense_chain(
     BlockStats bs;
     __shared__ unsigned long long s_c[kBlock / kWave], s_m[kBlock / kWave], s_b[kBlock / kWave];
     for (int64_t k = wave; k < t_count; k += nwaves) {
-        const double2 tp = tpos[k];
         const int rq = treq[k];
+        if (P.D.list && P.D.tflag[k]) {  // a guard-band pair: deferred to the libm pass (SRC_ALL)
+            if (lane == 0) {
+                P.D.list[atomicAdd(P.D.count, 1ull)] = int32_t(k);
+                bs.bad += bad_req(rq) ? 1 : 0;
+            }
+            continue;
+        }
+        const double2 tp = tpos[k];
         const int w0 = P.winner[k];
         const double u0 = P.util[k];
         const float *mk = tmax + k * ntiles;
@@ -648,6 +776,115 @@ __global__ __launch_bounds__(kBlock) void k_utility(int64_t m, const double2 *__
 }  // namespace
 static_assert(sizeof(swarm_grid) == sizeof(Grid), "swarm_grid mirrors the internal Grid");
 
+#define SW_TRY(call)                 \
+    do {                             \
+        const int rc_ = (call);      \
+        if (rc_ != SWARM_OK) return rc_; \
+    } while (0)
+
+namespace {
+
+// A per-task pass's candidate source (SRC_* and what it reads).
+struct Cand {
+    int src = SRC_ALL;
+    const int32_t *sorted = nullptr;
+    const uint32_t *off = nullptr;
+    HashGrid hg{1.0, 0};
+    Grid g{};
+    double rp = 0.0;
+};
+
+template <int SRC, int PASS>
+int launch_one(const Cand &c, int64_t count, int64_t n, const double *tpos, const int8_t *treq, const int32_t *ids,
+               const double *apos, const uint32_t *acaps, const Params &P, hipStream_t s) {
+    const int64_t chk = (SRC == SRC_ROWS && PASS == PASS_MAIN) ? P.check_blocks : 0;
+    hipLaunchKernelGGL((k_alloc_binned<SRC, PASS>), dim3(grid_for(count, kBlock / kWave, 4096) + unsigned(chk)),
+                       dim3(kBlock), 0, s,
+                       count, reinterpret_cast<const double2 *>(tpos), treq, ids,
+                       reinterpret_cast<const double2 *>(apos), acaps, c.sorted, c.off, c.hg, c.g, c.rp, n, P);
+    SW_LAUNCHED();
+    return SWARM_OK;
+}
+
+template <int PASS>
+int launch_tasks(const Cand &c, int64_t count, int64_t n, const double *tpos, const int8_t *treq, const int32_t *ids,
+                 const double *apos, const uint32_t *acaps, const Params &P, hipStream_t s) {
+    if (count <= 0) return SWARM_OK;
+    switch (c.src) {
+        case SRC_HASH: return launch_one<SRC_HASH, PASS>(c, count, n, tpos, treq, ids, apos, acaps, P, s);
+        case SRC_ROWS: return launch_one<SRC_ROWS, PASS>(c, count, n, tpos, treq, ids, apos, acaps, P, s);
+        default: return launch_one<SRC_ALL, PASS>(c, count, n, tpos, treq, ids, apos, acaps, P, s);
+    }
+}
+
+// The reference's utility on the HOST, for guard-band pairs only (agent.py:338-347).  `**2` is
+// CPython's float_pow, which calls libm pow(|x|, 2.0) (it strips a negative base's sign before the
+// call).  Called through a volatile pointer: a compiler folds pow(x, 2.0) into x*x -- the device's
+// arithmetic, not the reference's.
+double (*volatile g_libm_pow)(double, double) = static_cast<double (*)(double, double)>(std::pow);
+
+double ref_utility(const FlagPair &q, double u_scale) {
+    const double dx = q.ax - q.tx, dy = q.ay - q.ty;
+    const double d = std::sqrt(g_libm_pow(std::fabs(dx), 2.0) + g_libm_pow(std::fabs(dy), 2.0));
+    return (u_scale / (1.0 + d)) * (q.has ? 1.0 : 0.0);
+}
+
+// Deferred tasks (P.D.list[0, deferred)): collect their guard-band pairs, decide each on the host
+// with libm pow, resolve the tasks once with those decisions.  One host sync per step; only runs
+// when some pair fell inside the guard band.
+int resolve_deferred(swarm_ctx *ctx, Params P, const Cand &cand, int64_t deferred, int64_t n, const double *tpos,
+                     const int8_t *treq, const int32_t *ids, const double *apos, const uint32_t *acaps,
+                     double claim_thr, double u_scale, hipStream_t s) {
+    unsigned long long *hc = static_cast<unsigned long long *>(pinned(ctx, 128));
+    if (!hc) return SWARM_ERR_OOM;
+    int64_t cap = deferred * 32 > 4096 ? deferred * 32 : 4096;
+    unsigned long long npairs = 0;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        SW_ALLOC(P.D.pairs, ctx, S_FPAIRS, size_t(cap) * sizeof(FlagPair));
+        P.D.pair_cap = cap;
+        SW_HIP(hipMemsetAsync(P.D.count + 1, 0, 8, s));
+        SW_TRY(launch_tasks<PASS_COLLECT>(cand, deferred, n, tpos, treq, ids, apos, acaps, P, s));
+        SW_HIP(hipMemcpyAsync(hc, P.D.count + 1, 8, hipMemcpyDeviceToHost, s));
+        SW_HIP(hipStreamSynchronize(s));
+        npairs = hc[0];
+        if (int64_t(npairs) <= cap) break;
+        cap = int64_t(npairs);  // the second attempt holds every pair (the same ones are flagged)
+    }
+    if (int64_t(npairs) > cap) {
+        set_error("guard-band pair list overflow (%llu > %lld)", npairs, (long long)cap);
+        return SWARM_ERR_HIP;
+    }
+    std::vector<FlagPair> pairs(npairs);
+    if (npairs) {
+        SW_HIP(hipMemcpyAsync(pairs.data(), P.D.pairs, npairs * sizeof(FlagPair), hipMemcpyDeviceToHost, s));
+        SW_HIP(hipStreamSynchronize(s));
+    }
+    std::sort(pairs.begin(), pairs.end(), [](const FlagPair &a, const FlagPair &b) {
+        return a.j != b.j ? a.j < b.j : a.agent < b.agent;
+    });
+    std::vector<uint32_t> ov_off(size_t(deferred) + 1, 0);
+    std::vector<Override> ov(npairs);
+    for (size_t q = 0; q < pairs.size(); ++q) {
+        const double U = ref_utility(pairs[q], u_scale);
+        ov[q] = Override{pairs[q].agent, float(U), U > claim_thr ? 1 : 0, 0};
+        ov_off[size_t(pairs[q].j) + 1] += 1;
+    }
+    for (size_t j = 0; j < size_t(deferred); ++j) ov_off[j + 1] += ov_off[j];
+    const size_t off_bytes = ((ov_off.size() * 4) + 63) & ~size_t(63);
+    uint8_t *ob;
+    SW_ALLOC(ob, ctx, S_OVR, off_bytes + ov.size() * sizeof(Override) + 64);
+    SW_HIP(hipMemcpyAsync(ob, ov_off.data(), ov_off.size() * 4, hipMemcpyHostToDevice, s));
+    if (!ov.empty())
+        SW_HIP(hipMemcpyAsync(ob + off_bytes, ov.data(), ov.size() * sizeof(Override), hipMemcpyHostToDevice, s));
+    P.D.ov_off = reinterpret_cast<const uint32_t *>(ob);
+    P.D.ov = reinterpret_cast<const Override *>(ob + off_bytes);
+    SW_TRY(launch_tasks<PASS_RESOLVE>(cand, deferred, n, tpos, treq, ids, apos, acaps, P, s));
+    SW_HIP(hipStreamSynchronize(s));  // the host vectors above are the copies' sources
+    return SWARM_OK;
+}
+
+}  // namespace
+
 // ix / ix_off: a cell index (swarm_cell_index) of the agents' storage order, or NULL.
 int alloc_impl(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos, const uint32_t *acaps,
                int64_t t, const double *tpos, const int8_t *treq, double claim_thr, double hysteresis,
@@ -681,32 +918,35 @@ int alloc_impl(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos
     P.winner = winner; P.util = util; P.won = won; P.id_to_index = id_to_index;
     P.id_span = id_span; P.nclaim = nclaim; P.nmsg = nmsg; P.stats = dstats;
 
+    // guard-band deferral (FlagPair / Override above): list + counters + per-task flags
+    const size_t defer_list_off = 64, defer_flag_off = 64 + ((size_t(t) * 4 + 63) & ~size_t(63));
+    uint8_t *dbase;
+    SW_ALLOC(dbase, ctx, S_DEFER, defer_flag_off + size_t(t) + 64);
+    P.D.count = reinterpret_cast<unsigned long long *>(dbase);
+    P.D.list = reinterpret_cast<int32_t *>(dbase + defer_list_off);
+    SW_HIP(hipMemsetAsync(P.D.count, 0, 16, s));
+
     const bool nothing = (n == 0) || (used == SWARM_ALLOC_BINNED && rc <= 0.0);
+    Cand cand;  // the main pass's candidate source, reused by the deferred passes
     if (t > 0 && nothing) {
         // no agent can claim: every task keeps its current claim (won credited via id_to_index)
         uint32_t *off;
         SW_ALLOC(off, ctx, S_CELL_START, 16);
         SW_HIP(hipMemsetAsync(off, 0, 16, s));
         P.rp2 = -1.0;
-        hipLaunchKernelGGL(k_alloc_binned<true>, dim3(grid_for(t, kBlock / kWave, 4096)), dim3(kBlock), 0, s, t,
-                           reinterpret_cast<const double2 *>(tpos), treq, ids,
-                           reinterpret_cast<const double2 *>(apos), acaps, (const int32_t *)nullptr, off,
-                           HashGrid{1.0, 0}, Grid{}, 0.0, P);
-        SW_LAUNCHED();
+        cand = Cand{SRC_HASH, nullptr, off, HashGrid{1.0, 0}, Grid{}, 0.0};
+        SW_TRY(launch_tasks<PASS_MAIN>(cand, t, n, tpos, treq, ids, apos, acaps, P, s));
     } else if (t > 0 && used == SWARM_ALLOC_BINNED && ix) {
         // the caller's cell index: the window's grid rows are contiguous storage ranges
         const double rp = rc * (1.0 + 1e-9) + 1e-12;
         P.rp2 = rp * rp;
         SW_ARG(std::floor(2.0 * rp * ix->inv_cell) + 2.0 <= double(kMaxCells),
                "claim radius spans more than 16 rows of the index's cells (use swarm_allocate)");
-        hipLaunchKernelGGL(k_check_index, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s,
-                           reinterpret_cast<const double2 *>(apos), n, *ix, ix_off, dstats + 7);
-        SW_LAUNCHED();
-        hipLaunchKernelGGL(k_alloc_binned<false>, dim3(grid_for(t, kBlock / kWave, 4096)), dim3(kBlock), 0, s, t,
-                           reinterpret_cast<const double2 *>(tpos), treq, ids,
-                           reinterpret_cast<const double2 *>(apos), acaps, (const int32_t *)nullptr, ix_off,
-                           HashGrid{1.0, 0}, *ix, rp, P);
-        SW_LAUNCHED();
+        // the staleness check runs as extra workgroups of the same launch (check_index_part)
+        P.check_blocks = int64_t(grid_for(n, kBlock * 8, 2048));
+        cand = Cand{SRC_ROWS, nullptr, ix_off, HashGrid{1.0, 0}, *ix, rp};
+        SW_TRY(launch_tasks<PASS_MAIN>(cand, t, n, tpos, treq, ids, apos, acaps, P, s));
+        P.check_blocks = 0;
     } else if (t > 0 && used == SWARM_ALLOC_BINNED) {
         // agents bucketed by hashed cell of side Rp (counting sort, no host round trip)
         const double rp = rc * (1.0 + 1e-9) + 1e-12;
@@ -733,12 +973,12 @@ int alloc_impl(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos
         hipLaunchKernelGGL(k_hash_scatter, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s, n, key, rank, off,
                            sorted);
         SW_LAUNCHED();
-        hipLaunchKernelGGL(k_alloc_binned<true>, dim3(grid_for(t, kBlock / kWave, 4096)), dim3(kBlock), 0, s, t,
-                           reinterpret_cast<const double2 *>(tpos), treq, ids,
-                           reinterpret_cast<const double2 *>(apos), acaps, sorted, off, hg, Grid{}, rp, P);
-        SW_LAUNCHED();
+        cand = Cand{SRC_HASH, sorted, off, hg, Grid{}, rp};
+        SW_TRY(launch_tasks<PASS_MAIN>(cand, t, n, tpos, treq, ids, apos, acaps, P, s));
     } else if (t > 0) {
         P.rp2 = 0;
+        P.D.tflag = dbase + defer_flag_off;
+        SW_HIP(hipMemsetAsync(P.D.tflag, 0, size_t(t), s));
         const int64_t ntiles = (n + kTileA - 1) / kTileA;
         uint32_t *kin, *kout;
         int32_t *vin, *order;
@@ -767,13 +1007,18 @@ int alloc_impl(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos
                            reinterpret_cast<const double2 *>(apos), acaps, order, kout, ntiles, tmax,
                            tcnt, P);
         SW_LAUNCHED();
+        // deferred tasks: every agent is a candidate (no radius: rp2 = +inf keeps all finite ones,
+        // the tile kernel's NaN utilities never claim either)
+        P.rp2 = INFINITY;
+        cand = Cand{SRC_ALL, nullptr, nullptr, HashGrid{1.0, 0}, Grid{}, 0.0};
     }
-    unsigned long long *hs = static_cast<unsigned long long *>(pinned(ctx, 64));
+    unsigned long long *hs = static_cast<unsigned long long *>(pinned(ctx, 128));
     if (!hs) return SWARM_ERR_OOM;
     unsigned long long *folded = dstats + size_t(kStatShards) * kStatStride;
     hipLaunchKernelGGL(k_fold_stats, dim3(1), dim3(kWave), 0, s, dstats, folded);
     SW_LAUNCHED();
     SW_HIP(hipMemcpyAsync(hs, folded, 8 * kNumStats, hipMemcpyDeviceToHost, s));
+    SW_HIP(hipMemcpyAsync(hs + kNumStats, P.D.count, 8, hipMemcpyDeviceToHost, s));
     SW_HIP(hipStreamSynchronize(s));
     if (hs[7]) {
         set_error("stale cell index: %llu agent(s) outside their cell's range (positions moved since "
@@ -788,6 +1033,14 @@ int alloc_impl(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos
         set_error("invalid argument: %llu task(s) with treq outside [-1, 31]", (unsigned long long)hs[5]);
         return SWARM_ERR_ARG;
     }
+    const int64_t deferred = int64_t(hs[kNumStats]);
+    if (deferred > 0) {
+        SW_TRY(resolve_deferred(ctx, P, cand, deferred, n, tpos, treq, ids, apos, acaps, claim_thr, u_scale, s));
+        hipLaunchKernelGGL(k_fold_stats, dim3(1), dim3(kWave), 0, s, dstats, folded);
+        SW_LAUNCHED();
+        SW_HIP(hipMemcpyAsync(hs, folded, 8 * kNumStats, hipMemcpyDeviceToHost, s));
+        SW_HIP(hipStreamSynchronize(s));
+    }
     if (stats) {
         stats->n_claims = int64_t(hs[0]);
         stats->n_conflicts = int64_t(hs[1]);
@@ -795,6 +1048,7 @@ int alloc_impl(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos
         stats->n_candidates = used == SWARM_ALLOC_DENSE ? n * t : int64_t(hs[3]);
         stats->n_overflow = int64_t(hs[4]);
         stats->mode_used = used;
+        stats->n_resolved = deferred;
     }
     return SWARM_OK;
 }

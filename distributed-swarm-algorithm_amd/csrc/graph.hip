@@ -3,6 +3,8 @@
 // this builds the synthetic "who hears whom" CSR of SURVEY.md §8d on the device.
 #include "binning.h"
 
+#include <cstring>
+
 namespace swarm {
 namespace {
 
@@ -12,7 +14,7 @@ __global__ __launch_bounds__(kBlock) void k_rgg_rows(const double2 *__restrict__
                                                     int32_t *__restrict__ deg,
                                                     const int32_t *__restrict__ row_ptr,
                                                     int32_t *__restrict__ col,
-                                                    unsigned long long *__restrict__ total) {
+                                                    unsigned long long *__restrict__ total, int sort_rows) {
     unsigned long long mine = 0;
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
         const double2 p = pos[i];
@@ -34,7 +36,7 @@ __global__ __launch_bounds__(kBlock) void k_rgg_rows(const double2 *__restrict__
                 }
             }
         }
-        if (col) {  // rows ascending (insertion sort; rows are short)
+        if (col && sort_rows) {  // rows ascending (insertion sort: every window is short)
             for (int a = 1; a < cnt; ++a) {
                 const int32_t key = col[base + a];
                 int b = a - 1;
@@ -44,7 +46,7 @@ __global__ __launch_bounds__(kBlock) void k_rgg_rows(const double2 *__restrict__
                 }
                 col[base + b + 1] = key;
             }
-        } else {
+        } else if (!col) {
             deg[i] = cnt;
         }
         mine += unsigned(cnt);
@@ -54,7 +56,73 @@ __global__ __launch_bounds__(kBlock) void k_rgg_rows(const double2 *__restrict__
     if ((threadIdx.x & 63) == 0 && mine) atomicAdd(total, mine);
 }
 
+// Work the row kernel will do, from the cell occupancies alone: each agent scans the agents of its
+// 3 x 3 cell window, so W = sum over agents of their window's occupancy (a double: a bound, not a
+// count) and the longest serial scan is the largest window (max_win).
+__global__ __launch_bounds__(kBlock) void k_window_work(const uint32_t *__restrict__ off, Grid g,
+                                                       double *__restrict__ out,
+                                                       unsigned long long *__restrict__ max_win) {
+    double w = 0.0;
+    unsigned long long mx = 0;
+    const int64_t ncells = g.ncx * g.ncy;
+    for (int64_t c = int64_t(blockIdx.x) * kBlock + threadIdx.x; c < ncells; c += int64_t(gridDim.x) * kBlock) {
+        const uint32_t occ = off[c + 1] - off[c];
+        if (occ == 0) continue;
+        const int64_t cx = c % g.ncx, cy = c / g.ncx;
+        const int64_t x0 = cx > 0 ? cx - 1 : 0, x1 = cx + 1 < g.ncx ? cx + 1 : g.ncx - 1;
+        unsigned long long win = 0;
+        for (int64_t yy = (cy > 0 ? cy - 1 : 0); yy <= cy + 1 && yy < g.ncy; ++yy)
+            win += off[yy * g.ncx + x1 + 1] - off[yy * g.ncx + x0];
+        w += double(occ) * double(win);
+        mx = win > mx ? win : mx;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        w += __shfl_xor(w, o, 64);
+        const unsigned long long m = __shfl_xor(mx, o, 64);
+        mx = m > mx ? m : mx;
+    }
+    if ((threadIdx.x & 63) == 0 && w > 0.0) {
+        atomicAdd(out, w);
+        atomicMax(max_win, mx);
+    }
+}
+
+// Bounds on the row kernel's work (one thread per agent): a radius graph over co-located agents
+// (a million agents in one cell) would make swarm_build_rgg run for hours on the device.  A deg-16
+// RGG has windows of ~45 agents: W ~ 45 n (100M agents: 4.5e9), far below these.
+constexpr double kMaxScanPairs = 68719476736.0;          // 2^36 candidate checks in all
+constexpr unsigned long long kMaxWindow = 1ull << 20;    // candidates one thread scans
+constexpr unsigned long long kInKernelSort = 64;         // longer windows: rows sorted by hipCUB
+
 }  // namespace
+}  // namespace swarm
+
+namespace swarm {
+static int check_window_work(swarm_ctx *ctx, const uint32_t *off, const Grid &g, hipStream_t s,
+                             unsigned long long *max_window) {
+    double *acc;
+    SW_ALLOC(acc, ctx, S_CELL_END, 64);
+    SW_HIP(hipMemsetAsync(acc, 0, 16, s));
+    unsigned long long *mx = reinterpret_cast<unsigned long long *>(acc + 1);
+    hipLaunchKernelGGL(k_window_work, dim3(grid_for(g.ncx * g.ncy, kBlock, 8192)), dim3(kBlock), 0, s, off, g, acc,
+                       mx);
+    SW_LAUNCHED();
+    double *h = static_cast<double *>(pinned(ctx, 64));
+    if (!h) return SWARM_ERR_OOM;
+    SW_HIP(hipMemcpyAsync(h, acc, 16, hipMemcpyDeviceToHost, s));
+    SW_HIP(hipStreamSynchronize(s));
+    unsigned long long m;
+    memcpy(&m, h + 1, 8);
+    *max_window = m;
+    if (h[0] > kMaxScanPairs || m > kMaxWindow) {
+        set_error("radius graph too dense to build: %.3g candidate pairs to scan (limit %.3g), the largest 3x3-cell "
+                  "window holds %llu agents (limit %llu) -- co-located agents?",
+                  h[0], kMaxScanPairs, m, kMaxWindow);
+        return SWARM_ERR_RANGE;
+    }
+    return SWARM_OK;
+}
 }  // namespace swarm
 
 extern "C" {
@@ -80,6 +148,9 @@ int swarm_build_rgg(swarm_ctx *ctx, int64_t n, const double *pos, double radius,
     int32_t *sorted;
     uint32_t *off;
     if ((rc = bin_agents(ctx, n, pos, g, &sorted, &off, s))) return rc;
+    unsigned long long max_win = 0;
+    if ((rc = check_window_work(ctx, off, g, s, &max_win))) return rc;
+    const int sort_rows = max_win <= kInKernelSort ? 1 : 0;
     int32_t *deg;
     unsigned long long *total;
     SW_ALLOC(deg, ctx, S_DEG, size_t(n + 1) * 4);
@@ -93,7 +164,7 @@ int swarm_build_rgg(swarm_ctx *ctx, int64_t n, const double *pos, double radius,
         SW_HIP(hipMemsetAsync(total, 0, 8, s));
         SW_HIP(hipMemsetAsync(deg + n, 0, 4, s));
         hipLaunchKernelGGL(k_rgg_rows, grid, dim3(kBlock), 0, s, p2, n, g, r2, sorted, off, deg,
-                           nullptr, nullptr, total);
+                           nullptr, nullptr, total, 0);
         SW_LAUNCHED();
         SW_HIP(hipMemcpyAsync(htot, total, 8, hipMemcpyDeviceToHost, s));
         SW_HIP(hipStreamSynchronize(s));
@@ -116,8 +187,20 @@ int swarm_build_rgg(swarm_ctx *ctx, int64_t n, const double *pos, double radius,
     SW_ARG(int64_t(e) <= col_capacity, "col_capacity smaller than the edge count");
     SW_HIP(hipMemsetAsync(total, 0, 8, s));
     hipLaunchKernelGGL(k_rgg_rows, grid, dim3(kBlock), 0, s, p2, n, g, r2, sorted, off, deg,
-                       row_ptr, col, total);
+                       row_ptr, col, total, sort_rows);
     SW_LAUNCHED();
+    if (!sort_rows && e > 0) {  // long rows: one segmented radix sort instead of O(deg^2) per thread
+        int32_t *tmpcol;
+        SW_ALLOC(tmpcol, ctx, S_TMP1, size_t(e) * 4);
+        SW_HIP(hipMemcpyAsync(tmpcol, col, size_t(e) * 4, hipMemcpyDeviceToDevice, s));
+        size_t tmp_bytes = 0;
+        SW_HIP(hipcub::DeviceSegmentedRadixSort::SortKeys(nullptr, tmp_bytes, tmpcol, col, int(e), int(n), row_ptr,
+                                                          row_ptr + 1, 0, 32, s));
+        void *tmp;
+        SW_ALLOC(tmp, ctx, S_CUB_TMP, tmp_bytes);
+        SW_HIP(hipcub::DeviceSegmentedRadixSort::SortKeys(tmp, tmp_bytes, tmpcol, col, int(e), int(n), row_ptr,
+                                                          row_ptr + 1, 0, 32, s));
+    }
     SW_HIP(hipStreamSynchronize(s));
     *n_edges = e;
     return SWARM_OK;

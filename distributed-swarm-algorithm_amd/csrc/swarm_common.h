@@ -50,6 +50,9 @@ enum Slot {
     S_FSM_LIST,       // protocol: receivers of the current tick
     S_FSM_FROM,       // protocol: each receiver's sender when it has exactly one
     S_FSM_SEND,       // protocol: per-workgroup sender segments + counts
+    S_DEFER,          // allocation: guard-band tasks deferred to the libm pass (list + per-task flags)
+    S_FPAIRS,         // allocation: the deferred tasks' guard-band pairs (device -> host)
+    S_OVR,            // allocation: host libm decisions for those pairs (host -> device)
     S_NUM
 };
 

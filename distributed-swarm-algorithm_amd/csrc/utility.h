@@ -28,7 +28,9 @@ __device__ __forceinline__ double utility(double ax, double ay, uint32_t caps, d
 __host__ __device__ __forceinline__ bool bad_req(int rq) { return rq < -1 || rq > 31; }
 
 // Could the reference (libm pow for the squares, <= 2 ulp away) decide or round differently?
+// U == 0 is exact under either arithmetic (has_cap = 0, u_scale = 0 or an infinite distance).
 __device__ __forceinline__ bool guard_flag(double U, double thr) {
+    if (U == 0.0) return false;
     const double band = fmax(fabs(thr), fabs(U)) * 0x1p-49;
     if (fabs(U - thr) <= band) return true;
     if (U > thr) {

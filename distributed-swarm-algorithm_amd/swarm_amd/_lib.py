@@ -49,7 +49,7 @@ class Fsm(ctypes.Structure):
 class AllocStats(ctypes.Structure):
     _fields_ = [("n_claims", ctypes.c_int64), ("n_conflicts", ctypes.c_int64),
                 ("n_flagged", ctypes.c_int64), ("n_candidates", ctypes.c_int64),
-                ("n_overflow", ctypes.c_int64), ("mode_used", ctypes.c_int64)]
+                ("n_overflow", ctypes.c_int64), ("mode_used", ctypes.c_int64), ("n_resolved", ctypes.c_int64)]
 
 
 class ElectStats(ctypes.Structure):
@@ -149,9 +149,14 @@ def lib():
     return _lib if _lib is not None else load()
 
 
+def last_error() -> str:
+    """This thread's libswarm error text (swarm_last_error)."""
+    return lib().swarm_last_error().decode(errors="replace")
+
+
 def check(rc: int):
     if rc < 0:
-        raise SwarmError(rc, lib().swarm_last_error().decode(errors="replace"))
+        raise SwarmError(rc, last_error())
     return rc
 
 

@@ -1,9 +1,11 @@
 """Multi-GPU swarm step: agents sharded across ranks, one process per GPU.
 
 Partition.  The global square is cut into horizontal strips, one per rank (the agent storage
-order inside a shard is row-major cell order, so a strip is a contiguous ID-free range of the
-spatial order).  Each rank owns the agents inside its strip and keeps *ghost* copies of the
-neighbouring ranks' agents within k radio radii of the shared border (k = halo depth).
+order inside a shard is row-major cell order, so a strip is a contiguous range of the spatial
+order).  north_star partitions agents by ID range: with strip-major IDs (gen.strip_ids,
+gen.shard_inputs) each rank's contiguous ID range IS its strip, and partition(by="id") cuts by
+ID and checks exactly that.  Each rank owns the agents inside its strip and keeps *ghost* copies
+of the neighbouring ranks' agents within k radio radii of the shared border (k = halo depth).
 
 Election (exact, contract E2).  Rounds run on every rank in lockstep through the frontier
 stepper (include/swarm.h: swarm_frontier_*): round t gathers owned AND ghost agents over the
@@ -53,6 +55,7 @@ class Part:
     cuts: np.ndarray         # the world - 1 interior strip boundaries (the same on every rank)
     agents: np.ndarray       # int64 indices of the owned agents, ascending
     tasks: np.ndarray        # int64 indices of the tasks this rank resolves, ascending
+    id_range: tuple = None   # by="id": [lo, hi) of the IDs this rank owns
 
 
 def strip_cuts(y, world: int) -> np.ndarray:
@@ -65,10 +68,29 @@ def strip_cuts(y, world: int) -> np.ndarray:
     return np.partition(y, ks)[ks].astype(np.float64)
 
 
-def partition(x, y, world: int, rank: int, *, ty=None, min_height: float = 0.0) -> Part:
+def id_cuts(ids, world: int) -> np.ndarray:
+    """world - 1 ID boundaries at the ID quantiles k / world: ranges of (nearly) equal agent
+    counts.  Agent i belongs to range searchsorted(cuts, ids[i], 'right')."""
+    ids = np.asarray(ids, np.int64)
+    if world <= 1 or len(ids) == 0:
+        return np.zeros(0, np.int64)
+    ks = [(k * len(ids)) // world for k in range(1, world)]
+    return np.partition(ids, ks)[ks].astype(np.int64)
+
+
+def partition(x, y, world: int, rank: int, *, ty=None, min_height: float = 0.0, by: str = "y",
+              ids=None) -> Part:
     """Split ONE global swarm (every rank passes the same arrays) into `world` horizontal strips
     of equal agent count; rank `rank` owns the agents of strip `rank` and the tasks whose y falls
     in it (tasks outside the agents' y-range go to the first / last strip).
+
+    by="id" (north_star / SURVEY §8e: "agents are partitioned by ID range"): rank k owns the
+    k-th of `world` contiguous ID ranges of equal agent count.  The halo machinery is a chain of
+    strips, so the ranges must BE strips -- every agent of range k below every agent of range
+    k + 1 in y (strip-major IDs: gen.strip_ids, gen.shard_inputs).  The strip cuts are then read
+    off the ranges (the lowest y of each range above the first), and the function checks that
+    cutting by those y values assigns every agent to its own ID range (ValueError otherwise:
+    random or Morton IDs give ranges with up to 8 spatial neighbours, not a chain).
 
     Why the strips reproduce the single-swarm results: every agent is owned by
     exactly one rank, every RGG edge joins agents of the same or of adjacent strips when strips
@@ -80,8 +102,24 @@ def partition(x, y, world: int, rank: int, *, ty=None, min_height: float = 0.0) 
         raise ValueError("rank out of range")
     x = np.asarray(x, np.float64)
     y = np.asarray(y, np.float64)
-    cuts = strip_cuts(y, world)
-    who = np.searchsorted(cuts, y, side="right")
+    id_range = None
+    if by == "y":
+        cuts = strip_cuts(y, world)
+        who = np.searchsorted(cuts, y, side="right")
+    elif by == "id":
+        if ids is None:
+            raise ValueError('partition(by="id") needs ids')
+        ids = np.asarray(ids, np.int64)
+        icut = id_cuts(ids, world)
+        who = np.searchsorted(icut, ids, side="right")
+        cuts = np.array([y[who == k].min() for k in range(1, world)], np.float64) if world > 1 else np.zeros(0)
+        if not np.array_equal(np.searchsorted(cuts, y, side="right"), who):
+            raise ValueError("the ID ranges are not horizontal strips (every agent of range k must lie below every "
+                             "agent of range k + 1): ID-range sharding needs strip-major IDs (gen.strip_ids)")
+        edges_id = np.concatenate([[ids.min() if len(ids) else 0], icut, [ids.max() + 1 if len(ids) else 0]])
+        id_range = (int(edges_id[rank]), int(edges_id[rank + 1]))
+    else:
+        raise ValueError(f"unknown partition key {by!r}")
     agents = np.nonzero(who == rank)[0].astype(np.int64)
     lo = float(y.min()) if len(y) else 0.0
     hi = float(y.max()) if len(y) else 0.0
@@ -94,7 +132,7 @@ def partition(x, y, world: int, rank: int, *, ty=None, min_height: float = 0.0) 
     if ty is not None:
         tw = np.searchsorted(cuts, np.asarray(ty, np.float64), side="right")
         tasks = np.nonzero(tw == rank)[0].astype(np.int64)
-    return Part(rank, world, strip, cuts, agents, tasks)
+    return Part(rank, world, strip, cuts, agents, tasks, id_range)
 
 
 def _neighbors(rank, world):
@@ -392,15 +430,16 @@ class ShardedSwarm:
 
     @classmethod
     def from_global(cls, ids, x, y, caps=None, *, ty=None, radius: float = 1.0, group=None, device=None,
-                    backend=None, halo=None, halo_depth: int | None = None):
+                    backend=None, halo=None, halo_depth: int | None = None, by: str = "y"):
         """This rank's shard of ONE global swarm (every rank passes the same arrays): strips of
-        equal agent count (partition()).  self.part holds the global indices of the owned agents
-        and of the tasks this rank resolves (allocate_global)."""
+        equal agent count (partition(); by="id": contiguous ID ranges, which must be strips).
+        self.part holds the global indices of the owned agents and of the tasks this rank
+        resolves (allocate_global)."""
         if halo is not None:
             rank, world = halo.rank, halo.world
         else:
             rank, world = dist.get_rank(group), dist.get_world_size(group)
-        part = partition(x, y, world, rank, ty=ty, min_height=radius)
+        part = partition(x, y, world, rank, ty=ty, min_height=radius, by=by, ids=ids)
         a = part.agents
         caps_a = None if caps is None else np.asarray(caps)[a]
         sh = cls(np.asarray(ids)[a], np.asarray(x)[a], np.asarray(y)[a], caps_a, part.strip, radius=radius,
@@ -562,7 +601,7 @@ class ShardedSwarm:
             won.index_add_(0, s_lo, back_lo)
         if back_hi.numel():
             won.index_add_(0, s_hi, back_hi)
-        keys = ("n_claims", "n_conflicts", "n_flagged", "n_candidates", "n_overflow")
+        keys = ("n_claims", "n_conflicts", "n_flagged", "n_candidates", "n_overflow", "n_resolved")
         st = h.all_reduce_sum([res.stats[k] for k in keys])
         gstats = dict(zip(keys, (int(v) for v in st)))
         return res, won, gstats

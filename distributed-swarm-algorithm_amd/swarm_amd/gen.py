@@ -91,24 +91,57 @@ def feistel_ids(index: np.ndarray, total: int, seed: int, rounds: int = 4) -> np
     return out.astype(np.int64)
 
 
-def shard_inputs(n_per: int, seed: int, world: int, rank: int, deg: float = 16.0, t: int = 0):
+def shard_inputs(n_per: int, seed: int, world: int, rank: int, deg: float = 16.0, t: int = 0,
+                 ids: str = "range"):
     """Rank `rank`'s part of a world-wide synthetic swarm of n_per*world agents: uniform
-    positions inside the rank's horizontal strip of the global square, IDs from a global
-    seeded bijection (unique across ranks), tasks inside the strip."""
+    positions inside the rank's horizontal strip of the global square, tasks inside the strip.
+    ids="range" (north_star: agents partitioned by ID range): rank k owns exactly the contiguous
+    ID range [k n_per, (k+1) n_per), in a seeded random order inside its strip -- the ID range IS
+    the strip.  ids="global": one global seeded bijection (IDs unrelated to ranks)."""
     total = n_per * world
     side = side_length(total, deg)
     h = side / world
     sseed = seed * 1000003 + rank
     x = uniform(sseed, TAG_X, n_per) * side
     y = rank * h + uniform(sseed, TAG_Y, n_per) * h
-    gidx = np.arange(n_per, dtype=np.int64) + np.int64(rank) * n_per
-    ids = feistel_ids(gidx, total, seed).astype(np.int32)
+    if ids == "range":
+        loc = feistel_ids(np.arange(n_per, dtype=np.int64), n_per, seed * 7919 + rank)
+        idv = (loc + np.int64(rank) * n_per).astype(np.int32)
+    elif ids == "global":
+        gidx = np.arange(n_per, dtype=np.int64) + np.int64(rank) * n_per
+        idv = feistel_ids(gidx, total, seed).astype(np.int32)
+    else:
+        raise ValueError(f"unknown ids {ids!r}")
     out = dict(n=n_per, total=total, seed=seed, deg=deg, side=side, strip=(rank * h, (rank + 1) * h),
-               x=x, y=y, ids=ids, caps=capabilities(n_per, sseed))
+               x=x, y=y, ids=idv, id_range=(rank * n_per, (rank + 1) * n_per), caps=capabilities(n_per, sseed))
     if t:
         tx, ty, treq = tasks(t, sseed, side)
         out["tx"], out["ty"], out["treq"] = tx, rank * h + ty / side * h, treq
     return out
+
+
+def strip_ids(y: np.ndarray, world: int, seed: int) -> np.ndarray:
+    """IDs 0..n-1 for one global swarm such that the `world` contiguous ID ranges of equal size
+    are the `world` horizontal strips of equal agent count (y-quantile cuts, as
+    dist.strip_cuts): strip k holds IDs [sum of the strips below, + its count), in a seeded
+    random order.  dist.partition(by="id") then cuts exactly the strips ("agents are
+    partitioned by ID range"; strip-major ranks instead of Morton ranks keep each range's
+    neighbours to the two adjacent ranges -- the chain halo of dist.py)."""
+    y = np.asarray(y, np.float64)
+    n = len(y)
+    if world <= 1 or n == 0:
+        who = np.zeros(n, np.int64)
+    else:
+        ks = [(k * n) // world for k in range(1, world)]
+        cuts = np.partition(y, ks)[ks]
+        who = np.searchsorted(cuts, y, side="right")
+    out = np.empty(n, np.int64)
+    base = 0
+    for k in range(max(world, 1)):
+        idx = np.nonzero(who == k)[0]
+        out[idx] = base + feistel_ids(np.arange(len(idx), dtype=np.int64), max(len(idx), 1), seed * 31 + k)
+        base += len(idx)
+    return out.astype(np.int32)
 
 
 def capabilities(n: int, seed: int, ncaps: int = 4, p: float = 0.5) -> np.ndarray:

@@ -26,6 +26,10 @@ from . import _lib
 
 CAP_VOCAB_DEFAULT = ("extinguisher", "sonar", "camera", "gripper")
 STATUS_NAMES = ("OPEN", "TENTATIVE", "LOCKED", "ASSIGNED")
+# Capability bit reserved for "a required capability no agent holds" (a task dict naming a
+# capability outside the vocabulary: agent.py:344 gives every agent has_cap = 0 for it).  The
+# bridge never sets it on an agent, so vocabularies hold at most 31 names.
+CAP_UNHELD_BIT = 31
 
 
 def _dev(device):
@@ -219,7 +223,7 @@ class Swarm:
         if self.row_ptr is None:
             raise RuntimeError("no neighbour graph: call build_graph() or set_graph()")
         if wide is None:
-            wide = self.n_edges >= (1 << 30)
+            wide = self.n_edges >= (1 << 30) or self.n >= (1 << 30)
         if wide:
             return self._elect_wide(mode, max_rounds, timed, compact)
         m = {"dense": _lib.ELECT_DENSE, "frontier": _lib.ELECT_FRONTIER}[mode] | (_lib.ELECT_TIMED if timed else 0)
@@ -290,7 +294,9 @@ class Swarm:
         res.changes_total = st.changes_total
         res.gather_ms, res.apply_ms, res.timed_launches = st.gather_ms, st.apply_ms, st.gather_launches
         res.sparse_ms, res.sparse_launches, res.sparse_bytes = st.sparse_ms, st.sparse_launches, st.sparse_bytes
-        res.compact = c16 is not None
+        # the int64-offset DENSE rounds read the int32 columns (elect.hip launch_dense_round takes
+        # col16 only with 32-bit offsets): only the frontier's sparse rounds read the 16-bit ones
+        res.compact = c16 is not None and mode == "frontier"
         return res
 
     # ------------------------------------------------------------------ allocation
@@ -314,14 +320,27 @@ class Swarm:
 
     def _cell_index(self):
         """(Grid, cell_off) of the storage order (swarm_cell_index), built once; the allocation
-        verifies it on the device every call and drops it when positions have moved."""
+        verifies it on the device every call and drops it when positions have moved.  None when
+        the current positions are no longer in cell order (after physics_step moved agents across
+        cells): allocate() then bins by hashed cells, and the index is tried again only after
+        the positions change again (self._cindex = False marks 'not indexable' for the position
+        tensor and version in self._cindex_bad)."""
+        pos_key = (self.pos.data_ptr(), self.pos._version)
+        if self._cindex is False:
+            if getattr(self, "_cindex_bad", None) == pos_key:
+                return None
+            self._cindex = None
         if self._cindex is None:
             L, g, nc = _lib.lib(), _lib.Grid(), ctypes.c_int64(0)
             _lib.check(L.swarm_cell_index(_lib.ctx(), self.n, _lib.ptr(self.pos), self.cell, ctypes.byref(g), None, 0,
                                           ctypes.byref(nc), _lib.stream()))
             off = torch.empty(nc.value + 1, dtype=torch.int32, device=self.device)
-            _lib.check(L.swarm_cell_index(_lib.ctx(), self.n, _lib.ptr(self.pos), self.cell, ctypes.byref(g),
-                                          _lib.ptr(off), off.numel(), ctypes.byref(nc), _lib.stream()))
+            rc = L.swarm_cell_index(_lib.ctx(), self.n, _lib.ptr(self.pos), self.cell, ctypes.byref(g),
+                                    _lib.ptr(off), off.numel(), ctypes.byref(nc), _lib.stream())
+            if rc == _lib.ERR_ARG and "not in cell order" in _lib.last_error():
+                self._cindex, self._cindex_bad = False, pos_key
+                return None
+            _lib.check(rc)
             self._cindex = (g, off)
         return self._cindex
 
@@ -358,7 +377,7 @@ class Swarm:
                     0 if idx is None else idx.numel(), _lib.ptr(nclaim), _lib.ptr(nmsg), ctypes.byref(st),
                     _lib.stream())
                 if rc == _lib.ERR_STALE:  # positions moved since the index: bin them this call
-                    self._cindex = None
+                    self._cindex = None  # rebuilt next call if they are still in cell order
                     w.copy_(w0) if w0 is not None else w.fill_(-1)
                     u.copy_(u0) if u0 is not None else u.zero_()
                 else:
@@ -522,6 +541,9 @@ class Swarm:
 
         neighbors: list of neighbour-index lists (who agent i hears), or None to build the
         radius-1 graph from positions on the GPU."""
+        if len(cap_vocab) > CAP_UNHELD_BIT:
+            raise ValueError(f"at most {CAP_UNHELD_BIT} capability names (bit {CAP_UNHELD_BIT} is reserved for "
+                             f"capabilities no agent holds), got {len(cap_vocab)}")
         vocab = {c: k for k, c in enumerate(cap_vocab)}
         ids = np.array([a.agent_id for a in agents], np.int32)
         x = np.array([a.position[0] for a in agents], np.float64)
@@ -558,8 +580,8 @@ class Swarm:
         tid = np.array(list(tasks.keys()), np.int64)
         tx = np.array([tasks[k]["pos"][0] for k in tid], np.float64)
         ty = np.array([tasks[k]["pos"][1] for k in tid], np.float64)
-        # a required cap nobody can have still blocks every agent: bit 31 is never set
-        treq = np.array([vocab.get(tasks[k]["required_cap"], 31) if "required_cap" in tasks[k] else -1
+        # a required cap outside the vocabulary blocks every agent: the reserved bit no agent holds
+        treq = np.array([vocab.get(tasks[k]["required_cap"], CAP_UNHELD_BIT) if "required_cap" in tasks[k] else -1
                          for k in tid], np.int8)
         return tid, tx, ty, treq
 

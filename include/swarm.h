@@ -65,6 +65,7 @@ typedef struct swarm_alloc_stats {
     int64_t n_candidates;    /* agent x task pairs evaluated exactly in fp64 */
     int64_t n_overflow;      /* tasks whose claims exceeded the on-chip list (slow exact path) */
     int64_t mode_used;       /* SWARM_ALLOC_BINNED or SWARM_ALLOC_DENSE */
+    int64_t n_resolved;      /* tasks with a guard-band pair, decided with the host's libm pow */
 } swarm_alloc_stats;
 
 typedef struct swarm_elect_stats {
@@ -239,6 +240,12 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sha
  * _handle_task_conflict (agent.py:327-336).
  *   U(a,k) = (u_scale / (1 + sqrt(dx*dx + dy*dy))) * has_cap   (fp64, no FMA contraction)
  *   claim iff U > claim_thr; claim value x = f32(U) (round to nearest even)
+ *   Guard band: the reference squares with libm pow(|d|, 2.0), which can
+ *   differ from d*d by an ulp.  Every task with a pair whose decision or f32 value such an ulp
+ *   could change (stats->n_flagged pairs) is deferred; those pairs are decided on the HOST with
+ *   this process's libm pow, exactly as agent.py:297/302/340 compute them, and the task is then
+ *   resolved once with them (stats->n_resolved tasks; one extra host round trip when > 0).  The
+ *   outputs are therefore the reference's on this host's libm, not only the x*x arithmetic's.
  *   per task, claims in ascending agent ID: the first claim wins if the task has no current
  *   winner, otherwise a claim replaces the winner iff x > util + hysteresis (fp64).
  * apos (n*2 f64), acaps (n u32: bit k = capability k), tpos (t*2 f64), treq (t i8: -1 none).
@@ -295,7 +302,9 @@ int swarm_utility(swarm_ctx *ctx, int64_t m, const double *apos, const uint32_t 
  * Radius graph builder (synthetic/sensor input side of the round):
  * edge i~j (i != j) iff dx*dx + dy*dy <= radius*radius (fp64).  Rows ascending.
  * Call with col == NULL to get row_ptr (device, n+1) and *n_edges (host); then again with col
- * (device, capacity col_capacity) to fill.
+ * (device, capacity col_capacity) to fill.  SWARM_ERR_RANGE (before any row is built) when the
+ * cell occupancies say the build would scan more than 2^36 candidate pairs in all or more than
+ * 2^20 in one agent's 3 x 3 cell window (co-located agents), or the graph has >= 2^31 edges.
  */
 int swarm_build_rgg(swarm_ctx *ctx, int64_t n, const double *pos, double radius,
                     int32_t *row_ptr, int32_t *col, int64_t col_capacity, int64_t *n_edges,

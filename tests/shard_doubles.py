@@ -83,7 +83,7 @@ class NumpyBackend:
         out.nmsg = torch.as_tensor(r["nmsg"])
         out.nclaim = torch.as_tensor(r["nclaim"])
         out.stats = dict(n_claims=r["n_claims"], n_conflicts=r["n_conflicts"], n_flagged=0,
-                         n_candidates=len(ids) * len(tx), n_overflow=0)
+                         n_candidates=len(ids) * len(tx), n_overflow=0, n_resolved=0)
         return out
 
 

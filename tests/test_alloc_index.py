@@ -104,3 +104,54 @@ def test_cell_index_rejects_unsorted(mods):
     with pytest.raises(_lib.SwarmError, match="not in cell order"):
         _lib.check(L.swarm_cell_index(_lib.ctx(), 10_000, _lib.ptr(pos), 1.0, ctypes.byref(g), _lib.ptr(off),
                                       off.numel(), ctypes.byref(nc), _lib.stream()))
+
+
+def _oracle_now(oracle_mod, s, tx, ty, tq, **kw):
+    """The oracle over the Swarm's CURRENT storage-order state (x*x arithmetic, as the GPU)."""
+    ids, x, y = s.ids.cpu().numpy(), s.pos[:, 0].cpu().numpy(), s.pos[:, 1].cpu().numpy()
+    return oracle_mod.allocate_binned(ids, x, y, s.caps.cpu().numpy().view(np.uint32), tx, ty, tq, use_pow=False,
+                                      **kw)
+
+
+def test_physics_then_allocate(mods, oracle_mod):
+    """physics_step moves agents across cells, so the storage order is no longer cell order: the
+    next allocate() must bin by hashed cells (not fail building the index), and so must the one
+    after it (both used to raise SwarmError)."""
+    swm, _lib, gen = mods
+    d = gen.swarm_inputs(30_000, 21, t=1_500)
+    s = swm.Swarm(d["ids"], d["x"], d["y"], d["caps"], device="cuda").build_graph(1.0)
+    s.allocate(d["tx"], d["ty"], d["treq"])
+    assert s._cindex not in (None, False)
+    s.elect()
+    obs = np.array([[30.0, 30.0, 2.0], [60.0, 20.0, 1.0]])
+    s.physics_step(obs, steps=6)
+    moved = int((s.to_input_order(s.pos) != np.stack([d["x"], d["y"]], 1)).any(1).sum())
+    assert moved > 1000
+    for _ in range(2):
+        a = s.allocate(d["tx"], d["ty"], d["treq"])
+        want = _oracle_now(oracle_mod, s, d["tx"], d["ty"], d["treq"])
+        for k in ("winner", "nclaim", "nmsg", "won"):
+            np.testing.assert_array_equal(getattr(a, k).cpu().numpy(), want[k], err_msg=k)
+        np.testing.assert_array_equal(a.util.cpu().numpy(), want["util"])
+    assert s._cindex is False  # not indexable until the positions change again
+
+
+def test_edge_agent_moved_past_bbox(mods, oracle_mod):
+    """An edge-cell agent moved just past the indexed bounding box maps (clamped) to its old cell;
+    the index must report itself stale instead of dropping that agent's claims."""
+    swm, _lib, gen = mods
+    d = gen.swarm_inputs(20_000, 23, t=200)
+    s = swm.Swarm(d["ids"], d["x"], d["y"], d["caps"], device="cuda")
+    xmax = float(d["x"].max())
+    tx = np.concatenate([d["tx"], [xmax + 5.0]])
+    ty = np.concatenate([d["ty"], [float(d["y"][np.argmax(d["x"])])]])
+    tq = np.concatenate([d["treq"], [-1]]).astype(np.int8)
+    s.allocate(tx, ty, tq)
+    assert s._cindex not in (None, False)
+    i = int(torch.argmax(s.pos[:, 0]))
+    s.pos[i, 0] = xmax + 3.0  # in place, behind the Swarm's back: 2.0 from the last task
+    a = s.allocate(tx, ty, tq)
+    want = _oracle_now(oracle_mod, s, tx, ty, tq)
+    assert want["nclaim"][-1] >= 1
+    for k in ("winner", "nclaim", "won"):
+        np.testing.assert_array_equal(getattr(a, k).cpu().numpy(), want[k], err_msg=k)

@@ -112,6 +112,37 @@ def test_shard_ids_are_a_global_permutation():
     from swarm_amd import gen
     ids = np.concatenate([gen.shard_inputs(777, 3, 5, r)["ids"] for r in range(5)])
     assert (np.sort(ids) == np.arange(777 * 5)).all()
+    for r in range(5):  # ids="range": rank r owns exactly the ID range [777 r, 777 (r + 1)) -- its strip
+        d = gen.shard_inputs(777, 3, 5, r)
+        assert (np.sort(d["ids"]) == np.arange(*d["id_range"])).all() and d["id_range"] == (777 * r, 777 * (r + 1))
+        assert (d["y"] >= d["strip"][0]).all() and (d["y"] < d["strip"][1]).all()
+    ids = np.concatenate([gen.shard_inputs(777, 3, 5, r, ids="global")["ids"] for r in range(5)])
+    assert (np.sort(ids) == np.arange(777 * 5)).all()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_partition_by_id_range_is_the_strip_partition(world):
+    """north_star's ID-range partition: with strip-major IDs each rank's contiguous ID range is
+    exactly its y-strip (the same owned agents and tasks as partition(by='y')); IDs that are not
+    strip-major are refused."""
+    from swarm_amd import gen
+    from swarm_amd.dist import partition
+    d = gen.swarm_inputs(6_000, 17, t=300)
+    ids = gen.strip_ids(d["y"], world, 17)
+    assert np.array_equal(np.sort(ids), np.arange(6_000))
+    covered = []
+    for r in range(world):
+        pi = partition(d["x"], d["y"], world, r, ty=d["ty"], by="id", ids=ids)
+        py = partition(d["x"], d["y"], world, r, ty=d["ty"])
+        np.testing.assert_array_equal(pi.agents, py.agents)
+        np.testing.assert_array_equal(pi.tasks, py.tasks)
+        lo, hi = pi.id_range
+        assert np.array_equal(np.sort(ids[pi.agents]), np.arange(lo, hi))
+        covered.append((lo, hi))
+    assert covered[0][0] == 0 and covered[-1][1] == 6_000
+    assert all(covered[k][1] == covered[k + 1][0] for k in range(world - 1))
+    with pytest.raises(ValueError, match="not horizontal strips"):
+        partition(d["x"], d["y"], world, 0, by="id", ids=d["ids"])  # random IDs
 
 
 # ----------------------------------------------------------------------------- sharded auction
@@ -172,7 +203,15 @@ def test_sharded_auction_matches_single_auction(world, check_every, oracle_mod):
 G_N, G_T = 4000, 150
 
 
-def _global_worker(rank, world, port, out_q, depth):
+def _global_inputs(world, by):
+    from swarm_amd import gen
+    d = gen.swarm_inputs(G_N, SEED + 3, t=G_T)  # the same global arrays on every rank
+    if by == "id":
+        d["ids"] = gen.strip_ids(d["y"], world, SEED + 3)
+    return d
+
+
+def _global_worker(rank, world, port, out_q, depth, by="y"):
     import sys
     for p in (PKG, ROOT, os.path.join(ROOT, "tests")):
         sys.path.insert(0, p)
@@ -182,9 +221,9 @@ def _global_worker(rank, world, port, out_q, depth):
         from shard_doubles import NumpyBackend
         from swarm_amd import gen
         from swarm_amd.dist import ShardedSwarm
-        d = gen.swarm_inputs(G_N, SEED + 3, t=G_T)  # the same global arrays on every rank
+        d = _global_inputs(world, by)
         sh = ShardedSwarm.from_global(d["ids"], d["x"], d["y"], d["caps"], ty=d["ty"], device="cpu",
-                                      backend=NumpyBackend(), halo_depth=depth)
+                                      backend=NumpyBackend(), halo_depth=depth, by=by)
         r = sh.elect(check_every=5)
         res, won, gst = sh.allocate_global(d["tx"], d["ty"], d["treq"])
         out_q.put(dict(rank=rank, rounds=r.rounds_exec, changes=r.changes, ids=sh.ids.numpy(),
@@ -195,23 +234,23 @@ def _global_worker(rank, world, port, out_q, depth):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,depth", [(2, 4), (3, 16)])
-def test_partitioned_global_swarm_matches_single_swarm(world, depth, oracle_mod):
-    """ShardedSwarm.from_global: one global input (random IDs, tasks anywhere) cut into strips of
-    equal agent count on every rank; the union of the shards' results equals the single-swarm
+@pytest.mark.parametrize("world,depth,by", [(2, 4, "y"), (3, 16, "y"), (2, 4, "id"), (3, 16, "id")])
+def test_partitioned_global_swarm_matches_single_swarm(world, depth, by, oracle_mod):
+    """ShardedSwarm.from_global: one global input (tasks anywhere) cut into strips of equal agent
+    count on every rank -- by y with random IDs, or by contiguous ID range with strip-major IDs
+    (north_star's ID-range partition); the union of the shards' results equals the single-swarm
     oracle (leaders, rounds, per-round changes, winners, claim values, conflicts, won counts)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_global_worker, args=(r, world, port, q, depth)) for r in range(world)]
+    procs = [ctx.Process(target=_global_worker, args=(r, world, port, q, depth, by)) for r in range(world)]
     for p in procs:
         p.start()
     outs = sorted([q.get(timeout=240) for _ in range(world)], key=lambda o: o["rank"])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    from swarm_amd import gen
-    d = gen.swarm_inputs(G_N, SEED + 3, t=G_T)
+    d = _global_inputs(world, by)
     # every agent and every task owned exactly once, strips of near-equal size
     agents = np.concatenate([o["agents"] for o in outs])
     assert np.array_equal(np.sort(agents), np.arange(G_N))

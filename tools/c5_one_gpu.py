@@ -54,18 +54,27 @@ if "--no-oracle" in sys.argv:
 
 from oracle import oracle as orc  # noqa: E402  (the checker, never the measured path)
 
+# the stored SoA must be the INPUTS permuted on the host (take_rows guards the > 2^26-row
+# gather bug; this checks it, so the oracle below never sees a wrong GPU gather)
+perm = s.perm.cpu().numpy().astype(np.int64)
+hx, hy, hids = d["x"][perm], d["y"][perm], d["ids"][perm].astype(np.int32)
+hcaps = np.asarray(d["caps"], np.uint32)[perm]
+soa_ok = {"perm_is_permutation": bool(np.array_equal(np.sort(perm), np.arange(s.n))),
+          "pos_x": bool(np.array_equal(s.pos[:, 0].cpu().numpy(), hx)),
+          "pos_y": bool(np.array_equal(s.pos[:, 1].cpu().numpy(), hy)),
+          "ids": bool(np.array_equal(s.ids.cpu().numpy(), hids)),
+          "caps": bool(np.array_equal(s.caps.cpu().numpy().view(np.uint32), hcaps))}
+print(json.dumps({"soa_equals_host_permuted_inputs": soa_ok}), flush=True)
 rp = s.row_ptr.cpu().numpy().astype(np.int64)
 col = s.col.cpu().numpy()
-ids = s.ids.cpu().numpy()
+ids = hids
 lead_gpu, state_gpu = s.leader.cpu().numpy(), s.state.cpu().numpy()
 res = {}
 
 
 def run():
     res["elect"] = orc.elect_frontier(rp, col, ids)
-    res["alloc"] = orc.allocate_binned(ids, s.pos[:, 0].cpu().numpy(), s.pos[:, 1].cpu().numpy(),
-                                       s.caps.cpu().numpy().view(np.uint32), d["tx"], d["ty"], d["treq"],
-                                       use_pow=False)
+    res["alloc"] = orc.allocate_binned(ids, hx, hy, hcaps, d["tx"], d["ty"], d["treq"], use_pow=False)
 
 
 th = threading.Thread(target=run)
@@ -76,7 +85,7 @@ while th.is_alive():
     print(f"oracle running {time.time() - t4:.0f}s", flush=True)
 lead, state, rounds, changes = res["elect"]
 al = res["alloc"]
-ok = {"rounds": rounds == r.rounds_exec, "changes": bool(np.array_equal(changes, r.changes)),
+ok = {**soa_ok, "rounds": rounds == r.rounds_exec, "changes": bool(np.array_equal(changes, r.changes)),
       "leader": bool(np.array_equal(lead, lead_gpu)), "state": bool(np.array_equal(state, state_gpu)),
       "alloc_winner": bool(np.array_equal(al["winner"], a.winner.cpu().numpy())),
       "alloc_nclaim": bool(np.array_equal(al["nclaim"], a.nclaim.cpu().numpy())),
