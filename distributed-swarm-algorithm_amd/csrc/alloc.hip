@@ -87,7 +87,6 @@ struct Params {
     int64_t *nmsg;
     unsigned long long *stats;  // kStatShards x 16 u64: [claims, conflicts, flagged, candidates, overflow, bad treq]
     Defer D;
-    int64_t check_blocks = 0;   // SRC_ROWS main pass: the last check_blocks workgroups verify the index
 };
 
 // candidate sources of the per-task wave kernel
@@ -335,10 +334,10 @@ __device__ __forceinline__ void window_setup_all(int64_t n, CellWindow &w, int l
 // Staleness test of a cell index: every agent must lie in its cell's range AND inside the indexed
 // bounding box.  cell_coord clamps, so an edge-cell agent that moved past [xmin, xmax] x [ymin,
 // ymax] still maps to its old cell; window_setup_rows skips every task whose disc misses that box,
-// so such an agent would lose its claims silently.  Run by `nb` extra workgroups of the indexed
-// allocation's own launch (b = 0..nb-1): the check streams the positions while the task waves
-// wait on their dependent loads; the host reads the count after the launch and reports
-// SWARM_ERR_STALE (outputs undefined) instead of the results.
+// so such an agent would lose its claims silently.  k_check_index runs on the ctx's side stream,
+// concurrently with the indexed allocation (it streams the positions while the task waves wait on
+// their dependent loads); the host reads the count after both and reports SWARM_ERR_STALE
+// (outputs undefined) instead of the results.
 __device__ __forceinline__ void check_index_part(const double2 *__restrict__ apos, int64_t n, const Grid &g,
                                                  const uint32_t *__restrict__ off,
                                                  unsigned long long *__restrict__ bad_out, int64_t b, int64_t nb) {
@@ -352,6 +351,12 @@ __device__ __forceinline__ void check_index_part(const double2 *__restrict__ apo
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) bad += __shfl_xor(bad, o, 64);
     if ((threadIdx.x & 63) == 0 && bad) atomicAdd(bad_out, bad);
+}
+
+__global__ __launch_bounds__(kBlock) void k_check_index(const double2 *__restrict__ apos, int64_t n, Grid g,
+                                                       const uint32_t *__restrict__ off,
+                                                       unsigned long long *__restrict__ bad_out) {
+    check_index_part(apos, n, g, off, bad_out, blockIdx.x, gridDim.x);
 }
 
 // ------------------------------------------------------------------------------ binned
@@ -392,16 +397,7 @@ __global__ __launch_bounds__(kBlock) void k_alloc_binned(
     const unsigned long long below = (1ull << lane) - 1ull;
     long long my_cand = 0, my_flag = 0;
     BlockStats bs;
-    int64_t task_blocks = gridDim.x;
-    if (SRC == SRC_ROWS && PASS == PASS_MAIN && P.check_blocks > 0) {
-        task_blocks -= P.check_blocks;
-        if (int64_t(blockIdx.x) >= task_blocks) {  // whole workgroup: no barrier below is reached
-            check_index_part(apos, n_all, g, bucket_off, P.stats + 7,  // shard 0, slot 7: folded into hs[7]
-                             int64_t(blockIdx.x) - task_blocks, P.check_blocks);
-            return;
-        }
-    }
-    const int64_t nw = task_blocks * kW;
+    const int64_t nw = int64_t(gridDim.x) * kW;
     for (int64_t kk = int64_t(blockIdx.x) * kW + wid; kk < t_count; kk += nw) {
         const int64_t k = PASS == PASS_MAIN ? kk : int64_t(P.D.list[kk]);
         const double2 tp = tpos[k];
@@ -797,9 +793,7 @@ struct Cand {
 template <int SRC, int PASS>
 int launch_one(const Cand &c, int64_t count, int64_t n, const double *tpos, const int8_t *treq, const int32_t *ids,
                const double *apos, const uint32_t *acaps, const Params &P, hipStream_t s) {
-    const int64_t chk = (SRC == SRC_ROWS && PASS == PASS_MAIN) ? P.check_blocks : 0;
-    hipLaunchKernelGGL((k_alloc_binned<SRC, PASS>), dim3(grid_for(count, kBlock / kWave, 4096) + unsigned(chk)),
-                       dim3(kBlock), 0, s,
+    hipLaunchKernelGGL((k_alloc_binned<SRC, PASS>), dim3(grid_for(count, kBlock / kWave, 4096)), dim3(kBlock), 0, s,
                        count, reinterpret_cast<const double2 *>(tpos), treq, ids,
                        reinterpret_cast<const double2 *>(apos), acaps, c.sorted, c.off, c.hg, c.g, c.rp, n, P);
     SW_LAUNCHED();
@@ -942,11 +936,20 @@ int alloc_impl(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos
         P.rp2 = rp * rp;
         SW_ARG(std::floor(2.0 * rp * ix->inv_cell) + 2.0 <= double(kMaxCells),
                "claim radius spans more than 16 rows of the index's cells (use swarm_allocate)");
-        // the staleness check runs as extra workgroups of the same launch (check_index_part)
-        P.check_blocks = int64_t(grid_for(n, kBlock * 8, 2048));
+        // the staleness check on the side stream, concurrent with the allocation (joined before the
+        // counters are folded)
+        hipStream_t s2;
+        hipEvent_t fork, join;
+        SW_TRY(side_stream(ctx, &s2, &fork, &join));
+        SW_HIP(hipEventRecord(fork, s));
+        SW_HIP(hipStreamWaitEvent(s2, fork, 0));
+        hipLaunchKernelGGL(k_check_index, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s2,
+                           reinterpret_cast<const double2 *>(apos), n, *ix, ix_off, dstats + 7);
+        SW_LAUNCHED();
+        SW_HIP(hipEventRecord(join, s2));
         cand = Cand{SRC_ROWS, nullptr, ix_off, HashGrid{1.0, 0}, *ix, rp};
         SW_TRY(launch_tasks<PASS_MAIN>(cand, t, n, tpos, treq, ids, apos, acaps, P, s));
-        P.check_blocks = 0;
+        SW_HIP(hipStreamWaitEvent(s, join, 0));
     } else if (t > 0 && used == SWARM_ALLOC_BINNED) {
         // agents bucketed by hashed cell of side Rp (counting sort, no host round trip)
         const double rp = rc * (1.0 + 1e-9) + 1e-12;

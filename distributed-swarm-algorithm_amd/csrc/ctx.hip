@@ -70,6 +70,19 @@ void *pinned(swarm_ctx *ctx, size_t bytes) {
     return p;
 }
 
+int side_stream(swarm_ctx *ctx, hipStream_t *side, hipEvent_t *fork, hipEvent_t *join) {
+    if (!ctx_on_current_device(ctx)) return SWARM_ERR_ARG;
+    if (!ctx->side) {
+        SW_HIP(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+        SW_HIP(hipEventCreateWithFlags(&ctx->side_ev[0], hipEventDisableTiming));
+        SW_HIP(hipEventCreateWithFlags(&ctx->side_ev[1], hipEventDisableTiming));
+    }
+    *side = ctx->side;
+    *fork = ctx->side_ev[0];
+    *join = ctx->side_ev[1];
+    return SWARM_OK;
+}
+
 // Host memory the device writes directly (coherent, mapped): the election's per-batch counter
 // read-back lands here from the totals kernel itself, with no copy in the stream.
 void *mapped(swarm_ctx *ctx, size_t bytes, void **dev) {
@@ -124,6 +137,9 @@ int swarm_ctx_destroy(swarm_ctx *ctx) {
         if (ctx->slot[s]) (void)hipFree(ctx->slot[s]);
     if (ctx->host_pinned) (void)hipHostFree(ctx->host_pinned);
     if (ctx->host_mapped) (void)hipHostFree(ctx->host_mapped);
+    for (auto e : ctx->side_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->side) (void)hipStreamDestroy(ctx->side);
     delete ctx;
     return SWARM_OK;
 }

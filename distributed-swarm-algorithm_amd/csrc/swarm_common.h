@@ -88,6 +88,8 @@ struct swarm_ctx {
     size_t mapped_cap = 0;
     int64_t step_rows = 0;         // frontier stepper: owned rows / agents (rows + ghosts)
     int64_t step_all = 0;
+    hipStream_t side = nullptr;    // a second stream for work that overlaps the caller's (side_stream)
+    hipEvent_t side_ev[2] = {};    // fork / join events
 };
 
 namespace swarm {
@@ -101,6 +103,10 @@ void *scratch(swarm_ctx *ctx, Slot s, size_t bytes);
 int scratch_code();
 bool ctx_on_current_device(const swarm_ctx *ctx);
 void *pinned(swarm_ctx *ctx, size_t bytes);
+// The ctx's side stream and a fork / join event pair (created on first use, on the ctx's device):
+// record fork on the caller's stream, wait for it on *side, launch there, record join on *side,
+// wait for join on the caller's stream.
+int side_stream(swarm_ctx *ctx, hipStream_t *side, hipEvent_t *fork, hipEvent_t *join);
 void *mapped(swarm_ctx *ctx, size_t bytes, void **dev);
 
 }  // namespace swarm

@@ -348,7 +348,7 @@ class Swarm:
                  hysteresis: float = 5.0, u_scale: float = 100.0, mode: str = "auto") -> AllocResult:
         """One allocation round over t tasks (swarm_allocate).  winner/util = existing claims."""
         dev = self.device
-        tpos = torch.stack([_to(tx, torch.float64, dev), _to(ty, torch.float64, dev)], 1).contiguous()
+        tpos = self._task_pos(tx, ty)
         tq = _to(treq, torch.int8, dev)
         t = tq.numel()
         w = (torch.full((t,), -1, dtype=torch.int32, device=dev) if winner is None
@@ -391,6 +391,24 @@ class Swarm:
                     ctypes.byref(st), _lib.stream()))
         stats = {k: getattr(st, k) for k, _ in _lib.AllocStats._fields_}
         return AllocResult(w, u, won, nclaim, nmsg, stats)
+
+    def _task_pos(self, tx, ty) -> torch.Tensor:
+        """(t, 2) float64 task positions on the device.  When tx / ty are float64 device tensors the
+        stacked copy is kept and reused while both are unchanged (the same tensor objects at the
+        same version counters): a caller that allocates over the same tasks every step pays no
+        stacking kernel."""
+        dev = self.device
+        if isinstance(tx, torch.Tensor) and isinstance(ty, torch.Tensor) and tx.dtype == ty.dtype == torch.float64 \
+                and tx.device == ty.device == dev:
+            # the SAME tensor objects (held by the cache, so their storage cannot be recycled) at
+            # the same version counters
+            c = getattr(self, "_tpos_cache", None)
+            if c is not None and c[0] is tx and c[1] is ty and c[2] == (tx._version, ty._version):
+                return c[3]
+            tpos = torch.stack([tx, ty], 1).contiguous()
+            self._tpos_cache = (tx, ty, (tx._version, ty._version), tpos)
+            return tpos
+        return torch.stack([_to(tx, torch.float64, dev), _to(ty, torch.float64, dev)], 1).contiguous()
 
     def auction(self, tx, ty, treq, *, eps: float = 0.1, claim_thr: float = 20.0, u_scale: float = 100.0,
                 max_rounds: int = 1 << 20) -> AuctionResult:

@@ -155,3 +155,18 @@ def test_edge_agent_moved_past_bbox(mods, oracle_mod):
     assert want["nclaim"][-1] >= 1
     for k in ("winner", "nclaim", "won"):
         np.testing.assert_array_equal(getattr(a, k).cpu().numpy(), want[k], err_msg=k)
+
+
+def test_task_positions_cache_follows_in_place_writes(mods, oracle_mod):
+    """Swarm.allocate reuses its stacked task positions only for the same, unmodified tensors."""
+    swm, _lib, gen = mods
+    d = gen.swarm_inputs(20_000, 29, t=400)
+    s = swm.Swarm(d["ids"], d["x"], d["y"], d["caps"], device="cuda")
+    tx, ty = torch.as_tensor(d["tx"], device="cuda"), torch.as_tensor(d["ty"], device="cuda")
+    tq = torch.as_tensor(d["treq"], device="cuda")
+    a = s.allocate(tx, ty, tq)
+    tx[:200] += 3.0  # in place: the version counter moves, the cache must not serve the old copy
+    b = s.allocate(tx, ty, tq)
+    want = _oracle_now(oracle_mod, s, tx.cpu().numpy(), d["ty"], d["treq"])
+    np.testing.assert_array_equal(b.winner.cpu().numpy(), want["winner"])
+    assert not np.array_equal(a.winner.cpu().numpy(), b.winner.cpu().numpy())
