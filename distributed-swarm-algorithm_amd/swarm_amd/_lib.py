@@ -19,7 +19,7 @@ LIB_PATH = os.path.join(HERE, "libswarm.so")
 OK, NOT_CONVERGED = 0, 1
 ERR_ARG, ERR_HIP, ERR_OOM, ERR_RANGE, ERR_STALE = -1, -2, -3, -4, -5
 FOLLOWER, ELECTION_WAIT, LEADER = 1, 2, 3
-ELECT_DENSE, ELECT_FRONTIER, ELECT_TIMED = 0, 1, 0x100
+ELECT_DENSE, ELECT_FRONTIER, ELECT_TIMED, ELECT_TILES_EARLY = 0, 1, 0x100, 0x200
 ALLOC_AUTO, ALLOC_BINNED, ALLOC_DENSE = 0, 1, 2
 
 # every symbol include/swarm.h declares (tests/test_capi.py checks the two agree)
@@ -32,7 +32,7 @@ EXPORTS = ("swarm_last_error", "swarm_version", "swarm_ctx_create", "swarm_ctx_d
            "swarm_codec_decode", "swarm_protocol_run", "swarm_auction_begin",
            "swarm_auction_bid", "swarm_auction_resolve", "swarm_auction_sharded", "swarm_cell_index",
            "swarm_allocate_indexed", "swarm_graph_compact", "swarm_elect_compact",
-           "swarm_elect_compact_i64")
+           "swarm_elect_compact_i64", "swarm_tile_index", "swarm_elect_tiled")
 
 
 class SwarmError(RuntimeError):
@@ -58,7 +58,9 @@ class ElectStats(ctypes.Structure):
                 ("gather_ms", ctypes.c_double), ("apply_ms", ctypes.c_double),
                 ("gather_launches", ctypes.c_int64), ("dense_rounds", ctypes.c_int64),
                 ("bytes_total", ctypes.c_double), ("sparse_ms", ctypes.c_double),
-                ("sparse_launches", ctypes.c_int64), ("sparse_bytes", ctypes.c_double)]
+                ("sparse_launches", ctypes.c_int64), ("sparse_bytes", ctypes.c_double),
+                ("tile_rounds", ctypes.c_int64), ("tile_launches", ctypes.c_int64), ("tile_ms", ctypes.c_double),
+                ("tile_bytes", ctypes.c_double), ("tile_from", ctypes.c_int64)]
 
 
 class AuctionStats(ctypes.Structure):
@@ -109,6 +111,9 @@ def load(path: str = LIB_PATH):
         L.swarm_graph_compact.argtypes = [P, i64, P, P, P, P]
         L.swarm_elect_compact.argtypes = [P, i64, P, P, P, P, P, P, i32, i32, ctypes.POINTER(i32), P, P, P]
         L.swarm_elect_compact_i64.argtypes = [P, i64, P, P, P, P, P, P, i32, i32, ctypes.POINTER(i32), P, P, P]
+        L.swarm_tile_index.argtypes = [P, i64, P, P, ctypes.POINTER(Grid), P, P, ctypes.POINTER(i32), P]
+        L.swarm_elect_tiled.argtypes = [P, i64, P, P, P, P, P, P, ctypes.POINTER(Grid), P, P, i32, i32,
+                                        ctypes.POINTER(i32), P, P, P]
         L.swarm_allocate.argtypes = [P, i64, P, P, P, i64, P, P, d, d, d, i32, P, P, P, P, i64,
                                      P, P, P, P]
         L.swarm_utility.argtypes = [P, i64, P, P, P, P, d, P, P]

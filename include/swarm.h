@@ -50,6 +50,8 @@ extern "C" {
 #define SWARM_ELECT_FRONTIER 1 /* dense sweeps while many agents change, then only the agents
                                   marked by last round's risers gather (sparse rounds) */
 #define SWARM_ELECT_TIMED 0x100 /* OR into mode: time every kernel with HIP events (stats) */
+#define SWARM_ELECT_TILES_EARLY 0x200 /* OR into mode (swarm_elect_tiled): tiled rounds from the first
+                                        sparse round on, whatever the changes (tests, A/B) */
 
 /* Allocation execution strategies (all exact). */
 #define SWARM_ALLOC_AUTO 0
@@ -57,6 +59,13 @@ extern "C" {
 #define SWARM_ALLOC_DENSE 2    /* every agent x every task, ID-ordered tiles */
 
 typedef struct swarm_ctx swarm_ctx;
+
+/* A uniform cell grid over agent positions (swarm_cell_index). */
+typedef struct swarm_grid {
+    double xmin, ymin, xmax, ymax;  /* bounding box of the indexed positions */
+    double cell, inv_cell;          /* cell side (>= the requested one if the grid was capped) */
+    int64_t ncx, ncy;               /* cells per row, rows */
+} swarm_grid;
 
 typedef struct swarm_alloc_stats {
     int64_t n_claims;        /* TASK_CLAIM messages the round produced (agent.py:302) */
@@ -81,6 +90,11 @@ typedef struct swarm_elect_stats {
     double sparse_ms;        /* SWARM_ELECT_TIMED: device time of every launched sparse round */
     int64_t sparse_launches; /* SWARM_ELECT_TIMED: sparse rounds launched (incl. no-ops) */
     double sparse_bytes;     /* algorithmic HBM bytes of the executed sparse rounds */
+    int64_t tile_rounds;     /* swarm_elect_tiled: rounds run as tiled launches (rounds_exec included) */
+    int64_t tile_launches;   /* swarm_elect_tiled: tiled launches (up to 4 rounds each) */
+    double tile_ms;          /* SWARM_ELECT_TIMED: device time of the tiled launches */
+    double tile_bytes;       /* SURVEY 8(d) bytes of the agents / edges the tiled rounds stand for */
+    int64_t tile_from;       /* first tiled round (0: none) */
 } swarm_elect_stats;
 
 const char *swarm_last_error(void);
@@ -143,6 +157,28 @@ int swarm_elect_i64(swarm_ctx *ctx, int64_t n, const int64_t *row_ptr, const int
                     const int32_t *ids, int32_t *leader, uint8_t *state, int32_t max_rounds,
                     int32_t mode, int32_t *rounds_exec, int64_t *changes_per_round,
                     swarm_elect_stats *stats, void *stream);
+
+/*
+ * Tiled rounds for the tail of an election (DESIGN.md §4 "tiled rounds").  A swarm stored in cell
+ * order (swarm_cell_order; its cell index from swarm_cell_index) whose every edge joins cells at
+ * most one apart in x and y (a radius graph with radius <= the cell side) can run its late rounds
+ * as launches of 4 rounds each over 16 x 16-cell tiles held on chip, only where the fronts are.
+ * swarm_tile_index: acell (device, n int32) = each agent's cell; *ok = 1 when the graph is local in
+ * that sense and every tile region fits on chip, else 0 (then run swarm_elect_compact).
+ * swarm_elect_tiled: swarm_elect_compact (same results: leaders, states, rounds_exec, every per-round
+ * change count) that switches to tiled rounds once a round changes fewer than SWARM_TILE_MIN_CHANGES
+ * agents (default 0: never -- at 10M agents a launch costs ~80 us per tile, slower than the sparse
+ * rounds it replaces) or, with SWARM_ELECT_TILES_EARLY in mode, from the first sparse
+ * round on.  acell must come from swarm_tile_index with *ok = 1 for THIS graph and cell index
+ * (acell = NULL: plain swarm_elect_compact).  Symmetric graphs, int32 offsets.
+ * Replaces the same handlers as swarm_elect (agent.py:243-275).
+ */
+int swarm_tile_index(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col, const swarm_grid *grid,
+                     const uint32_t *cell_off, int32_t *acell, int32_t *ok, void *stream);
+int swarm_elect_tiled(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col, const int16_t *col16,
+                      const int32_t *ids, int32_t *leader, uint8_t *state, const swarm_grid *grid,
+                      const uint32_t *cell_off, const int32_t *acell, int32_t max_rounds, int32_t mode,
+                      int32_t *rounds_exec, int64_t *changes_per_round, swarm_elect_stats *stats, void *stream);
 
 /* swarm_elect_compact with int64 row offsets (graphs of >= 2^30 edges; the 16-bit columns are
  * built by swarm_graph_compact from the int32 row offsets, which hold up to 2^31 - 1 edges).
@@ -271,11 +307,7 @@ int swarm_allocate(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *
  * SWARM_ERR_STALE and the outputs are undefined -- rebuild the index, or call swarm_allocate.
  * Claim radius (u_scale / claim_thr - 1) must span at most 16 grid rows (SWARM_ERR_ARG).
  */
-typedef struct swarm_grid {
-    double xmin, ymin, xmax, ymax;  /* bounding box of the indexed positions */
-    double cell, inv_cell;          /* cell side (>= the requested one if the grid was capped) */
-    int64_t ncx, ncy;               /* cells per row, rows */
-} swarm_grid;
+
 
 /* grid (host) and cell_off (device, ncells + 1): agents of cell c = cy * ncx + cx are storage
  * indices [cell_off[c], cell_off[c + 1]).  cell_off == NULL: fill grid and *ncells only.
