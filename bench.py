@@ -342,7 +342,10 @@ def cpu_baseline_step(h, d, r, args):
     oracle.set_threads(threads)
     t1_est = t_k * float(active.sum()) / float(active[:k].sum()) + t_ts * len(d["tx"]) / ts
     return {"value": n * rounds / (t_el + t_al), "unit": "agent-rounds/s", "cores": threads, "kind": "port",
-            "value_1core": n * rounds / t1_est, "elect_s": t_el, "alloc_s": t_al, "same_result_as_gpu": same,
+            "value_1core": n * rounds / t1_est,
+            "value_1core_kind": f"ESTIMATE, not a measurement: one thread timed on rounds 1-{k} and {ts} tasks, "
+                                f"scaled by the agents recomputed per round and by the task count",
+            "elect_s": t_el, "alloc_s": t_al, "same_result_as_gpu": same,
             "sample": f"C oracle, the GPU's algorithms (orc_elect_frontier + orc_allocate_binned), the whole C3 step "
                       f"on the same {n}-agent swarm: election {rounds} rounds {t_el:.2f} s + {len(d['tx'])}-task "
                       f"allocation {t_al:.2f} s on {threads} threads (measured, not extrapolated); 1 thread: "
