@@ -636,10 +636,13 @@ def sharded_state_check(sh, r):
     L = sh.leaders[r.rounds_exec & 1]
     lout = torch.empty_like(L)
     changed = torch.zeros(1, dtype=torch.int64, device=L.device)
+    # one round over every shard row (owned rows sit between the two ghost blocks); the outermost
+    # ghosts may still move, so only the owned slice is compared
+    own = slice(sh.own_begin, sh.own_begin + sh.n_own)
     with torch.cuda.device(L.device):
-        _lib.check(_lib.lib().swarm_elect_round(_lib.ctx(), sh.n_own, _lib.ptr(sh.row_ptr), _lib.ptr(sh.col),
+        _lib.check(_lib.lib().swarm_elect_round(_lib.ctx(), L.numel(), _lib.ptr(sh.row_ptr), _lib.ptr(sh.col),
                                                 _lib.ptr(L), _lib.ptr(lout), _lib.ptr(changed), _lib.stream()))
-    ok = torch.tensor([int(changed.item() == 0 and torch.equal(lout[: sh.n_own], L[: sh.n_own])),
+    ok = torch.tensor([int(torch.equal(lout[own], L[own])),
                        int(torch.equal(r.state == _lib.LEADER, r.leader == sh.ids))], dtype=torch.int64,
                       device=L.device if dist.get_backend() == "nccl" else "cpu")
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
@@ -682,14 +685,17 @@ def shard_roofline(sh, dev):
     state = torch.empty(n, dtype=torch.uint8, device=dev)
     rounds = ctypes.c_int32(0)
     st = _lib.ElectStats()
+    # the shard's rows are in cell order ([ghosts-lo | owned | ghosts-hi]), so its 16-bit columns
+    # (sh.c16) normally exist and the election reads them, as the sharded run does
     with torch.cuda.device(dev):
-        _lib.check(_lib.lib().swarm_elect(_lib.ctx(), n, _lib.ptr(sh.row_ptr), _lib.ptr(sh.col),
-                                          _lib.ptr(sh.all_ids), _lib.ptr(lead), _lib.ptr(state), 1 << 16,
-                                          _lib.ELECT_FRONTIER | _lib.ELECT_TIMED, ctypes.byref(rounds), None,
-                                          ctypes.byref(st), _lib.stream()))
+        _lib.check(_lib.lib().swarm_elect_compact(_lib.ctx(), n, _lib.ptr(sh.row_ptr), _lib.ptr(sh.col),
+                                                  _lib.ptr(sh.c16) if sh.c16 is not None else None,
+                                                  _lib.ptr(sh.all_ids), _lib.ptr(lead), _lib.ptr(state), 1 << 16,
+                                                  _lib.ELECT_FRONTIER | _lib.ELECT_TIMED, ctypes.byref(rounds), None,
+                                                  ctypes.byref(st), _lib.stream()))
     torch.cuda.synchronize()
-    sb = sparse_round_bytes(st.active_total, st.edges_total, st.dense_rounds, rounds.value, n, int(sh.col.numel()),
-                            max(st.sparse_launches, 1), False)
+    sb = sparse_round_bytes(st.active_total, st.edges_total, st.dense_rounds, rounds.value, n,
+                            int(sh.row_ptr[-1].item()), max(st.sparse_launches, 1), sh.c16 is not None)
     bpl = sb["bytes_per_launch"]
     ms = st.sparse_ms / max(st.sparse_launches, 1)
     # the committed PMC figure is the N = 1 C3 bench's (10M agents): it stands for shards of about

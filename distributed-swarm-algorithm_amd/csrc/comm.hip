@@ -174,14 +174,13 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sh,
     SW_ARG(ctx && comm && sh && rounds_exec, "NULL argument");
     SW_ARG(max_rounds >= 1, "max_rounds < 1");
     SW_ARG(sh->n_rows >= 0 && sh->n_all >= sh->n_rows, "shard sizes");
-    SW_ARG(sh->ghost_lo_begin >= sh->n_rows && sh->ghost_lo_begin + sh->n_ghost_lo <= sh->n_all &&
-           sh->ghost_hi_begin >= sh->n_rows && sh->ghost_hi_begin + sh->n_ghost_hi <= sh->n_all,
-           "ghost ranges must lie in [n_rows, n_all)");
+    SW_ARG(sh->own_begin >= 0 && sh->own_begin + sh->n_rows <= sh->n_all, "owned range out of [0, n_all)");
     SW_ARG((sh->peer_lo >= 0 || (sh->n_send_lo == 0 && sh->n_ghost_lo == 0)) &&
            (sh->peer_hi >= 0 || (sh->n_send_hi == 0 && sh->n_ghost_hi == 0)), "halo without a peer");
     hipStream_t s = static_cast<hipStream_t>(stream);
-    int rc = swarm_frontier_begin(ctx, sh->n_rows, sh->n_all, sh->init, leader0, leader1, stream);
+    int rc = swarm_frontier_begin_range(ctx, sh->own_begin, sh->n_rows, sh->n_all, sh->init, leader0, leader1, stream);
     if (rc) return rc;
+    if ((rc = swarm_frontier_set_compact(ctx, sh->col16))) return rc;
     int32_t *bufs;
     const size_t nb = size_t(sh->n_send_lo + sh->n_send_hi + sh->n_ghost_lo + sh->n_ghost_hi) + 4;
     SW_ALLOC(bufs, ctx, S_TMP0, nb * 4);

@@ -274,7 +274,7 @@ __device__ __forceinline__ int row_max_from_lds(const int *s_col, Off w0, Off lo
 template <typename Off, bool MARK, bool DIR = false, bool FLAT = false, typename CT = Col32>
 __global__ __launch_bounds__(kBlock) void k_elect_dense(
     const Off *__restrict__ rp, CT cols, const int32_t *__restrict__ lin,
-    int32_t *__restrict__ lout, int64_t n, int64_t n_count, unsigned long long *__restrict__ ring,
+    int32_t *__restrict__ lout, int64_t n, int64_t c_lo, int64_t n_count, unsigned long long *__restrict__ ring,
     unsigned long long *__restrict__ tot, uint8_t *__restrict__ act_w, StampMap sm, int t, int guard,
     const Off *__restrict__ hrp = nullptr, const int32_t *__restrict__ hcol = nullptr) {
     __shared__ int s_col[kWavesPerBlock][kWin];
@@ -341,7 +341,7 @@ __global__ __launch_bounds__(kBlock) void k_elect_dense(
         }
         const bool up = valid && m > own;
         if (valid) lout[v] = up ? m : own;
-        mine += __popcll(__ballot(up && v < n_count));  // sharded: ghost rows step, owners count
+        mine += __popcll(__ballot(up && v >= c_lo && v < n_count));  // sharded: ghost rows step, owners count
         if (MARK && up) {
             act_w[stamp_slot(sm, v)] = sw;
             if (DIR)
@@ -405,7 +405,7 @@ struct Frontier {
     // the layout at any round boundary (stamp_map).
     unsigned long long *ring, *tot;
     int64_t n_rows, n_all;   // rows stepped (owned + ghosts in sharded runs), all agents
-    int64_t n_count;         // rows [0, n_count) are owned: only their changes are counted
+    int64_t c_lo, n_count;   // rows [c_lo, n_count) are owned: only their changes are counted
     StampMap sm, wsm;
     const int16_t *c16;      // Col16 columns of the same graph (swarm_graph_compact), or nullptr
 };
@@ -459,7 +459,8 @@ __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, CT col
                                               const Off *__restrict__ hrp, const int32_t *__restrict__ hcol,
                                               const int32_t *__restrict__ P, int32_t *__restrict__ Q,
                                               uint8_t *__restrict__ aw, const StampMap &sm, uint8_t sw,
-                                              const int *lst, int total, int first, int step, int64_t n_count,
+                                              const int *lst, int total, int first, int step, int64_t c_lo,
+                                              int64_t n_count,
                                               long long &my_chg, int &my_act, int &my_edges) {
     const int lane = threadIdx.x & 63, sub = lane & (G - 1);
     using Ix = Off;  // 32-bit offsets in the int32-CSR instantiation (host: < 2^30 agents and edges)
@@ -508,7 +509,7 @@ __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, CT col
                 mark_row<Off>(aw, sm, cols, v & ~63, b + sub, e, Off(G), sw);
             }
         }
-        my_chg += __popcll(__ballot(up && sub == 0 && v < n_count));
+        my_chg += __popcll(__ballot(up && sub == 0 && v >= c_lo && v < n_count));
         if (valid && sub == 0) {
             my_act += 1;
             my_edges += int(e - b);
@@ -656,7 +657,7 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
             __syncthreads();  // list entries visible
             if (listed < kListCap) break;  // everything fitted
             gather_listed<Off, G, K, DIR>(rp, cols, hrp, hcol, P, Q, aw, f.wsm, sw, s_list, listed, wid * (64 / G),
-                                          kBlock / G, f.n_count, my_chg, my_act, my_edges);
+                                          kBlock / G, f.c_lo, f.n_count, my_chg, my_act, my_edges);
             listed = 0;
             __syncthreads();  // the list is reused
         }
@@ -666,7 +667,7 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
 #endif
     if (listed > 0)
         gather_listed<Off, G, K, DIR>(rp, cols, hrp, hcol, P, Q, aw, f.wsm, sw, s_list, listed, wid * (64 / G),
-                                      kBlock / G, f.n_count, my_chg, my_act, my_edges);
+                                      kBlock / G, f.c_lo, f.n_count, my_chg, my_act, my_edges);
 #ifdef SWARM_PHASES
     ph_gathered = wall_clock64() + (my_chg & 0);
 #endif
@@ -830,7 +831,8 @@ size_t act_bytes(int64_t n_all) {  // one parity: every chunk of the stamp layou
 }
 
 template <typename Off>
-int launch_dense_round(const Off *rp, const int32_t *col, const int32_t *lin, int32_t *lout, int64_t n, int64_t n_count,
+int launch_dense_round(const Off *rp, const int32_t *col, const int32_t *lin, int32_t *lout, int64_t n, int64_t c_lo,
+                       int64_t n_count,
                        unsigned long long *ring, unsigned long long *tot, uint8_t *act_w, StampMap sm, int t,
                        int guard, hipStream_t s, const Off *hrp = nullptr, const int32_t *hcol = nullptr,
                        const int16_t *c16 = nullptr) {
@@ -840,25 +842,25 @@ int launch_dense_round(const Off *rp, const int32_t *col, const int32_t *lin, in
         const Col16 cc{c16};
         if (act_w)
             hipLaunchKernelGGL((k_elect_dense<Off, true, false, true, Col16>), dim3(grid), dim3(kBlock), 0, s, rp, cc,
-                               lin, lout, n, n_count, ring, tot, act_w, sm, t, guard, nullptr, nullptr);
+                               lin, lout, n, c_lo, n_count, ring, tot, act_w, sm, t, guard, nullptr, nullptr);
         else
             hipLaunchKernelGGL((k_elect_dense<Off, false, false, true, Col16>), dim3(grid), dim3(kBlock), 0, s, rp, cc,
-                               lin, lout, n, n_count, ring, tot, act_w, sm, t, guard, nullptr, nullptr);
+                               lin, lout, n, c_lo, n_count, ring, tot, act_w, sm, t, guard, nullptr, nullptr);
     } else if (!hrp && sizeof(Off) == 4 && tuning().dense_flat) {
         if (act_w)
             hipLaunchKernelGGL((k_elect_dense<Off, true, false, true>), dim3(grid), dim3(kBlock), 0, s, rp, c32, lin,
-                               lout, n, n_count, ring, tot, act_w, sm, t, guard, nullptr, nullptr);
+                               lout, n, c_lo, n_count, ring, tot, act_w, sm, t, guard, nullptr, nullptr);
         else
             hipLaunchKernelGGL((k_elect_dense<Off, false, false, true>), dim3(grid), dim3(kBlock), 0, s, rp, c32, lin,
-                               lout, n, n_count, ring, tot, act_w, sm, t, guard, nullptr, nullptr);
+                               lout, n, c_lo, n_count, ring, tot, act_w, sm, t, guard, nullptr, nullptr);
     } else if (act_w && hrp)
         hipLaunchKernelGGL((k_elect_dense<Off, true, true>), dim3(grid), dim3(kBlock), 0, s, rp, c32, lin, lout, n,
-                           n_count, ring, tot, act_w, sm, t, guard, hrp, hcol);
+                           c_lo, n_count, ring, tot, act_w, sm, t, guard, hrp, hcol);
     else if (act_w)
-        hipLaunchKernelGGL((k_elect_dense<Off, true>), dim3(grid), dim3(kBlock), 0, s, rp, c32, lin, lout, n, n_count, ring,
+        hipLaunchKernelGGL((k_elect_dense<Off, true>), dim3(grid), dim3(kBlock), 0, s, rp, c32, lin, lout, n, c_lo, n_count, ring,
                            tot, act_w, sm, t, guard, nullptr, nullptr);
     else
-        hipLaunchKernelGGL((k_elect_dense<Off, false>), dim3(grid), dim3(kBlock), 0, s, rp, c32, lin, lout, n, n_count, ring,
+        hipLaunchKernelGGL((k_elect_dense<Off, false>), dim3(grid), dim3(kBlock), 0, s, rp, c32, lin, lout, n, c_lo, n_count, ring,
                            tot, act_w, sm, t, guard, nullptr, nullptr);
     SW_LAUNCHED();
     return SWARM_OK;
@@ -871,8 +873,10 @@ int frontier_bind(swarm_ctx *ctx, int32_t *L0, int32_t *L1, Frontier *f) {
     if (!ctx_on_current_device(ctx)) return SWARM_ERR_ARG;
     SW_ARG(ctx->slot[S_ACT] != nullptr && ctx->slot[S_CHANGES] != nullptr, "swarm_frontier_begin first");
     f->n_rows = ctx->step_all;
-    f->n_count = ctx->step_rows;
+    f->c_lo = ctx->step_lo;
+    f->n_count = ctx->step_lo + ctx->step_rows;
     f->n_all = ctx->step_all;
+    f->c16 = ctx->step_c16;
     f->L[0] = L0;
     f->L[1] = L1;
     uint8_t *a = static_cast<uint8_t *>(ctx->slot[S_ACT]);
@@ -895,6 +899,8 @@ int frontier_alloc(swarm_ctx *ctx, int64_t n_rows, int64_t n_all, int32_t *L0, i
     (void)p;
     ctx->step_rows = n_rows;
     ctx->step_all = n_all;
+    ctx->step_lo = 0;
+    ctx->step_c16 = nullptr;
     int rc = frontier_bind(ctx, L0, L1, f);
     if (rc) return rc;
     SW_HIP(hipMemsetAsync(f->ring, 0, ring_bytes(), s));
@@ -921,7 +927,7 @@ template <typename Off>
 int launch_frontier_round(const Off *rp, const int32_t *col, const Frontier &f, int t, RoundKind k, int guard,
                           hipStream_t s, const Off *hrp = nullptr, const int32_t *hcol = nullptr) {
     if (k == RK_DENSE || k == RK_DENSE_MARK)
-        return launch_dense_round<Off>(rp, col, f.L[(t - 1) & 1], f.L[t & 1], f.n_rows, f.n_count, f.ring,
+        return launch_dense_round<Off>(rp, col, f.L[(t - 1) & 1], f.L[t & 1], f.n_rows, f.c_lo, f.n_count, f.ring,
                                        f.tot,
                                        k == RK_DENSE_MARK ? f.act[(t + 1) & 1] : nullptr, f.wsm, t, guard, s, hrp,
                                        hcol, f.c16);
@@ -1592,7 +1598,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
             if (e2) SW_HIP(hipEventRecord(e2[0], s));
             if (mode == SWARM_ELECT_DENSE) {
                 kinds[r - t] = RK_DENSE;
-                rc = launch_dense_round<Off>(rp, col, bufs[(r - 1) & 1], bufs[r & 1], n, n, ring, nullptr, nullptr,
+                rc = launch_dense_round<Off>(rp, col, bufs[(r - 1) & 1], bufs[r & 1], n, 0, n, ring, nullptr, nullptr,
                                              StampMap{}, r, 1, s, nullptr, nullptr, c16);
             } else {
                 kinds[r - t] = plan_round(r);
@@ -1738,8 +1744,10 @@ int frontier_ghosts_both(swarm_ctx *ctx, int t, const int32_t *rp, const int32_t
     Frontier f{};
     int rc = frontier_bind(ctx, L0, L1, &f);
     if (rc) return rc;
-    SW_ARG(b_lo >= f.n_count && b_lo + n_lo <= f.n_all && b_hi >= f.n_count && b_hi + n_hi <= f.n_all,
-           "ghost ranges must lie in [n_rows, n_all)");
+    const auto outside = [&](int64_t b, int64_t c) {  // [b, b + c) within [0, n_all) and off the owned rows
+        return c == 0 || (b >= 0 && b + c <= f.n_all && (b + c <= f.c_lo || b >= f.n_count));
+    };
+    SW_ARG(outside(b_lo, n_lo) && outside(b_hi, n_hi), "ghost ranges must lie in [0, n_all) outside the owned rows");
     if (n_lo + n_hi == 0) return SWARM_OK;
     hipLaunchKernelGGL((k_frontier_ghosts<int32_t>), dim3(grid_for(n_lo + n_hi, kBlock / 8, 1024)), dim3(kBlock), 0,
                        s, rp, col, f, b_lo, n_lo, in_lo, b_hi, n_hi, in_hi, t);
@@ -1904,6 +1912,23 @@ int swarm_frontier_begin(swarm_ctx *ctx, int64_t n_rows, int64_t n_all, const in
     return SWARM_OK;
 }
 
+int swarm_frontier_begin_range(swarm_ctx *ctx, int64_t own_begin, int64_t n_own, int64_t n_all, const int32_t *init,
+                               int32_t *leader0, int32_t *leader1, void *stream) {
+    using namespace swarm;
+    SW_ARG(own_begin >= 0 && n_own >= 0 && own_begin + n_own <= n_all, "owned range out of [0, n_all)");
+    int rc = swarm_frontier_begin(ctx, n_own, n_all, init, leader0, leader1, stream);
+    if (rc) return rc;
+    ctx->step_lo = own_begin;
+    return SWARM_OK;
+}
+
+int swarm_frontier_set_compact(swarm_ctx *ctx, const int16_t *col16) {
+    using namespace swarm;
+    SW_ARG(ctx != nullptr, "ctx is NULL");
+    ctx->step_c16 = tuning().use_c16 ? col16 : nullptr;
+    return SWARM_OK;
+}
+
 int swarm_frontier_step(swarm_ctx *ctx, int32_t t, const int32_t *row_ptr, const int32_t *col,
                         int32_t *leader0, int32_t *leader1, void *stream) {
     using namespace swarm;
@@ -1967,7 +1992,7 @@ int swarm_elect_round(swarm_ctx *ctx, int64_t n_rows, const int32_t *row_ptr,
     unsigned long long *ring;
     SW_ALLOC(ring, ctx, S_TMP0, size_t(kCounters) * kRoundWords * 8);
     SW_HIP(hipMemsetAsync(ring, 0, size_t(kRoundWords) * 8, s));
-    int rc = launch_dense_round<int32_t>(row_ptr, col, leader_in, leader_out, n_rows, n_rows, ring, nullptr, nullptr,
+    int rc = launch_dense_round<int32_t>(row_ptr, col, leader_in, leader_out, n_rows, 0, n_rows, ring, nullptr, nullptr,
                                         StampMap{}, 0, 0, s);
     if (rc) return rc;
     hipLaunchKernelGGL(k_sum_shards, dim3(1), dim3(kWave), 0, s, ring, 0,

@@ -89,6 +89,8 @@ struct swarm_ctx {
     size_t mapped_cap = 0;
     int64_t step_rows = 0;         // frontier stepper: owned rows / agents (rows + ghosts)
     int64_t step_all = 0;
+    int64_t step_lo = 0;           // frontier stepper: the owned rows are [step_lo, step_lo + step_rows)
+    const int16_t *step_c16 = nullptr;  // frontier stepper: 16-bit columns of the shard graph, or NULL
     hipStream_t side = nullptr;    // a second stream for work that overlaps the caller's (side_stream)
     hipEvent_t side_ev[2] = {};    // fork / join events
 };

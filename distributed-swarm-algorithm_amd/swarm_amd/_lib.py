@@ -32,7 +32,8 @@ EXPORTS = ("swarm_last_error", "swarm_version", "swarm_ctx_create", "swarm_ctx_d
            "swarm_codec_decode", "swarm_protocol_run", "swarm_auction_begin",
            "swarm_auction_bid", "swarm_auction_resolve", "swarm_auction_sharded", "swarm_cell_index",
            "swarm_allocate_indexed", "swarm_graph_compact", "swarm_elect_compact",
-           "swarm_elect_compact_i64", "swarm_tile_index", "swarm_elect_tiled")
+           "swarm_elect_compact_i64", "swarm_tile_index", "swarm_elect_tiled", "swarm_frontier_begin_range",
+           "swarm_frontier_set_compact")
 
 
 class SwarmError(RuntimeError):
@@ -80,7 +81,8 @@ class Shard(ctypes.Structure):
                 ("n_send_lo", ctypes.c_int64), ("send_hi", ctypes.c_void_p), ("n_send_hi", ctypes.c_int64),
                 ("ghost_lo_begin", ctypes.c_int64), ("n_ghost_lo", ctypes.c_int64),
                 ("ghost_hi_begin", ctypes.c_int64), ("n_ghost_hi", ctypes.c_int64),
-                ("peer_lo", ctypes.c_int32), ("peer_hi", ctypes.c_int32), ("halo_depth", ctypes.c_int32)]
+                ("peer_lo", ctypes.c_int32), ("peer_hi", ctypes.c_int32), ("halo_depth", ctypes.c_int32),
+                ("own_begin", ctypes.c_int64), ("col16", ctypes.c_void_p)]
 
 
 _lib = None
@@ -123,6 +125,8 @@ def load(path: str = LIB_PATH):
         L.swarm_build_rgg.argtypes = [P, i64, P, d, P, P, i64, ctypes.POINTER(i64), P]
         L.swarm_cell_order.argtypes = [P, i64, P, d, P, P]
         L.swarm_frontier_begin.argtypes = [P, i64, i64, P, P, P, P]
+        L.swarm_frontier_begin_range.argtypes = [P, i64, i64, i64, P, P, P, P]
+        L.swarm_frontier_set_compact.argtypes = [P, P]
         L.swarm_frontier_step.argtypes = [P, i32, P, P, P, P, P]
         L.swarm_frontier_ghosts.argtypes = [P, i32, i64, i64, P, P, P, P, P, P]
         L.swarm_frontier_changes.argtypes = [P, i32, i32, P, P]

@@ -262,10 +262,23 @@ class GpuBackend:
                                         col.numel(), ctypes.byref(ne), L.stream()))
         return rp, col
 
-    def begin(self, n_rows, init, leaders):
+    def graph_compact(self, rp, col):
+        """16-bit columns of the shard graph (swarm_graph_compact), or None when a delta does not fit."""
+        L, n = self.L, rp.numel() - 1
+        if n <= 0 or col.numel() == 0:
+            return None
+        c16 = torch.empty(col.numel(), dtype=torch.int16, device=self.device)
+        rc = L.lib().swarm_graph_compact(self.ctx, n, L.ptr(rp), L.ptr(col), L.ptr(c16), L.stream())
+        if rc == L.ERR_RANGE:
+            return None
+        L.check(rc)
+        return c16
+
+    def begin(self, own_begin, n_own, init, leaders, col16=None):
         L = self.L
-        L.check(L.lib().swarm_frontier_begin(self.ctx, n_rows, init.numel(), L.ptr(init), L.ptr(leaders[0]),
-                                             L.ptr(leaders[1]), L.stream()))
+        L.check(L.lib().swarm_frontier_begin_range(self.ctx, own_begin, n_own, init.numel(), L.ptr(init),
+                                                   L.ptr(leaders[0]), L.ptr(leaders[1]), L.stream()))
+        L.check(L.lib().swarm_frontier_set_compact(self.ctx, L.ptr(col16) if col16 is not None else None))
 
     def step(self, t, rp, col, leaders):
         L = self.L
@@ -297,8 +310,18 @@ class GpuBackend:
         dist.broadcast(uid, src=halo._peer(0), group=halo.group)
         raw = (ctypes.c_uint8 * 128)(*uid.cpu().tolist())
         comm = ctypes.c_void_p()
-        L.check(L.lib().swarm_comm_create(ctypes.byref(comm), halo.world, halo.rank,
-                                          ctypes.cast(raw, ctypes.c_void_p)))
+        rc = L.lib().swarm_comm_create(ctypes.byref(comm), halo.world, halo.rank, ctypes.cast(raw, ctypes.c_void_p))
+        # every rank must agree on the path: a rank whose RCCL communicator failed makes all of them
+        # take the torch.distributed halo (a MIN over ranks of "ok")
+        ok = torch.tensor([1 if rc == 0 else 0], dtype=torch.int64, device=self.device)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=halo.group)
+        if int(ok.item()) == 0:
+            if rc == 0:
+                L.lib().swarm_comm_destroy(comm)
+            import sys
+            print(f"[swarm_amd.dist] native RCCL communicator unavailable ({L.last_error() if rc else 'a peer failed'}):"
+                  " using the torch.distributed halo", file=sys.stderr, flush=True)
+            return None
         return comm
 
     def elect_sharded(self, comm, sh, max_rounds):
@@ -306,11 +329,12 @@ class GpuBackend:
         L = self.L
         z = ctypes.c_void_p(0)
         desc = L.Shard(sh.n_own, sh.all_ids.numel(), L.ptr(sh.row_ptr), L.ptr(sh.col) if sh.col.numel() else z,
-                       L.ptr(sh.all_ids), L.ptr(sh.send_lo) if sh.send_lo.numel() else z, sh.send_lo.numel(),
-                       L.ptr(sh.send_hi) if sh.send_hi.numel() else z, sh.send_hi.numel(),
-                       sh.n_own, sh.n_glo, sh.n_own + sh.n_glo, sh.n_ghi,
+                       L.ptr(sh.all_ids), L.ptr(sh.send_lo_all) if sh.send_lo.numel() else z, sh.send_lo.numel(),
+                       L.ptr(sh.send_hi_all) if sh.send_hi.numel() else z, sh.send_hi.numel(),
+                       0, sh.n_glo, sh.n_glo + sh.n_own, sh.n_ghi,
                        sh.halo.lo if sh.halo.lo is not None else -1,
-                       sh.halo.hi if sh.halo.hi is not None else -1, sh.halo_depth)
+                       sh.halo.hi if sh.halo.hi is not None else -1, sh.halo_depth, sh.own_begin,
+                       L.ptr(sh.c16) if sh.c16 is not None else z)
         rounds = ctypes.c_int32(0)
         changes = np.zeros(max_rounds, np.int64)
         rc = L.check(L.lib().swarm_elect_sharded(self.ctx, comm, ctypes.byref(desc), L.ptr(sh.leaders[0]),
@@ -422,9 +446,16 @@ class ShardedSwarm:
         # ghosts within one radius of the border: exact at every round (the end-of-run check)
         self.inner_lo = gp_lo[:, 1] >= self.strip[0] - self.radius - 1e-9
         self.inner_hi = gp_hi[:, 1] <= self.strip[1] + self.radius + 1e-9
-        self.all_pos = torch.cat([self.pos, gp_lo, gp_hi]).contiguous()
-        self.all_ids = torch.cat([self.ids, gi_lo, gi_hi]).contiguous()
+        # shard graph rows: [ghosts from below | owned | ghosts from above] -- each block in its owner's
+        # cell order, so the whole shard is in (near) row-major cell order and its 16-bit columns fit
+        self.own_begin = self.n_glo
+        self.all_pos = torch.cat([gp_lo, self.pos, gp_hi]).contiguous()
+        self.all_ids = torch.cat([gi_lo, self.ids, gi_hi]).contiguous()
+        self.send_lo_all = (self.send_lo + self.own_begin).contiguous()  # owned send rows as shard rows
+        self.send_hi_all = (self.send_hi + self.own_begin).contiguous()
         self.row_ptr, self.col = self.backend.build_graph(self.all_pos, self.radius)
+        self.c16 = self.backend.graph_compact(self.row_ptr, self.col) if hasattr(self.backend, "graph_compact") \
+            else None
         self.leaders = (torch.empty(self.all_ids.numel(), dtype=torch.int32, device=dev),
                         torch.empty(self.all_ids.numel(), dtype=torch.int32, device=dev))
 
@@ -480,15 +511,16 @@ class ShardedSwarm:
         be, h = self.backend, self.halo
         if getattr(self, "_native", "unset") == "unset":
             self._native = be.native_comm(h) if hasattr(be, "native_comm") else None
+        own_sl = slice(self.own_begin, self.own_begin + self.n_own)
         if self._native is not None:
             rounds, changes, conv = be.elect_sharded(self._native, self, max_rounds)
-            own = self.leaders[rounds & 1][: self.n_own]
+            own = self.leaders[rounds & 1][own_sl]
             self._check_ghosts(self.leaders[rounds & 1])
             state = torch.where(own == self.ids, 3, 1).to(torch.uint8)
             return ShardElectResult(rounds, changes, own, state, conv)
         rp, col, lead = self.row_ptr, self.col, self.leaders
-        be.begin(self.n_own, self.all_ids, lead)
-        g_lo, g_hi = self.n_own, self.n_own + self.n_glo
+        be.begin(self.own_begin, self.n_own, self.all_ids, lead, self.c16)
+        g_lo, g_hi = 0, self.own_begin + self.n_own
         changes = []
         t, found = 1, -1
         check_every = max(1, min(int(check_every), 256))
@@ -499,7 +531,7 @@ class ShardedSwarm:
                 if r % self.halo_depth:
                     continue  # ghosts stepped locally between exchanges
                 cur = lead[r & 1]  # state after round r
-                in_lo, in_hi = h.exchange(cur[self.send_lo], cur[self.send_hi], self.n_glo, self.n_ghi, cur)
+                in_lo, in_hi = h.exchange(cur[self.send_lo_all], cur[self.send_hi_all], self.n_glo, self.n_ghi, cur)
                 be.ghosts(r, g_lo, in_lo, rp, col, lead)
                 be.ghosts(r, g_hi, in_hi, rp, col, lead)
             glob = h.all_reduce_sum(be.changes(t, tend))
@@ -510,7 +542,7 @@ class ShardedSwarm:
                     break
             t = tend + 1
         rounds = found if found > 0 else max_rounds
-        own = lead[rounds & 1][: self.n_own]
+        own = lead[rounds & 1][own_sl]
         state = torch.where(own == self.ids, 3, 1).to(torch.uint8)
         return ShardElectResult(rounds, np.array(changes[:rounds], np.int64), own, state, found > 0)
 
@@ -518,9 +550,9 @@ class ShardedSwarm:
         """Every ghost within one radius of the border must hold its owner's final leader (cheap
         end-to-end halo check; the deeper ghosts may lag between exchanges by design)."""
         h = self.halo
-        in_lo, in_hi = h.exchange(cur[self.send_lo], cur[self.send_hi], self.n_glo, self.n_ghi, cur)
-        g_lo = cur[self.n_own:self.n_own + self.n_glo]
-        g_hi = cur[self.n_own + self.n_glo:self.n_own + self.n_glo + self.n_ghi]
+        in_lo, in_hi = h.exchange(cur[self.send_lo_all], cur[self.send_hi_all], self.n_glo, self.n_ghi, cur)
+        g_lo = cur[: self.n_glo]
+        g_hi = cur[self.own_begin + self.n_own:self.own_begin + self.n_own + self.n_ghi]
         il, ih = self.inner_lo.to(cur.device), self.inner_hi.to(cur.device)
         if not (torch.equal(in_lo[il], g_lo[il]) and torch.equal(in_hi[ih], g_hi[ih])):
             raise RuntimeError("sharded election: ghost leaders disagree with their owners")

@@ -218,6 +218,12 @@ int swarm_elect_round(swarm_ctx *ctx, int64_t n_rows, const int32_t *row_ptr,
  */
 int swarm_frontier_begin(swarm_ctx *ctx, int64_t n_rows, int64_t n_all, const int32_t *init,
                          int32_t *leader0, int32_t *leader1, void *stream);
+/* swarm_frontier_begin with the owned rows at [own_begin, own_begin + n_own) (ghost rows on both
+ * sides); swarm_frontier_set_compact: the shard graph's 16-bit columns for the following steps
+ * (swarm_graph_compact; NULL: the int32 columns), reset by every begin. */
+int swarm_frontier_begin_range(swarm_ctx *ctx, int64_t own_begin, int64_t n_own, int64_t n_all, const int32_t *init,
+                               int32_t *leader0, int32_t *leader1, void *stream);
+int swarm_frontier_set_compact(swarm_ctx *ctx, const int16_t *col16);
 int swarm_frontier_step(swarm_ctx *ctx, int32_t t, const int32_t *row_ptr, const int32_t *col,
                         int32_t *leader0, int32_t *leader1, void *stream);
 int swarm_frontier_ghosts(swarm_ctx *ctx, int32_t t, int64_t begin, int64_t count,
@@ -237,7 +243,7 @@ int swarm_frontier_changes(swarm_ctx *ctx, int32_t t0, int32_t t1, int64_t *out,
 typedef struct swarm_comm swarm_comm;
 
 typedef struct swarm_shard {
-    int64_t n_rows;          /* owned agents (rows gathered), stored first */
+    int64_t n_rows;          /* owned agents: rows [own_begin, own_begin + n_rows) */
     int64_t n_all;           /* owned + ghost agents */
     const int32_t *row_ptr;  /* CSR over all n_all rows (ghost rows list their local neighbours) */
     const int32_t *col;
@@ -256,6 +262,9 @@ typedef struct swarm_shard {
                                 border; all n_all rows are stepped, the halo is exchanged after
                                 every k-th round only (owned rows stay exact: a wrong value
                                 starts at the halo's outer edge and moves one radius per round) */
+    int64_t own_begin;       /* first owned row (round 3: [ghosts lo | owned | ghosts hi] keeps the shard
+                                graph in spatial order, so its 16-bit columns fit) */
+    const int16_t *col16;    /* swarm_graph_compact of row_ptr / col, or NULL (int32 columns) */
 } swarm_shard;
 
 int swarm_comm_available(void);
@@ -276,14 +285,14 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sha
  * _handle_task_conflict (agent.py:327-336).
  *   U(a,k) = (u_scale / (1 + sqrt(dx*dx + dy*dy))) * has_cap   (fp64, no FMA contraction)
  *   claim iff U > claim_thr; claim value x = f32(U) (round to nearest even)
+ *   per task, claims in ascending agent ID: the first claim wins if the task has no current
+ *   winner, otherwise a claim replaces the winner iff x > util + hysteresis (fp64).
  *   Guard band: the reference squares with libm pow(|d|, 2.0), which can
  *   differ from d*d by an ulp.  Every task with a pair whose decision or f32 value such an ulp
  *   could change (stats->n_flagged pairs) is deferred; those pairs are decided on the HOST with
  *   this process's libm pow, exactly as agent.py:297/302/340 compute them, and the task is then
  *   resolved once with them (stats->n_resolved tasks; one extra host round trip when > 0).  The
  *   outputs are therefore the reference's on this host's libm, not only the x*x arithmetic's.
- *   per task, claims in ascending agent ID: the first claim wins if the task has no current
- *   winner, otherwise a claim replaces the winner iff x > util + hysteresis (fp64).
  * apos (n*2 f64), acaps (n u32: bit k = capability k), tpos (t*2 f64), treq (t i8: -1 none).
  * winner/util (device, t): in = current claim table (-1 = no claim; util fp64), out = final.
  * won (device, n, may be NULL): out, tasks won per agent.  id_to_index (device, may be NULL,

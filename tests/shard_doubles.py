@@ -29,15 +29,15 @@ class NumpyBackend:
         return torch.as_tensor(rp), torch.as_tensor(col)
 
     # leaders: two buffers, round t reads [(t-1)&1] and writes [t&1] (swarm_frontier_* contract)
-    def begin(self, n_rows, init, leaders):
+    def begin(self, own_begin, n_own, init, leaders, col16=None):
         leaders[0].copy_(init)
         leaders[1].copy_(init)
-        self.n_rows = n_rows
+        self.own = (own_begin, own_begin + n_own)
         self.act = np.ones(init.numel(), np.int64)
         self.counts = {}
 
     def step(self, t, rp, col, leaders):
-        # every row steps (ghost rows too: deep halos); only owned rows [0, n_rows) count
+        # every row steps (ghost rows too: deep halos); only the owned rows count
         Lr, Lw = leaders[(t - 1) & 1].numpy(), leaders[t & 1].numpy()
         rp_, col_ = rp.numpy(), col.numpy()
         Lw[:] = Lr
@@ -52,7 +52,7 @@ class NumpyBackend:
             Lw[v] = m
             self.act[v] = t + 1
             self.act[col_[rp_[v]:rp_[v + 1]]] = t + 1
-        self.counts[t] = sum(1 for v, _ in changed if v < self.n_rows)
+        self.counts[t] = sum(1 for v, _ in changed if self.own[0] <= v < self.own[1])
 
     def ghosts(self, t, begin, incoming, rp, col, leaders):
         cur = leaders[t & 1].numpy()
