@@ -786,8 +786,17 @@ struct Tuning {
                                // (-1: 8e-4 x agents, measured best at 100k, 1M and 10M agents)
     int64_t tile_min_changes = 0;  // swarm_elect_tiled: tiled rounds once a read round changed fewer than
                                    // this (0: never -- measured slower than the sparse rounds)
+    int64_t rec_min_changes = -1;  // swarm_elect_records: record tail once a read round changed fewer than this
+                                   // (-1: 0.006 x agents)
+    int rec_delta = 8;             // record tail: rounds admitted per launch (the window, records.hip)
+    int rec_grid = 0;              // record tail: workgroups (one wave, one tile at a time) per launch (0: 2 per CU)
+    int rec_batch = 8;             // record tail: launches per host check of the tile count
     Tuning() {
         if (const char *e = getenv("SWARM_TILE_MIN_CHANGES")) tile_min_changes = atoll(e);
+        if (const char *e = getenv("SWARM_REC_MIN_CHANGES")) rec_min_changes = atoll(e);
+        rec_delta = env_int("SWARM_REC_DELTA", 8);
+        rec_grid = env_int("SWARM_REC_GRID", 0);
+        rec_batch = env_int("SWARM_REC_BATCH", 8);
         il_min_changes = env_int("SWARM_IL_MIN_CHANGES", -1);
         use_c16 = env_int("SWARM_C16", 1);
         dense_flat = env_int("SWARM_DENSE_FLAT", 1);
@@ -1389,19 +1398,48 @@ __global__ __launch_bounds__(kBlock) void k_tile_regions(const uint32_t *__restr
     }
 }
 
+// ------------------------------------------------------------------ record tail (records.hip)
+// The first launch of a record tail: every agent marked for round t (the stamps the last sparse
+// round wrote, layout sm) is marked for launch 1 and its tile flagged (the first flagger appends
+// the tile to launch 1's list).  Stale stamps only mark more agents (more work, same results).
+__global__ __launch_bounds__(kBlock) void k_rec_marks(const uint8_t *__restrict__ act, StampMap sm, uint8_t stamp,
+                                                     int64_t n, const int32_t *__restrict__ acell, int64_t ncx,
+                                                     int64_t ntx, uint32_t tag, uint32_t *__restrict__ gmark,
+                                                     uint32_t *__restrict__ tflag, int32_t *__restrict__ tlist,
+                                                     uint32_t *__restrict__ tcnt) {
+    const int64_t slots = int64_t(sm.M) << sm.cshift;
+    for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < slots; j += int64_t(gridDim.x) * kBlock) {
+        if (act[j] != stamp) continue;
+        const int64_t v = stamp_agent(sm, j >> sm.cshift, int(j & ((int64_t(1) << sm.cshift) - 1)));
+        if (v >= n) continue;
+        gmark[v] = tag;
+        const int64_t c = acell[v];
+        const int64_t tile = (c / ncx) / kRecTile * ntx + (c % ncx) / kRecTile;
+        const uint32_t old = atomicMax(&tflag[tile], tag);
+        if (old < tag) tlist[atomicAdd(&tcnt[1], 1u)] = int32_t(tile);
+    }
+}
+
+struct RecArg {  // swarm_elect_records: the record index of this graph and its cell grid
+    const void *index;
+    int64_t ncx, ncy;
+    const int32_t *acell;
+};
+
 template <typename Off>
 int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, const int32_t *ids,
                int32_t *leader, uint8_t *state, int32_t max_rounds, int32_t mode,
                int32_t *rounds_exec, int64_t *changes_host, swarm_elect_stats *st,
                void *stream, const Off *hrp = nullptr, const int32_t *hcol = nullptr,
-               const int16_t *c16 = nullptr, const TileGeom *tg = nullptr) {
+               const int16_t *c16 = nullptr, const TileGeom *tg = nullptr, const RecArg *rec = nullptr) {
     SW_ARG(ctx != nullptr, "ctx is NULL");
     SW_ARG(n >= 0, "n < 0");
     SW_ARG(n < (int64_t(1) << 31), "n must be < 2^31");
     SW_ARG(max_rounds >= 1, "max_rounds < 1");
     const bool timed = (mode & SWARM_ELECT_TIMED) != 0;
     const bool tiles_early = (mode & SWARM_ELECT_TILES_EARLY) != 0;
-    mode &= ~(SWARM_ELECT_TIMED | SWARM_ELECT_TILES_EARLY);
+    const bool rec_early = (mode & SWARM_ELECT_RECORDS_EARLY) != 0;
+    mode &= ~(SWARM_ELECT_TIMED | SWARM_ELECT_TILES_EARLY | SWARM_ELECT_RECORDS_EARLY);
     SW_ARG(mode == SWARM_ELECT_DENSE || mode == SWARM_ELECT_FRONTIER, "unknown mode");
     SW_ARG(rounds_exec != nullptr, "rounds_exec is NULL");
     SW_ARG(n == 0 || (rp && ids && leader && state), "NULL array (col may be NULL only without edges)");
@@ -1504,8 +1542,103 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     int64_t tdbg_n = 0;
     int tgrid = 0;
     const int64_t tile_min = !tg ? -1 : tiles_early ? INT64_MAX : tuning().tile_min_changes;
+    // record tail (rec != NULL): from the first batch boundary at which the last read round changed
+    // fewer than rec_min agents, the remaining rounds as record lists (records.hip)
+    const int64_t rec_min = !rec ? -1
+                            : rec_early ? INT64_MAX
+                            : tuning().rec_min_changes >= 0 ? tuning().rec_min_changes
+                                                            : std::max<int64_t>(1, int64_t(0.006 * double(n)));
+    bool rec_tried = false, rec_used = false;
+    RecTail rt;
+    // the per-round counters of rounds (read_upto, tread], read back into hbuf: hist, stats, found
+    auto consume = [&](int tread) {
+        for (int r = read_upto + 1; r <= tread; ++r) {
+            const unsigned long long *rb = hbuf + size_t(r - read_upto - 1) * kCounters;
+            const int64_t c = int64_t(rb[C_CHG]);
+            hist.push_back(c);
+            const bool tr = r >= tile_from;  // a tiled round: act / ed = core agents and edges of its tiles
+            const RoundKind kind = mode == SWARM_ELECT_DENSE ? RK_DENSE : plan_round(r);
+            const bool dn = !tr && (kind == RK_DENSE || kind == RK_DENSE_MARK);
+            if (changes_host) changes_host[r - 1] = c;
+            const int64_t act = dn ? n : int64_t(rb[C_ACT]);
+            const int64_t ed = dn ? int64_t(e_total) : int64_t(rb[C_EDGE]);
+            act_sum += act;
+            edge_sum += ed;
+            chg_sum += c;
+            dense_rounds += dn ? 1 : 0;
+            // tiled rounds: SURVEY 8(d)'s per-unit bytes of the agents they stand for (12 B per agent,
+            // 8 B per edge), though a launch reads its region from HBM once for kTileHalo rounds
+            const double rbytes = tr ? 12.0 * double(act) + 8.0 * double(ed) : round_bytes(dn, n, int64_t(e_total), act, ed);
+            bytes += rbytes;
+            if (tr) {
+                tile_bytes += rbytes;
+                ++tile_rounds;
+            } else if (kind == RK_SPARSE) {
+                sp_bytes += rbytes;
+            }
+            if (rlog)
+                fprintf(rlog, "%d %lld %lld %lld %d %.2f\n", r, (long long)c, (long long)act, (long long)ed,
+                        tr ? 3 : int(kind), timed && !tr && r >= t ? ktime[r - t] * 1e3 : 0.0);
+            if (c == 0) {
+                found = r;
+                break;
+            }
+        }
+        read_upto = tread;
+    };
     while (read_upto < max_rounds && found < 0) {
         t = launched + 1;  // first round launched in this batch (> tend when only a read is left)
+        if (rec && !rec_tried && mode == SWARM_ELECT_FRONTIER && launched < max_rounds && !hist.empty() &&
+            plan_round(launched) == RK_SPARSE && hist.back() < rec_min) {
+            rec_tried = true;
+            if (read_upto < launched) {  // the look-ahead's unread rounds first (one may be the last)
+                hipLaunchKernelGGL(k_batch_totals, dim3(launched - read_upto), dim3(kWave), 0, s, ring, read_upto + 1,
+                                   dtot);
+                SW_LAUNCHED();
+                SW_HIP(hipEventRecord(ev_read, s));
+                SW_HIP(hipEventSynchronize(ev_read));
+                consume(launched);
+                if (found > 0) break;
+            }
+            // rounds launched + 1 ... as record lists over the state after round T0 = launched
+            rt.n = n;
+            rt.n_edges = int64_t(e_total);
+            rt.ncx = rec->ncx;
+            rt.ncy = rec->ncy;
+            rt.index = rec->index;
+            rt.acell = rec->acell;
+            rt.L = bufs[launched & 1];
+            rt.T0 = launched;
+            rt.max_rounds = max_rounds;
+            rt.delta = tuning().rec_delta;
+            rt.grid = tuning().rec_grid;
+            rt.batch = tuning().rec_batch;
+            rt.timed = timed;
+            int rc1 = rec_tail_prepare(ctx, &rt, s);
+            if (rc1) return rc1;
+            const int64_t ntx = (rec->ncx + kRecTile - 1) / kRecTile;
+            hipLaunchKernelGGL(k_rec_marks, dim3(grid_for(int64_t(rd_map.M) << rd_map.cshift, kBlock, 4096)),
+                               dim3(kBlock), 0, s, f.act[(launched + 1) & 1], rd_map, stamp_of(launched + 1), n,
+                               rec->acell, rec->ncx, ntx, rt.tag1, rt.gmark, rt.tflag, rt.tlist1, rt.tcnt);
+            SW_LAUNCHED();
+            rc1 = rec_tail_run(ctx, &rt, leader, s);
+            if (rc1) return rc1;
+            if (rt.fallback == 0) {  // leaders after round min(T0 + dmax, max_rounds) are in `leader`
+                rec_used = true;
+                for (int d = 1; d <= rt.dmax; ++d) {
+                    if (changes_host) changes_host[rt.T0 + d - 1] = rt.hist[size_t(d)];
+                    chg_sum += rt.hist[size_t(d)];
+                }
+                if (rt.T0 + rt.dmax < max_rounds) {  // the first round without a change
+                    found = rt.T0 + rt.dmax + 1;
+                    if (changes_host) changes_host[found - 1] = 0;
+                }
+                read_upto = max_rounds;
+                break;
+            }
+            // fallback (list overflow / capacity): the frontier rounds continue from T0 + 1, whose
+            // marks and leader buffers the tail only read
+        }
         if (tg && tile_from == INT_MAX && mode == SWARM_ELECT_FRONTIER && t <= max_rounds &&
             plan_round(t) == RK_SPARSE && plan_round(t - 1) == RK_SPARSE && !hist.empty() && hist.back() < tile_min) {
             // switch to tiled rounds from round t: the tiles within kTileHalo cells of an agent
@@ -1639,39 +1772,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
                 sp_launches += seg_n;
             }
         }
-        for (int r = read_upto + 1; r <= tread; ++r) {
-            const unsigned long long *rb = hbuf + size_t(r - read_upto - 1) * kCounters;
-            const int64_t c = int64_t(rb[C_CHG]);
-            hist.push_back(c);
-            const bool tr = r >= tile_from;  // a tiled round: act / ed = core agents and edges of its tiles
-            const RoundKind kind = mode == SWARM_ELECT_DENSE ? RK_DENSE : plan_round(r);
-            const bool dn = !tr && (kind == RK_DENSE || kind == RK_DENSE_MARK);
-            if (changes_host) changes_host[r - 1] = c;
-            const int64_t act = dn ? n : int64_t(rb[C_ACT]);
-            const int64_t ed = dn ? int64_t(e_total) : int64_t(rb[C_EDGE]);
-            act_sum += act;
-            edge_sum += ed;
-            chg_sum += c;
-            dense_rounds += dn ? 1 : 0;
-            // tiled rounds: SURVEY 8(d)'s per-unit bytes of the agents they stand for (12 B per agent,
-            // 8 B per edge), though a launch reads its region from HBM once for kTileHalo rounds
-            const double rbytes = tr ? 12.0 * double(act) + 8.0 * double(ed) : round_bytes(dn, n, int64_t(e_total), act, ed);
-            bytes += rbytes;
-            if (tr) {
-                tile_bytes += rbytes;
-                ++tile_rounds;
-            } else if (kind == RK_SPARSE) {
-                sp_bytes += rbytes;
-            }
-            if (rlog)
-                fprintf(rlog, "%d %lld %lld %lld %d %.2f\n", r, (long long)c, (long long)act, (long long)ed,
-                        tr ? 3 : int(kind), timed && !tr ? ktime[r - t] * 1e3 : 0.0);
-            if (c == 0) {
-                found = r;
-                break;
-            }
-        }
-        read_upto = tread;
+        consume(tread);
         // a batch spans at most kRing/2 rounds of counter slots, look-ahead included (bookkeeping
         // recycles the slot of round t - kRing/2 in round t)
         batch = next_round_batch(hist.data(), hist.size(), batch, kMaxBatch - kLook);
@@ -1694,9 +1795,9 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
             return SWARM_ERR_ARG;
         }
         if (tile_cur == 1) SW_HIP(hipMemcpyAsync(leader, bufs[1], size_t(n) * 4, hipMemcpyDeviceToDevice, s));
-    } else if (found < 0 && (last & 1)) {
+    } else if (!rec_used && found < 0 && (last & 1)) {
         // after a zero-change round both buffers hold the final state (dense and frontier alike);
-        // otherwise the newest is bufs[last & 1]
+        // otherwise the newest is bufs[last & 1] (a record tail wrote its leaders into `leader`)
         SW_HIP(hipMemcpyAsync(leader, bufs[1], size_t(n) * 4, hipMemcpyDeviceToDevice, s));
     }
     hipLaunchKernelGGL(k_state, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s, leader,
@@ -1721,6 +1822,13 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         st->tile_ms = tile_ms;
         st->tile_bytes = tile_bytes;
         st->tile_from = tile_from == INT_MAX ? 0 : tile_from;
+        st->record_from = rec_used ? rt.T0 + 1 : 0;
+        st->record_launches = rt.launches;
+        st->record_activations = rt.activations;
+        st->record_recomputes = rt.recomputes;
+        st->record_ms = rt.ms;
+        st->record_fallback = rt.fallback;
+        st->record_levels = rt.levels;
     }
     return found > 0 ? SWARM_OK : SWARM_NOT_CONVERGED;
 }
@@ -1866,6 +1974,21 @@ int swarm_elect_tiled(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const i
                      (grid->ncy + kTileCore - 1) / kTileCore};
     return elect_impl<int32_t>(ctx, n, row_ptr, col, ids, leader, state, max_rounds, mode, rounds_exec,
                                changes_per_round, stats, stream, nullptr, nullptr, c16, &g);
+}
+
+int swarm_elect_records(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col, const int16_t *col16,
+                        const int32_t *ids, int32_t *leader, uint8_t *state, const swarm_grid *grid,
+                        const int32_t *acell, const void *index, int32_t max_rounds, int32_t mode,
+                        int32_t *rounds_exec, int64_t *changes_per_round, swarm_elect_stats *stats, void *stream) {
+    using namespace swarm;
+    const int16_t *c16 = tuning().use_c16 ? col16 : nullptr;
+    if (!index || !acell || !grid)
+        return elect_impl<int32_t>(ctx, n, row_ptr, col, ids, leader, state, max_rounds, mode, rounds_exec,
+                                   changes_per_round, stats, stream, nullptr, nullptr, c16);
+    SW_ARG(grid->ncx >= 1 && grid->ncy >= 1, "bad grid");
+    const RecArg ra{index, grid->ncx, grid->ncy, acell};
+    return elect_impl<int32_t>(ctx, n, row_ptr, col, ids, leader, state, max_rounds, mode, rounds_exec,
+                               changes_per_round, stats, stream, nullptr, nullptr, c16, nullptr, &ra);
 }
 
 int swarm_elect_directed(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col,

@@ -49,7 +49,7 @@ static int ins(ent_t *l, int *len, int32_t b, int32_t d, int32_t val) {
  * [5] overflow, [6] relaxations (vertex recomputes), [7] edge reads */
 long rec_sim(long n, const int64_t *rp, const int32_t *col, const int32_t *L, const uint8_t *mark0,
              const int32_t *tile_of, long ntiles, const int64_t *toff, const int32_t *tmem, int64_t *hist,
-             long hist_cap, int32_t *final_leader, int64_t *stats, long max_launches) {
+             long hist_cap, int32_t *final_leader, int64_t *stats, long max_launches, long delta) {
     ent_t *G = (ent_t *)calloc((size_t)n * RMAX, sizeof(ent_t));
     int32_t *Gn = (int32_t *)calloc((size_t)n, sizeof(int32_t));
     ent_t *G2 = (ent_t *)calloc((size_t)n * RMAX, sizeof(ent_t));
@@ -98,6 +98,8 @@ long rec_sim(long n, const int64_t *rp, const int32_t *col, const int32_t *L, co
             uint8_t *chg = (uint8_t *)calloc((size_t)m, 1);
             int32_t *stamp = (int32_t *)calloc((size_t)m, sizeof(int32_t)); /* level a slot last changed */
             uint8_t *first = (uint8_t *)calloc((size_t)m, 1);
+            uint8_t *deferred = (uint8_t *)calloc((size_t)m, 1);
+            const long wb = delta > 0 ? (launches) * delta : 0; /* window bound of this launch */
             for (long k = 0; k < m; ++k) first[k] = cur[k];
             while (nc) {
                 ++levels;
@@ -123,10 +125,16 @@ long rec_sim(long n, const int64_t *rp, const int32_t *col, const int32_t *L, co
                         ++edges;
                         const ent_t *lu = in ? &G2[(size_t)u * RMAX] : &G[(size_t)u * RMAX];
                         const int32_t nu = in ? G2n[u] : Gn[u];
-                        int r = ins(lv, &tmp_n[k], L[v], 1, L[u]);
+                        int r = (wb && 1 > wb) ? 0 : ins(lv, &tmp_n[k], L[v], 1, L[u]);
                         if (r < 0) { ++ovf; r = 0; }
                         changed |= r;
                         for (int32_t i = 0; i < nu; ++i) {
+                            if (wb && lu[i].d + 1 > wb) { /* beyond this launch's window: later */
+                                int32_t f = L[v];
+                                for (int32_t q = 0; q < tmp_n[k]; ++q) if (lv[q].d <= lu[i].d + 1 && lv[q].v > f) f = lv[q].v;
+                                if (lu[i].v > f) deferred[k] = 1;
+                                continue;
+                            }
                             r = ins(lv, &tmp_n[k], L[v], lu[i].d + 1, lu[i].v);
                             if (r < 0) { ++ovf; r = 0; }
                             changed |= r;
@@ -159,7 +167,12 @@ long rec_sim(long n, const int64_t *rp, const int32_t *col, const int32_t *L, co
                 uint8_t *tmp = cur; cur = nxt; nxt = tmp;
                 nc = nn;
             }
-            free(tmp_l); free(tmp_n); free(chg); free(stamp); free(first);
+            for (long k = 0; k < m; ++k)
+                if (deferred[k]) {
+                    __atomic_store_n(&mk2[tmem[a0 + k]], 1, __ATOMIC_RELAXED);
+                    __atomic_store_n(&tact2[t], 1, __ATOMIC_RELAXED);
+                }
+            free(tmp_l); free(tmp_n); free(chg); free(stamp); free(first); free(deferred);
             lev_sum += levels;
             tlev[t] = (int32_t)levels;
             if (levels > launch_max) launch_max = levels;

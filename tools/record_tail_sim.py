@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--t0", type=int, nargs="+", default=[300])
     ap.add_argument("--tile", type=int, nargs="+", default=[16])
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--delta", type=int, nargs="+", default=[0])
     a = ap.parse_args()
     so = f"/tmp/librecord_sim_{os.getpid()}.so"
     subprocess.check_call(["gcc", "-O2", "-fopenmp", "-shared", "-fPIC", "-o", so,
@@ -50,7 +51,7 @@ def main():
         src = np.repeat(np.arange(n), np.diff(rp))
         mark[col[rise[src]]] = True
         mark = mark.astype(np.uint8)
-        for ts in a.tile:
+        for ts, delta in [(ts, dl) for ts in a.tile for dl in a.delta]:
             tx, ty = cx // ts, cy // ts
             ntx = int(tx.max()) + 1
             tile_of = (ty * ntx + tx).astype(np.int32)
@@ -65,12 +66,12 @@ def main():
             t_1 = time.time()
             dmax = lib.rec_sim(ctypes.c_long(n), P(rp), P(col), P(L), P(mark), P(tile_of),
                                ctypes.c_long(ntiles), P(toff), P(order), P(hist), ctypes.c_long(len(hist)),
-                               P(fin), P(stats), ctypes.c_long(100000))
+                               P(fin), P(stats), ctypes.c_long(100000), ctypes.c_long(delta))
             ok_lead = bool(np.array_equal(fin, lead))
             tail = np.asarray(ch[t0:rounds - 1])
             ok_ch = bool(np.array_equal(hist[1:dmax + 1], tail)) and t0 + dmax + 1 == rounds
             agents_per_tile = n / ntiles
-            print(f"T0 {t0} tile {ts}x{ts} cells (~{agents_per_tile:.0f} agents, {ntiles} tiles): "
+            print(f"T0 {t0} delta {delta} tile {ts}x{ts} cells (~{agents_per_tile:.0f} agents, {ntiles} tiles): "
                   f"launches {stats[0]} activations {stats[1]} levels/act {stats[2] / max(1, stats[1]):.1f} "
                   f"critical levels {stats[3]} (256 WGs: {stats[8]} levels, {stats[9]} tiles in sequence) (jacobi tail rounds {rounds - t0}) maxlen {stats[4]} ovf {stats[5]} "
                   f"recomputes {stats[6] / 1e6:.1f}M edges {stats[7] / 1e6:.1f}M | leaders {ok_lead} changes {ok_ch} "
