@@ -46,6 +46,8 @@
 #include <algorithm>
 #include <climits>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "swarm_common.h"
@@ -59,7 +61,7 @@ constexpr int kRSlots = 640;           // region agents per tile held in LDS
 constexpr int kRCore = 448;            // core agents per tile
 constexpr int kREdges = 8192;          // core edges per tile
 constexpr int kRRuns = 3 * kRT + 2;    // region runs: kRT core rows, bottom row, left+right cells, top row
-constexpr int kRLevelCap = 1 << 15;    // levels per activation (a safety net: never reached)
+constexpr int kRLevelCap = 4095;       // levels per activation (a safety net: never reached)
 constexpr int kRHist = 4096;           // LDS histogram bins of the finalize pass
 
 __device__ __forceinline__ uint32_t rtag(uint32_t gen, uint32_t k) { return (gen << kRecDBits) | k; }
@@ -245,11 +247,14 @@ struct RecState {
     const int32_t *L;          // state after round T0 (the records' base values)
     unsigned long long *glist; // kRR entries per agent
     uint32_t *gmark;           // agent marks (rtag of the launch that must recompute the agent)
+    uint32_t *gchg;            // rtag of the launch an agent's list last changed in
+    uint32_t *gpull;           // rtag of the launch an agent last pulled in (0: pull every neighbour)
     uint32_t *tflag;           // tile flags (rtag of the launch that processes the tile)
     int32_t *tlist[2];         // tiles of launch k in tlist[k & 1]
     uint32_t *tcnt;            // tiles of launch k: tcnt[k]
     unsigned *err;             // 1: region over capacity, 2: list overflow, 4: level cap
-    unsigned long long *stats; // [0] activations, [1] levels, [2] agent recomputes, [3] region agents loaded
+    unsigned long long *stats; // [0] activations, [1] levels, [2] agent recomputes, [3] region agents loaded,
+                               // [4..6] wall clock of the load / levels / end phases
     const int32_t *acell;
     int64_t ncx, ntx;
     uint32_t gen;
@@ -269,8 +274,8 @@ __device__ __forceinline__ unsigned long long rpack(int d, int32_t val) {
 __device__ __forceinline__ int rdist(unsigned long long x) { return int(uint32_t(x >> 32)); }
 __device__ __forceinline__ int32_t rval(unsigned long long x) { return int32_t(uint32_t(x)); }
 
-// An agent's list while it recomputes: R entries in registers (d = INT_MAX past the end), the LDS
-// copy own[0, n) written only when a candidate survives (rare: most are dominated).
+// An agent's list while it recomputes, in registers: d = INT_MAX past the end.  Sorted by d
+// ascending with values ascending (a pareto list); the base (0, L_v) is implicit.
 template <int R>
 struct OwnList {
     int d[R];
@@ -278,38 +283,66 @@ struct OwnList {
     int n;
     __device__ __forceinline__ void load(const unsigned long long *own, int len) {
         n = len;
+        const ulonglong2 *p = reinterpret_cast<const ulonglong2 *>(own);
 #pragma unroll
-        for (int q = 0; q < R; ++q) {
-            const unsigned long long x = own[q];
-            d[q] = q < len ? rdist(x) : INT_MAX;
-            v[q] = q < len ? rval(x) : INT_MIN;
+        for (int q = 0; q < R / 2; ++q) {
+            const ulonglong2 w = p[q];
+            d[2 * q] = 2 * q < len ? rdist(w.x) : INT_MAX;
+            v[2 * q] = 2 * q < len ? rval(w.x) : INT_MIN;
+            d[2 * q + 1] = 2 * q + 1 < len ? rdist(w.y) : INT_MAX;
+            v[2 * q + 1] = 2 * q + 1 < len ? rval(w.y) : INT_MIN;
         }
     }
-    // (dd, val) dominated by the base or by an entry (d' <= dd and v' >= val)
-    __device__ __forceinline__ bool dominated(int dd, int32_t val, int32_t base) const {
-        bool dom = val <= base;
+    __device__ __forceinline__ void store(unsigned long long *own) const {
+        ulonglong2 *p = reinterpret_cast<ulonglong2 *>(own);
 #pragma unroll
-        for (int q = 0; q < R; ++q) dom |= d[q] <= dd && v[q] >= val;
-        return dom;
+        for (int q = 0; q < R / 2; ++q) p[q] = ulonglong2{rpack(d[2 * q], v[2 * q]), rpack(d[2 * q + 1], v[2 * q + 1])};
     }
-    // insert a non-dominated (dd, val) into own[] (sorted by d ascending, values ascending): the
-    // entries [a, b) it dominates (d' >= dd, v' <= val) go, the rest shift; false on overflow
-    __device__ __forceinline__ bool insert(unsigned long long *own, int dd, int32_t val) {
+    // the list's value at distance dd: the last entry with d <= dd (values ascend), else the base
+    __device__ __forceinline__ int32_t at(int dd, int32_t base) const {
+        int32_t m = base;
+#pragma unroll
+        for (int q = 0; q < R; ++q) m = d[q] <= dd ? v[q] : m;
+        return m;
+    }
+    // insert (dd, val), not dominated (val > at(dd)): the c entries [a, a + c) it dominates
+    // (d >= dd, v <= val) go and the rest shift; false on overflow (list unchanged).  Usually
+    // c = 0 (shift right by one) or 1 (replace): a few selects per entry, no R x R network.
+    __device__ __forceinline__ bool insert(int dd, int32_t val) {
         int a = 0, c = 0;
 #pragma unroll
         for (int q = 0; q < R; ++q) {
             a += d[q] < dd ? 1 : 0;
-            c += (q < n && d[q] >= dd && v[q] <= val) ? 1 : 0;
+            c += (d[q] != INT_MAX && d[q] >= dd && v[q] <= val) ? 1 : 0;
         }
-        const int b = a + c, nn = a + 1 + (n - b);
+        const int nn = n + 1 - c;
         if (nn > R) return false;
-        if (b > a + 1) {
-            for (int q = b; q < n; ++q) own[q - (b - a - 1)] = own[q];
-        } else if (b == a) {
-            for (int q = n - 1; q >= a; --q) own[q + 1] = own[q];
+        if (c == 0) {
+#pragma unroll
+            for (int p = R - 1; p > 0; --p)
+                if (p > a) {
+                    d[p] = d[p - 1];
+                    v[p] = v[p - 1];
+                }
+        } else {
+            for (int t = 1; t < c; ++t) {
+#pragma unroll
+                for (int p = 1; p < R - 1; ++p)
+                    if (p > a) {
+                        d[p] = d[p + 1];
+                        v[p] = v[p + 1];
+                    }
+                d[R - 1] = INT_MAX;
+                v[R - 1] = INT_MIN;
+            }
         }
-        own[a] = rpack(dd, val);
-        load(own, nn);
+#pragma unroll
+        for (int p = 0; p < R; ++p)
+            if (p == a) {
+                d[p] = dd;
+                v[p] = val;
+            }
+        n = nn;
         return true;
     }
 };
@@ -322,15 +355,23 @@ __global__ __launch_bounds__(64) void k_rec_tiles(RecState S, int k, int W, int 
     __shared__ __attribute__((aligned(16))) uint16_t sCol[kREdges];
     __shared__ __attribute__((aligned(16))) uint16_t sRow[kRCore + 8];
     __shared__ uint8_t sN[kRSlots];
-    __shared__ uint8_t sMark[kRCore], sDirty[kRCore];
-    __shared__ uint16_t sList[kRCore], sLast[kRCore];
-    __shared__ uint16_t sChg[kRSlots];  // level of a slot's last change in this activation (0: none)
+    __shared__ unsigned sMark[kRCore];  // queued for the next level (LDS atomics: first marker appends)
+    __shared__ uint8_t sDirty[kRCore];  // 1: list changed, 2: pulled, 4: deferred a record
+    __shared__ uint16_t sList[2][kRCore];
+    // pull filter: times (launch << 12 | level) of a slot's last change and a core agent's last pull;
+    // an agent pulls only from neighbours that changed at or after its last pull
+    __shared__ uint32_t sLast[kRCore];
+    __shared__ int sCnt[2];
+    __shared__ uint32_t sChg[kRSlots];
+    __shared__ int32_t sMaxV[kRSlots];  // a slot's largest value (its last record, else its base)
+    __shared__ uint8_t sRing[kRSlots];  // ring slots next to a change in this activation
+    __shared__ int sDefer;              // an agent of this tile deferred a record past the window
     const int lane = threadIdx.x;
     const uint32_t cnt = S.tcnt[k];
     const uint32_t tgk = rtag(S.gen, uint32_t(k)), tg1 = rtag(S.gen, uint32_t(k + 1));
     const uint32_t genhi = S.gen << kRecDBits;
     const int32_t *list = S.tlist[k & 1];
-    unsigned long long my_lev = 0, my_rec = 0, my_load = 0, my_act = 0;
+    unsigned long long my_lev = 0, my_rec = 0, my_load = 0, my_act = 0, c_load = 0, c_lev = 0, c_end = 0;
     for (uint32_t li = blockIdx.x; li < cnt; li += gridDim.x) {
         const int64_t tile = list[li];
         const int32_t a0 = S.ix.ra[tile], m = S.ix.ra[tile + 1] - a0;
@@ -342,6 +383,8 @@ __global__ __launch_bounds__(64) void k_rec_tiles(RecState S, int k, int W, int 
             continue;
         }
         ++my_act;
+        if (lane == 0) sDefer = 0;
+        const unsigned long long w0 = wall_clock64();
         // (a) slot -> agent, the core rows and columns: 16-byte loads, 8 in flight per lane
         {
             const int n16 = nr >> 2, c16 = ne >> 3, r16 = nq >> 3;
@@ -378,7 +421,7 @@ __global__ __launch_bounds__(64) void k_rec_tiles(RecState S, int k, int W, int 
         constexpr int kU = 4;
         for (int l0 = 0; l0 < nr; l0 += 64 * kU) {
             int32_t v[kU], lv[kU];
-            uint32_t mk[kU];
+            uint32_t mk[kU], gc[kU], gp[kU];
             ulonglong2 w[kU][R / 2];
 #pragma unroll
             for (int j = 0; j < kU; ++j) {
@@ -389,6 +432,8 @@ __global__ __launch_bounds__(64) void k_rec_tiles(RecState S, int k, int W, int 
             for (int j = 0; j < kU; ++j) {
                 lv[j] = S.L[v[j]];
                 mk[j] = S.gmark[v[j]];
+                gc[j] = S.gchg[v[j]];
+                gp[j] = S.gpull[v[j]];
                 const ulonglong2 *g = reinterpret_cast<const ulonglong2 *>(S.glist + size_t(v[j]) * R);
 #pragma unroll
                 for (int i = 0; i < R / 2; ++i) w[j][i] = g[i];
@@ -409,71 +454,95 @@ __global__ __launch_bounds__(64) void k_rec_tiles(RecState S, int k, int W, int 
                     }
                 }
                 sN[l] = uint8_t(c);
-                sChg[l] = 0;
+                sMaxV[l] = c ? rval(sE[l * R + c - 1]) : lv[j];
+                // a change in launch kc (any level: 0xFFF), a pull in launch kp (level 0)
+                sChg[l] = (gc[j] >> kRecDBits) == S.gen ? ((gc[j] & kRecDMask) << 12) | 0xFFFu : 0u;
+                sRing[l] = 0;
                 if (l < m) {
                     const bool marked = mk[j] >= tgk;
-                    sMark[l] = marked ? 1 : 0;
-                    sLast[l] = marked ? 0 : 1;  // marked from outside: pull every neighbour first
+                    sMark[l] = marked ? 1u : 0u;
+                    // unmarked: consistent with every neighbour as loaded -> only this launch's changes
+                    sLast[l] = marked ? ((gp[j] >> kRecDBits) == S.gen ? (gp[j] & kRecDMask) << 12 : 0u)
+                                      : (uint32_t(k) << 12) | 1u;
                     sDirty[l] = 0;
                 }
             }
         }
         my_load += uint64_t(nr);
         __syncthreads();
-        // (c) levels: every marked core agent pulls from all its neighbours (in place: a reader
-        // sees each entry whole, old or new, and every change re-marks the readers)
-        int lev = 0;
-        for (;;) {
-            int total = 0;
+        const unsigned long long w1 = wall_clock64();
+        // (c) levels: the queued core agents pull from the neighbours that changed since their last
+        // pull (every neighbour the first time); a change queues the agent's core neighbours for the
+        // next level (in place: a reader sees each entry whole, old or new, and every change
+        // re-queues its readers)
+        {
+            int total = 0;  // level 1's queue: the agents marked from outside
             for (int j0 = 0; j0 < m; j0 += 64) {
                 const int l = j0 + lane;
                 const bool f = l < m && sMark[l] != 0;
                 const unsigned long long b = __ballot(f);
-                if (f) {
-                    sMark[l] = 0;
-                    sList[total + int(__popcll(b & ((1ull << lane) - 1ull)))] = uint16_t(l);
-                }
+                if (f) sList[0][total + int(__popcll(b & ((1ull << lane) - 1ull)))] = uint16_t(l);
                 total += int(__popcll(b));
             }
-            __syncthreads();
+            if (lane == 0) sCnt[0] = total;
+        }
+        __syncthreads();
+        int lev = 0, cur = 0;
+        for (;;) {
+            const int total = sCnt[cur];
             if (total == 0) break;
             if (++lev > kRLevelCap) {
                 if (lane == 0) atomicOr(S.err, 4u);
                 break;
             }
+            if (lane == 0) sCnt[cur ^ 1] = 0;
+            __syncthreads();
             my_rec += uint64_t(total);
             for (int i = lane; i < total; i += 64) {
-                const int l = sList[i];
+                const int l = sList[cur][i];
+                sMark[l] = 0u;
                 const int32_t base = sL[l];
-                unsigned long long *own = &sE[l * R];
                 OwnList<R> ol;
-                ol.load(own, sN[l]);
-                // neighbours that changed since this agent's last pull (all of them the first time)
-                const int since = sLast[l];
-                sLast[l] = uint16_t(lev);
+                ol.load(&sE[l * R], sN[l]);
+                const uint32_t since = sLast[l];
+                const uint32_t now = (uint32_t(k) << 12) | uint32_t(lev);
+                sLast[l] = now;
                 bool changed = false, defer = false, ovf = false;
                 const int eb = sRow[l], ee = sRow[l + 1];
+                // one copy of the candidate code, not unrolled (an unrolled 8 x 8 nest of inlined
+                // inserts made the kernel ~200 KB of code); a neighbour's records are loaded at once
+                // and walked in registers (no LDS round trip per record); a neighbour whose largest
+                // value does not beat this agent's value after one round offers nothing
+                const int32_t v1 = ol.at(1, base);
+#pragma unroll 1
                 for (int e = eb; e < ee; ++e) {
                     const int u = sCol[e];
-                    if (sChg[u] < since) continue;
+                    if (sChg[u] < since || sMaxV[u] <= v1) continue;
                     const int nu = sN[u];
+                    const ulonglong2 *pu = reinterpret_cast<const ulonglong2 *>(&sE[u * R]);
+                    unsigned long long x[R];
+#pragma unroll
+                    for (int q = 0; q < R / 2; ++q) {
+                        const ulonglong2 w = pu[q];
+                        x[2 * q] = w.x;
+                        x[2 * q + 1] = w.y;
+                    }
+                    int dd = 1;
+                    int32_t val = sL[u];
+#pragma unroll 1
                     for (int q = -1; q < nu; ++q) {
-                        int dd;
-                        int32_t val;
-                        if (q < 0) {
-                            dd = 1;
-                            val = sL[u];
-                        } else {
-                            const unsigned long long x = sE[u * R + q];
-                            dd = rdist(x) + 1;
-                            val = rval(x);
+                        if (q >= 0) {
+                            dd = rdist(x[0]) + 1;
+                            val = rval(x[0]);
+#pragma unroll
+                            for (int t = 0; t + 1 < R; ++t) x[t] = x[t + 1];  // next record to the front
                         }
-                        if (dd > dcap || ol.dominated(dd, val, base)) continue;
+                        if (dd > dcap || val <= ol.at(dd, base)) continue;
                         if (dd > W) {  // beyond this launch's window: next launch
                             defer = true;
                             continue;
                         }
-                        if (ol.insert(own, dd, val))
+                        if (ol.insert(dd, val))
                             changed = true;
                         else
                             ovf = true;
@@ -481,33 +550,56 @@ __global__ __launch_bounds__(64) void k_rec_tiles(RecState S, int k, int W, int 
                 }
                 if (ovf) atomicOr(S.err, 2u);
                 if (changed) {
+                    ol.store(&sE[l * R]);
                     sN[l] = uint8_t(ol.n);
-                    sChg[l] = uint16_t(lev);
-                    sDirty[l] = 1;
-                    for (int e = eb; e < ee; ++e) {
-                        const int u = sCol[e];
-                        if (u < m) {
-                            sMark[u] = 1;
-                        } else {  // a ring agent: its own tile recomputes it next launch
-                            const int32_t vu = sA[u];
-                            S.gmark[vu] = tg1;
-                            flag_tile(S, tile_of_cell(S.acell[vu], S.ncx, S.ntx), tg1, k + 1);
+                    sMaxV[l] = ol.at(INT_MAX - 1, base);
+                    sChg[l] = now;
+#pragma unroll 1
+                    for (int e0 = eb; e0 < ee; e0 += 8) {  // queue the core neighbours, 8 at a time
+                        int u[8];
+                        unsigned old[8];
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) u[j] = sCol[e0 + j < ee ? e0 + j : ee - 1];
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) old[j] = (e0 + j < ee && u[j] < m) ? atomicOr(&sMark[u[j]], 1u) : 1u;
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            if (e0 + j < ee && u[j] >= m) sRing[u[j]] = 1;  // a ring agent: flagged below
+                            if (old[j] == 0u) sList[cur ^ 1][atomicAdd(&sCnt[cur ^ 1], 1)] = uint16_t(u[j]);
                         }
                     }
                 }
+                // pulled; changed; deferred (its next pull must see every neighbour again)
+                sDirty[l] |= uint8_t(2 | (changed ? 1 : 0) | (defer ? 4 : 0));
                 if (defer) {  // a record beyond the window: this agent again next launch
                     S.gmark[sA[l]] = tg1;
-                    flag_tile(S, tile, tg1, k + 1);
+                    sDefer = 1;
                 }
             }
             __syncthreads();
+            cur ^= 1;
         }
         my_lev += uint64_t(lev);
+        const unsigned long long w2 = wall_clock64();
+        // ring agents next to a change: marked for the next launch, their tiles flagged (once per
+        // activation, all lanes' flags at once: a flag is a returning atomic round trip)
+        for (int l = m + lane; l < nr; l += 64) {
+            if (!sRing[l]) continue;
+            const int32_t vu = sA[l];
+            S.gmark[vu] = tg1;
+            flag_tile(S, tile_of_cell(S.acell[vu], S.ncx, S.ntx), tg1, k + 1);
+        }
+        if (sDefer && lane == 0) flag_tile(S, tile, tg1, k + 1);
         // (d) changed core lists back to HBM, whole entries, tagged with this election's gen
         for (int l = lane; l < m; l += 64) {
-            if (!sDirty[l]) continue;
+            const int dirty = sDirty[l];
+            if (!dirty) continue;
+            const int32_t va = sA[l];
+            S.gpull[va] = (dirty & 4) ? 0u : tgk;
+            if (!(dirty & 1)) continue;
+            S.gchg[va] = tgk;
             const int n = sN[l];
-            ulonglong2 *g = reinterpret_cast<ulonglong2 *>(S.glist + size_t(sA[l]) * R);
+            ulonglong2 *g = reinterpret_cast<ulonglong2 *>(S.glist + size_t(va) * R);
 #pragma unroll
             for (int i = 0; i < R / 2; ++i) {
                 const unsigned long long x0 = 2 * i < n ? sE[l * R + 2 * i] | (static_cast<unsigned long long>(genhi) << 32) : 0ull;
@@ -517,12 +609,20 @@ __global__ __launch_bounds__(64) void k_rec_tiles(RecState S, int k, int W, int 
             }
         }
         __syncthreads();  // LDS reused by the next tile
+        const unsigned long long w3 = wall_clock64();
+        c_load += w1 - w0;
+        c_lev += w2 - w1;
+        c_end += w3 - w2;
     }
     if (lane == 0 && my_act) {
         atomicAdd(&S.stats[0], my_act);
         atomicAdd(&S.stats[1], my_lev);
         atomicAdd(&S.stats[2], my_rec);
         atomicAdd(&S.stats[3], my_load);
+        atomicAdd(&S.stats[4], c_load);  // wall_clock64 ticks (100 MHz) per phase, summed over activations
+        atomicAdd(&S.stats[5], c_lev);
+        atomicAdd(&S.stats[6], c_end);
+
     }
 }
 
@@ -628,12 +728,13 @@ int rec_tail_prepare(swarm_ctx *ctx, RecTail *rt, hipStream_t s) {
     void *old_list = ctx->slot[S_REC_LIST], *old_mark = ctx->slot[S_REC_MARK];
     unsigned long long *glist;
     SW_ALLOC(glist, ctx, S_REC_LIST, lbytes);
-    const size_t mbytes = size_t(n) * 4 + size_t(ntiles) * 4 * 3 + size_t(kRecMaxLaunch + 2) * 4 + 64 * 8 + 256;
+    const size_t mbytes = size_t(n) * 12 + size_t(ntiles) * 4 * 3 + size_t(kRecMaxLaunch + 2) * 4 + 64 * 8 + 256;
     char *mb;
     SW_ALLOC(mb, ctx, S_REC_MARK, mbytes);
     const bool fresh = glist != old_list || static_cast<void *>(mb) != old_mark || ctx->rec_gen + 1 >= (1u << kRecGenBits);
     uint32_t *gmark = reinterpret_cast<uint32_t *>(mb);
-    uint32_t *tflag = gmark + n;
+    uint32_t *gchg = gmark + n, *gpull = gchg + n;
+    uint32_t *tflag = gpull + n;
     int32_t *tl0 = reinterpret_cast<int32_t *>(tflag + ntiles);
     int32_t *tl1 = tl0 + ntiles;
     uint32_t *tcnt = reinterpret_cast<uint32_t *>(tl1 + ntiles);
@@ -653,12 +754,14 @@ int rec_tail_prepare(swarm_ctx *ctx, RecTail *rt, hipStream_t s) {
     S.L = rt->L;
     S.glist = glist;
     S.gmark = gmark;
+    S.gchg = gchg;
+    S.gpull = gpull;
     S.tflag = tflag;
     S.tlist[0] = tl0;
     S.tlist[1] = tl1;
     S.tcnt = tcnt;
     S.err = reinterpret_cast<unsigned *>(misc);         // misc[0]: err (u32), misc[0] hi: dmax
-    S.stats = misc + 2;                                  // misc[2..5]
+    S.stats = misc + 2;                                  // misc[2..10]
     S.acell = rt->acell;
     S.ncx = rt->ncx;
     S.ntx = (rt->ncx + kRT - 1) / kRT;
@@ -732,10 +835,10 @@ int rec_tail_run(swarm_ctx *ctx, RecTail *rt, int32_t *out, hipStream_t s) {
                        S.gen, dcap, out, hist, int(hlen), dmax);
     SW_LAUNCHED();
     if (rt->timed) SW_HIP(hipEventRecord(ev1, s));
-    unsigned long long hs[4] = {0, 0, 0, 0};
+    unsigned long long hs[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned hd = 0;
     SW_HIP(hipMemcpyAsync(&hd, dmax, 4, hipMemcpyDeviceToHost, s));
-    SW_HIP(hipMemcpyAsync(hs, S.stats, 32, hipMemcpyDeviceToHost, s));
+    SW_HIP(hipMemcpyAsync(hs, S.stats, 80, hipMemcpyDeviceToHost, s));
     SW_HIP(hipStreamSynchronize(s));
     rt->dmax = int(hd);
     rt->hist.assign(size_t(hd) + 1, 0);
@@ -748,6 +851,13 @@ int rec_tail_run(swarm_ctx *ctx, RecTail *rt, int32_t *out, hipStream_t s) {
     rt->levels = int64_t(hs[1]);
     rt->recomputes = int64_t(hs[2]);
     rt->loaded = int64_t(hs[3]);
+    if (getenv("SWARM_REC_DEBUG"))
+        fprintf(stderr, "record tail: T0 %d launches %lld activations %lld levels %lld recomputes %lld loaded %lld | "
+                        "us per activation: load %.2f levels %.2f end %.2f | dmax %d\n", rt->T0, (long long)rt->launches,
+                (long long)hs[0], (long long)hs[1], (long long)hs[2], (long long)hs[3],
+                hs[0] ? double(hs[4]) / 100.0 / double(hs[0]) : 0.0, hs[0] ? double(hs[5]) / 100.0 / double(hs[0]) : 0.0,
+                hs[0] ? double(hs[6]) / 100.0 / double(hs[0]) : 0.0,
+                rt->dmax);
     if (rt->timed) {
         float x = 0;
         SW_HIP(hipEventElapsedTime(&x, ev0, ev1));

@@ -9,9 +9,9 @@ mkdir -p $O
 timeout -k 10 400 python3 -u -m pytest tests/test_records.py -x -v --timeout 120 --timeout-method thread > $O/tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -5 $O/tests.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
-timeout -k 10 300 python3 -u tools/records_ab.py 1000000 0,1,early > $O/ab_1m.json 2> $O/ab_1m.err
+SWARM_REC_DEBUG=1 timeout -k 10 300 python3 -u tools/records_ab.py 1000000 0,1,early > $O/ab_1m.json 2> $O/ab_1m.err
 rc=$?; echo "ab1m rc=$rc"; tail -1 $O/ab_1m.json; tail -3 $O/ab_1m.err
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python3 -u tools/records_ab.py 10000000 0,1 > $O/ab_10m.json 2> $O/ab_10m.err
+SWARM_REC_DEBUG=1 timeout -k 10 300 python3 -u tools/records_ab.py 10000000 1 > $O/ab_10m.json 2> $O/ab_10m.err
 rc=$?; echo "ab10m rc=$rc"; tail -1 $O/ab_10m.json; tail -3 $O/ab_10m.err
 exit $rc
