@@ -24,4 +24,5 @@ for _ in range(5):
     torch.cuda.synchronize()
     ts.append(time.perf_counter() - t0)
 print(f"{sys.argv[1]}: n={n} rounds={r.rounds_exec} launched={r.rounds_launched} "
-      f"elect ms min {min(ts) * 1e3:.2f} med {sorted(ts)[2] * 1e3:.2f}")
+      f"elect ms min {min(ts) * 1e3:.2f} med {sorted(ts)[2] * 1e3:.2f} "
+      f"leader_sum {int(r.leader.to(torch.int64).sum())} changes_sum {int(sum(r.changes))}")

@@ -1,5 +1,5 @@
 """Per-round-range kernel durations of the last election in a rocprofv3 kernel trace
-(tools/trace_ab.sh): rounds are the k_elect_dense / k_sparse_block dispatches in order.
+(tools/trace_ab.sh): rounds are the k_elect_dense / k_sparse_block / k_list_round dispatches in order.
 Usage: python tools/trace_ranges.py TRACE.csv [LABEL]"""
 import csv
 import sys
@@ -8,7 +8,8 @@ import numpy as np
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows
-            if "k_elect_dense" in r["Kernel_Name"] or "k_sparse_block" in r["Kernel_Name"])
+            if "k_elect_dense" in r["Kernel_Name"] or "k_sparse_block" in r["Kernel_Name"]
+            or "k_list_round" in r["Kernel_Name"])
 elections, cur, prev_sparse = [], [], False
 for k in ks:
     dense = "k_elect_dense" in k[2]
@@ -23,7 +24,8 @@ d = np.array([b - a for a, b, _ in e]) / 1e3
 span = (e[-1][1] - e[0][0]) / 1e6
 label = sys.argv[2] if len(sys.argv) > 2 else ""
 print(f"{label} rounds launched {len(e)}: span {span:.2f} ms, kernels {d.sum() / 1e3:.2f} ms")
-for lo, hi in [(1, 8), (9, 99), (100, 399), (400, 906), (907, 1364), (1365, 100000)]:
+for lo, hi in [(1, 8), (9, 9), (10, 30), (31, 100), (101, 200), (201, 400), (401, 700), (701, 1000), (1001, 1364),
+               (1365, 100000)]:
     x = d[lo - 1:hi]
     if len(x):
         print(f"   rounds {lo}-{min(hi, len(d))}: med {np.median(x):.1f} us, p90 {np.percentile(x, 90):.1f}, "
