@@ -162,6 +162,9 @@ def main():
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         ev[0].record()
         r = sw.elect(mode=args.elect_mode, max_rounds=1 << 16)
+        # elect() returns with its last kernels queued and then builds its result on the host:
+        # wait, so that host tail counts as election time, not as the allocation's
+        torch.cuda.synchronize()
         ev[1].record()
         a = sw.allocate(tpos_x, tpos_y, treq)
         ev[2].record()

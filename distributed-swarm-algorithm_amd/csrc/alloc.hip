@@ -134,13 +134,28 @@ __device__ __forceinline__ void flush_stats(const Params &P, unsigned long long 
     if (overflow) atomicAdd(sh + 4, overflow);
 }
 
-__global__ void k_fold_stats(const unsigned long long *__restrict__ sh, unsigned long long *__restrict__ out) {
+// One launch before a round: the stat shards, the deferred counters and won zeroed.
+__global__ __launch_bounds__(kBlock) void k_alloc_init(unsigned long long *__restrict__ stats,
+                                                      unsigned long long *__restrict__ dcount,
+                                                      int32_t *__restrict__ won, int64_t n) {
+    const int64_t i0 = int64_t(blockIdx.x) * kBlock + threadIdx.x, stride = int64_t(gridDim.x) * kBlock;
+    for (int64_t i = i0; i < int64_t(kStatShards) * kStatStride; i += stride) stats[i] = 0;
+    if (i0 == 0) dcount[0] = dcount[1] = 0;
+    if (won)
+        for (int64_t i = i0; i < n; i += stride) won[i] = 0;
+}
+
+// out[0, kNumStats): the shard sums; out[kNumStats] = *dcount (the deferred tasks) when given.  out may
+// be host-mapped memory (the round's stats reach the host without a copy).
+__global__ void k_fold_stats(const unsigned long long *__restrict__ sh, unsigned long long *__restrict__ out,
+                             const unsigned long long *__restrict__ dcount = nullptr) {
     for (int c = 0; c < kNumStats; ++c) {
         unsigned long long v = sh[size_t(threadIdx.x) * kStatStride + c];
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
         if (threadIdx.x == 0) out[c] = v;
     }
+    if (dcount && threadIdx.x == 0) out[kNumStats] = *dcount;
 }
 
 // Per-task epilogue shared by both strategies.
@@ -331,32 +346,46 @@ __device__ __forceinline__ void window_setup_all(int64_t n, CellWindow &w, int l
     __builtin_amdgcn_wave_barrier();
 }
 
+constexpr int kCheckPer = 4;  // agents per thread in flight (k_check_index)
+
 // Staleness test of a cell index: every agent must lie in its cell's range AND inside the indexed
 // bounding box.  cell_coord clamps, so an edge-cell agent that moved past [xmin, xmax] x [ymin,
 // ymax] still maps to its old cell; window_setup_rows skips every task whose disc misses that box,
 // so such an agent would lose its claims silently.  k_check_index runs on the ctx's side stream,
 // concurrently with the indexed allocation (it streams the positions while the task waves wait on
-// their dependent loads); the host reads the count after both and reports SWARM_ERR_STALE
-// (outputs undefined) instead of the results.
-__device__ __forceinline__ void check_index_part(const double2 *__restrict__ apos, int64_t n, const Grid &g,
-                                                 const uint32_t *__restrict__ off,
-                                                 unsigned long long *__restrict__ bad_out, int64_t b, int64_t nb) {
+// their dependent loads); the host reads the count with the folded stats and reports
+// SWARM_ERR_STALE (outputs undefined) instead of the results.
+__global__ __launch_bounds__(kBlock) void k_check_index(const double2 *__restrict__ apos, int64_t n, Grid g,
+                                                       const uint32_t *__restrict__ off,
+                                                       unsigned long long *__restrict__ bad_out) {
     unsigned long long bad = 0;
-    for (int64_t i = b * kBlock + threadIdx.x; i < n; i += nb * kBlock) {
-        const double2 p = apos[i];
-        const int64_t c = cell_coord(p.y, g.ymin, g.inv_cell, g.ncy) * g.ncx + cell_coord(p.x, g.xmin, g.inv_cell, g.ncx);
-        const bool inside = p.x >= g.xmin && p.x <= g.xmax && p.y >= g.ymin && p.y <= g.ymax;  // false for NaN
-        bad += (inside && off[c] <= uint32_t(i) && uint32_t(i) < off[c + 1]) ? 0 : 1;
+    const int64_t stride = int64_t(gridDim.x) * kBlock * kCheckPer;
+    for (int64_t i0 = int64_t(blockIdx.x) * kBlock * kCheckPer + threadIdx.x; i0 < n; i0 += stride) {
+        double2 p[kCheckPer];
+#pragma unroll
+        for (int j = 0; j < kCheckPer; ++j) {
+            const int64_t i = i0 + int64_t(j) * kBlock;
+            p[j] = apos[i < n ? i : n - 1];
+        }
+        uint32_t lo[kCheckPer], hi[kCheckPer];
+        bool inside[kCheckPer];
+#pragma unroll
+        for (int j = 0; j < kCheckPer; ++j) {
+            const int64_t c = cell_coord(p[j].y, g.ymin, g.inv_cell, g.ncy) * g.ncx +
+                              cell_coord(p[j].x, g.xmin, g.inv_cell, g.ncx);
+            inside[j] = p[j].x >= g.xmin && p[j].x <= g.xmax && p[j].y >= g.ymin && p[j].y <= g.ymax;  // false for NaN
+            lo[j] = off[c];
+            hi[j] = off[c + 1];
+        }
+#pragma unroll
+        for (int j = 0; j < kCheckPer; ++j) {
+            const int64_t i = i0 + int64_t(j) * kBlock;
+            if (i < n) bad += (inside[j] && lo[j] <= uint32_t(i) && uint32_t(i) < hi[j]) ? 0 : 1;
+        }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) bad += __shfl_xor(bad, o, 64);
     if ((threadIdx.x & 63) == 0 && bad) atomicAdd(bad_out, bad);
-}
-
-__global__ __launch_bounds__(kBlock) void k_check_index(const double2 *__restrict__ apos, int64_t n, Grid g,
-                                                       const uint32_t *__restrict__ off,
-                                                       unsigned long long *__restrict__ bad_out) {
-    check_index_part(apos, n, g, off, bad_out, blockIdx.x, gridDim.x);
 }
 
 // ------------------------------------------------------------------------------ binned
@@ -364,8 +393,14 @@ __global__ __launch_bounds__(kBlock) void k_check_index(const double2 *__restric
 // lane with all their loads in flight, and keeps the claims in the wave's LDS list (ballot
 // slots, no atomics); pass 2 walks the record chain with wave-wide min-ID reductions.  A task is
 // latency-bound (dependent loads, then the chain), so the point is tasks in flight: 32 per CU.
-constexpr int kWCap = 512;  // claims per task kept in LDS (beyond: exact recompute path; C3 max ~350)
-constexpr int kWU = 4;      // candidates in flight per lane
+#ifndef SWARM_ALLOC_WCAP  // A/B builds (tools/build_variant_alloc.sh) override these two
+#define SWARM_ALLOC_WCAP 512
+#endif
+#ifndef SWARM_ALLOC_WU
+#define SWARM_ALLOC_WU 4
+#endif
+constexpr int kWCap = SWARM_ALLOC_WCAP;  // claims per task kept in LDS (beyond: exact recompute path; C3 max ~350)
+constexpr int kWU = SWARM_ALLOC_WU;      // candidates in flight per lane
 
 __device__ __forceinline__ int wave_min_int(int v) {
 #pragma unroll
@@ -895,10 +930,8 @@ int alloc_impl(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos
     SW_ARG(n == 0 || (ids && apos && acaps), "NULL agent array");
     SW_ARG(t == 0 || (tpos && treq && winner && util), "NULL task array");
     hipStream_t s = static_cast<hipStream_t>(stream);
-    unsigned long long *dstats;
+    unsigned long long *dstats;  // the shards, then the folded stats
     SW_ALLOC(dstats, ctx, S_ASTATS, (size_t(kStatShards) * kStatStride + 8) * 8);
-    SW_HIP(hipMemsetAsync(dstats, 0, size_t(kStatShards) * kStatStride * 8, s));
-    if (won && n) SW_HIP(hipMemsetAsync(won, 0, size_t(n) * 4, s));
 
     // claim radius: U > thr  <=>  d < u_scale / thr - 1  (thr > 0, u_scale > 0, has_cap)
     const bool finite_r = claim_thr > 0 && u_scale > 0;
@@ -918,7 +951,8 @@ int alloc_impl(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos
     SW_ALLOC(dbase, ctx, S_DEFER, defer_flag_off + size_t(t) + 64);
     P.D.count = reinterpret_cast<unsigned long long *>(dbase);
     P.D.list = reinterpret_cast<int32_t *>(dbase + defer_list_off);
-    SW_HIP(hipMemsetAsync(P.D.count, 0, 16, s));
+    hipLaunchKernelGGL(k_alloc_init, dim3(grid_for(n, kBlock, 2048)), dim3(kBlock), 0, s, dstats, P.D.count, won, n);
+    SW_LAUNCHED();
 
     const bool nothing = (n == 0) || (used == SWARM_ALLOC_BINNED && rc <= 0.0);
     Cand cand;  // the main pass's candidate source, reused by the deferred passes
@@ -937,13 +971,15 @@ int alloc_impl(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos
         SW_ARG(std::floor(2.0 * rp * ix->inv_cell) + 2.0 <= double(kMaxCells),
                "claim radius spans more than 16 rows of the index's cells (use swarm_allocate)");
         // the staleness check on the side stream, concurrent with the allocation (joined before the
-        // counters are folded)
+        // counters are folded).  Measured and rejected: the check as extra workgroups of the
+        // allocation's grid, with the stats folded by the last workgroup through a ticket counter
+        // (one launch and no side stream): 245 us for the grid against ~90 us for the pair.
         hipStream_t s2;
         hipEvent_t fork, join;
         SW_TRY(side_stream(ctx, &s2, &fork, &join));
         SW_HIP(hipEventRecord(fork, s));
         SW_HIP(hipStreamWaitEvent(s2, fork, 0));
-        hipLaunchKernelGGL(k_check_index, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s2,
+        hipLaunchKernelGGL(k_check_index, dim3(grid_for(n, kBlock * kCheckPer, 4096)), dim3(kBlock), 0, s2,
                            reinterpret_cast<const double2 *>(apos), n, *ix, ix_off, dstats + 7);
         SW_LAUNCHED();
         SW_HIP(hipEventRecord(join, s2));
@@ -1018,11 +1054,16 @@ int alloc_impl(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos
     unsigned long long *hs = static_cast<unsigned long long *>(pinned(ctx, 128));
     if (!hs) return SWARM_ERR_OOM;
     unsigned long long *folded = dstats + size_t(kStatShards) * kStatStride;
-    hipLaunchKernelGGL(k_fold_stats, dim3(1), dim3(kWave), 0, s, dstats, folded);
-    SW_LAUNCHED();
-    SW_HIP(hipMemcpyAsync(hs, folded, 8 * kNumStats, hipMemcpyDeviceToHost, s));
-    SW_HIP(hipMemcpyAsync(hs + kNumStats, P.D.count, 8, hipMemcpyDeviceToHost, s));
-    SW_HIP(hipStreamSynchronize(s));
+    {  // the stats and the deferred count folded straight into host-mapped memory: no copies
+        void *fold_dev = nullptr;
+        volatile unsigned long long *hfold = static_cast<unsigned long long *>(mapped(ctx, 16 * 8, &fold_dev));
+        if (!hfold) return SWARM_ERR_OOM;
+        hipLaunchKernelGGL(k_fold_stats, dim3(1), dim3(kWave), 0, s, dstats,
+                           static_cast<unsigned long long *>(fold_dev), P.D.count);
+        SW_LAUNCHED();
+        SW_HIP(hipStreamSynchronize(s));
+        for (int c = 0; c <= kNumStats; ++c) hs[c] = hfold[c];
+    }
     if (hs[7]) {
         set_error("stale cell index: %llu agent(s) outside their cell's range (positions moved since "
                   "swarm_cell_index)", (unsigned long long)hs[7]);

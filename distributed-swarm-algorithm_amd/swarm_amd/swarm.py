@@ -84,6 +84,12 @@ class AllocResult:
     stats: dict = field(default_factory=dict)
 
 
+def _fast_ptr(t):
+    """Device pointer of a tensor this module made or owns (contiguous, on the right device): no
+    validation (allocate's per-call host cost; user tensors go through _lib.ptr)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
 def take_rows(t: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
     """t[idx] for a 2-D tensor, gathered one column at a time.  On this PyTorch-ROCm build the
     row gathers of an (N, 2) float64 tensor (t[idx], index_select, gather) return wrong rows
@@ -444,14 +450,16 @@ class Swarm:
              else _to(winner, torch.int32, dev).clone())
         u = (torch.zeros(t, dtype=torch.float64, device=dev) if util is None
              else _to(util, torch.float64, dev).clone())
-        # libswarm zeroes won and writes nclaim / nmsg for every task
+        # libswarm zeroes won and writes nclaim / nmsg for every task (one buffer for both)
         won = torch.empty(self.n, dtype=torch.int32, device=dev)
-        nclaim = torch.empty(t, dtype=torch.int64, device=dev)
-        nmsg = torch.empty(t, dtype=torch.int64, device=dev)
+        nc_nm = torch.empty((2, t), dtype=torch.int64, device=dev)
+        nclaim, nmsg = nc_nm[0], nc_nm[1]
         idx = self.id_index()
         st = _lib.AllocStats()
         m = {"auto": _lib.ALLOC_AUTO, "binned": _lib.ALLOC_BINNED, "dense": _lib.ALLOC_DENSE}[mode]
         L = _lib.lib()
+        # every tensor below is this call's or the Swarm's own (contiguous, on dev): raw pointers
+        p = _fast_ptr
         with torch.cuda.device(dev):
             ci = self._cell_index() if self._indexable(mode, claim_thr, u_scale) else None
             rc = _lib.ERR_STALE
@@ -460,10 +468,10 @@ class Swarm:
                 w0 = None if winner is None else w.clone()
                 u0 = None if util is None else u.clone()
                 rc = L.swarm_allocate_indexed(
-                    _lib.ctx(), self.n, _lib.ptr(self.ids), _lib.ptr(self.pos), _lib.ptr(self.caps),
-                    ctypes.byref(ci[0]), _lib.ptr(ci[1]), t, _lib.ptr(tpos), _lib.ptr(tq), float(claim_thr),
-                    float(hysteresis), float(u_scale), _lib.ptr(w), _lib.ptr(u), _lib.ptr(won), _lib.ptr(idx),
-                    0 if idx is None else idx.numel(), _lib.ptr(nclaim), _lib.ptr(nmsg), ctypes.byref(st),
+                    _lib.ctx(), self.n, p(self.ids), p(self.pos), p(self.caps),
+                    ctypes.byref(ci[0]), p(ci[1]), t, p(tpos), p(tq), float(claim_thr),
+                    float(hysteresis), float(u_scale), p(w), p(u), p(won), p(idx),
+                    0 if idx is None else idx.numel(), p(nclaim), p(nmsg), ctypes.byref(st),
                     _lib.stream())
                 if rc == _lib.ERR_STALE:  # positions moved since the index: bin them this call
                     self._cindex = None  # rebuilt next call if they are still in cell order
@@ -473,10 +481,10 @@ class Swarm:
                     _lib.check(rc)
             if rc == _lib.ERR_STALE:
                 _lib.check(L.swarm_allocate(
-                    _lib.ctx(), self.n, _lib.ptr(self.ids), _lib.ptr(self.pos), _lib.ptr(self.caps), t,
-                    _lib.ptr(tpos), _lib.ptr(tq), float(claim_thr), float(hysteresis), float(u_scale), m,
-                    _lib.ptr(w), _lib.ptr(u), _lib.ptr(won), _lib.ptr(idx),
-                    0 if idx is None else idx.numel(), _lib.ptr(nclaim), _lib.ptr(nmsg),
+                    _lib.ctx(), self.n, p(self.ids), p(self.pos), p(self.caps), t,
+                    p(tpos), p(tq), float(claim_thr), float(hysteresis), float(u_scale), m,
+                    p(w), p(u), p(won), p(idx),
+                    0 if idx is None else idx.numel(), p(nclaim), p(nmsg),
                     ctypes.byref(st), _lib.stream()))
         stats = {k: getattr(st, k) for k, _ in _lib.AllocStats._fields_}
         return AllocResult(w, u, won, nclaim, nmsg, stats)
