@@ -45,6 +45,7 @@
 // instead of interleaved edge slices per lane (+14 %), paired / edge-flat / wave-flat / run-unit
 // gathers (+16..66 %).
 #include <algorithm>
+#include <type_traits>
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
@@ -220,6 +221,10 @@ struct Col16 {
     }
 };
 
+// Col16 whose base is 16-byte aligned: the dense rounds read it 8 columns per 16-byte load
+struct Col16A : Col16 {};
+
+
 constexpr int kKm = 8;  // marking re-walks: col loads in flight per lane
 
 // Mark col[k] for k = k0, k0 + step, ... < e with kKm loads in flight per batch.
@@ -277,7 +282,9 @@ __global__ __launch_bounds__(kBlock) void k_elect_dense(
     int32_t *__restrict__ lout, int64_t n, int64_t c_lo, int64_t n_count, unsigned long long *__restrict__ ring,
     unsigned long long *__restrict__ tot, uint8_t *__restrict__ act_w, StampMap sm, int t, int guard,
     const Off *__restrict__ hrp = nullptr, const int32_t *__restrict__ hcol = nullptr) {
-    __shared__ int s_col[kWavesPerBlock][kWin];
+    // VEC: 16-bit columns read 8 per lane with one 16-byte load (FLAT windows start 8-aligned)
+    constexpr bool VEC = FLAT && std::is_same_v<CT, Col16A>;
+    __shared__ __attribute__((aligned(16))) int s_col[kWavesPerBlock][kWin];
     __shared__ unsigned long long s_bc, s_cnt[kWavesPerBlock];
     if (guard && t > 1 && round_total(ring, t - 1, &s_bc) == 0) return;  // converged: no-op
     if (guard || tot) bookkeeping(ring, tot, t);
@@ -297,6 +304,7 @@ __global__ __launch_bounds__(kBlock) void k_elect_dense(
     };
     Off b = 0, e = 0;
     if (task < ntask) bounds(task, b, e);
+    const Off e_all = VEC ? rp[n] : Off(0);  // VEC: a 16-byte load must end inside the column array
     for (; task < ntask; task += stride) {
         const int64_t v = task * 64 + lane;
         const int32_t tbase = int32_t(task * 64);  // Col16 deltas are relative to the task's first agent
@@ -306,9 +314,48 @@ __global__ __launch_bounds__(kBlock) void k_elect_dense(
         Off nb = 0, ne = 0;
         if (task + stride < ntask) bounds(task + stride, nb, ne);  // wave-uniform branch
         int m = INT_MIN;
-        for (Off w0 = W0; w0 < W1; w0 += kWin) {
+        for (Off w0 = VEC ? (W0 & ~Off(7)) : W0; w0 < W1; w0 += kWin) {
             const Off wend = (W1 - w0 < kWin) ? W1 : w0 + kWin;
-            if constexpr (FLAT) {
+            if constexpr (VEC) {
+                // the window's columns 8 per lane (one 16-byte load: an eighth of the column load
+                // instructions of the 64-lane form -- the round is bound by the texture unit's cost
+                // per instruction), their leaders gathered and stored to LDS 4 per store; slots
+                // outside [W0, wend) (the 8-alignment prefix, the next task's edges) read agent tbase
+#pragma unroll 1
+                for (int h = 0; h < 2; ++h) {
+                    const Off kb = w0 + h * (kWin / 2) + lane * 8;
+                    int c[8];
+                    if (kb + 8 <= e_all) {
+                        const int4 q = *reinterpret_cast<const int4 *>(cols.p + kb);
+                        const int w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            c[2 * i] = tbase + int32_t(int16_t(w[i] & 0xffff));
+                            c[2 * i + 1] = tbase + (w[i] >> 16);
+                        }
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) {
+                            const Off k = kb + i;
+                            c[i] = cols.at(k < e_all ? k : e_all - 1, tbase);
+                        }
+                    }
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const Off k = kb + i;
+                        if (!(k >= W0 && k < wend)) c[i] = tbase;
+                    }
+                    int val[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) val[i] = lin[c[i]];
+                    int4 *dst = reinterpret_cast<int4 *>(sc + h * (kWin / 2) + lane * 8);
+                    dst[0] = make_int4(val[0], val[1], val[2], val[3]);
+                    dst[1] = make_int4(val[4], val[5], val[6], val[7]);
+                }
+                __builtin_amdgcn_wave_barrier();
+                const Off lo = b > w0 ? b : w0, hi = e < wend ? e : wend;
+                for (Off k = lo; k < hi; ++k) m = max(m, sc[k - w0]);
+            } else if constexpr (FLAT) {
                 // flat: the window's columns AND their leaders, 64 consecutive edges per load (the
                 // neighbours of ~4 consecutive agents: few cache lines per instruction), leaders
                 // into LDS, each lane then maxes its own row from LDS
@@ -781,6 +828,7 @@ struct Tuning {
     int small_chunks = 512;   // fewer 2048-agent chunks than this: 512-agent chunks instead
     int stamp_bshift = 5;     // log2 of the stamp layout's block (stamp_slot)
     int dense_flat = 1;       // dense rounds gather leaders 64 consecutive edges per load (FLAT)
+    int dense_vec = 1;        // FLAT with 16-bit columns: 8 columns per lane per 16-byte load
     int use_c16 = 1;          // swarm_elect_compact reads the 16-bit columns (0: its int32 ones; A/B aid)
     int il_min_changes = -1;   // interleaved stamp layout while the last read round changed >= this
                                // (-1: 8e-4 x agents, measured best at 100k, 1M and 10M agents)
@@ -800,6 +848,7 @@ struct Tuning {
         il_min_changes = env_int("SWARM_IL_MIN_CHANGES", -1);
         use_c16 = env_int("SWARM_C16", 1);
         dense_flat = env_int("SWARM_DENSE_FLAT", 1);
+        dense_vec = env_int("SWARM_DENSE_VEC", 1);
         stamp_bshift = env_int("SWARM_STAMP_BSHIFT", 5);
         dense_blocks = env_int("SWARM_DENSE_BLOCKS", 2048);
         dense_rounds = env_int("SWARM_DENSE_ROUNDS", 9);
@@ -849,7 +898,16 @@ int launch_dense_round(const Off *rp, const int32_t *col, const int32_t *lin, in
     const Col32 c32{col};
     if (!hrp && sizeof(Off) == 4 && tuning().dense_flat && c16) {
         const Col16 cc{c16};
-        if (act_w)
+        Col16A ca;
+        ca.p = c16;
+        const bool vec = tuning().dense_vec && (reinterpret_cast<uintptr_t>(c16) & 15) == 0;
+        if (act_w && vec)
+            hipLaunchKernelGGL((k_elect_dense<Off, true, false, true, Col16A>), dim3(grid), dim3(kBlock), 0, s, rp, ca,
+                               lin, lout, n, c_lo, n_count, ring, tot, act_w, sm, t, guard, nullptr, nullptr);
+        else if (vec)
+            hipLaunchKernelGGL((k_elect_dense<Off, false, false, true, Col16A>), dim3(grid), dim3(kBlock), 0, s, rp, ca,
+                               lin, lout, n, c_lo, n_count, ring, tot, act_w, sm, t, guard, nullptr, nullptr);
+        else if (act_w)
             hipLaunchKernelGGL((k_elect_dense<Off, true, false, true, Col16>), dim3(grid), dim3(kBlock), 0, s, rp, cc,
                                lin, lout, n, c_lo, n_count, ring, tot, act_w, sm, t, guard, nullptr, nullptr);
         else
