@@ -1,4 +1,4 @@
-"""Per-round-range kernel durations of the last election in a rocprofv3 kernel trace
+"""Per-round-range kernel durations of the longest election in a rocprofv3 kernel trace
 (tools/trace_ab.sh): rounds are the k_elect_dense / k_sparse_block / k_list_round dispatches in order.
 Usage: python tools/trace_ranges.py TRACE.csv [LABEL]"""
 import csv
@@ -19,7 +19,7 @@ for k in ks:
     cur.append(k)
     prev_sparse = not dense
 elections.append(cur)
-e = elections[-1]
+e = max(elections, key=len)  # the longest election (the C3 one in a bench trace)
 d = np.array([b - a for a, b, _ in e]) / 1e3
 span = (e[-1][1] - e[0][0]) / 1e6
 label = sys.argv[2] if len(sys.argv) > 2 else ""
