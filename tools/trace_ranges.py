@@ -9,7 +9,7 @@ import numpy as np
 rows = list(csv.DictReader(open(sys.argv[1])))
 ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows
             if "k_elect_dense" in r["Kernel_Name"] or "k_sparse_block" in r["Kernel_Name"]
-            or "k_list_round" in r["Kernel_Name"])
+            or "k_list_round" in r["Kernel_Name"] or "k_task_round" in r["Kernel_Name"])
 elections, cur, prev_sparse = [], [], False
 for k in ks:
     dense = "k_elect_dense" in k[2]
