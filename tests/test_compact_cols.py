@@ -106,3 +106,36 @@ def test_elect_compact_null_is_int32_path(sw, oracle_mod):
     assert rounds.value == o_rounds
     np.testing.assert_array_equal(lead.cpu().numpy(), o_lead)
     np.testing.assert_array_equal(state.cpu().numpy(), o_state)
+
+
+@pytest.mark.parametrize("offset", [0, 1, 4, 8])
+def test_elect_compact_any_column_alignment(sw, oracle_mod, offset):
+    """The dense rounds read 16-byte aligned 16-bit columns 8 per lane (Col16A); a column array
+    that is not 16-byte aligned (a view 2, 8 or 16 bytes into a buffer) takes the 2-byte loads.
+    Both through the C-ABI, same results as the oracle (including the array's last rows, whose
+    16-byte groups run past the end and are read one column at a time)."""
+    from swarm_amd import _lib, gen
+    d = gen.swarm_inputs(150_000, 61 + offset)
+    s = sw.Swarm(d["ids"], d["x"], d["y"], device="cuda").build_graph(1.0)
+    c = s.graph_compact()
+    assert c is not None
+    buf = torch.empty(c.numel() + 16, dtype=torch.int16, device=c.device)
+    view = buf[offset:offset + c.numel()]
+    view.copy_(c)
+    lead, state, rounds, changes = oracle_mod.elect(s.row_ptr.cpu().numpy(), s.col.cpu().numpy(),
+                                                    s.ids.cpu().numpy())
+    n = s.n
+    leader = torch.empty(n, dtype=torch.int32, device=c.device)
+    st = torch.empty(n, dtype=torch.uint8, device=c.device)
+    got = np.zeros(1 << 16, np.int64)
+    rx = ctypes.c_int32(0)
+    for mode in (_lib.ELECT_FRONTIER, _lib.ELECT_DENSE):
+        _lib.check(_lib.lib().swarm_elect_compact(
+            _lib.ctx(), n, _lib.ptr(s.row_ptr), _lib.ptr(s.col), _lib.ptr(view), _lib.ptr(s.ids),
+            _lib.ptr(leader), _lib.ptr(st), 1 << 16, mode, ctypes.byref(rx),
+            got.ctypes.data_as(ctypes.c_void_p), None, _lib.stream()))
+        torch.cuda.synchronize()
+        assert rx.value == rounds
+        np.testing.assert_array_equal(got[:rounds], changes)
+        np.testing.assert_array_equal(leader.cpu().numpy(), lead)
+        np.testing.assert_array_equal(st.cpu().numpy(), state)
