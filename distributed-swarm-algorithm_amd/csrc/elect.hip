@@ -832,19 +832,7 @@ struct Tuning {
     int use_c16 = 1;          // swarm_elect_compact reads the 16-bit columns (0: its int32 ones; A/B aid)
     int il_min_changes = -1;   // interleaved stamp layout while the last read round changed >= this
                                // (-1: 8e-4 x agents, measured best at 100k, 1M and 10M agents)
-    int64_t tile_min_changes = 0;  // swarm_elect_tiled: tiled rounds once a read round changed fewer than
-                                   // this (0: never -- measured slower than the sparse rounds)
-    int64_t rec_min_changes = -1;  // swarm_elect_records: record tail once a read round changed fewer than this
-                                   // (-1: 0.006 x agents)
-    int rec_delta = 8;             // record tail: rounds admitted per launch (the window, records.hip)
-    int rec_grid = 0;              // record tail: workgroups (one wave, one tile at a time) per launch (0: 2 per CU)
-    int rec_batch = 8;             // record tail: launches per host check of the tile count
     Tuning() {
-        if (const char *e = getenv("SWARM_TILE_MIN_CHANGES")) tile_min_changes = atoll(e);
-        if (const char *e = getenv("SWARM_REC_MIN_CHANGES")) rec_min_changes = atoll(e);
-        rec_delta = env_int("SWARM_REC_DELTA", 8);
-        rec_grid = env_int("SWARM_REC_GRID", 0);
-        rec_batch = env_int("SWARM_REC_BATCH", 8);
         il_min_changes = env_int("SWARM_IL_MIN_CHANGES", -1);
         use_c16 = env_int("SWARM_C16", 1);
         dense_flat = env_int("SWARM_DENSE_FLAT", 1);
@@ -1032,472 +1020,18 @@ double round_bytes(bool dense, int64_t n, int64_t e, int64_t active, int64_t edg
     return double(n) + 16.0 * active + 8.0 * edges;
 }
 
-// ------------------------------------------------------------------ tiled rounds (the tail)
-// Late in an election the changes sit on a few thin fronts, and a sparse round costs its fixed
-// latency chain (kernel boundary, stamp words, list, row bounds, columns, leaders: ~9 us at 10M
-// agents) for a few thousand changes.  The tiled rounds run kTileHalo rounds per launch instead:
-// the cell grid of the storage order (swarm_cell_index) is cut into tiles of kTileCore x kTileCore
-// cells; a workgroup takes one ACTIVE tile, loads its region -- the core plus kTileHalo cells on
-// every side -- into LDS (leaders, and each region agent's neighbours as region-local slots), and
-// runs the rounds there, Jacobi, one workgroup barrier per round.  Exact by the deep-halo argument
-// (dist.py): an edge joins cells at most one apart (swarm_tile_index checks), so a core agent's
-// value after j <= kTileHalo rounds depends only on agents within j cells -- all in the region --
-// and region agents whose neighbourhood is cut off by the region's edge are wrong only at
-// distances the core never reads within those rounds.  Only core agents are counted and written.
-// A tile is active in a launch iff an agent that changed in the previous launch's LAST round lies
-// within kTileHalo cells of its core (a change in round t+s needs a chain of changes back to a
-// neighbour of round t, s hops away), or it changed anything in the previous launch (so both leader
-// buffers agree on every tile that is left alone).  Marks are byte flags per tile; k_tile_list
-// compacts them into the next launch's list.
-constexpr int kTileCore = 16;                               // core cells per tile side
-constexpr int kTileHalo = 4;                                // halo cells = rounds per launch
-constexpr int kTileThreads = 1024;
-constexpr int kTileWaves = kTileThreads / kWave;
-constexpr int kTileRowsMax = kTileCore + 2 * kTileHalo;     // region cell rows
-constexpr int kTileCap = 3584;                              // region agents held in LDS
-constexpr int kTileECap = 57344;                            // region edges held in LDS (u16 slots)
-constexpr uint16_t kTileOut = 0xFFFF;                       // a neighbour outside the region
-
-struct TileGeom {
-    const uint32_t *cell_off;  // cell c = cy * ncx + cx holds storage indices [cell_off[c], cell_off[c + 1])
-    const int32_t *acell;      // each agent's cell
-    int64_t ncx, ncy, ntx, nty;
-};
-
-struct TileLaunch {
-    const int32_t *list;        // tiles of this launch
-    const uint32_t *count;      // how many (device)
-    uint8_t *flags;             // tiles of the next launch (set here)
-    const int32_t *Gin;         // state after round t0
-    int32_t *Gout;              // state after round t0 + k (core agents of the listed tiles)
-    unsigned long long *ring;
-    unsigned *err;              // set when a region exceeds the LDS capacity
-    int t0, k;
-    unsigned long long *dbg;    // SWARM_TILE_DEBUG: per-workgroup phase clocks of its first tile, or NULL
-};
-
-__device__ __forceinline__ void mark_tiles_around(uint8_t *flags, const TileGeom &g, int32_t cell) {
-    const int64_t cx = cell % g.ncx, cy = cell / g.ncx;
-    const int64_t x0 = (cx > kTileHalo ? cx - kTileHalo : 0) / kTileCore;
-    const int64_t x1 = (cx + kTileHalo < g.ncx ? cx + kTileHalo : g.ncx - 1) / kTileCore;
-    const int64_t y0 = (cy > kTileHalo ? cy - kTileHalo : 0) / kTileCore;
-    const int64_t y1 = (cy + kTileHalo < g.ncy ? cy + kTileHalo : g.ncy - 1) / kTileCore;
-    for (int64_t ty = y0; ty <= y1; ++ty)
-        for (int64_t tx = x0; tx <= x1; ++tx) flags[ty * g.ntx + tx] = 1;
-}
-
-// The tiles a switch to tiled rounds starts with: every agent marked for round t (the stamps the
-// last sparse round wrote) flags the tiles within kTileHalo cells of it.  Stale stamps only flag
-// more tiles (more work, same results).
-__global__ __launch_bounds__(kBlock) void k_tile_flags_from_marks(const uint8_t *__restrict__ act, StampMap sm,
-                                                                 uint8_t stamp, int64_t n, TileGeom g,
-                                                                 uint8_t *__restrict__ flags) {
-    const int64_t slots = int64_t(sm.M) << sm.cshift;
-    for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < slots; j += int64_t(gridDim.x) * kBlock) {
-        if (act[j] != stamp) continue;
-        const int64_t v = stamp_agent(sm, j >> sm.cshift, int(j & ((int64_t(1) << sm.cshift) - 1)));
-        if (v < n) mark_tiles_around(flags, g, g.acell[v]);
-    }
-}
-
-// One workgroup: flags -> list (+ count), flags cleared; ring slots of rounds r0..r1 + kRing/2 zeroed
-// (the sparse rounds' bookkeeping, for the rounds this launch stands for).
-__global__ __launch_bounds__(kTileThreads) void k_tile_list(uint8_t *__restrict__ flags, int64_t ntiles,
-                                                           int32_t *__restrict__ list, uint32_t *__restrict__ count,
-                                                           unsigned long long *__restrict__ ring, int r0, int r1) {
-    __shared__ unsigned s_w[kTileWaves];
-    __shared__ unsigned s_base;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int r = r0; r <= r1; ++r)
-        for (int i = threadIdx.x; i < kCounters * kShards; i += kTileThreads)
-            *slot(ring, r + kRing / 2, i / kShards, i % kShards) = 0;
-    if (threadIdx.x == 0) s_base = 0;
-    __syncthreads();
-    for (int64_t c0 = 0; c0 < ntiles; c0 += kTileThreads) {
-        const int64_t i = c0 + threadIdx.x;
-        const bool f = i < ntiles && flags[i] != 0;
-        if (f) flags[i] = 0;
-        const unsigned long long b = __ballot(f);
-        const unsigned below = unsigned(__popcll(b & ((1ull << lane) - 1ull)));
-        if (lane == 0) s_w[wid] = unsigned(__popcll(b));
-        __syncthreads();
-        unsigned off = s_base, tot = 0;
-        for (int w = 0; w < kTileWaves; ++w) {
-            off += w < wid ? s_w[w] : 0;
-            tot += s_w[w];
-        }
-        if (f) list[off + below] = int32_t(i);
-        __syncthreads();
-        if (threadIdx.x == 0) s_base += tot;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) *count = s_base;
-}
-
-// region row of region slot l: base[r] <= l < base[r + 1]
-__device__ __forceinline__ int tile_row_of(const int32_t *base, int nrows, int l) {
-    int lo = 0, hi = nrows - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (base[mid] <= l) lo = mid; else hi = mid - 1;
-    }
-    return lo;
-}
-
-#define TILE_PHASE(k)                                                                         \
-    do {                                                                                      \
-        if (L.dbg && tid == 0 && li == blockIdx.x) L.dbg[blockIdx.x * 8 + (k)] = wall_clock64(); \
-    } while (0)
-
-__global__ __launch_bounds__(kTileThreads, 1) void k_tile_rounds(const int32_t *__restrict__ rp,
-                                                                const int32_t *__restrict__ col, TileGeom g,
-                                                                TileLaunch L) {
-    __shared__ int32_t sA[kTileCap];
-    __shared__ int32_t sB[kTileCap];
-    __shared__ int32_t sR[kTileCap + 1];   // loading: global row starts; rounds: region row pointers
-    __shared__ uint16_t sD[kTileECap];     // region neighbour slots (kTileOut: outside the region)
-    __shared__ int32_t s_start[kTileRowsMax], s_len[kTileRowsMax], s_base[kTileRowsMax + 1];
-    __shared__ int32_t s_clo[kTileRowsMax], s_chi[kTileRowsMax];
-    __shared__ uint32_t s_core[(kTileCap + 31) / 32];
-    __shared__ unsigned s_cnt[kTileHalo];
-    __shared__ unsigned s_misc[4];         // [0] core agents, [1] their edges, [2] region edges
-    __shared__ int32_t s_scan[kTileWaves];
-    __shared__ int32_t s_le0[kTileRowsMax + 1], s_e0[kTileRowsMax];  // per row segment: local / global first edge
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, sub = tid & 3;
-    const unsigned nt = *L.count;
-    for (unsigned li = blockIdx.x; li < nt; li += gridDim.x) {
-        const int64_t tile = L.list[li];
-        const int64_t tx = tile % g.ntx, ty = tile / g.ntx;
-        const int64_t x0c = tx * kTileCore, x1c = x0c + kTileCore < g.ncx ? x0c + kTileCore : g.ncx;
-        const int64_t y0c = ty * kTileCore, y1c = y0c + kTileCore < g.ncy ? y0c + kTileCore : g.ncy;
-        const int64_t rx0 = x0c > kTileHalo ? x0c - kTileHalo : 0, rx1 = x1c + kTileHalo < g.ncx ? x1c + kTileHalo : g.ncx;
-        const int64_t ry0 = y0c > kTileHalo ? y0c - kTileHalo : 0, ry1 = y1c + kTileHalo < g.ncy ? y1c + kTileHalo : g.ncy;
-        const int nrows = int(ry1 - ry0);
-        TILE_PHASE(0);
-        // (a) the region's row segments: every grid row of the region is ONE contiguous storage range
-        if (wid == 0) {
-            int len = 0;
-            if (lane < nrows) {
-                const int64_t y = ry0 + lane;
-                const int32_t st = int32_t(g.cell_off[y * g.ncx + rx0]);
-                len = int32_t(g.cell_off[y * g.ncx + rx1]) - st;
-                s_start[lane] = st;
-                s_len[lane] = len;
-                const bool core = y >= y0c && y < y1c;
-                s_clo[lane] = core ? int32_t(g.cell_off[y * g.ncx + x0c]) : 0;
-                s_chi[lane] = core ? int32_t(g.cell_off[y * g.ncx + x1c]) : 0;
-            }
-            int incl = len;
-#pragma unroll
-            for (int o = 1; o < 32; o <<= 1) {
-                const int x = __shfl_up(incl, o, 64);
-                if (lane >= o) incl += x;
-            }
-            if (lane < nrows) s_base[lane + 1] = incl;
-            if (lane == 0) s_base[0] = 0;
-        }
-        if (tid < (kTileCap + 31) / 32) s_core[tid] = 0;
-        if (tid < kTileHalo) s_cnt[tid] = 0;
-        if (tid < 4) s_misc[tid] = 0;
-        __syncthreads();
-        const int nr = s_base[nrows];
-        if (nr > kTileCap) {  // swarm_tile_index bounds every region: never taken with a valid index
-            if (tid == 0) atomicOr(L.err, 1u);
-            __syncthreads();
-            continue;
-        }
-        TILE_PHASE(1);
-        // (b) leaders after round t0, global row starts, degrees, core membership: a thread's (up to)
-        // four agents' loads all in flight at once
-        unsigned my_core = 0, my_cedges = 0;
-        {
-            constexpr int kAg = (kTileCap + kTileThreads - 1) / kTileThreads;
-            int32_t vv[kAg], a[kAg], b[kAg], e[kAg];
-            bool core[kAg];
-#pragma unroll
-            for (int j = 0; j < kAg; ++j) {
-                const int l = tid + j * kTileThreads;
-                const int r = tile_row_of(s_base, nrows, l < nr ? l : 0);
-                vv[j] = l < nr ? s_start[r] + (l - s_base[r]) : s_start[r];
-                core[j] = l < nr && vv[j] >= s_clo[r] && vv[j] < s_chi[r];
-            }
-#pragma unroll
-            for (int j = 0; j < kAg; ++j) {
-                a[j] = L.Gin[vv[j]];
-                b[j] = rp[vv[j]];
-                e[j] = rp[vv[j] + 1];
-            }
-#pragma unroll
-            for (int j = 0; j < kAg; ++j) {
-                const int l = tid + j * kTileThreads;
-                if (l < nr) {
-                    sA[l] = a[j];
-                    sR[l] = b[j];
-                    sB[l] = e[j] - b[j];
-                    if (core[j]) {
-                        atomicOr(&s_core[l >> 5], 1u << (l & 31));
-                        ++my_core;
-                        my_cedges += unsigned(e[j] - b[j]);
-                    }
-                }
-            }
-        }
-        __syncthreads();
-        TILE_PHASE(2);
-        // (c) exclusive scan of the degrees (4 consecutive slots per thread) -> region row pointers
-        {
-            int loc[4], sum = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int idx = tid * 4 + j;
-                loc[j] = idx < nr ? sB[idx] : 0;
-                sum += loc[j];
-            }
-            int incl = sum;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int x = __shfl_up(incl, o, 64);
-                if (lane >= o) incl += x;
-            }
-            if (lane == 63) s_scan[wid] = incl;
-            __syncthreads();
-            int before = 0, total = 0;
-            for (int w = 0; w < kTileWaves; ++w) {
-                before += w < wid ? s_scan[w] : 0;
-                total += s_scan[w];
-            }
-            int run = before + incl - sum;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int idx = tid * 4 + j;
-                if (idx < nr) sB[idx] = run;
-                run += loc[j];
-            }
-            if (tid == 0) s_misc[2] = unsigned(total);
-        }
-        __syncthreads();
-        const int ne = int(s_misc[2]);
-        if (ne > kTileECap) {
-            if (tid == 0) atomicOr(L.err, 2u);
-            __syncthreads();
-            continue;
-        }
-        TILE_PHASE(3);
-        // (d) neighbours as region slots.  A row segment's agents are consecutive storage indices, so
-        // their CSR rows are ONE contiguous range of col, and contiguous in the region's edge list
-        // too: the region's edges are copied flat (thread T takes edges T, T + 1024, ...), kTileEB
-        // column loads in flight per thread, then each column is turned into a region slot (its
-        // agent's cell row is the segment's row +-1).
-        if (tid < nrows) {
-            const int f = s_base[tid];
-            s_le0[tid] = f < nr ? sB[f] : ne;
-            s_e0[tid] = f < nr ? sR[f] : 0;
-        }
-        if (tid == 0) s_le0[nrows] = ne;
-        __syncthreads();
-        {
-            constexpr int kTileEB = 14;
-            for (int e0 = tid; e0 < ne; e0 += kTileEB * kTileThreads) {
-                int32_t u[kTileEB];
-                int rw[kTileEB];
-#pragma unroll
-                for (int i = 0; i < kTileEB; ++i) {
-                    const int e = e0 + i * kTileThreads;
-                    const int r = tile_row_of(s_le0, nrows, e < ne ? e : ne - 1);
-                    rw[i] = r;
-                    u[i] = col[s_e0[r] + ((e < ne ? e : ne - 1) - s_le0[r])];
-                }
-#pragma unroll
-                for (int i = 0; i < kTileEB; ++i) {
-                    const int e = e0 + i * kTileThreads;
-                    if (e >= ne) break;
-                    const int r = rw[i];
-                    const int ra = r > 0 ? r - 1 : 0, rb = r + 1 < nrows ? r + 1 : nrows - 1;
-                    uint16_t d = kTileOut;
-                    for (int rr = ra; rr <= rb; ++rr) {
-                        const uint32_t off = uint32_t(u[i] - s_start[rr]);
-                        if (off < uint32_t(s_len[rr])) d = uint16_t(s_base[rr] + int32_t(off));
-                    }
-                    sD[e] = d;
-                }
-            }
-        }
-        __syncthreads();
-        for (int l = tid; l <= nr; l += kTileThreads) sR[l] = l < nr ? sB[l] : ne;
-        __syncthreads();
-        TILE_PHASE(4);
-        // (e) the rounds: Jacobi over the region, one barrier per round
-        int32_t *cur = sA, *nxt = sB;
-        for (int j = 0; j < L.k; ++j) {
-            unsigned chg = 0;
-            for (int l = tid >> 2; l < nr; l += kTileThreads / 4) {  // the 4 lanes of a quad share l
-                const int own = cur[l];
-                int m = own;
-                const int eb = sR[l], ee = sR[l + 1];
-                for (int e = eb + sub; e < ee; e += 4 * 6) {  // 6 slots, then their 6 leaders, in flight
-                    uint16_t d[6];
-#pragma unroll
-                    for (int i = 0; i < 6; ++i) d[i] = e + 4 * i < ee ? sD[e + 4 * i] : kTileOut;
-#pragma unroll
-                    for (int i = 0; i < 6; ++i)
-                        if (d[i] != kTileOut) m = max(m, cur[d[i]]);
-                }
-                m = group_max<4>(m);
-                if (sub == 0) {
-                    nxt[l] = m;
-                    if (m > own && ((s_core[l >> 5] >> (l & 31)) & 1u)) {
-                        ++chg;
-                        if (j == L.k - 1) {  // a change of the launch's last round: the next launch's tiles
-                            const int r = tile_row_of(s_base, nrows, l);
-                            mark_tiles_around(L.flags, g, g.acell[s_start[r] + (l - s_base[r])]);
-                        }
-                    }
-                }
-            }
-            const int c = wave_sum(int(chg));
-            if (lane == 0 && c) atomicAdd(&s_cnt[j], unsigned(c));
-            __syncthreads();
-            int32_t *tmp = cur;
-            cur = nxt;
-            nxt = tmp;
-        }
-        TILE_PHASE(5);
-        // (f) core agents' values after round t0 + k; counters; the tile itself next time if it changed
-        for (int l = tid; l < nr; l += kTileThreads)
-            if ((s_core[l >> 5] >> (l & 31)) & 1u) {
-                const int r = tile_row_of(s_base, nrows, l);
-                L.Gout[s_start[r] + (l - s_base[r])] = cur[l];
-            }
-        const int cc = wave_sum(int(my_core)), ce = wave_sum(int(my_cedges));
-        if (lane == 0) {
-            if (cc) atomicAdd(&s_misc[0], unsigned(cc));
-            if (ce) atomicAdd(&s_misc[1], unsigned(ce));
-        }
-        __syncthreads();
-        if (tid < L.k) {
-            const int shard = int(tile & (kShards - 1));
-            if (s_cnt[tid]) atomicAdd(slot(L.ring, L.t0 + 1 + tid, C_CHG, shard), (unsigned long long)s_cnt[tid]);
-            if (s_misc[0]) atomicAdd(slot(L.ring, L.t0 + 1 + tid, C_ACT, shard), (unsigned long long)s_misc[0]);
-            if (s_misc[1]) atomicAdd(slot(L.ring, L.t0 + 1 + tid, C_EDGE, shard), (unsigned long long)s_misc[1]);
-        }
-        if (tid == 0) {
-            unsigned any = 0;
-            for (int j = 0; j < L.k; ++j) any |= s_cnt[j];
-            if (any) L.flags[tile] = 1;
-        }
-        __syncthreads();  // LDS reused by the next tile
-        TILE_PHASE(6);
-        if (L.dbg && tid == 0 && li == blockIdx.x) {
-            L.dbg[blockIdx.x * 8 + 7] = (unsigned long long)nr | ((unsigned long long)ne << 32);
-        }
-    }
-}
-
-// swarm_tile_index: acell (per agent: its cell) from the cell offsets
-__global__ __launch_bounds__(kBlock) void k_tile_acell(const uint32_t *__restrict__ off, int64_t ncells,
-                                                      int32_t *__restrict__ acell) {
-    for (int64_t c = int64_t(blockIdx.x) * kBlock + threadIdx.x; c < ncells; c += int64_t(gridDim.x) * kBlock)
-        for (uint32_t v = off[c]; v < off[c + 1]; ++v) acell[v] = int32_t(c);
-}
-
-// every edge joins cells at most one apart in x and in y (else *bad += 1)
-__global__ __launch_bounds__(kBlock) void k_tile_local(const int32_t *__restrict__ rp, const int32_t *__restrict__ col,
-                                                      const int32_t *__restrict__ acell, int64_t n, int64_t ncx,
-                                                      unsigned long long *__restrict__ bad) {
-    unsigned long long b = 0;
-    for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < n; v += int64_t(gridDim.x) * kBlock) {
-        const int32_t cv = acell[v];
-        const int64_t vx = cv % ncx, vy = cv / ncx;
-        for (int32_t k = rp[v]; k < rp[v + 1]; ++k) {
-            const int32_t u = col[k];
-            if (u < 0 || u >= n) {
-                ++b;
-                continue;
-            }
-            const int32_t cu = acell[u];
-            const int64_t dx = cu % ncx - vx, dy = cu / ncx - vy;
-            b += (dx < -1 || dx > 1 || dy < -1 || dy > 1) ? 1 : 0;
-        }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) b += __shfl_xor(b, o, 64);
-    if ((threadIdx.x & 63) == 0 && b) atomicAdd(bad, b);
-}
-
-// the largest region (agents, edges) over all tiles
-__global__ __launch_bounds__(kBlock) void k_tile_regions(const uint32_t *__restrict__ off, const int32_t *__restrict__ rp,
-                                                        TileGeom g, unsigned long long *__restrict__ mx) {
-    unsigned long long ma = 0, me = 0;
-    for (int64_t tile = int64_t(blockIdx.x) * kBlock + threadIdx.x; tile < g.ntx * g.nty;
-         tile += int64_t(gridDim.x) * kBlock) {
-        const int64_t tx = tile % g.ntx, ty = tile / g.ntx;
-        const int64_t x0c = tx * kTileCore, x1c = x0c + kTileCore < g.ncx ? x0c + kTileCore : g.ncx;
-        const int64_t y0c = ty * kTileCore, y1c = y0c + kTileCore < g.ncy ? y0c + kTileCore : g.ncy;
-        const int64_t rx0 = x0c > kTileHalo ? x0c - kTileHalo : 0, rx1 = x1c + kTileHalo < g.ncx ? x1c + kTileHalo : g.ncx;
-        const int64_t ry0 = y0c > kTileHalo ? y0c - kTileHalo : 0, ry1 = y1c + kTileHalo < g.ncy ? y1c + kTileHalo : g.ncy;
-        unsigned long long a = 0, e = 0;
-        for (int64_t y = ry0; y < ry1; ++y) {
-            const uint32_t s0 = off[y * g.ncx + rx0], s1 = off[y * g.ncx + rx1];
-            a += s1 - s0;
-            e += uint64_t(rp[s1] - rp[s0]);
-        }
-        ma = a > ma ? a : ma;
-        me = e > me ? e : me;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long x = __shfl_xor(ma, o, 64), y = __shfl_xor(me, o, 64);
-        ma = x > ma ? x : ma;
-        me = y > me ? y : me;
-    }
-    if ((threadIdx.x & 63) == 0) {
-        atomicMax(mx, ma);
-        atomicMax(mx + 1, me);
-    }
-}
-
-// ------------------------------------------------------------------ record tail (records.hip)
-// The first launch of a record tail: every agent marked for round t (the stamps the last sparse
-// round wrote, layout sm) is marked for launch 1 and its tile flagged (the first flagger appends
-// the tile to launch 1's list).  Stale stamps only mark more agents (more work, same results).
-__global__ __launch_bounds__(kBlock) void k_rec_marks(const uint8_t *__restrict__ act, StampMap sm, uint8_t stamp,
-                                                     int64_t n, const int32_t *__restrict__ acell, int64_t ncx,
-                                                     int64_t ntx, uint32_t tag, uint32_t *__restrict__ gmark,
-                                                     uint32_t *__restrict__ tflag, int32_t *__restrict__ tlist,
-                                                     uint32_t *__restrict__ tcnt) {
-    const int64_t slots = int64_t(sm.M) << sm.cshift;
-    for (int64_t j = int64_t(blockIdx.x) * kBlock + threadIdx.x; j < slots; j += int64_t(gridDim.x) * kBlock) {
-        if (act[j] != stamp) continue;
-        const int64_t v = stamp_agent(sm, j >> sm.cshift, int(j & ((int64_t(1) << sm.cshift) - 1)));
-        if (v >= n) continue;
-        gmark[v] = tag;
-        const int64_t c = acell[v];
-        const int64_t tile = (c / ncx) / kRecTile * ntx + (c % ncx) / kRecTile;
-        const uint32_t old = atomicMax(&tflag[tile], tag);
-        if (old < tag) tlist[atomicAdd(&tcnt[1], 1u)] = int32_t(tile);
-    }
-}
-
-struct RecArg {  // swarm_elect_records: the record index of this graph and its cell grid
-    const void *index;
-    int64_t ncx, ncy;
-    const int32_t *acell;
-};
-
 template <typename Off>
 int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, const int32_t *ids,
                int32_t *leader, uint8_t *state, int32_t max_rounds, int32_t mode,
                int32_t *rounds_exec, int64_t *changes_host, swarm_elect_stats *st,
                void *stream, const Off *hrp = nullptr, const int32_t *hcol = nullptr,
-               const int16_t *c16 = nullptr, const TileGeom *tg = nullptr, const RecArg *rec = nullptr) {
+               const int16_t *c16 = nullptr) {
     SW_ARG(ctx != nullptr, "ctx is NULL");
     SW_ARG(n >= 0, "n < 0");
     SW_ARG(n < (int64_t(1) << 31), "n must be < 2^31");
     SW_ARG(max_rounds >= 1, "max_rounds < 1");
     const bool timed = (mode & SWARM_ELECT_TIMED) != 0;
-    const bool tiles_early = (mode & SWARM_ELECT_TILES_EARLY) != 0;
-    const bool rec_early = (mode & SWARM_ELECT_RECORDS_EARLY) != 0;
-    mode &= ~(SWARM_ELECT_TIMED | SWARM_ELECT_TILES_EARLY | SWARM_ELECT_RECORDS_EARLY);
+    mode &= ~SWARM_ELECT_TIMED;
     SW_ARG(mode == SWARM_ELECT_DENSE || mode == SWARM_ELECT_FRONTIER, "unknown mode");
     SW_ARG(rounds_exec != nullptr, "rounds_exec is NULL");
     SW_ARG(n == 0 || (rp && ids && leader && state), "NULL array (col may be NULL only without edges)");
@@ -1587,36 +1121,14 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         ~EvReadFree() { (void)hipEventDestroy(e); }
     } ev_read_free{ev_read};
     int read_upto = 0;  // rounds whose counters the host has read
-    // tiled rounds (the tail, tg != NULL): from round tile_from on, launches of up to kTileHalo rounds
-    int tile_from = INT_MAX, tile_cur = 0, tile_launches = 0;
-    double tile_ms = 0.0, tile_bytes = 0.0;
-    int64_t tile_rounds = 0;
-    uint8_t *tflags = nullptr;
-    int32_t *tlist = nullptr;
-    uint32_t *tcount = nullptr;
-    unsigned *terr = nullptr;
-    unsigned long long *tdbg = nullptr;  // SWARM_TILE_DEBUG
-    std::vector<double> tdbg_sum(8, 0.0);
-    int64_t tdbg_n = 0;
-    int tgrid = 0;
-    const int64_t tile_min = !tg ? -1 : tiles_early ? INT64_MAX : tuning().tile_min_changes;
-    // record tail (rec != NULL): from the first batch boundary at which the last read round changed
-    // fewer than rec_min agents, the remaining rounds as record lists (records.hip)
-    const int64_t rec_min = !rec ? -1
-                            : rec_early ? INT64_MAX
-                            : tuning().rec_min_changes >= 0 ? tuning().rec_min_changes
-                                                            : std::max<int64_t>(1, int64_t(0.006 * double(n)));
-    bool rec_tried = false, rec_used = false;
-    RecTail rt;
     // the per-round counters of rounds (read_upto, tread], read back into hbuf: hist, stats, found
     auto consume = [&](int tread) {
         for (int r = read_upto + 1; r <= tread; ++r) {
             const unsigned long long *rb = hbuf + size_t(r - read_upto - 1) * kCounters;
             const int64_t c = int64_t(rb[C_CHG]);
             hist.push_back(c);
-            const bool tr = r >= tile_from;  // a tiled round: act / ed = core agents and edges of its tiles
             const RoundKind kind = mode == SWARM_ELECT_DENSE ? RK_DENSE : plan_round(r);
-            const bool dn = !tr && (kind == RK_DENSE || kind == RK_DENSE_MARK);
+            const bool dn = kind == RK_DENSE || kind == RK_DENSE_MARK;
             if (changes_host) changes_host[r - 1] = c;
             const int64_t act = dn ? n : int64_t(rb[C_ACT]);
             const int64_t ed = dn ? int64_t(e_total) : int64_t(rb[C_EDGE]);
@@ -1624,19 +1136,12 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
             edge_sum += ed;
             chg_sum += c;
             dense_rounds += dn ? 1 : 0;
-            // tiled rounds: SURVEY 8(d)'s per-unit bytes of the agents they stand for (12 B per agent,
-            // 8 B per edge), though a launch reads its region from HBM once for kTileHalo rounds
-            const double rbytes = tr ? 12.0 * double(act) + 8.0 * double(ed) : round_bytes(dn, n, int64_t(e_total), act, ed);
+            const double rbytes = round_bytes(dn, n, int64_t(e_total), act, ed);
             bytes += rbytes;
-            if (tr) {
-                tile_bytes += rbytes;
-                ++tile_rounds;
-            } else if (kind == RK_SPARSE) {
-                sp_bytes += rbytes;
-            }
+            if (kind == RK_SPARSE) sp_bytes += rbytes;
             if (rlog)
                 fprintf(rlog, "%d %lld %lld %lld %d %.2f\n", r, (long long)c, (long long)act, (long long)ed,
-                        tr ? 3 : int(kind), timed && !tr && r >= t ? ktime[r - t] * 1e3 : 0.0);
+                        int(kind), timed && r >= t ? ktime[r - t] * 1e3 : 0.0);
             if (c == 0) {
                 found = r;
                 break;
@@ -1646,88 +1151,9 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     };
     while (read_upto < max_rounds && found < 0) {
         t = launched + 1;  // first round launched in this batch (> tend when only a read is left)
-        if (rec && !rec_tried && mode == SWARM_ELECT_FRONTIER && launched < max_rounds && !hist.empty() &&
-            plan_round(launched) == RK_SPARSE && hist.back() < rec_min) {
-            rec_tried = true;
-            if (read_upto < launched) {  // the look-ahead's unread rounds first (one may be the last)
-                hipLaunchKernelGGL(k_batch_totals, dim3(launched - read_upto), dim3(kWave), 0, s, ring, read_upto + 1,
-                                   dtot);
-                SW_LAUNCHED();
-                SW_HIP(hipEventRecord(ev_read, s));
-                SW_HIP(hipEventSynchronize(ev_read));
-                consume(launched);
-                if (found > 0) break;
-            }
-            // rounds launched + 1 ... as record lists over the state after round T0 = launched
-            rt.n = n;
-            rt.n_edges = int64_t(e_total);
-            rt.ncx = rec->ncx;
-            rt.ncy = rec->ncy;
-            rt.index = rec->index;
-            rt.acell = rec->acell;
-            rt.L = bufs[launched & 1];
-            rt.T0 = launched;
-            rt.max_rounds = max_rounds;
-            rt.delta = tuning().rec_delta;
-            rt.grid = tuning().rec_grid;
-            rt.batch = tuning().rec_batch;
-            rt.timed = timed;
-            int rc1 = rec_tail_prepare(ctx, &rt, s);
-            if (rc1) return rc1;
-            const int64_t ntx = (rec->ncx + kRecTile - 1) / kRecTile;
-            hipLaunchKernelGGL(k_rec_marks, dim3(grid_for(int64_t(rd_map.M) << rd_map.cshift, kBlock, 4096)),
-                               dim3(kBlock), 0, s, f.act[(launched + 1) & 1], rd_map, stamp_of(launched + 1), n,
-                               rec->acell, rec->ncx, ntx, rt.tag1, rt.gmark, rt.tflag, rt.tlist1, rt.tcnt);
-            SW_LAUNCHED();
-            rc1 = rec_tail_run(ctx, &rt, leader, s);
-            if (rc1) return rc1;
-            if (rt.fallback == 0) {  // leaders after round min(T0 + dmax, max_rounds) are in `leader`
-                rec_used = true;
-                for (int d = 1; d <= rt.dmax; ++d) {
-                    if (changes_host) changes_host[rt.T0 + d - 1] = rt.hist[size_t(d)];
-                    chg_sum += rt.hist[size_t(d)];
-                }
-                if (rt.T0 + rt.dmax < max_rounds) {  // the first round without a change
-                    found = rt.T0 + rt.dmax + 1;
-                    if (changes_host) changes_host[found - 1] = 0;
-                }
-                read_upto = max_rounds;
-                break;
-            }
-            // fallback (list overflow / capacity): the frontier rounds continue from T0 + 1, whose
-            // marks and leader buffers the tail only read
-        }
-        if (tg && tile_from == INT_MAX && mode == SWARM_ELECT_FRONTIER && t <= max_rounds &&
-            plan_round(t) == RK_SPARSE && plan_round(t - 1) == RK_SPARSE && !hist.empty() && hist.back() < tile_min) {
-            // switch to tiled rounds from round t: the tiles within kTileHalo cells of an agent
-            // marked for round t (the last sparse round's stamps, layout rd_map)
-            const int64_t ntiles = tg->ntx * tg->nty;
-            uint8_t *tb;
-            SW_ALLOC(tb, ctx, S_TILES, size_t(ntiles) * 5 + 64);
-            tflags = tb;
-            tlist = reinterpret_cast<int32_t *>(tb + ((size_t(ntiles) + 15) & ~size_t(15)));
-            tcount = reinterpret_cast<uint32_t *>(tlist + ntiles + 4);
-            terr = tcount + 1;
-            SW_HIP(hipMemsetAsync(tflags, 0, size_t(ntiles), s));
-            SW_HIP(hipMemsetAsync(terr, 0, 4, s));
-            hipLaunchKernelGGL(k_tile_flags_from_marks, dim3(grid_for(int64_t(rd_map.M) << rd_map.cshift, kBlock, 4096)),
-                               dim3(kBlock), 0, s, f.act[t & 1], rd_map, stamp_of(t), n, *tg, tflags);
-            SW_LAUNCHED();
-            int dev = 0, ncu = 0;
-            SW_HIP(hipGetDevice(&dev));
-            SW_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-            tgrid = std::max(1, ncu);
-            tile_from = t;
-            tile_cur = (t - 1) & 1;  // bufs[(t-1) & 1] holds the state after round t-1
-            if (getenv("SWARM_TILE_DEBUG")) {
-                SW_ALLOC(tdbg, ctx, S_TMP1, size_t(tgrid) * 64);
-                SW_HIP(hipMemsetAsync(tdbg, 0, size_t(tgrid) * 64, s));
-            }
-        }
         const int tend = std::min(max_rounds, launched + batch);
         // read rounds (read_upto, tread]: at least one (the first batches are shorter than kLook)
-        const bool tiled = t >= tile_from;
-        const int tread = (tend == max_rounds || tiled) ? tend : std::max(read_upto + 1, tend - kLook);
+        const int tread = tend == max_rounds ? tend : std::max(read_upto + 1, tend - kLook);
         int rc = 0;
         // per-round totals of rounds (read_upto, tread], reduced on device into mapped host memory, an event
         auto enqueue_read = [&]() -> int {
@@ -1737,51 +1163,12 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
             return SWARM_OK;
         };
         if (tread <= launched && (rc = enqueue_read())) return rc;
-        if (tiled && t <= tend) {  // this batch as tiled launches of up to kTileHalo rounds
-            if (timed) SW_HIP(hipEventRecord(ev[2 * kMaxBatch], s));
-            const int64_t ntiles = tg->ntx * tg->nty;
-            for (int r = t; r <= tend; r += kTileHalo) {
-                const int kk = std::min(kTileHalo, tend - r + 1);
-                hipLaunchKernelGGL(k_tile_list, dim3(1), dim3(kTileThreads), 0, s, tflags, ntiles, tlist, tcount, ring,
-                                   r, r + kk - 1);
-                SW_LAUNCHED();
-                const TileLaunch tl{tlist, tcount, tflags, bufs[tile_cur], bufs[tile_cur ^ 1], ring, terr, r - 1, kk,
-                                    tdbg};
-                hipLaunchKernelGGL(k_tile_rounds, dim3(tgrid), dim3(kTileThreads), 0, s,
-                                   reinterpret_cast<const int32_t *>(rp), col, *tg, tl);
-                SW_LAUNCHED();
-                tile_cur ^= 1;
-                ++tile_launches;
-                if (tdbg) {  // phase clocks of every workgroup's first tile (debug aid: one sync per launch)
-                    std::vector<unsigned long long> h(size_t(tgrid) * 8);
-                    SW_HIP(hipMemcpyAsync(h.data(), tdbg, h.size() * 8, hipMemcpyDeviceToHost, s));
-                    SW_HIP(hipStreamSynchronize(s));
-                    for (int b = 0; b < tgrid; ++b) {
-                        const unsigned long long *q = &h[size_t(b) * 8];
-                        if (!q[0] || !q[6]) continue;
-                        for (int k = 1; k <= 6; ++k) tdbg_sum[k - 1] += double(q[k] - q[k - 1]);
-                        tdbg_sum[6] += double(q[7] & 0xffffffffull);
-                        tdbg_sum[7] += double(q[7] >> 32);
-                        ++tdbg_n;
-                    }
-                    SW_HIP(hipMemsetAsync(tdbg, 0, size_t(tgrid) * 64, s));
-                }
-            }
-            if (timed) {
-                SW_HIP(hipEventRecord(ev[2 * kMaxBatch + 1], s));
-                SW_HIP(hipEventSynchronize(ev[2 * kMaxBatch + 1]));
-                float x = 0;
-                SW_HIP(hipEventElapsedTime(&x, ev[2 * kMaxBatch], ev[2 * kMaxBatch + 1]));
-                tile_ms += x;
-            }
-            if ((rc = enqueue_read())) return rc;
-        }
         // timing: dense rounds (and every round when a per-round log is written) get an event pair
         // each; a batch's run of back-to-back sparse rounds gets ONE pair around it -- events
         // between every launch would add their own cost to each round (rocprof's per-dispatch
         // durations are the reference for this figure)
         int seg_n = 0;  // sparse launches inside this batch's segment
-        for (int r = t; r <= tend && !tiled; ++r) {
+        for (int r = t; r <= tend; ++r) {
             const bool sparse = mode == SWARM_ELECT_FRONTIER && plan_round(r) == RK_SPARSE;
             const bool seg = timed && sparse && !rlog;
             if (seg && seg_n++ == 0) SW_HIP(hipEventRecord(ev[2 * kMaxBatch], s));
@@ -1807,7 +1194,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         if (seg_n) SW_HIP(hipEventRecord(ev[2 * kMaxBatch + 1], s));
         launched = std::max(launched, tend);
         SW_HIP(hipEventSynchronize(ev_read));
-        if (timed && !tiled) {  // kLook == 0: this batch's rounds are exactly the rounds read
+        if (timed) {  // kLook == 0: this batch's rounds are exactly the rounds read
             SW_HIP(hipStreamSynchronize(s));
             for (int r = t; r <= tend; ++r) {  // every launched round's kernel time (rocprof's view)
                 if (seg_n && kinds[r - t] == RK_SPARSE) continue;  // in the segment
@@ -1836,26 +1223,9 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         batch = next_round_batch(hist.data(), hist.size(), batch, kMaxBatch - kLook);
     }
     const int last = found > 0 ? found : max_rounds;
-    if (tdbg && tdbg_n)  // wall_clock64 runs at 100 MHz on gfx950
-        fprintf(stderr, "tile phases (us, mean over %lld first tiles): seg %.2f load %.2f scan %.2f cols %.2f rounds %.2f "
-                        "store %.2f | agents %.0f edges %.0f\n", (long long)tdbg_n, tdbg_sum[0] / tdbg_n / 100.0,
-                tdbg_sum[1] / tdbg_n / 100.0, tdbg_sum[2] / tdbg_n / 100.0, tdbg_sum[3] / tdbg_n / 100.0,
-                tdbg_sum[4] / tdbg_n / 100.0, tdbg_sum[5] / tdbg_n / 100.0, tdbg_sum[6] / tdbg_n, tdbg_sum[7] / tdbg_n);
-    if (tile_from != INT_MAX) {
-        // tiled rounds: bufs[tile_cur] holds the state after the last launched round on every tile
-        // (a tile left alone holds the same values in both buffers)
-        unsigned herr = 0;
-        SW_HIP(hipMemcpyAsync(&herr, terr, 4, hipMemcpyDeviceToHost, s));
-        SW_HIP(hipStreamSynchronize(s));
-        if (herr) {
-            set_error("tiled rounds: a tile region exceeded the on-chip capacity (flags %u): the tile index does "
-                      "not belong to this graph", herr);
-            return SWARM_ERR_ARG;
-        }
-        if (tile_cur == 1) SW_HIP(hipMemcpyAsync(leader, bufs[1], size_t(n) * 4, hipMemcpyDeviceToDevice, s));
-    } else if (!rec_used && found < 0 && (last & 1)) {
+    if (found < 0 && (last & 1)) {
         // after a zero-change round both buffers hold the final state (dense and frontier alike);
-        // otherwise the newest is bufs[last & 1] (a record tail wrote its leaders into `leader`)
+        // otherwise the newest is bufs[last & 1]
         SW_HIP(hipMemcpyAsync(leader, bufs[1], size_t(n) * 4, hipMemcpyDeviceToDevice, s));
     }
     hipLaunchKernelGGL(k_state, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s, leader,
@@ -1875,18 +1245,6 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         st->sparse_ms = sp_ms;
         st->sparse_launches = sp_launches;
         st->sparse_bytes = sp_bytes;
-        st->tile_rounds = tile_rounds;
-        st->tile_launches = tile_launches;
-        st->tile_ms = tile_ms;
-        st->tile_bytes = tile_bytes;
-        st->tile_from = tile_from == INT_MAX ? 0 : tile_from;
-        st->record_from = rec_used ? rt.T0 + 1 : 0;
-        st->record_launches = rt.launches;
-        st->record_activations = rt.activations;
-        st->record_recomputes = rt.recomputes;
-        st->record_ms = rt.ms;
-        st->record_fallback = rt.fallback;
-        st->record_levels = rt.levels;
     }
     return found > 0 ? SWARM_OK : SWARM_NOT_CONVERGED;
 }
@@ -1977,76 +1335,6 @@ int swarm_elect_compact(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const
     return swarm::elect_impl<int32_t>(ctx, n, row_ptr, col, ids, leader, state, max_rounds, mode, rounds_exec,
                                       changes_per_round, stats, stream, nullptr, nullptr,
                                       swarm::tuning().use_c16 ? col16 : nullptr);
-}
-
-int swarm_tile_index(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col, const swarm_grid *grid,
-                     const uint32_t *cell_off, int32_t *acell, int32_t *ok, void *stream) {
-    using namespace swarm;
-    SW_ARG(ctx != nullptr && grid != nullptr && ok != nullptr, "NULL argument");
-    if (!ctx_on_current_device(ctx)) return SWARM_ERR_ARG;
-    SW_ARG(n >= 1 && n < (int64_t(1) << 30), "n out of range (1 .. 2^30 - 1)");
-    SW_ARG(row_ptr && cell_off && acell, "NULL array");
-    SW_ARG(grid->ncx >= 1 && grid->ncy >= 1, "bad grid");
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    *ok = 0;
-    int32_t e_total = 0;
-    SW_HIP(hipMemcpyAsync(&e_total, row_ptr + n, 4, hipMemcpyDeviceToHost, s));
-    SW_HIP(hipStreamSynchronize(s));
-    SW_ARG(e_total == 0 || col != nullptr, "col is NULL but the graph has edges");
-    const int64_t ncells = grid->ncx * grid->ncy;
-    TileGeom g{cell_off, acell, grid->ncx, grid->ncy, (grid->ncx + kTileCore - 1) / kTileCore,
-               (grid->ncy + kTileCore - 1) / kTileCore};
-    unsigned long long *w;
-    SW_ALLOC(w, ctx, S_TMP0, 64);
-    SW_HIP(hipMemsetAsync(w, 0, 24, s));
-    hipLaunchKernelGGL(k_tile_acell, dim3(grid_for(ncells, kBlock, 8192)), dim3(kBlock), 0, s, cell_off, ncells, acell);
-    SW_LAUNCHED();
-    hipLaunchKernelGGL(k_tile_local, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, row_ptr, col, acell, n,
-                       grid->ncx, w);
-    SW_LAUNCHED();
-    hipLaunchKernelGGL(k_tile_regions, dim3(grid_for(g.ntx * g.nty, kBlock, 4096)), dim3(kBlock), 0, s, cell_off,
-                       row_ptr, g, w + 1);
-    SW_LAUNCHED();
-    unsigned long long h[3] = {0, 0, 0};
-    SW_HIP(hipMemcpyAsync(h, w, 24, hipMemcpyDeviceToHost, s));
-    SW_HIP(hipStreamSynchronize(s));
-    // the cell offsets must cover exactly the n agents
-    uint32_t last = 0;
-    SW_HIP(hipMemcpy(&last, cell_off + ncells, 4, hipMemcpyDeviceToHost));
-    SW_ARG(int64_t(last) == n, "cell_off[ncells] != n (the index of another swarm?)");
-    *ok = (h[0] == 0 && h[1] <= uint64_t(kTileCap) && h[2] <= uint64_t(kTileECap)) ? 1 : 0;
-    return SWARM_OK;
-}
-
-int swarm_elect_tiled(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col, const int16_t *col16,
-                      const int32_t *ids, int32_t *leader, uint8_t *state, const swarm_grid *grid,
-                      const uint32_t *cell_off, const int32_t *acell, int32_t max_rounds, int32_t mode,
-                      int32_t *rounds_exec, int64_t *changes_per_round, swarm_elect_stats *stats, void *stream) {
-    using namespace swarm;
-    const int16_t *c16 = tuning().use_c16 ? col16 : nullptr;
-    if (!acell || !grid || !cell_off || (tuning().tile_min_changes <= 0 && !(mode & SWARM_ELECT_TILES_EARLY)))
-        return elect_impl<int32_t>(ctx, n, row_ptr, col, ids, leader, state, max_rounds, mode, rounds_exec,
-                                   changes_per_round, stats, stream, nullptr, nullptr, c16);
-    SW_ARG(grid->ncx >= 1 && grid->ncy >= 1, "bad grid");
-    const TileGeom g{cell_off, acell, grid->ncx, grid->ncy, (grid->ncx + kTileCore - 1) / kTileCore,
-                     (grid->ncy + kTileCore - 1) / kTileCore};
-    return elect_impl<int32_t>(ctx, n, row_ptr, col, ids, leader, state, max_rounds, mode, rounds_exec,
-                               changes_per_round, stats, stream, nullptr, nullptr, c16, &g);
-}
-
-int swarm_elect_records(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col, const int16_t *col16,
-                        const int32_t *ids, int32_t *leader, uint8_t *state, const swarm_grid *grid,
-                        const int32_t *acell, const void *index, int32_t max_rounds, int32_t mode,
-                        int32_t *rounds_exec, int64_t *changes_per_round, swarm_elect_stats *stats, void *stream) {
-    using namespace swarm;
-    const int16_t *c16 = tuning().use_c16 ? col16 : nullptr;
-    if (!index || !acell || !grid)
-        return elect_impl<int32_t>(ctx, n, row_ptr, col, ids, leader, state, max_rounds, mode, rounds_exec,
-                                   changes_per_round, stats, stream, nullptr, nullptr, c16);
-    SW_ARG(grid->ncx >= 1 && grid->ncy >= 1, "bad grid");
-    const RecArg ra{index, grid->ncx, grid->ncy, acell};
-    return elect_impl<int32_t>(ctx, n, row_ptr, col, ids, leader, state, max_rounds, mode, rounds_exec,
-                               changes_per_round, stats, stream, nullptr, nullptr, c16, nullptr, &ra);
 }
 
 int swarm_elect_directed(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col,

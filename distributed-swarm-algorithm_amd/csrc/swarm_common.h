@@ -54,9 +54,6 @@ enum Slot {
     S_DEFER,          // allocation: guard-band tasks deferred to the libm pass (list + per-task flags)
     S_FPAIRS,         // allocation: the deferred tasks' guard-band pairs (device -> host)
     S_OVR,            // allocation: host libm decisions for those pairs (host -> device)
-    S_TILES,          // election: tiled rounds' tile flags, list, count, error word
-    S_REC_LIST,       // election record tail: kRecEntries list entries per agent (records.hip)
-    S_REC_MARK,       // election record tail: agent marks, tile flags, tile lists, per-launch counts
     S_NUM
 };
 
@@ -170,53 +167,6 @@ inline int next_round_batch(const int64_t *hist, size_t nh, int batch, int max_b
     }
     return b;
 }
-
-// ---- election record tail (records.hip; elect.hip drives it) ----
-constexpr int kRecTile = 8;             // core cells per tile side
-constexpr int kRecEntries = 8;          // record list entries per agent
-constexpr int kRecDBits = 20;           // list entries / tags: (gen << kRecDBits) | d (or launch)
-constexpr uint32_t kRecDMask = (1u << kRecDBits) - 1;
-constexpr int kRecGenBits = 12;
-constexpr int kRecMaxLaunch = 1 << 16;
-
-struct RecGeom {
-    int64_t ncx, ncy, ntx, nty;  // grid cells, tiles of kRecTile x kRecTile cells
-};
-
-// Views into a swarm_record_index blob.
-struct RecIndex {
-    int32_t *ra, *re, *rs, *rq;  // per-tile prefixes: core agents, core edges, region slots, core rows (padded)
-    uint16_t *rrow, *rcol;       // core rows' local edge offsets; core columns as region slots
-    int32_t *ragent;             // region slot -> storage index
-};
-
-struct RecTail {
-    // in
-    int64_t n = 0, n_edges = 0, ncx = 0, ncy = 0;
-    const void *index = nullptr;
-    const int32_t *acell = nullptr;
-    const int32_t *L = nullptr;  // state after round T0
-    int T0 = 0, max_rounds = 0, delta = 0, grid = 0, batch = 0;
-    bool timed = false;
-    // device state (rec_tail_prepare) -- the marks kernel writes launch 1's marks into these
-    alignas(16) unsigned char state[256];
-    uint32_t *gmark = nullptr, *tflag = nullptr, *tcnt = nullptr;
-    int32_t *tlist0 = nullptr, *tlist1 = nullptr;
-    uint32_t gen = 0, tag1 = 0;
-    int64_t ntiles = 0;
-    // out
-    int fallback = 0;            // nonzero: nothing computed, continue with the frontier rounds
-    int dmax = 0;
-    std::vector<int64_t> hist;   // hist[d]: changes of round T0 + d
-    int64_t launches = 0, activations = 0, levels = 0, recomputes = 0, loaded = 0;
-    double ms = 0.0;
-};
-
-int64_t rec_ntiles(int64_t ncx, int64_t ncy);
-RecGeom rec_geom(int64_t ncx, int64_t ncy);
-int rec_index_view(const void *index, int64_t n, int64_t e, int64_t ncx, int64_t ncy, RecIndex *out);
-int rec_tail_prepare(swarm_ctx *ctx, RecTail *rt, hipStream_t s);
-int rec_tail_run(swarm_ctx *ctx, RecTail *rt, int32_t *out, hipStream_t s);
 
 // Grid for a grid-stride kernel over `work` items with `per_block` items per block pass.
 inline unsigned grid_for(int64_t work, int64_t per_block, unsigned cap = 8192) {

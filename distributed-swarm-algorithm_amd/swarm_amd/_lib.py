@@ -19,7 +19,7 @@ LIB_PATH = os.path.join(HERE, "libswarm.so")
 OK, NOT_CONVERGED = 0, 1
 ERR_ARG, ERR_HIP, ERR_OOM, ERR_RANGE, ERR_STALE = -1, -2, -3, -4, -5
 FOLLOWER, ELECTION_WAIT, LEADER = 1, 2, 3
-ELECT_DENSE, ELECT_FRONTIER, ELECT_TIMED, ELECT_TILES_EARLY, ELECT_RECORDS_EARLY = 0, 1, 0x100, 0x200, 0x400
+ELECT_DENSE, ELECT_FRONTIER, ELECT_TIMED = 0, 1, 0x100
 ALLOC_AUTO, ALLOC_BINNED, ALLOC_DENSE = 0, 1, 2
 
 # every symbol include/swarm.h declares (tests/test_capi.py checks the two agree)
@@ -32,8 +32,7 @@ EXPORTS = ("swarm_last_error", "swarm_version", "swarm_ctx_create", "swarm_ctx_d
            "swarm_codec_decode", "swarm_protocol_run", "swarm_auction_begin",
            "swarm_auction_bid", "swarm_auction_resolve", "swarm_auction_sharded", "swarm_cell_index",
            "swarm_allocate_indexed", "swarm_graph_compact", "swarm_elect_compact",
-           "swarm_elect_compact_i64", "swarm_tile_index", "swarm_elect_tiled", "swarm_frontier_begin_range",
-           "swarm_frontier_set_compact", "swarm_record_index_bytes", "swarm_record_index", "swarm_elect_records")
+           "swarm_elect_compact_i64", "swarm_frontier_begin_range", "swarm_frontier_set_compact")
 
 
 class SwarmError(RuntimeError):
@@ -59,13 +58,7 @@ class ElectStats(ctypes.Structure):
                 ("gather_ms", ctypes.c_double), ("apply_ms", ctypes.c_double),
                 ("gather_launches", ctypes.c_int64), ("dense_rounds", ctypes.c_int64),
                 ("bytes_total", ctypes.c_double), ("sparse_ms", ctypes.c_double),
-                ("sparse_launches", ctypes.c_int64), ("sparse_bytes", ctypes.c_double),
-                ("tile_rounds", ctypes.c_int64), ("tile_launches", ctypes.c_int64), ("tile_ms", ctypes.c_double),
-                ("tile_bytes", ctypes.c_double), ("tile_from", ctypes.c_int64),
-                ("record_from", ctypes.c_int64), ("record_launches", ctypes.c_int64),
-                ("record_activations", ctypes.c_int64), ("record_recomputes", ctypes.c_int64),
-                ("record_ms", ctypes.c_double), ("record_fallback", ctypes.c_int64),
-                ("record_levels", ctypes.c_int64)]
+                ("sparse_launches", ctypes.c_int64), ("sparse_bytes", ctypes.c_double)]
 
 
 class AuctionStats(ctypes.Structure):
@@ -117,13 +110,6 @@ def load(path: str = LIB_PATH):
         L.swarm_graph_compact.argtypes = [P, i64, P, P, P, P]
         L.swarm_elect_compact.argtypes = [P, i64, P, P, P, P, P, P, i32, i32, ctypes.POINTER(i32), P, P, P]
         L.swarm_elect_compact_i64.argtypes = [P, i64, P, P, P, P, P, P, i32, i32, ctypes.POINTER(i32), P, P, P]
-        L.swarm_tile_index.argtypes = [P, i64, P, P, ctypes.POINTER(Grid), P, P, ctypes.POINTER(i32), P]
-        L.swarm_elect_tiled.argtypes = [P, i64, P, P, P, P, P, P, ctypes.POINTER(Grid), P, P, i32, i32,
-                                        ctypes.POINTER(i32), P, P, P]
-        L.swarm_record_index_bytes.argtypes = [i64, i64, ctypes.POINTER(Grid)]
-        L.swarm_record_index.argtypes = [P, i64, P, P, ctypes.POINTER(Grid), P, P, P, i64, ctypes.POINTER(i32), P]
-        L.swarm_elect_records.argtypes = [P, i64, P, P, P, P, P, P, ctypes.POINTER(Grid), P, P, i32, i32,
-                                          ctypes.POINTER(i32), P, P, P]
         L.swarm_allocate.argtypes = [P, i64, P, P, P, i64, P, P, d, d, d, i32, P, P, P, P, i64,
                                      P, P, P, P]
         L.swarm_utility.argtypes = [P, i64, P, P, P, P, d, P, P]
@@ -158,7 +144,6 @@ def load(path: str = LIB_PATH):
         for name in EXPORTS:
             if name not in ("swarm_last_error", "swarm_version"):
                 getattr(L, name).restype = ctypes.c_int
-        L.swarm_record_index_bytes.restype = ctypes.c_int64
         _lib = L
         return L
 

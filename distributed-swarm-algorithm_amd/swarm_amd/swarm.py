@@ -219,79 +219,13 @@ class Swarm:
             self._c16 = cached = (key, c16)
         return cached[1]
 
-    def tile_index(self):
-        """(Grid, cell_off, acell) for the tiled tail rounds (swarm_tile_index), or None: built once
-        per graph version and cell index; None when the swarm is not in cell order, the graph is
-        directed, or an edge joins cells more than one apart (the tiled rounds need local edges)."""
-        if self.row_ptr is None or getattr(self, "_hear", None) is not None or not 0 < self.n < (1 << 30) \
-                or self.layout != "spatial" or self.n < 2:
-            return None
-        ci = self._cell_index()
-        if ci is None:
-            return None
-        key = (self.row_ptr.data_ptr(), self.col.data_ptr(), self.row_ptr._version, self.col._version,
-               self.n, self.col.numel())
-        cached = getattr(self, "_tix", None)
-        if cached is None or cached[0] != key or cached[2] is not ci:
-            acell = torch.empty(self.n, dtype=torch.int32, device=self.device)
-            ok = ctypes.c_int32(0)
-            with torch.cuda.device(self.device):
-                _lib.check(_lib.lib().swarm_tile_index(
-                    _lib.ctx(), self.n, _lib.ptr(self.row_ptr, torch.int32),
-                    _lib.ptr(self.col, torch.int32) if self.col.numel() else None, ctypes.byref(ci[0]),
-                    _lib.ptr(ci[1]), _lib.ptr(acell), ctypes.byref(ok), _lib.stream()))
-            self._tix = cached = (key, (ci[0], ci[1], acell) if ok.value else None, ci)
-        return cached[1]
-
-    def record_index(self):
-        """(Grid, acell, index) for the record tail (swarm_record_index), or None: built once per graph
-        version and cell index; None when the swarm is not in cell order, the graph is directed, an
-        edge joins cells more than one apart, or a tile does not fit on chip."""
-        if self.row_ptr is None or getattr(self, "_hear", None) is not None or not 1 < self.n < (1 << 30) \
-                or self.layout != "spatial":
-            return None
-        ci = self._cell_index()
-        if ci is None:
-            return None
-        key = (self.row_ptr.data_ptr(), self.col.data_ptr(), self.row_ptr._version, self.col._version,
-               self.n, self.col.numel())
-        cached = getattr(self, "_rix", None)
-        if cached is None or cached[0] != key or cached[2] is not ci:
-            L = _lib.lib()
-            res = None
-            with torch.cuda.device(self.device):
-                acell = torch.empty(self.n, dtype=torch.int32, device=self.device)
-                ok = ctypes.c_int32(0)
-                colp = _lib.ptr(self.col, torch.int32) if self.col.numel() else None
-                _lib.check(L.swarm_tile_index(_lib.ctx(), self.n, _lib.ptr(self.row_ptr, torch.int32), colp,
-                                              ctypes.byref(ci[0]), _lib.ptr(ci[1]), _lib.ptr(acell), ctypes.byref(ok),
-                                              _lib.stream()))
-                nb = int(L.swarm_record_index_bytes(self.n, self.n_edges, ctypes.byref(ci[0])))
-                if nb > 0:
-                    blob = torch.empty(nb, dtype=torch.uint8, device=self.device)
-                    _lib.check(L.swarm_record_index(_lib.ctx(), self.n, _lib.ptr(self.row_ptr, torch.int32), colp,
-                                                    ctypes.byref(ci[0]), _lib.ptr(ci[1]), _lib.ptr(acell),
-                                                    _lib.ptr(blob), nb, ctypes.byref(ok), _lib.stream()))
-                    if ok.value:
-                        res = (ci[0], acell, blob)
-            self._rix = cached = (key, res, ci)
-        return cached[1]
-
     def elect(self, mode: str = "frontier", max_rounds: int = 1 << 16, timed: bool = False,
-              compact: bool = True, wide: bool | None = None, tiles: bool | str = False,
-              records: bool | str = False) -> ElectResult:
+              compact: bool = True, wide: bool | None = None) -> ElectResult:
         """Contract E2 to convergence on the GPU (swarm_elect_compact with the graph's 16-bit
         columns when they fit; swarm_elect_directed when the neighbour lists are not symmetric).
         timed: per-kernel HIP events.  compact=False: the int32-column entry point swarm_elect
         (same results).  wide: int64 row offsets (swarm_elect_i64) -- chosen by itself for
-        graphs of >= 2^30 edges (C5's 100M agents on one GPU: ~1.6e9), True forces it.
-        tiles: swarm_elect_tiled when the swarm's cell index allows it (tile_index()): tiled tail
-        rounds once a round changes fewer than SWARM_TILE_MIN_CHANGES agents (default: never);
-        tiles="early": tiled from the first sparse round.  Same results; measured slower at C3
-        (DESIGN.md §4), kept as an exact A/B path.
-        records: swarm_elect_records when the swarm's record index exists (record_index()): the late
-        rounds as record lists, ~8 rounds per launch; records="early": from the first
-        sparse round (tests).  Same results."""
+        graphs of >= 2^30 edges (C5's 100M agents on one GPU: ~1.6e9), True forces it."""
         if self.row_ptr is None:
             raise RuntimeError("no neighbour graph: call build_graph() or set_graph()")
         if wide is None:
@@ -307,25 +241,7 @@ class Swarm:
         hear = getattr(self, "_hear", None)
         with torch.cuda.device(self.device):
             c16 = self.graph_compact() if (compact and hear is None) else None
-            tix = self.tile_index() if (tiles and mode == "frontier" and hear is None) else None
-            rix = self.record_index() if (records and not tiles and mode == "frontier" and hear is None) else None
-            if rix is not None:  # symmetric, local graph in cell order: record tail
-                m |= _lib.ELECT_RECORDS_EARLY if records == "early" else 0
-                rc = _lib.check(_lib.lib().swarm_elect_records(
-                    _lib.ctx(), n, _lib.ptr(self.row_ptr, torch.int32), _lib.ptr(self.col, torch.int32),
-                    _lib.ptr(c16) if c16 is not None else None, _lib.ptr(self.ids, torch.int32),
-                    _lib.ptr(self.leader, torch.int32), _lib.ptr(self.state, torch.uint8), ctypes.byref(rix[0]),
-                    _lib.ptr(rix[1]), _lib.ptr(rix[2]), cap, m, ctypes.byref(rounds),
-                    changes.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st), _lib.stream()))
-            elif tix is not None:  # symmetric, local graph in cell order: tiled tail rounds
-                m |= _lib.ELECT_TILES_EARLY if tiles == "early" else 0
-                rc = _lib.check(_lib.lib().swarm_elect_tiled(
-                    _lib.ctx(), n, _lib.ptr(self.row_ptr, torch.int32), _lib.ptr(self.col, torch.int32),
-                    _lib.ptr(c16) if c16 is not None else None, _lib.ptr(self.ids, torch.int32),
-                    _lib.ptr(self.leader, torch.int32), _lib.ptr(self.state, torch.uint8), ctypes.byref(tix[0]),
-                    _lib.ptr(tix[1]), _lib.ptr(tix[2]), cap, m, ctypes.byref(rounds),
-                    changes.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st), _lib.stream()))
-            elif c16 is not None:  # symmetric graph, 16-bit columns
+            if c16 is not None:  # symmetric graph, 16-bit columns
                 rc = _lib.check(_lib.lib().swarm_elect_compact(
                     _lib.ctx(), n, _lib.ptr(self.row_ptr, torch.int32), _lib.ptr(self.col, torch.int32),
                     _lib.ptr(c16), _lib.ptr(self.ids, torch.int32), _lib.ptr(self.leader, torch.int32),
@@ -351,11 +267,6 @@ class Swarm:
         res.changes_total = st.changes_total
         res.gather_ms, res.apply_ms, res.timed_launches = st.gather_ms, st.apply_ms, st.gather_launches
         res.sparse_ms, res.sparse_launches, res.sparse_bytes = st.sparse_ms, st.sparse_launches, st.sparse_bytes
-        res.tile_rounds, res.tile_launches, res.tile_ms = st.tile_rounds, st.tile_launches, st.tile_ms
-        res.tile_bytes, res.tile_from = st.tile_bytes, st.tile_from
-        res.record_from, res.record_launches, res.record_ms = st.record_from, st.record_launches, st.record_ms
-        res.record_activations, res.record_recomputes = st.record_activations, st.record_recomputes
-        res.record_fallback, res.record_levels = st.record_fallback, st.record_levels
         res.compact = c16 is not None  # the rounds read the 16-bit columns (2 of the 4 column bytes)
         return res
 

@@ -50,10 +50,6 @@ extern "C" {
 #define SWARM_ELECT_FRONTIER 1 /* dense sweeps while many agents change, then only the agents
                                   marked by last round's risers gather (sparse rounds) */
 #define SWARM_ELECT_TIMED 0x100 /* OR into mode: time every kernel with HIP events (stats) */
-#define SWARM_ELECT_TILES_EARLY 0x200 /* OR into mode (swarm_elect_tiled): tiled rounds from the first
-                                        sparse round on, whatever the changes (tests, A/B) */
-#define SWARM_ELECT_RECORDS_EARLY 0x400 /* OR into mode (swarm_elect_records): record tail from the first
-                                           sparse round's batch boundary (tests, A/B) */
 
 /* Allocation execution strategies (all exact). */
 #define SWARM_ALLOC_AUTO 0
@@ -92,19 +88,6 @@ typedef struct swarm_elect_stats {
     double sparse_ms;        /* SWARM_ELECT_TIMED: device time of every launched sparse round */
     int64_t sparse_launches; /* SWARM_ELECT_TIMED: sparse rounds launched (incl. no-ops) */
     double sparse_bytes;     /* algorithmic HBM bytes of the executed sparse rounds */
-    int64_t tile_rounds;     /* swarm_elect_tiled: rounds run as tiled launches (rounds_exec included) */
-    int64_t tile_launches;   /* swarm_elect_tiled: tiled launches (up to 4 rounds each) */
-    double tile_ms;          /* SWARM_ELECT_TIMED: device time of the tiled launches */
-    double tile_bytes;       /* SURVEY 8(d) bytes of the agents / edges the tiled rounds stand for */
-    int64_t tile_from;       /* first tiled round (0: none) */
-    int64_t record_from;        /* swarm_elect_records: first round computed by the record tail (0: none) */
-    int64_t record_launches;    /* record-tail launches (k_rec_tiles), no-op launches past the end included */
-    int64_t record_activations; /* tiles processed, summed over those launches */
-    int64_t record_recomputes;  /* agent list recomputes in the record tail */
-    double record_ms;           /* SWARM_ELECT_TIMED: device time of the record tail (launches + finalize) */
-    int64_t record_fallback;    /* nonzero: the tail gave up (list overflow / capacity: bit flags) and the
-                                   frontier rounds finished the election from record_from - 1 */
-    int64_t record_levels;      /* on-chip relaxation levels, summed over the tail's tile activations */
 } swarm_elect_stats;
 
 const char *swarm_last_error(void);
@@ -167,56 +150,6 @@ int swarm_elect_i64(swarm_ctx *ctx, int64_t n, const int64_t *row_ptr, const int
                     const int32_t *ids, int32_t *leader, uint8_t *state, int32_t max_rounds,
                     int32_t mode, int32_t *rounds_exec, int64_t *changes_per_round,
                     swarm_elect_stats *stats, void *stream);
-
-/*
- * Tiled rounds for the tail of an election (DESIGN.md §4 "tiled rounds").  A swarm stored in cell
- * order (swarm_cell_order; its cell index from swarm_cell_index) whose every edge joins cells at
- * most one apart in x and y (a radius graph with radius <= the cell side) can run its late rounds
- * as launches of 4 rounds each over 16 x 16-cell tiles held on chip, only where the fronts are.
- * swarm_tile_index: acell (device, n int32) = each agent's cell; *ok = 1 when the graph is local in
- * that sense and every tile region fits on chip, else 0 (then run swarm_elect_compact).
- * swarm_elect_tiled: swarm_elect_compact (same results: leaders, states, rounds_exec, every per-round
- * change count) that switches to tiled rounds once a round changes fewer than SWARM_TILE_MIN_CHANGES
- * agents (default 0: never -- at 10M agents a launch costs ~80 us per tile, slower than the sparse
- * rounds it replaces) or, with SWARM_ELECT_TILES_EARLY in mode, from the first sparse
- * round on.  acell must come from swarm_tile_index with *ok = 1 for THIS graph and cell index
- * (acell = NULL: plain swarm_elect_compact).  Symmetric graphs, int32 offsets.
- * Replaces the same handlers as swarm_elect (agent.py:243-275).
- */
-int swarm_tile_index(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col, const swarm_grid *grid,
-                     const uint32_t *cell_off, int32_t *acell, int32_t *ok, void *stream);
-int swarm_elect_tiled(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col, const int16_t *col16,
-                      const int32_t *ids, int32_t *leader, uint8_t *state, const swarm_grid *grid,
-                      const uint32_t *cell_off, const int32_t *acell, int32_t max_rounds, int32_t mode,
-                      int32_t *rounds_exec, int64_t *changes_per_round, swarm_elect_stats *stats, void *stream);
-
-/*
- * Record-list tail (an MI355X schedule of the same rounds; DESIGN.md §4 "record tail").
- * After round T0 every agent holds L_v = max id within T0 hops; its leader after round T0 + d is
- * max{ L_w : w within d hops }, a step function held as its pareto list of RECORDS (d, value).  The
- * lists are the least fixpoint of a relaxation that may run in any order, so tiles of 8 x 8 cells
- * (swarm_cell_index's grid) run to a local fixpoint on chip and only their borders wait for the next
- * launch: ~8 rounds per launch instead of one.  The per-round change counts are the histogram of the
- * records' d, the leaders the last records: the same leaders, states, rounds_exec and per-round
- * changes as swarm_elect_compact, bit for bit.
- * swarm_record_index_bytes: size of the device index blob for n agents, n_edges edges and the grid.
- * swarm_record_index: build it (per graph: tile-local CSR of 16-bit region slots, region slot ->
- * agent) from the CSR, the grid and cell offsets of swarm_cell_index, and acell of swarm_tile_index;
- * *ok = 1 when every tile fits on chip and every edge joins cells at most one apart.
- * swarm_elect_records: swarm_elect_compact that switches to the record tail once a round changes
- * fewer than SWARM_REC_MIN_CHANGES agents (default 0.006 n); index = NULL (or acell / grid NULL):
- * plain swarm_elect_compact.  A list that overflows its 8 entries or a tile over capacity makes the
- * frontier rounds finish the election (stats->record_fallback).  Symmetric graphs, int32 offsets.
- * Replaces the same handlers as swarm_elect (agent.py:243-275).
- */
-int64_t swarm_record_index_bytes(int64_t n, int64_t n_edges, const swarm_grid *grid);
-int swarm_record_index(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col, const swarm_grid *grid,
-                       const uint32_t *cell_off, const int32_t *acell, void *index, int64_t index_bytes, int32_t *ok,
-                       void *stream);
-int swarm_elect_records(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col, const int16_t *col16,
-                        const int32_t *ids, int32_t *leader, uint8_t *state, const swarm_grid *grid,
-                        const int32_t *acell, const void *index, int32_t max_rounds, int32_t mode,
-                        int32_t *rounds_exec, int64_t *changes_per_round, swarm_elect_stats *stats, void *stream);
 
 /* swarm_elect_compact with int64 row offsets (graphs of >= 2^30 edges; the 16-bit columns are
  * built by swarm_graph_compact from the int32 row offsets, which hold up to 2^31 - 1 edges).
