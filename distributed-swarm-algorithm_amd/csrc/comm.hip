@@ -5,19 +5,55 @@
 // RCCL is resolved at run time (dlopen/dlsym) from the instance already loaded in the process
 // (torch's, SONAME librccl.so.1) so that libswarm.so never links a second copy; only the
 // header types come from /opt/rocm/include/rccl.
+//
+// A second transport runs the same C loops between processes of ONE host whatever their GPUs
+// (RCCL refuses two ranks on one device): SWARM_COMM_SHM, a POSIX shared-memory segment with one
+// mailbox per rank and op parity and a process-shared barrier.  Each exchange copies the send
+// buffers device -> mailbox, meets the barrier, and copies the peers' mailboxes -> device; an
+// all-reduce combines every rank's mailbox on the host.  Host-staged and synchronous per op: a
+// test and rehearsal transport for the native loops, not a fast one.
 #include <dlfcn.h>
+#include <fcntl.h>
 #include <rccl/rccl.h>
+#include <sched.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstring>
 #include <cstdlib>
+#include <random>
 #include <vector>
 
 #include "swarm_common.h"
 
+namespace swarm {
+struct ShmHeader {
+    std::atomic<uint32_t> magic;    // kShmMagic once rank 0 has initialised the segment
+    std::atomic<uint32_t> arrived;  // barrier arrivals in the current generation
+    std::atomic<uint32_t> gen;      // barrier generation
+    std::atomic<uint32_t> abort;    // a rank gave up waiting: every later barrier fails
+    uint32_t nranks;
+    uint64_t cap;                   // bytes per mailbox (one per rank and op parity)
+};
+constexpr uint32_t kShmMagic = 0x5357524Du;  // "SWRM"
+constexpr size_t kShmHeader = 4096;
+static_assert(std::atomic<uint32_t>::is_always_lock_free, "process-shared atomics must be lock-free");
+}  // namespace swarm
+
 struct swarm_comm {
+    int kind = SWARM_COMM_RCCL;
     ncclComm_t comm = nullptr;
     int rank = 0, nranks = 1;
+    // SWARM_COMM_SHM
+    void *base = nullptr;
+    size_t bytes = 0;
+    swarm::ShmHeader *hdr = nullptr;
+    uint64_t ops = 0;                // ops issued (every rank issues the same sequence): parity
+    double timeout_s = 120.0;
 };
 
 namespace swarm {
@@ -84,6 +120,149 @@ __global__ __launch_bounds__(kBlock) void k_pack(const int32_t *__restrict__ L, 
     }
 }
 
+// ---- shared-memory transport
+char *shm_box(swarm_comm *c, int rank, uint64_t parity) {
+    return static_cast<char *>(c->base) + kShmHeader + (size_t(rank) * 2 + parity) * c->hdr->cap;
+}
+
+// Process-shared generation barrier with a deadline (a peer that died must not hang the rest).
+int shm_barrier(swarm_comm *c) {
+    ShmHeader *h = c->hdr;
+    const uint32_t g = h->gen.load(std::memory_order_acquire);
+    if (h->arrived.fetch_add(1, std::memory_order_acq_rel) == uint32_t(c->nranks) - 1) {
+        h->arrived.store(0, std::memory_order_relaxed);
+        h->gen.fetch_add(1, std::memory_order_release);
+        return SWARM_OK;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t spin = 0; h->gen.load(std::memory_order_acquire) == g; ++spin) {
+        if (h->abort.load(std::memory_order_relaxed)) {
+            set_error("shared-memory transport: a peer gave up");
+            return SWARM_ERR_HIP;
+        }
+        if ((spin & 255) == 255) {
+            const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            if (dt > c->timeout_s) {
+                h->abort.store(1, std::memory_order_relaxed);
+                set_error("shared-memory transport: barrier timed out after %.0f s (a peer is gone?)", dt);
+                return SWARM_ERR_HIP;
+            }
+            sched_yield();
+        }
+    }
+    return SWARM_OK;
+}
+
+// Halo exchange over the mailboxes: this rank's to-lo buffer goes in the first half of its mailbox,
+// its to-hi buffer in the second; the ghosts from below are the lower peer's to-hi half.
+int shm_halo(swarm_comm *c, const int32_t *s_lo, int64_t n_s_lo, int peer_lo, int32_t *r_lo, int64_t n_r_lo,
+             const int32_t *s_hi, int64_t n_s_hi, int peer_hi, int32_t *r_hi, int64_t n_r_hi, hipStream_t s) {
+    const uint64_t par = c->ops++ & 1;
+    const uint64_t half = c->hdr->cap / 2;
+    SW_ARG(uint64_t(std::max({n_s_lo, n_s_hi, n_r_lo, n_r_hi})) * 4 <= half,
+           "halo larger than the shared-memory mailboxes (raise SWARM_SHM_MB)");
+    char *mine = shm_box(c, c->rank, par);
+    if (n_s_lo) SW_HIP(hipMemcpyAsync(mine, s_lo, size_t(n_s_lo) * 4, hipMemcpyDeviceToHost, s));
+    if (n_s_hi) SW_HIP(hipMemcpyAsync(mine + half, s_hi, size_t(n_s_hi) * 4, hipMemcpyDeviceToHost, s));
+    SW_HIP(hipStreamSynchronize(s));
+    if (int rc = shm_barrier(c)) return rc;
+    if (n_r_lo) SW_HIP(hipMemcpyAsync(r_lo, shm_box(c, peer_lo, par) + half, size_t(n_r_lo) * 4, hipMemcpyHostToDevice, s));
+    if (n_r_hi) SW_HIP(hipMemcpyAsync(r_hi, shm_box(c, peer_hi, par), size_t(n_r_hi) * 4, hipMemcpyHostToDevice, s));
+    // the mailboxes of this parity are rewritten two ops later, after every rank has passed the
+    // next op's barrier -- which this rank reaches only once its reads here are done
+    SW_HIP(hipStreamSynchronize(s));
+    return SWARM_OK;
+}
+
+int shm_allreduce_u64(swarm_comm *c, unsigned long long *buf, size_t count, bool is_max, hipStream_t s) {
+    const uint64_t par = c->ops++ & 1;
+    SW_ARG(uint64_t(count) * 8 <= c->hdr->cap, "all-reduce larger than the shared-memory mailboxes (raise SWARM_SHM_MB)");
+    SW_HIP(hipMemcpyAsync(shm_box(c, c->rank, par), buf, count * 8, hipMemcpyDeviceToHost, s));
+    SW_HIP(hipStreamSynchronize(s));
+    if (int rc = shm_barrier(c)) return rc;
+    std::vector<unsigned long long> acc(count);
+    memcpy(acc.data(), shm_box(c, 0, par), count * 8);
+    for (int r = 1; r < c->nranks; ++r) {
+        const unsigned long long *q = reinterpret_cast<const unsigned long long *>(shm_box(c, r, par));
+        for (size_t i = 0; i < count; ++i) acc[i] = is_max ? std::max(acc[i], q[i]) : acc[i] + q[i];
+    }
+    SW_HIP(hipMemcpyAsync(buf, acc.data(), count * 8, hipMemcpyHostToDevice, s));
+    SW_HIP(hipStreamSynchronize(s));
+    return SWARM_OK;
+}
+
+int shm_create(swarm_comm *c, const char *name) {
+    const char *mb = getenv("SWARM_SHM_MB");
+    const char *to = getenv("SWARM_SHM_TIMEOUT_S");
+    if (to) c->timeout_s = atof(to);
+    int fd = -1;
+    if (c->rank == 0) {
+        const uint64_t cap = (mb ? uint64_t(atoll(mb)) : 16ull) << 20;
+        c->bytes = kShmHeader + size_t(c->nranks) * 2 * cap;
+        fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+        if (fd < 0) {
+            set_error("shm_open(%s, O_CREAT) failed: %s", name, strerror(errno));
+            return SWARM_ERR_HIP;
+        }
+        if (ftruncate(fd, off_t(c->bytes)) != 0) {
+            set_error("ftruncate(%zu) of the shared-memory segment failed: %s", c->bytes, strerror(errno));
+            close(fd);
+            shm_unlink(name);
+            return SWARM_ERR_OOM;
+        }
+    } else {  // wait for rank 0 to create and size it
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            fd = shm_open(name, O_RDWR, 0600);
+            struct stat st{};
+            if (fd >= 0 && fstat(fd, &st) == 0 && st.st_size >= off_t(kShmHeader)) {
+                c->bytes = size_t(st.st_size);
+                break;
+            }
+            if (fd >= 0) close(fd);
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s) {
+                set_error("shared-memory segment %s never appeared (rank 0 failed?)", name);
+                return SWARM_ERR_HIP;
+            }
+            usleep(1000);
+        }
+    }
+    c->base = mmap(nullptr, c->bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (c->base == MAP_FAILED) {
+        c->base = nullptr;
+        set_error("mmap of the shared-memory segment failed: %s", strerror(errno));
+        if (c->rank == 0) shm_unlink(name);
+        return SWARM_ERR_OOM;
+    }
+    c->hdr = static_cast<ShmHeader *>(c->base);
+    if (c->rank == 0) {
+        new (c->hdr) ShmHeader();
+        c->hdr->arrived.store(0);
+        c->hdr->gen.store(0);
+        c->hdr->abort.store(0);
+        c->hdr->nranks = uint32_t(c->nranks);
+        c->hdr->cap = (c->bytes - kShmHeader) / (size_t(c->nranks) * 2);
+        c->hdr->magic.store(kShmMagic, std::memory_order_release);
+    } else {
+        const auto t0 = std::chrono::steady_clock::now();
+        while (c->hdr->magic.load(std::memory_order_acquire) != kShmMagic) {
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s) {
+                set_error("shared-memory segment %s never initialised", name);
+                return SWARM_ERR_HIP;
+            }
+            usleep(1000);
+        }
+        if (c->hdr->nranks != uint32_t(c->nranks)) {
+            set_error("shared-memory segment %s is for %u ranks, not %d", name, c->hdr->nranks, c->nranks);
+            return SWARM_ERR_ARG;
+        }
+    }
+    int rc = shm_barrier(c);  // everyone has mapped it: the name can go
+    if (c->rank == 0) shm_unlink(name);
+    return rc;
+}
+
 }  // namespace
 
 // Element-wise MAX all-reduce of u64 words in place on the device stream (the auction's
@@ -94,6 +273,7 @@ int comm_allreduce_max_u64(swarm_comm *comm, unsigned long long *buf, size_t cou
         return SWARM_ERR_ARG;
     }
     if (comm->nranks <= 1 || count == 0) return SWARM_OK;
+    if (comm->kind == SWARM_COMM_SHM) return shm_allreduce_u64(comm, buf, count, true, s);
     SW_NCCL(rccl().allReduce(buf, buf, count, ncclUint64, ncclMax, comm->comm, s));
     return SWARM_OK;
 }
@@ -124,6 +304,18 @@ extern "C" {
 
 int swarm_comm_available(void) { return swarm::rccl().ok ? 1 : 0; }
 
+int swarm_comm_unique_id_kind(int kind, void *out128) {
+    using namespace swarm;
+    SW_ARG(out128 != nullptr, "out is NULL");
+    SW_ARG(kind == SWARM_COMM_RCCL || kind == SWARM_COMM_SHM, "unknown transport kind");
+    if (kind == SWARM_COMM_RCCL) return swarm_comm_unique_id(out128);
+    std::random_device rd;
+    char name[128] = {};
+    snprintf(name, sizeof(name), "/swarm-shm-%d-%08x%08x", int(getpid()), unsigned(rd()), unsigned(rd()));
+    memcpy(out128, name, sizeof(name));
+    return SWARM_OK;
+}
+
 int swarm_comm_unique_id(void *out128) {
     using namespace swarm;
     SW_ARG(out128 != nullptr, "out is NULL");
@@ -136,6 +328,29 @@ int swarm_comm_unique_id(void *out128) {
     memcpy(out128, &id, sizeof(id));
     return SWARM_OK;
 }
+
+int swarm_comm_create_kind(swarm_comm **out, int kind, int nranks, int rank, const void *id128) {
+    using namespace swarm;
+    SW_ARG(out && id128, "NULL argument");
+    SW_ARG(kind == SWARM_COMM_RCCL || kind == SWARM_COMM_SHM, "unknown transport kind");
+    SW_ARG(nranks >= 1 && rank >= 0 && rank < nranks, "rank / nranks out of range");
+    if (kind == SWARM_COMM_RCCL) return swarm_comm_create(out, nranks, rank, id128);
+    char name[129] = {};
+    memcpy(name, id128, 128);
+    SW_ARG(name[0] == '/' && strlen(name) > 1, "not a shared-memory transport id (swarm_comm_unique_id_kind)");
+    auto *c = new swarm_comm();
+    c->kind = SWARM_COMM_SHM;
+    c->rank = rank;
+    c->nranks = nranks;
+    if (int rc = shm_create(c, name)) {
+        swarm_comm_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return SWARM_OK;
+}
+
+int swarm_comm_kind(const swarm_comm *comm) { return comm ? comm->kind : -1; }
 
 int swarm_comm_create(swarm_comm **out, int nranks, int rank, const void *id128) {
     using namespace swarm;
@@ -162,6 +377,7 @@ int swarm_comm_create(swarm_comm **out, int nranks, int rank, const void *id128)
 
 int swarm_comm_destroy(swarm_comm *c) {
     if (!c) return SWARM_OK;
+    if (c->base) munmap(c->base, c->bytes);
     if (c->comm && swarm::rccl().ok) (void)swarm::rccl().commDestroy(c->comm);
     delete c;
     return SWARM_OK;
@@ -177,6 +393,14 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sh,
     SW_ARG(sh->own_begin >= 0 && sh->own_begin + sh->n_rows <= sh->n_all, "owned range out of [0, n_all)");
     SW_ARG((sh->peer_lo >= 0 || (sh->n_send_lo == 0 && sh->n_ghost_lo == 0)) &&
            (sh->peer_hi >= 0 || (sh->n_send_hi == 0 && sh->n_ghost_hi == 0)), "halo without a peer");
+    SW_ARG(sh->peer_lo < comm->nranks && sh->peer_hi < comm->nranks, "peer rank out of range");
+    // the ghost ranges are checked here, before any collective: a rank that failed inside the loop
+    // would leave its peers blocked in their next exchange
+    const auto outside = [&](int64_t b, int64_t c) {
+        return c == 0 || (b >= 0 && b + c <= sh->n_all && (b + c <= sh->own_begin || b >= sh->own_begin + sh->n_rows));
+    };
+    SW_ARG(outside(sh->ghost_lo_begin, sh->n_ghost_lo) && outside(sh->ghost_hi_begin, sh->n_ghost_hi),
+           "ghost ranges must lie in [0, n_all) outside the owned rows");
     hipStream_t s = static_cast<hipStream_t>(stream);
     int rc = swarm_frontier_begin_range(ctx, sh->own_begin, sh->n_rows, sh->n_all, sh->init, leader0, leader1, stream);
     if (rc) return rc;
@@ -191,7 +415,12 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sh,
     SW_ALLOC(dtot, ctx, S_ESTATS, size_t(kC) * 8 * kMaxBatch);
     unsigned long long *h = static_cast<unsigned long long *>(pinned(ctx, size_t(kC) * 8 * kMaxBatch));
     if (!h) return SWARM_ERR_OOM;
+    const bool shm = comm->kind == SWARM_COMM_SHM;
     const Rccl &R = rccl();
+    if (!shm && comm->nranks > 1 && !R.ok) {
+        set_error("RCCL not found in the process");
+        return SWARM_ERR_ARG;
+    }
     const int depth = sh->halo_depth > 1 ? sh->halo_depth : 1;
     int found = -1, t = 1, batch = 8;
     std::vector<int64_t> hist;
@@ -207,6 +436,12 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sh,
                                    sh->n_send_lo, sh->send_hi, sh->n_send_hi, s_lo, s_hi);
                 SW_LAUNCHED();
             }
+            if (shm) {
+                if ((rc = shm_halo(comm, s_lo, sh->peer_lo >= 0 ? sh->n_send_lo : 0, sh->peer_lo, r_lo,
+                                   sh->peer_lo >= 0 ? sh->n_ghost_lo : 0, s_hi, sh->peer_hi >= 0 ? sh->n_send_hi : 0,
+                                   sh->peer_hi, r_hi, sh->peer_hi >= 0 ? sh->n_ghost_hi : 0, s)))
+                    return rc;
+            } else {
             SW_NCCL(R.groupStart());
             if (sh->peer_lo >= 0) {
                 if (sh->n_send_lo) SW_NCCL(R.send(s_lo, size_t(sh->n_send_lo), ncclInt32, sh->peer_lo, comm->comm, s));
@@ -217,13 +452,18 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sh,
                 if (sh->n_ghost_hi) SW_NCCL(R.recv(r_hi, size_t(sh->n_ghost_hi), ncclInt32, sh->peer_hi, comm->comm, s));
             }
             SW_NCCL(R.groupEnd());
+            }
             if ((rc = frontier_ghosts_both(ctx, r, sh->row_ptr, sh->col, sh->ghost_lo_begin, sh->n_ghost_lo, r_lo,
                                            sh->ghost_hi_begin, sh->n_ghost_hi, r_hi, leader0, leader1, s)))
                 return rc;
         }
         const int nr = tend - t + 1;
         if ((rc = frontier_round_totals(ctx, t, tend, dtot, s))) return rc;
-        SW_NCCL(R.allReduce(dtot, dtot, size_t(nr) * kC, ncclUint64, ncclSum, comm->comm, s));
+        if (shm) {
+            if (comm->nranks > 1 && (rc = shm_allreduce_u64(comm, dtot, size_t(nr) * kC, false, s))) return rc;
+        } else if (comm->nranks > 1 || comm->comm) {
+            SW_NCCL(R.allReduce(dtot, dtot, size_t(nr) * kC, ncclUint64, ncclSum, comm->comm, s));
+        }
         SW_HIP(hipMemcpyAsync(h, dtot, size_t(nr) * kC * 8, hipMemcpyDeviceToHost, s));
         SW_HIP(hipStreamSynchronize(s));
         for (int r = t; r <= tend; ++r) {

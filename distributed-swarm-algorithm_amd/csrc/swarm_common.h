@@ -54,6 +54,7 @@ enum Slot {
     S_DEFER,          // allocation: guard-band tasks deferred to the libm pass (list + per-task flags)
     S_FPAIRS,         // allocation: the deferred tasks' guard-band pairs (device -> host)
     S_OVR,            // allocation: host libm decisions for those pairs (host -> device)
+    S_PIPE,           // election: pipelined tail's epochs, census, error word
     S_NUM
 };
 
@@ -91,7 +92,6 @@ struct swarm_ctx {
     int64_t step_all = 0;
     int64_t step_lo = 0;           // frontier stepper: the owned rows are [step_lo, step_lo + step_rows)
     const int16_t *step_c16 = nullptr;  // frontier stepper: 16-bit columns of the shard graph, or NULL
-    uint32_t rec_gen = 0;          // record tail: generation of the list entries / marks (records.hip)
     hipStream_t side = nullptr;    // a second stream for work that overlaps the caller's (side_stream)
     hipEvent_t side_ev[2] = {};    // fork / join events
 };

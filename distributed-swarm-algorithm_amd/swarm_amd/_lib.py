@@ -19,7 +19,7 @@ LIB_PATH = os.path.join(HERE, "libswarm.so")
 OK, NOT_CONVERGED = 0, 1
 ERR_ARG, ERR_HIP, ERR_OOM, ERR_RANGE, ERR_STALE = -1, -2, -3, -4, -5
 FOLLOWER, ELECTION_WAIT, LEADER = 1, 2, 3
-ELECT_DENSE, ELECT_FRONTIER, ELECT_TIMED = 0, 1, 0x100
+ELECT_DENSE, ELECT_FRONTIER, ELECT_TIMED, ELECT_PIPE_EARLY, ELECT_NO_PIPE = 0, 1, 0x100, 0x200, 0x400
 ALLOC_AUTO, ALLOC_BINNED, ALLOC_DENSE = 0, 1, 2
 
 # every symbol include/swarm.h declares (tests/test_capi.py checks the two agree)
@@ -58,7 +58,10 @@ class ElectStats(ctypes.Structure):
                 ("gather_ms", ctypes.c_double), ("apply_ms", ctypes.c_double),
                 ("gather_launches", ctypes.c_int64), ("dense_rounds", ctypes.c_int64),
                 ("bytes_total", ctypes.c_double), ("sparse_ms", ctypes.c_double),
-                ("sparse_launches", ctypes.c_int64), ("sparse_bytes", ctypes.c_double)]
+                ("sparse_launches", ctypes.c_int64), ("sparse_bytes", ctypes.c_double),
+                ("pipe_from", ctypes.c_int64), ("pipe_launches", ctypes.c_int64), ("pipe_rounds", ctypes.c_int64),
+                ("pipe_ms", ctypes.c_double), ("pipe_bytes", ctypes.c_double), ("pipe_grid", ctypes.c_int64),
+                ("pipe_reach", ctypes.c_int64)]
 
 
 class AuctionStats(ctypes.Structure):

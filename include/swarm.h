@@ -50,6 +50,9 @@ extern "C" {
 #define SWARM_ELECT_FRONTIER 1 /* dense sweeps while many agents change, then only the agents
                                   marked by last round's risers gather (sparse rounds) */
 #define SWARM_ELECT_TIMED 0x100 /* OR into mode: time every kernel with HIP events (stats) */
+#define SWARM_ELECT_PIPE_EARLY 0x200 /* OR into mode: agent-order marks from the first sparse round, so the
+                                       pipelined tail (k_pipe_rounds) takes over early (tests, A/B) */
+#define SWARM_ELECT_NO_PIPE 0x400    /* OR into mode: no pipelined tail (every round its own launch; A/B) */
 
 /* Allocation execution strategies (all exact). */
 #define SWARM_ALLOC_AUTO 0
@@ -88,6 +91,13 @@ typedef struct swarm_elect_stats {
     double sparse_ms;        /* SWARM_ELECT_TIMED: device time of every launched sparse round */
     int64_t sparse_launches; /* SWARM_ELECT_TIMED: sparse rounds launched (incl. no-ops) */
     double sparse_bytes;     /* algorithmic HBM bytes of the executed sparse rounds */
+    int64_t pipe_from;       /* first round run by the pipelined tail (k_pipe_rounds; 0: none) */
+    int64_t pipe_launches;   /* pipelined launches (each runs a run of rounds in one grid) */
+    int64_t pipe_rounds;     /* rounds 1..rounds_exec run pipelined */
+    double pipe_ms;          /* SWARM_ELECT_TIMED: device time of the pipelined launches */
+    double pipe_bytes;       /* algorithmic HBM bytes of the executed pipelined rounds (as sparse rounds) */
+    int64_t pipe_grid;       /* resident workgroups of the pipelined launches */
+    int64_t pipe_reach;      /* chunks each side a chunk's round waits for */
 } swarm_elect_stats;
 
 const char *swarm_last_error(void);
@@ -242,6 +252,17 @@ int swarm_comm_available(void);
 int swarm_comm_unique_id(void *out128);
 int swarm_comm_create(swarm_comm **out, int nranks, int rank, const void *id128);
 int swarm_comm_destroy(swarm_comm *comm);
+/* Transport kinds.  SWARM_COMM_RCCL: the calls above (one rank per GPU, RCCL over xGMI).
+ * SWARM_COMM_SHM: processes of ONE host, any GPUs (several may share one): the same sharded C loops
+ * (swarm_elect_sharded, swarm_auction_sharded) with every exchange staged through a POSIX shared-memory
+ * segment and a process-shared barrier (synchronous per op; SWARM_SHM_MB mailbox MiB per rank and
+ * parity, default 16; SWARM_SHM_TIMEOUT_S, default 120, before a barrier gives up).  Rank 0 makes the
+ * id (swarm_comm_unique_id_kind), every rank passes the same 128 bytes to swarm_comm_create_kind. */
+#define SWARM_COMM_RCCL 0
+#define SWARM_COMM_SHM 1
+int swarm_comm_unique_id_kind(int kind, void *out128);
+int swarm_comm_create_kind(swarm_comm **out, int kind, int nranks, int rank, const void *id128);
+int swarm_comm_kind(const swarm_comm *comm);
 /* leader0 / leader1: n_all each; after rounds_exec rounds the state is leader[rounds_exec&1].
  * changes_per_round (host, capacity max_rounds): GLOBAL per-round change counts. */
 int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *shard,
