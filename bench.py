@@ -580,9 +580,7 @@ def sharded(args, rank, world, dev):
     dom = shard_roofline(sh, dev)
     fr = torch.tensor([dom["frac"], -dom["frac"]], dtype=torch.float64, device=cdev)
     dist.all_reduce(fr, op=dist.ReduceOp.MAX)
-    path = ("native RCCL loop (swarm_elect_sharded: ncclSend/ncclRecv halo + ncclAllReduce per batch)"
-            if getattr(sh, "_native", None) is not None else
-            f"torch.distributed {dist.get_backend()} halo" + (" (host-staged)" if sh.halo.host_staged else ""))
+    path = _shard_path(sh)
     if rank == 0:
         out = {
             "metric": "agent-rounds/sec (election+allocation) at 10M agents; % of HBM roofline",
@@ -761,7 +759,18 @@ def sharded_auction_row(args, rank, world, dev):
     dist.all_reduce(ms, op=dist.ReduceOp.MAX)
     return {"ms": float(ms[0]), "agents": n_tot, "tasks": len(tx), "gpus": world, "rounds": r.rounds_exec,
             "bids": int(r.bidders.sum()), "converged": r.converged,
-            "path": "native RCCL loop" if getattr(sh, "_native", None) is not None else "per-round torch.distributed"}
+            "path": _shard_path(sh)}
+
+
+def _shard_path(sh):
+    """Which halo path the sharded run took: libswarm's native C loop over RCCL or over the shared-memory
+    transport (gloo rehearsal: processes of one host), or the Python stepper over torch.distributed."""
+    import torch.distributed as dist
+    if getattr(sh, "_native", None) is not None:
+        if getattr(sh.backend, "comm_kind", "rccl") == "shm":
+            return "native C loop over the shared-memory transport (host-staged halo + all-reduce per batch)"
+        return "native RCCL loop (swarm_elect_sharded: ncclSend/ncclRecv halo + ncclAllReduce per batch)"
+    return f"torch.distributed {dist.get_backend()} halo" + (" (host-staged)" if sh.halo.host_staged else "")
 
 
 if __name__ == "__main__":

@@ -134,15 +134,23 @@ __device__ __forceinline__ void flush_stats(const Params &P, unsigned long long 
     if (overflow) atomicAdd(sh + 4, overflow);
 }
 
-// One launch before a round: the stat shards, the deferred counters and won zeroed.
+// One launch before a round: the stat shards, the deferred counters and won zeroed; with a fresh
+// claim table (SWARM_ALLOC_FRESH_CLAIMS, winner != NULL here) every task's winner / util too.
 __global__ __launch_bounds__(kBlock) void k_alloc_init(unsigned long long *__restrict__ stats,
                                                       unsigned long long *__restrict__ dcount,
-                                                      int32_t *__restrict__ won, int64_t n) {
+                                                      int32_t *__restrict__ won, int64_t n,
+                                                      int32_t *__restrict__ winner, double *__restrict__ util,
+                                                      int64_t t) {
     const int64_t i0 = int64_t(blockIdx.x) * kBlock + threadIdx.x, stride = int64_t(gridDim.x) * kBlock;
     for (int64_t i = i0; i < int64_t(kStatShards) * kStatStride; i += stride) stats[i] = 0;
     if (i0 == 0) dcount[0] = dcount[1] = 0;
     if (won)
         for (int64_t i = i0; i < n; i += stride) won[i] = 0;
+    if (winner)
+        for (int64_t i = i0; i < t; i += stride) {
+            winner[i] = -1;
+            util[i] = 0.0;
+        }
 }
 
 // out[0, kNumStats): the shard sums; out[kNumStats] = *dcount (the deferred tasks) when given.  out may
@@ -919,7 +927,7 @@ int alloc_impl(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos
                int64_t t, const double *tpos, const int8_t *treq, double claim_thr, double hysteresis,
                double u_scale, int32_t mode, int32_t *winner, double *util, int32_t *won,
                const int32_t *id_to_index, int64_t id_span, int64_t *nclaim, int64_t *nmsg,
-               swarm_alloc_stats *stats, void *stream, const Grid *ix, const uint32_t *ix_off) {
+               swarm_alloc_stats *stats, void *stream, const Grid *ix, const uint32_t *ix_off, int32_t flags = 0) {
     SW_ARG(ctx != nullptr, "ctx is NULL");
     SW_ARG(n >= 0 && n < (int64_t(1) << 31), "n out of range");
     SW_ARG(t >= 0 && t < (int64_t(1) << 31), "t out of range");
@@ -929,6 +937,8 @@ int alloc_impl(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos
            "unknown mode");
     SW_ARG(n == 0 || (ids && apos && acaps), "NULL agent array");
     SW_ARG(t == 0 || (tpos && treq && winner && util), "NULL task array");
+    SW_ARG((flags & ~(SWARM_ALLOC_TRUST_INDEX | SWARM_ALLOC_FRESH_CLAIMS)) == 0, "unknown flags");
+    const bool fresh = (flags & SWARM_ALLOC_FRESH_CLAIMS) != 0 && t > 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
     unsigned long long *dstats;  // the shards, then the folded stats
     SW_ALLOC(dstats, ctx, S_ASTATS, (size_t(kStatShards) * kStatStride + 8) * 8);
@@ -951,7 +961,8 @@ int alloc_impl(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos
     SW_ALLOC(dbase, ctx, S_DEFER, defer_flag_off + size_t(t) + 64);
     P.D.count = reinterpret_cast<unsigned long long *>(dbase);
     P.D.list = reinterpret_cast<int32_t *>(dbase + defer_list_off);
-    hipLaunchKernelGGL(k_alloc_init, dim3(grid_for(n, kBlock, 2048)), dim3(kBlock), 0, s, dstats, P.D.count, won, n);
+    hipLaunchKernelGGL(k_alloc_init, dim3(grid_for(std::max(n, fresh ? t : 0), kBlock, 2048)), dim3(kBlock), 0, s,
+                       dstats, P.D.count, won, n, fresh ? winner : nullptr, fresh ? util : nullptr, t);
     SW_LAUNCHED();
 
     const bool nothing = (n == 0) || (used == SWARM_ALLOC_BINNED && rc <= 0.0);
@@ -971,21 +982,26 @@ int alloc_impl(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos
         SW_ARG(std::floor(2.0 * rp * ix->inv_cell) + 2.0 <= double(kMaxCells),
                "claim radius spans more than 16 rows of the index's cells (use swarm_allocate)");
         // the staleness check on the side stream, concurrent with the allocation (joined before the
-        // counters are folded).  Measured and rejected: the check as extra workgroups of the
-        // allocation's grid, with the stats folded by the last workgroup through a ticket counter
-        // (one launch and no side stream): 245 us for the grid against ~90 us for the pair.
-        hipStream_t s2;
-        hipEvent_t fork, join;
-        SW_TRY(side_stream(ctx, &s2, &fork, &join));
-        SW_HIP(hipEventRecord(fork, s));
-        SW_HIP(hipStreamWaitEvent(s2, fork, 0));
-        hipLaunchKernelGGL(k_check_index, dim3(grid_for(n, kBlock * kCheckPer, 4096)), dim3(kBlock), 0, s2,
-                           reinterpret_cast<const double2 *>(apos), n, *ix, ix_off, dstats + 7);
-        SW_LAUNCHED();
-        SW_HIP(hipEventRecord(join, s2));
+        // counters are folded) -- skipped when the caller vouches that the positions are the ones the
+        // index was built from (SWARM_ALLOC_TRUST_INDEX: 160 MB of positions not streamed at 10M
+        // agents).  Measured and rejected: the check as extra workgroups of the allocation's grid,
+        // with the stats folded by the last workgroup through a ticket counter (one launch and no
+        // side stream): 245 us for the grid against ~90 us for the pair.
+        const bool check = (flags & SWARM_ALLOC_TRUST_INDEX) == 0;
+        hipStream_t s2 = nullptr;
+        hipEvent_t fork = nullptr, join = nullptr;
+        if (check) {
+            SW_TRY(side_stream(ctx, &s2, &fork, &join));
+            SW_HIP(hipEventRecord(fork, s));
+            SW_HIP(hipStreamWaitEvent(s2, fork, 0));
+            hipLaunchKernelGGL(k_check_index, dim3(grid_for(n, kBlock * kCheckPer, 4096)), dim3(kBlock), 0, s2,
+                               reinterpret_cast<const double2 *>(apos), n, *ix, ix_off, dstats + 7);
+            SW_LAUNCHED();
+            SW_HIP(hipEventRecord(join, s2));
+        }
         cand = Cand{SRC_ROWS, nullptr, ix_off, HashGrid{1.0, 0}, *ix, rp};
         SW_TRY(launch_tasks<PASS_MAIN>(cand, t, n, tpos, treq, ids, apos, acaps, P, s));
-        SW_HIP(hipStreamWaitEvent(s, join, 0));
+        if (check) SW_HIP(hipStreamWaitEvent(s, join, 0));
     } else if (t > 0 && used == SWARM_ALLOC_BINNED) {
         // agents bucketed by hashed cell of side Rp (counting sort, no host round trip)
         const double rp = rc * (1.0 + 1e-9) + 1e-12;
@@ -1160,19 +1176,29 @@ int swarm_cell_index(swarm_ctx *ctx, int64_t n, const double *pos, double cell, 
     return SWARM_OK;
 }
 
-int swarm_allocate_indexed(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos,
-                           const uint32_t *acaps, const swarm_grid *grid, const uint32_t *cell_off, int64_t t,
-                           const double *tpos, const int8_t *treq, double claim_thr, double hysteresis,
-                           double u_scale, int32_t *winner, double *util, int32_t *won,
-                           const int32_t *id_to_index, int64_t id_span, int64_t *nclaim, int64_t *nmsg,
-                           swarm_alloc_stats *stats, void *stream) {
+int swarm_allocate_indexed_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos,
+                              const uint32_t *acaps, const swarm_grid *grid, const uint32_t *cell_off, int64_t t,
+                              const double *tpos, const int8_t *treq, double claim_thr, double hysteresis,
+                              double u_scale, int32_t flags, int32_t *winner, double *util, int32_t *won,
+                              const int32_t *id_to_index, int64_t id_span, int64_t *nclaim, int64_t *nmsg,
+                              swarm_alloc_stats *stats, void *stream) {
     using namespace swarm;
     SW_ARG(grid != nullptr && cell_off != nullptr, "NULL index");
     SW_ARG(grid->ncx >= 1 && grid->ncy >= 1 && grid->inv_cell > 0, "bad grid");
     Grid g;
     memcpy(&g, grid, sizeof(g));
     return alloc_impl(ctx, n, ids, apos, acaps, t, tpos, treq, claim_thr, hysteresis, u_scale, SWARM_ALLOC_BINNED,
-                      winner, util, won, id_to_index, id_span, nclaim, nmsg, stats, stream, &g, cell_off);
+                      winner, util, won, id_to_index, id_span, nclaim, nmsg, stats, stream, &g, cell_off, flags);
+}
+
+int swarm_allocate_indexed(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos,
+                           const uint32_t *acaps, const swarm_grid *grid, const uint32_t *cell_off, int64_t t,
+                           const double *tpos, const int8_t *treq, double claim_thr, double hysteresis,
+                           double u_scale, int32_t *winner, double *util, int32_t *won,
+                           const int32_t *id_to_index, int64_t id_span, int64_t *nclaim, int64_t *nmsg,
+                           swarm_alloc_stats *stats, void *stream) {
+    return swarm_allocate_indexed_ex(ctx, n, ids, apos, acaps, grid, cell_off, t, tpos, treq, claim_thr, hysteresis,
+                                     u_scale, 0, winner, util, won, id_to_index, id_span, nclaim, nmsg, stats, stream);
 }
 
 int swarm_utility(swarm_ctx *ctx, int64_t m, const double *apos, const uint32_t *acaps,

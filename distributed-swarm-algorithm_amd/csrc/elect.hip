@@ -225,45 +225,10 @@ struct Col16 {
 struct Col16A : Col16 {};
 
 
-// How a round reads and writes the state other workgroups hand it (leaders, stamps).
-// AccPlain: plain loads and stores -- one kernel per round, the kernel boundary makes every store
-// visible to the next round.  AccCoh: agent-scope accesses (global_load / global_store ... sc1: L1
-// bypassed, stores written through) for rounds that follow each other INSIDE one launch (the
-// pipelined tail, k_pipe_rounds): every byte one workgroup hands another is stored sc1, drained
-// (s_waitcnt vmcnt(0)) before the epoch flag that publishes it, and loaded sc1 after the consumer's
-// poll of that flag (MI355X_MICROARCH.md, inter-workgroup visibility, the sc1 hand-off form).
-struct AccPlain {
-    template <typename I>
-    static __device__ __forceinline__ int32_t ld(const int32_t *__restrict__ b, I i) { return ld4(b, i); }
-    template <typename I>
-    static __device__ __forceinline__ void st(int32_t *__restrict__ b, I i, int32_t v) { st4(b, i, v); }
-    static __device__ __forceinline__ void mark(uint8_t *a, uint32_t slot, uint8_t s) { a[slot] = s; }
-};
-struct AccCoh {
-    template <typename I>
-    static __device__ __forceinline__ int32_t *at(const int32_t *b, I i) {
-        if constexpr (sizeof(I) == 4)
-            return reinterpret_cast<int32_t *>(const_cast<char *>(reinterpret_cast<const char *>(b)) + (uint32_t(i) << 2));
-        else
-            return const_cast<int32_t *>(b) + i;
-    }
-    template <typename I>
-    static __device__ __forceinline__ int32_t ld(const int32_t *__restrict__ b, I i) {
-        return __hip_atomic_load(at(b, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    template <typename I>
-    static __device__ __forceinline__ void st(int32_t *__restrict__ b, I i, int32_t v) {
-        __hip_atomic_store(at(b, i), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    static __device__ __forceinline__ void mark(uint8_t *a, uint32_t slot, uint8_t s) {
-        __hip_atomic_store(a + slot, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-};
-
 constexpr int kKm = 8;  // marking re-walks: col loads in flight per lane
 
 // Mark col[k] for k = k0, k0 + step, ... < e with kKm loads in flight per batch.
-template <typename Off, typename CT, typename Acc = AccPlain>
+template <typename Off, typename CT>
 __device__ __forceinline__ void mark_row(uint8_t *aw, const StampMap &sm, CT cols, int32_t base, Off k0, Off e,
                                          Off step, uint8_t s) {
     for (Off k = k0; k < e; k += step * kKm) {
@@ -275,7 +240,7 @@ __device__ __forceinline__ void mark_row(uint8_t *aw, const StampMap &sm, CT col
         }
 #pragma unroll
         for (int j = 0; j < kKm; ++j)
-            if (k + step * j < e) Acc::mark(aw, stamp_slot(sm, c[j]), s);
+            if (k + step * j < e) aw[stamp_slot(sm, c[j])] = s;
     }
 }
 
@@ -536,7 +501,7 @@ __device__ __forceinline__ int wave_excl_scan(int c, int &total) {
 // `first`/`step` select this wave's share; risers mark themselves and their neighbours.  Lane
 // `sub` of an agent takes edges b + sub + G*j (interleaved: one load instruction covers G
 // consecutive edges of every agent it serves, so each touches one cache line per agent).
-template <typename Off, int G, int K, bool DIR, typename CT, typename Acc = AccPlain>
+template <typename Off, int G, int K, bool DIR, typename CT>
 __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, CT cols,
                                               const Off *__restrict__ hrp, const int32_t *__restrict__ hcol,
                                               const int32_t *__restrict__ P, int32_t *__restrict__ Q,
@@ -551,7 +516,7 @@ __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, CT col
     // pass, so a pass's chain is columns -> leaders only
     int32_t nv = lst[first + lane / G < total ? first + lane / G : total - 1];
     Off nb = ld4(rp, Ix(nv)), ne = ld4(rp, Ix(nv + 1));
-    int nown = Acc::ld(P, Ix(nv));
+    int nown = ld4(P, Ix(nv));
     for (int base = first; base < total; base += step) {
         const int i = base + lane / G;
         const bool valid = i < total;
@@ -563,7 +528,7 @@ __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, CT col
             nv = lst[i2 < total ? i2 : total - 1];
             nb = ld4(rp, Ix(nv));
             ne = ld4(rp, Ix(nv + 1));
-            nown = Acc::ld(P, Ix(nv));
+            nown = ld4(P, Ix(nv));
         }
         int m = own;
         int c[K];
@@ -572,23 +537,23 @@ __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, CT col
             for (int j = 0; j < K; ++j) c[j] = cols.at32((k + G * j < e) ? k + G * j : e - 1, v & ~63);
             int val[K];
 #pragma unroll
-            for (int j = 0; j < K; ++j) val[j] = Acc::ld(P, Ix(c[j]));
+            for (int j = 0; j < K; ++j) val[j] = ld4(P, Ix(c[j]));
 #pragma unroll
             for (int j = 0; j < K; ++j) m = max(m, val[j]);
         }
         m = group_max<G>(m);
         const bool up = valid && m > own;
-        if (valid && sub == 0) Acc::st(Q, Ix(v), m);
+        if (valid && sub == 0) st4(Q, Ix(v), m);
         if (up) {
-            if (sub == 0) Acc::mark(aw, stamp_slot(sm, v), sw);
+            if (sub == 0) aw[stamp_slot(sm, v)] = sw;
             if (DIR) {  // the agents that hear v
-                mark_row<Off, Col32, Acc>(aw, sm, Col32{hcol}, 0, hrp[v] + sub, hrp[v + 1], Off(G), sw);
+                mark_row<Off>(aw, sm, Col32{hcol}, 0, hrp[v] + sub, hrp[v + 1], Off(G), sw);
             } else if (e - b <= G * K) {  // one pass: c[] still holds this lane's edges
 #pragma unroll
                 for (int j = 0; j < K; ++j)
-                    if (b + sub + G * j < e) Acc::mark(aw, stamp_slot(sm, c[j]), sw);
+                    if (b + sub + G * j < e) aw[stamp_slot(sm, c[j])] = sw;
             } else {
-                mark_row<Off, CT, Acc>(aw, sm, cols, v & ~63, b + sub, e, Off(G), sw);
+                mark_row<Off>(aw, sm, cols, v & ~63, b + sub, e, Off(G), sw);
             }
         }
         my_chg += __popcll(__ballot(up && sub == 0 && v >= c_lo && v < n_count));
@@ -767,243 +732,6 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
 #endif
 }
 
-// ------------------------------------------------------------------ pipelined tail rounds
-// Late in an election a sparse round is a short dependent chain (stamps -> list -> row bounds ->
-// columns -> leaders -> write + marks) behind a kernel boundary, and every round waits for the
-// whole device: the boundary is a global barrier.  In the agent-order stamp layout (the tail's) a
-// chunk of C consecutive agents is marked only by risers within `reach` chunks of it, and its
-// round t+1 reads leaders only from agents within `reach` chunks.  So the tail needs no global
-// barrier at all, only a local one: k_pipe_rounds runs rounds t0..t1 in ONE launch of G resident
-// workgroups (workgroup b owns the chunks b, b + G, ...), and workgroup b starts round t once the
-// workgroups b - reach .. b + reach (mod G: their chunks are the neighbours of b's) have
-// published round t - 1 in their epoch word.  Exact, as the frontier rounds are: round t of b
-// reads its agents' neighbours from L[(t-1) & 1] after their owners published round t - 1, and
-// an owner writes that buffer again only in round t + 1, which it starts after b has published
-// round t (the relation is symmetric); a chunk's stamps of parity t are read (and zeroed) by its
-// owner in round t and written again only by round t + 1's risers, who start after the owner
-// has published round t.  Workgroups farther apart run different rounds at the same time.
-// Hand-offs: leaders, marks and zeroed stamp words are stored sc1 and drained before the epoch
-// store; leaders and stamps are loaded sc1 (AccCoh).  Row offsets and columns are read-only.
-// Termination: a census (every workgroup resident, or all leave: nothing done) and bounded waits
-// (a wait past `timeout` sets err and every workgroup leaves at its next wait).
-struct PipeArgs {
-    int *epoch;              // [G] the last round each workgroup finished (k_pipe_init: t0 - 1)
-    unsigned *census;        // 8 shards 32 words apart: workgroups that started (k_pipe_init: 0)
-    unsigned *err;           // 0 ok, 1 not all workgroups resident, 2 a dependency wait timed out
-    int t0, t1;              // rounds of this launch
-    int reach;               // workgroups waited for on each side (2 reach + 1 <= 64)
-    unsigned long long timeout;  // wall_clock64 ticks (100 MHz) a wait may take
-};
-
-constexpr int kPipeCensus = 32;  // u32 stride of the census shards (one 128-B line each)
-
-__device__ __forceinline__ unsigned ld_coh_u32(const unsigned *p) {
-    return __hip_atomic_load(const_cast<unsigned *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint2 ld_coh(const uint2 *p) {
-    const unsigned long long x = __hip_atomic_load(reinterpret_cast<unsigned long long *>(const_cast<uint2 *>(p)),
-                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return make_uint2(uint32_t(x), uint32_t(x >> 32));
-}
-__device__ __forceinline__ uint16_t ld_coh(const uint16_t *p) {
-    return __hip_atomic_load(const_cast<uint16_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void zero_coh(uint2 *p) {
-    __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void zero_coh(uint16_t *p) {
-    __hip_atomic_store(p, uint16_t(0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Wave 0 of workgroup b: wait until the workgroups b - reach .. b + reach (mod G) have published
-// round `need` (lane 63 watches err).  false: abort (err set here on a timeout, or by another).
-__device__ __forceinline__ bool pipe_wait(const PipeArgs &a, int need, int G, int b) {
-    const int lane = threadIdx.x & 63;
-    const int span = 2 * a.reach + 1;
-    const int w = ((b - a.reach + lane) % G + G) % G;  // reach may exceed G on tiny grids
-    const bool watch = lane < span && lane != a.reach && w != b;
-    const unsigned long long t_start = wall_clock64();
-    for (;;) {
-        const int ep = watch ? __hip_atomic_load(a.epoch + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : INT_MAX;
-        const unsigned e = lane == 63 ? ld_coh_u32(a.err) : 0u;
-        if (__ballot(e != 0)) return false;
-        if (__ballot(ep < need) == 0) return true;
-        if (wall_clock64() - t_start > a.timeout) {
-            if (lane == 0) atomicMax(a.err, 2u);
-            return false;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-}
-
-// Wave 0: every workgroup of the grid has started (so every later wait can be met).
-__device__ __forceinline__ bool pipe_census(const PipeArgs &a, int G) {
-    const int lane = threadIdx.x & 63;
-    if (lane == 0) atomicAdd(a.census + (blockIdx.x & 7) * kPipeCensus, 1u);
-    const unsigned long long t_start = wall_clock64();
-    for (;;) {
-        const unsigned c = lane < 8 ? ld_coh_u32(a.census + lane * kPipeCensus) : 0u;
-        const unsigned e = lane == 63 ? ld_coh_u32(a.err) : 0u;
-        if (__ballot(e != 0)) return false;
-        int tot = int(c);
-#pragma unroll
-        for (int o = 4; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
-        if (__shfl(tot, 0, 64) >= G) return true;
-        if (wall_clock64() - t_start > a.timeout) {
-            if (lane == 0) atomicMax(a.err, 1u);
-            return false;
-        }
-        __builtin_amdgcn_s_sleep(2);
-    }
-}
-
-template <typename Off, int S = kScan, typename CT = Col32, int G = kG, int K = kKs>
-__global__ __launch_bounds__(kBlock, 4) void k_pipe_rounds(const Off *__restrict__ rp, CT cols, Frontier f,
-                                                          PipeArgs a) {
-    using W = typename StampWord<S>::T;
-    constexpr int kChunk = kBlock * S;
-    __shared__ int s_list[kListCap];
-    __shared__ int s_wave[kWavesPerBlock];
-    __shared__ long long s_red[3][kWavesPerBlock];
-    __shared__ int s_abort;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int NGi = int(gridDim.x), b = int(blockIdx.x);
-    if (wid == 0) {
-        const bool ok = pipe_census(a, NGi);
-        if (lane == 0) s_abort = ok ? 0 : 1;
-    }
-    __syncthreads();
-    if (s_abort) return;
-    const int64_t n = f.n_rows;
-    const int64_t nchunks = f.sm.M;
-    const int64_t NG = NGi;
-    const int j0 = threadIdx.x * S;
-    constexpr int kPre = 32 / S < 4 ? 32 / S : 4;
-    constexpr int kLogS = S == 8 ? 3 : 1;
-    for (int t = a.t0; t <= a.t1; ++t) {
-        if (t > a.t0) {  // round t0 - 1 is complete everywhere (the previous launch)
-            if (wid == 0) {
-                const bool ok = pipe_wait(a, t - 1, NGi, b);
-                if (lane == 0) s_abort = ok ? 0 : 1;
-            }
-            __syncthreads();
-            if (s_abort) return;
-        }
-        const int32_t *__restrict__ P = f.L[(t - 1) & 1];
-        int32_t *__restrict__ Q = f.L[t & 1];
-        uint8_t *ar = f.act[t & 1], *aw = f.act[(t + 1) & 1];
-        const unsigned stamp4 = unsigned(stamp_of(t)) * 0x01010101u;
-        const uint8_t sw = stamp_of(t + 1);
-        long long my_chg = 0;
-        int my_act = 0, my_edges = 0;
-        int listed = 0;
-        for (int64_t cg = b; cg < nchunks; cg += NG * kPre) {
-            W wv[kPre];
-#pragma unroll
-            for (int p = 0; p < kPre; ++p) {
-                const int64_t chunk = cg + p * NG < nchunks ? cg + p * NG : cg;
-                wv[p] = ld_coh(reinterpret_cast<const W *>(ar + chunk * kChunk + uint32_t(threadIdx.x * sizeof(W))));
-            }
-            unsigned masks = 0;
-#pragma unroll
-            for (int p = 0; p < kPre; ++p) {
-                const int64_t chunk = cg + p * NG;
-                if (chunk < nchunks) {
-                    masks |= take_stamps<S>(stamp_agent(f.sm, chunk, j0), n, wv[p], stamp4) << (p * S);
-                    // consumed: parity t of this chunk is written again only by round t + 1's risers,
-                    // who start after this workgroup has published round t
-                    if (any_stamp(wv[p]))
-                        zero_coh(reinterpret_cast<W *>(ar + chunk * kChunk + uint32_t(threadIdx.x * sizeof(W))));
-                }
-            }
-            for (;;) {
-                const int cnt = __popc(masks);
-                int wtot;
-                const int excl = wave_excl_scan<6>(cnt, wtot);
-                if (lane == 0) s_wave[wid] = wtot;
-                __syncthreads();
-                int off = 0, total = 0;
-#pragma unroll
-                for (int w = 0; w < kWavesPerBlock; ++w) {
-                    off += (w < wid) ? s_wave[w] : 0;
-                    total += s_wave[w];
-                }
-                __syncthreads();
-                if (total == 0) break;
-                int pos = listed + off + excl;
-                while (masks && pos < kListCap) {
-                    const int bit = __ffs(masks) - 1;
-                    masks &= masks - 1;
-                    s_list[pos++] = int(stamp_agent(f.sm, cg + (bit >> kLogS) * NG, j0)) + (bit & (S - 1));
-                }
-                listed = listed + total < kListCap ? listed + total : kListCap;
-                __syncthreads();
-                if (listed < kListCap) break;
-                gather_listed<Off, G, K, false, CT, AccCoh>(rp, cols, nullptr, nullptr, P, Q, aw, f.wsm, sw, s_list,
-                                                            listed, wid * (64 / G), kBlock / G, f.c_lo, f.n_count,
-                                                            my_chg, my_act, my_edges);
-                listed = 0;
-                __syncthreads();
-            }
-        }
-        if (listed > 0)
-            gather_listed<Off, G, K, false, CT, AccCoh>(rp, cols, nullptr, nullptr, P, Q, aw, f.wsm, sw, s_list, listed,
-                                                        wid * (64 / G), kBlock / G, f.c_lo, f.n_count, my_chg, my_act,
-                                                        my_edges);
-        flush_counts(f.ring, t, my_chg, my_act, my_edges, s_red);
-        // publish round t: every wave's stores drained, then one flag store
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) __hip_atomic_store(a.epoch + b, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-// Before a pipelined launch of rounds t0..t1: their counter slots zeroed (the sparse rounds'
-// bookkeeping recycles slots a round at a time; the pipelined rounds do not), epochs = t0 - 1,
-// census and err zeroed.
-__global__ __launch_bounds__(kBlock) void k_pipe_init(unsigned long long *__restrict__ ring, int t0, int t1,
-                                                     int *__restrict__ epoch, int G, unsigned *__restrict__ census,
-                                                     unsigned *__restrict__ err) {
-    const int64_t per = int64_t(kCounters) * kShards;
-    const int64_t total = int64_t(t1 - t0 + 1) * per;
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < total; i += int64_t(gridDim.x) * kBlock) {
-        const int r = t0 + int(i / per);
-        const int c = int((i % per) / kShards), sh = int(i % kShards);
-        *slot(ring, r, c, sh) = 0;
-    }
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < G; i += int64_t(gridDim.x) * kBlock)
-        epoch[i] = t0 - 1;
-    if (blockIdx.x == 0 && threadIdx.x < 8) census[threadIdx.x * kPipeCensus] = 0;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *err = 0;
-}
-
-// max |col16[k]| over the compact columns (the graph's reach in storage slots from a row's 64-agent
-// base), by wave reductions and one atomicMax per wave.
-__global__ __launch_bounds__(kBlock) void k_col16_reach(const int16_t *__restrict__ c16, int64_t e, int aligned,
-                                                       unsigned *__restrict__ out) {
-    int m = 0;
-    const int64_t nv = aligned ? e / 8 : 0;  // 16-byte loads only from a 16-byte aligned array
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < nv; i += int64_t(gridDim.x) * kBlock) {
-        const int4 q = reinterpret_cast<const int4 *>(c16)[i];
-        const int w[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            m = max(m, abs(int(int16_t(w[j] & 0xffff))));
-            m = max(m, abs(w[j] >> 16));
-        }
-    }
-    for (int64_t k = nv * 8 + int64_t(blockIdx.x) * kBlock + threadIdx.x; k < e; k += int64_t(gridDim.x) * kBlock)
-        m = max(m, abs(int(c16[k])));
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
-    if ((threadIdx.x & 63) == 0 && m) atomicMax(out, unsigned(m));
-}
-
-// err word -> mapped host memory (read with the batch's counters)
-__global__ void k_pipe_err(const unsigned *__restrict__ err, unsigned long long *__restrict__ dst) {
-    *dst |= *err;
-}
-
 // Sharded runs: halo values for ghosts [b_lo, b_lo + n_lo) and [b_hi, b_hi + n_hi) after round
 // t.  A ghost whose leader rose is written to BOTH leader buffers (ghosts are never gathered)
 // and its local neighbours are marked for round t+1 (ghost rows of the local CSR list them).
@@ -1102,17 +830,11 @@ struct Tuning {
     int dense_flat = 1;       // dense rounds gather leaders 64 consecutive edges per load (FLAT)
     int dense_vec = 1;        // FLAT with 16-bit columns: 8 columns per lane per 16-byte load
     int use_c16 = 1;          // swarm_elect_compact reads the 16-bit columns (0: its int32 ones; A/B aid)
-    int pipe = 1;             // pipelined tail rounds (k_pipe_rounds) once the marks are in agent order
-    int pipe_per_cu = 4;      // resident workgroups per CU of the pipelined launch (<= the occupancy)
-    int pipe_timeout_ms = 200; // a pipelined wait longer than this aborts the launch (SWARM_ERR_HIP)
     int il_min_changes = -1;   // interleaved stamp layout while the last read round changed >= this
                                // (-1: 8e-4 x agents, measured best at 100k, 1M and 10M agents)
     Tuning() {
         il_min_changes = env_int("SWARM_IL_MIN_CHANGES", -1);
         use_c16 = env_int("SWARM_C16", 1);
-        pipe = env_int("SWARM_PIPE", 1);
-        pipe_per_cu = env_int("SWARM_PIPE_PER_CU", 4);
-        pipe_timeout_ms = env_int("SWARM_PIPE_TIMEOUT_MS", 200);
         dense_flat = env_int("SWARM_DENSE_FLAT", 1);
         dense_vec = env_int("SWARM_DENSE_VEC", 1);
         stamp_bshift = env_int("SWARM_STAMP_BSHIFT", 5);
@@ -1298,93 +1020,6 @@ double round_bytes(bool dense, int64_t n, int64_t e, int64_t active, int64_t edg
     return double(n) + 16.0 * active + 8.0 * edges;
 }
 
-// ------------------------------------------------------------------ pipelined tail (host side)
-// S_PIPE layout: reach word (k_col16_reach), err word, census shards, epochs.
-constexpr size_t kPipeReachOff = 0, kPipeErrOff = 64, kPipeCensusOff = 128;
-constexpr size_t kPipeEpochOff = kPipeCensusOff + 8 * kPipeCensus * 4;
-constexpr int kPipeMaxG = 4096;
-constexpr size_t kPipeBytes = kPipeEpochOff + size_t(kPipeMaxG) * 4;
-
-struct PipeRun {
-    bool started = false;     // reach kernel launched (side stream)
-    bool decided = false, ok = false;
-    int G = 0, reach = 0, from = 0, launches = 0;
-    uint8_t *base = nullptr;
-    hipStream_t side = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-};
-
-// Launch the reach scan (max |col16|) on the ctx's side stream, overlapping the dense rounds.
-int pipe_start(swarm_ctx *ctx, PipeRun &p, const int16_t *c16, int64_t e, hipStream_t s) {
-    SW_ALLOC(p.base, ctx, S_PIPE, kPipeBytes);
-    int rc = side_stream(ctx, &p.side, &p.fork, &p.join);
-    if (rc) return rc;
-    SW_HIP(hipEventRecord(p.fork, s));
-    SW_HIP(hipStreamWaitEvent(p.side, p.fork, 0));
-    unsigned *rw = reinterpret_cast<unsigned *>(p.base + kPipeReachOff);
-    SW_HIP(hipMemsetAsync(rw, 0, 4, p.side));
-    if (e > 0) {
-        hipLaunchKernelGGL(k_col16_reach, dim3(grid_for(e / 8 + 1, kBlock, 2048)), dim3(kBlock), 0, p.side, c16, e,
-                           int((reinterpret_cast<uintptr_t>(c16) & 15) == 0), rw);
-        SW_LAUNCHED();
-    }
-    SW_HIP(hipEventRecord(p.join, p.side));
-    p.started = true;
-    return SWARM_OK;
-}
-
-// First eligible batch: the reach in chunks (a chunk's neighbours lie within `reach` chunks), the
-// resident grid.  ok = false keeps the sparse rounds (reach too long for one wave's watch list).
-template <typename Off>
-int pipe_decide(PipeRun &p, const StampMap &ag, int64_t n) {
-    p.decided = true;
-    unsigned D = 0;
-    SW_HIP(hipMemcpyAsync(&D, p.base + kPipeReachOff, 4, hipMemcpyDeviceToHost, p.side));
-    SW_HIP(hipStreamSynchronize(p.side));
-    const int64_t C = int64_t(1) << ag.cshift;
-    const int64_t reach = (int64_t(D) + 63 + C - 1) / C;  // |v - c| <= |c - (v & ~63)| + 63
-    if (2 * reach + 1 > 63) return SWARM_OK;
-    int dev = 0, ncu = 0, nb = 0;
-    SW_HIP(hipGetDevice(&dev));
-    SW_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    if (ag.cshift == 11)
-        SW_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pipe_rounds<Off, 8, Col16>, kBlock, 0));
-    else
-        SW_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pipe_rounds<Off, 2, Col16>, kBlock, 0));
-    const int per = std::min(nb, tuning().pipe_per_cu);
-    if (per < 1 || ncu < 1) return SWARM_OK;
-    p.G = int(std::min<int64_t>({int64_t(per) * ncu, int64_t(ag.M), int64_t(kPipeMaxG)}));
-    p.reach = int(reach);
-    p.ok = p.G >= 1;
-    (void)n;
-    return SWARM_OK;
-}
-
-// Rounds t0..t1 (t1 - t0 < kRing / 2) as one pipelined launch; its err word is OR-ed into *herr_dev.
-template <typename Off>
-int pipe_launch(PipeRun &p, const Off *rp, const int16_t *c16, Frontier f, const StampMap &ag, int t0, int t1,
-                unsigned long long *herr_dev, hipStream_t s) {
-    int *epoch = reinterpret_cast<int *>(p.base + kPipeEpochOff);
-    unsigned *census = reinterpret_cast<unsigned *>(p.base + kPipeCensusOff);
-    unsigned *err = reinterpret_cast<unsigned *>(p.base + kPipeErrOff);
-    if (!p.launches) SW_HIP(hipStreamWaitEvent(s, p.join, 0));  // the reach scan is done with S_PIPE
-    hipLaunchKernelGGL(k_pipe_init, dim3(grid_for(int64_t(t1 - t0 + 1) * kCounters * kShards, kBlock, 256)),
-                       dim3(kBlock), 0, s, f.ring, t0, t1, epoch, p.G, census, err);
-    SW_LAUNCHED();
-    f.sm = f.wsm = ag;
-    const PipeArgs pa{epoch, census, err, t0, t1, p.reach,
-                      (unsigned long long)tuning().pipe_timeout_ms * 100000ull};
-    if (ag.cshift == 11)
-        hipLaunchKernelGGL((k_pipe_rounds<Off, 8, Col16>), dim3(p.G), dim3(kBlock), 0, s, rp, Col16{c16}, f, pa);
-    else
-        hipLaunchKernelGGL((k_pipe_rounds<Off, 2, Col16>), dim3(p.G), dim3(kBlock), 0, s, rp, Col16{c16}, f, pa);
-    SW_LAUNCHED();
-    hipLaunchKernelGGL(k_pipe_err, dim3(1), dim3(1), 0, s, err, herr_dev);
-    SW_LAUNCHED();
-    ++p.launches;
-    return SWARM_OK;
-}
-
 template <typename Off>
 int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, const int32_t *ids,
                int32_t *leader, uint8_t *state, int32_t max_rounds, int32_t mode,
@@ -1396,8 +1031,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     SW_ARG(n < (int64_t(1) << 31), "n must be < 2^31");
     SW_ARG(max_rounds >= 1, "max_rounds < 1");
     const bool timed = (mode & SWARM_ELECT_TIMED) != 0;
-    const bool pipe_early = (mode & SWARM_ELECT_PIPE_EARLY) != 0, no_pipe = (mode & SWARM_ELECT_NO_PIPE) != 0;
-    mode &= ~(SWARM_ELECT_TIMED | SWARM_ELECT_PIPE_EARLY | SWARM_ELECT_NO_PIPE);
+    mode &= ~SWARM_ELECT_TIMED;
     SW_ARG(mode == SWARM_ELECT_DENSE || mode == SWARM_ELECT_FRONTIER, "unknown mode");
     SW_ARG(rounds_exec != nullptr, "rounds_exec is NULL");
     SW_ARG(n == 0 || (rp && ids && leader && state), "NULL array (col may be NULL only without edges)");
@@ -1443,19 +1077,9 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     // the per-round totals land in mapped host memory, written by k_batch_totals itself
     void *dmap = nullptr;
     unsigned long long *hbuf =
-        static_cast<unsigned long long *>(mapped(ctx, size_t(kCounters) * 8 * kMaxBatch + 64, &dmap));
+        static_cast<unsigned long long *>(mapped(ctx, size_t(kCounters) * 8 * kMaxBatch, &dmap));
     if (!hbuf) return SWARM_ERR_OOM;
     unsigned long long *dtot = static_cast<unsigned long long *>(dmap);
-    // pipelined tail: its abort flags land in the word after the counters
-    unsigned long long *herr = hbuf + size_t(kCounters) * kMaxBatch, *herr_dev = dtot + size_t(kCounters) * kMaxBatch;
-    *herr = 0;
-    PipeRun pipe;
-    if (mode == SWARM_ELECT_FRONTIER && tuning().pipe && !no_pipe && c16 && !hrp) {
-        int rcp = pipe_start(ctx, pipe, c16, int64_t(e_total), s);
-        if (rcp) return rcp;
-    }
-    double pipe_ms = 0.0, pipe_bytes = 0.0;
-    int64_t pipe_rounds = 0;
 
     int found = -1, t = 1, batch = 8, launched = 0;
     std::vector<int64_t> hist;  // per-round change counts read so far (batch sizing, layout)
@@ -1514,12 +1138,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
             dense_rounds += dn ? 1 : 0;
             const double rbytes = round_bytes(dn, n, int64_t(e_total), act, ed);
             bytes += rbytes;
-            if (pipe.from && r >= pipe.from) {
-                pipe_bytes += rbytes;
-                ++pipe_rounds;
-            } else if (kind == RK_SPARSE) {
-                sp_bytes += rbytes;
-            }
+            if (kind == RK_SPARSE) sp_bytes += rbytes;
             if (rlog)
                 fprintf(rlog, "%d %lld %lld %lld %d %.2f\n", r, (long long)c, (long long)act, (long long)ed,
                         int(kind), timed && r >= t ? ktime[r - t] * 1e3 : 0.0);
@@ -1544,29 +1163,12 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
             return SWARM_OK;
         };
         if (tread <= launched && (rc = enqueue_read())) return rc;
-        // pipelined tail: once the round about to run reads agent-order marks, every remaining round
-        // runs in pipelined launches (split at the read point)
-        bool piped = false;
-        if (pipe.started && t <= tend && plan_round(t) == RK_SPARSE && rd_map.bshift == rd_map.cshift) {
-            if (!pipe.decided && (rc = pipe_decide<Off>(pipe, ag_map, n))) return rc;
-            piped = pipe.ok;
-        }
-        if (piped) {
-            if (!pipe.from) pipe.from = t;
-            if (timed) SW_HIP(hipEventRecord(ev[2 * kMaxBatch], s));
-            const int cut = (tread >= t && tread < tend) ? tread : tend;
-            if ((rc = pipe_launch<Off>(pipe, rp, c16, f, ag_map, t, cut, herr_dev, s))) return rc;
-            if (cut == tread && (rc = enqueue_read())) return rc;
-            if (cut < tend && (rc = pipe_launch<Off>(pipe, rp, c16, f, ag_map, cut + 1, tend, herr_dev, s))) return rc;
-            if (timed) SW_HIP(hipEventRecord(ev[2 * kMaxBatch + 1], s));
-            rd_map = ag_map;
-        }
         // timing: dense rounds (and every round when a per-round log is written) get an event pair
         // each; a batch's run of back-to-back sparse rounds gets ONE pair around it -- events
         // between every launch would add their own cost to each round (rocprof's per-dispatch
         // durations are the reference for this figure)
         int seg_n = 0;  // sparse launches inside this batch's segment
-        for (int r = t; r <= tend && !piped; ++r) {
+        for (int r = t; r <= tend; ++r) {
             const bool sparse = mode == SWARM_ELECT_FRONTIER && plan_round(r) == RK_SPARSE;
             const bool seg = timed && sparse && !rlog;
             if (seg && seg_n++ == 0) SW_HIP(hipEventRecord(ev[2 * kMaxBatch], s));
@@ -1581,7 +1183,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
                 // marks for round r+1: interleaved layout while rounds are busy (balance), agent
                 // order once they are sparse (locality of the few gathers)
                 f.sm = rd_map;
-                f.wsm = (!pipe_early && (hist.empty() || hist.back() >= il_min)) ? il_map : ag_map;
+                f.wsm = (hist.empty() || hist.back() >= il_min) ? il_map : ag_map;
                 rc = launch_frontier_round<Off>(rp, col, f, r, kinds[r - t], 1, s, hrp, hcol);
                 rd_map = f.wsm;
             }
@@ -1592,21 +1194,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         if (seg_n) SW_HIP(hipEventRecord(ev[2 * kMaxBatch + 1], s));
         launched = std::max(launched, tend);
         SW_HIP(hipEventSynchronize(ev_read));
-        if (*herr) {
-            set_error("pipelined election rounds aborted (%s)", (*herr & 2) ? "a dependency wait timed out"
-                                                                          : "not every workgroup was resident");
-            SW_HIP(hipStreamSynchronize(s));
-            return SWARM_ERR_HIP;
-        }
-        if (timed && piped) {
-            SW_HIP(hipStreamSynchronize(s));
-            float x = 0;
-            SW_HIP(hipEventElapsedTime(&x, ev[2 * kMaxBatch], ev[2 * kMaxBatch + 1]));
-            k_ms += x;
-            pipe_ms += x;
-            timed_rounds += tend - t + 1;
-            for (int r = t; r <= tend; ++r) ktime[r - t] = 0.f;
-        } else if (timed) {  // kLook == 0: this batch's rounds are exactly the rounds read
+        if (timed) {  // kLook == 0: this batch's rounds are exactly the rounds read
             SW_HIP(hipStreamSynchronize(s));
             for (int r = t; r <= tend; ++r) {  // every launched round's kernel time (rocprof's view)
                 if (seg_n && kinds[r - t] == RK_SPARSE) continue;  // in the segment
@@ -1657,13 +1245,6 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         st->sparse_ms = sp_ms;
         st->sparse_launches = sp_launches;
         st->sparse_bytes = sp_bytes;
-        st->pipe_from = pipe.from;
-        st->pipe_launches = pipe.launches;
-        st->pipe_rounds = pipe_rounds;
-        st->pipe_ms = pipe_ms;
-        st->pipe_bytes = pipe_bytes;
-        st->pipe_grid = pipe.G;
-        st->pipe_reach = pipe.reach;
     }
     return found > 0 ? SWARM_OK : SWARM_NOT_CONVERGED;
 }

@@ -19,7 +19,8 @@ LIB_PATH = os.path.join(HERE, "libswarm.so")
 OK, NOT_CONVERGED = 0, 1
 ERR_ARG, ERR_HIP, ERR_OOM, ERR_RANGE, ERR_STALE = -1, -2, -3, -4, -5
 FOLLOWER, ELECTION_WAIT, LEADER = 1, 2, 3
-ELECT_DENSE, ELECT_FRONTIER, ELECT_TIMED, ELECT_PIPE_EARLY, ELECT_NO_PIPE = 0, 1, 0x100, 0x200, 0x400
+ELECT_DENSE, ELECT_FRONTIER, ELECT_TIMED = 0, 1, 0x100
+COMM_RCCL, COMM_SHM = 0, 1  # swarm_comm_create_kind transports
 ALLOC_AUTO, ALLOC_BINNED, ALLOC_DENSE = 0, 1, 2
 
 # every symbol include/swarm.h declares (tests/test_capi.py checks the two agree)
@@ -32,7 +33,8 @@ EXPORTS = ("swarm_last_error", "swarm_version", "swarm_ctx_create", "swarm_ctx_d
            "swarm_codec_decode", "swarm_protocol_run", "swarm_auction_begin",
            "swarm_auction_bid", "swarm_auction_resolve", "swarm_auction_sharded", "swarm_cell_index",
            "swarm_allocate_indexed", "swarm_graph_compact", "swarm_elect_compact",
-           "swarm_elect_compact_i64", "swarm_frontier_begin_range", "swarm_frontier_set_compact")
+           "swarm_elect_compact_i64", "swarm_frontier_begin_range", "swarm_frontier_set_compact",
+           "swarm_comm_unique_id_kind", "swarm_comm_create_kind", "swarm_comm_kind")
 
 
 class SwarmError(RuntimeError):
@@ -58,10 +60,7 @@ class ElectStats(ctypes.Structure):
                 ("gather_ms", ctypes.c_double), ("apply_ms", ctypes.c_double),
                 ("gather_launches", ctypes.c_int64), ("dense_rounds", ctypes.c_int64),
                 ("bytes_total", ctypes.c_double), ("sparse_ms", ctypes.c_double),
-                ("sparse_launches", ctypes.c_int64), ("sparse_bytes", ctypes.c_double),
-                ("pipe_from", ctypes.c_int64), ("pipe_launches", ctypes.c_int64), ("pipe_rounds", ctypes.c_int64),
-                ("pipe_ms", ctypes.c_double), ("pipe_bytes", ctypes.c_double), ("pipe_grid", ctypes.c_int64),
-                ("pipe_reach", ctypes.c_int64)]
+                ("sparse_launches", ctypes.c_int64), ("sparse_bytes", ctypes.c_double)]
 
 
 class AuctionStats(ctypes.Structure):
@@ -130,6 +129,9 @@ def load(path: str = LIB_PATH):
         L.swarm_comm_available.argtypes = []
         L.swarm_comm_unique_id.argtypes = [P]
         L.swarm_comm_create.argtypes = [ctypes.POINTER(P), ctypes.c_int, ctypes.c_int, P]
+        L.swarm_comm_unique_id_kind.argtypes = [ctypes.c_int, P]
+        L.swarm_comm_create_kind.argtypes = [ctypes.POINTER(P), ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
+        L.swarm_comm_kind.argtypes = [P]
         L.swarm_comm_destroy.argtypes = [P]
         L.swarm_elect_sharded.argtypes = [P, P, ctypes.POINTER(Shard), P, P, i32, ctypes.POINTER(i32), P, P]
         L.swarm_physics_step.argtypes = [P, i64, P, P, P, P, P, P, P, P, i64, P, P, P, d, d, ctypes.POINTER(i64), P]

@@ -292,36 +292,51 @@ class GpuBackend:
                                                   L.ptr(rp), L.ptr(col), L.ptr(leaders[0]), L.ptr(leaders[1]),
                                                   L.stream()))
 
-    # ---- native sharded loop (RCCL on the device stream; see csrc/comm.hip)
+    # ---- native sharded loop (csrc/comm.hip: RCCL on the device stream, or the shared-memory transport)
     def native_comm(self, halo):
-        """A libswarm RCCL communicator over the halo's group (None if unavailable)."""
+        """A libswarm communicator over the halo's group, or None.  A device (nccl) group gets an RCCL
+        communicator; a host-staged (gloo) group whose ranks all run on this host gets the
+        shared-memory transport (SWARM_COMM_SHM: the same C loops, every exchange staged through
+        host memory -- how 2-3 processes sharing one GPU run swarm_elect_sharded).  SWARM_NATIVE_HALO=0
+        disables both (the Python stepper then drives the rounds).  Every rank agrees on the outcome
+        before anything collective is started, and again after the (collective) create."""
         import ctypes
         import os
+        import socket
+        import sys
+        import zlib
         L = self.L
-        if os.environ.get("SWARM_NATIVE_HALO", "1") == "0" or halo.host_staged or halo.world < 2:
+        if os.environ.get("SWARM_NATIVE_HALO", "1") == "0" or halo.world < 2:
             return None
-        if not L.lib().swarm_comm_available():
+        kind = L.COMM_SHM if halo.host_staged else L.COMM_RCCL
+        dev = "cpu" if halo.host_staged else self.device
+        avail = 1 if (kind == L.COMM_SHM or L.lib().swarm_comm_available()) else 0
+        host = zlib.crc32(socket.gethostname().encode()) & 0x7FFFFFFF
+        agree = torch.tensor([avail, host, -host], dtype=torch.int64, device=dev)
+        dist.all_reduce(agree, op=dist.ReduceOp.MIN, group=halo.group)
+        same_host = int(agree[1]) == -int(agree[2])
+        if int(agree[0]) == 0 or (kind == L.COMM_SHM and not same_host):
             return None
-        uid = torch.zeros(128, dtype=torch.uint8, device=self.device)
+        uid = torch.zeros(128, dtype=torch.uint8, device=dev)
         if halo.rank == 0:
             buf = (ctypes.c_uint8 * 128)()
-            L.check(L.lib().swarm_comm_unique_id(ctypes.cast(buf, ctypes.c_void_p)))
+            L.check(L.lib().swarm_comm_unique_id_kind(kind, ctypes.cast(buf, ctypes.c_void_p)))
             uid.copy_(torch.frombuffer(bytearray(buf), dtype=torch.uint8))
         dist.broadcast(uid, src=halo._peer(0), group=halo.group)
         raw = (ctypes.c_uint8 * 128)(*uid.cpu().tolist())
         comm = ctypes.c_void_p()
-        rc = L.lib().swarm_comm_create(ctypes.byref(comm), halo.world, halo.rank, ctypes.cast(raw, ctypes.c_void_p))
-        # every rank must agree on the path: a rank whose RCCL communicator failed makes all of them
-        # take the torch.distributed halo (a MIN over ranks of "ok")
-        ok = torch.tensor([1 if rc == 0 else 0], dtype=torch.int64, device=self.device)
+        rc = L.lib().swarm_comm_create_kind(ctypes.byref(comm), kind, halo.world, halo.rank,
+                                           ctypes.cast(raw, ctypes.c_void_p))
+        # a rank whose communicator failed makes all of them take the torch.distributed halo
+        ok = torch.tensor([1 if rc == 0 else 0], dtype=torch.int64, device=dev)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=halo.group)
         if int(ok.item()) == 0:
             if rc == 0:
                 L.lib().swarm_comm_destroy(comm)
-            import sys
-            print(f"[swarm_amd.dist] native RCCL communicator unavailable ({L.last_error() if rc else 'a peer failed'}):"
+            print(f"[swarm_amd.dist] native communicator unavailable ({L.last_error() if rc else 'a peer failed'}):"
                   " using the torch.distributed halo", file=sys.stderr, flush=True)
             return None
+        self.comm_kind = "rccl" if kind == L.COMM_RCCL else "shm"
         return comm
 
     def elect_sharded(self, comm, sh, max_rounds):

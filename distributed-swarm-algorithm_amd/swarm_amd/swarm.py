@@ -220,24 +220,19 @@ class Swarm:
         return cached[1]
 
     def elect(self, mode: str = "frontier", max_rounds: int = 1 << 16, timed: bool = False,
-              compact: bool = True, wide: bool | None = None, pipe: bool | str = True) -> ElectResult:
+              compact: bool = True, wide: bool | None = None) -> ElectResult:
         """Contract E2 to convergence on the GPU (swarm_elect_compact with the graph's 16-bit
         columns when they fit; swarm_elect_directed when the neighbour lists are not symmetric).
         timed: per-kernel HIP events.  compact=False: the int32-column entry point swarm_elect
         (same results).  wide: int64 row offsets (swarm_elect_i64) -- chosen by itself for
-        graphs of >= 2^30 edges (C5's 100M agents on one GPU: ~1.6e9), True forces it.
-        pipe: the pipelined tail (k_pipe_rounds: the late rounds in one launch, each chunk of agents
-        waiting only for its neighbour chunks' previous round) once the marks are in agent order;
-        "early": agent-order marks from the first sparse round, so it takes over early (tests);
-        False: every round its own launch.  Same results."""
+        graphs of >= 2^30 edges (C5's 100M agents on one GPU: ~1.6e9), True forces it."""
         if self.row_ptr is None:
             raise RuntimeError("no neighbour graph: call build_graph() or set_graph()")
         if wide is None:
             wide = self.n_edges >= (1 << 30) or self.n >= (1 << 30)
         if wide:
-            return self._elect_wide(mode, max_rounds, timed, compact, pipe)
+            return self._elect_wide(mode, max_rounds, timed, compact)
         m = {"dense": _lib.ELECT_DENSE, "frontier": _lib.ELECT_FRONTIER}[mode] | (_lib.ELECT_TIMED if timed else 0)
-        m |= _lib.ELECT_PIPE_EARLY if pipe == "early" else (0 if pipe else _lib.ELECT_NO_PIPE)
         n = self.n
         rounds = ctypes.c_int32(0)
         cap = int(max_rounds)
@@ -272,13 +267,10 @@ class Swarm:
         res.changes_total = st.changes_total
         res.gather_ms, res.apply_ms, res.timed_launches = st.gather_ms, st.apply_ms, st.gather_launches
         res.sparse_ms, res.sparse_launches, res.sparse_bytes = st.sparse_ms, st.sparse_launches, st.sparse_bytes
-        res.pipe_from, res.pipe_launches, res.pipe_rounds = st.pipe_from, st.pipe_launches, st.pipe_rounds
-        res.pipe_ms, res.pipe_bytes, res.pipe_grid, res.pipe_reach = st.pipe_ms, st.pipe_bytes, st.pipe_grid, st.pipe_reach
         res.compact = c16 is not None  # the rounds read the 16-bit columns (2 of the 4 column bytes)
         return res
 
-    def _elect_wide(self, mode: str, max_rounds: int, timed: bool, compact: bool = True,
-                    pipe: bool | str = True) -> ElectResult:
+    def _elect_wide(self, mode: str, max_rounds: int, timed: bool, compact: bool = True) -> ElectResult:
         """swarm_elect_compact_i64 (16-bit columns when they fit) or swarm_elect_i64 over an int64
         copy of row_ptr (kept while row_ptr is unchanged)."""
         if getattr(self, "_hear", None) is not None:
@@ -289,7 +281,6 @@ class Swarm:
             self._rp64 = cached = (key, self.row_ptr.to(torch.int64))
         rp64 = cached[1]
         m = {"dense": _lib.ELECT_DENSE, "frontier": _lib.ELECT_FRONTIER}[mode] | (_lib.ELECT_TIMED if timed else 0)
-        m |= _lib.ELECT_PIPE_EARLY if pipe == "early" else (0 if pipe else _lib.ELECT_NO_PIPE)
         rounds = ctypes.c_int32(0)
         cap = int(max_rounds)
         changes = np.empty(cap, np.int64)
@@ -309,8 +300,6 @@ class Swarm:
         res.changes_total = st.changes_total
         res.gather_ms, res.apply_ms, res.timed_launches = st.gather_ms, st.apply_ms, st.gather_launches
         res.sparse_ms, res.sparse_launches, res.sparse_bytes = st.sparse_ms, st.sparse_launches, st.sparse_bytes
-        res.pipe_from, res.pipe_launches, res.pipe_rounds = st.pipe_from, st.pipe_launches, st.pipe_rounds
-        res.pipe_ms, res.pipe_bytes, res.pipe_grid, res.pipe_reach = st.pipe_ms, st.pipe_bytes, st.pipe_grid, st.pipe_reach
         # the int64-offset DENSE rounds read the int32 columns (elect.hip launch_dense_round takes
         # col16 only with 32-bit offsets): only the frontier's sparse rounds read the 16-bit ones
         res.compact = c16 is not None and mode == "frontier"

@@ -50,9 +50,6 @@ extern "C" {
 #define SWARM_ELECT_FRONTIER 1 /* dense sweeps while many agents change, then only the agents
                                   marked by last round's risers gather (sparse rounds) */
 #define SWARM_ELECT_TIMED 0x100 /* OR into mode: time every kernel with HIP events (stats) */
-#define SWARM_ELECT_PIPE_EARLY 0x200 /* OR into mode: agent-order marks from the first sparse round, so the
-                                       pipelined tail (k_pipe_rounds) takes over early (tests, A/B) */
-#define SWARM_ELECT_NO_PIPE 0x400    /* OR into mode: no pipelined tail (every round its own launch; A/B) */
 
 /* Allocation execution strategies (all exact). */
 #define SWARM_ALLOC_AUTO 0
@@ -91,13 +88,6 @@ typedef struct swarm_elect_stats {
     double sparse_ms;        /* SWARM_ELECT_TIMED: device time of every launched sparse round */
     int64_t sparse_launches; /* SWARM_ELECT_TIMED: sparse rounds launched (incl. no-ops) */
     double sparse_bytes;     /* algorithmic HBM bytes of the executed sparse rounds */
-    int64_t pipe_from;       /* first round run by the pipelined tail (k_pipe_rounds; 0: none) */
-    int64_t pipe_launches;   /* pipelined launches (each runs a run of rounds in one grid) */
-    int64_t pipe_rounds;     /* rounds 1..rounds_exec run pipelined */
-    double pipe_ms;          /* SWARM_ELECT_TIMED: device time of the pipelined launches */
-    double pipe_bytes;       /* algorithmic HBM bytes of the executed pipelined rounds (as sparse rounds) */
-    int64_t pipe_grid;       /* resident workgroups of the pipelined launches */
-    int64_t pipe_reach;      /* chunks each side a chunk's round waits for */
 } swarm_elect_stats;
 
 const char *swarm_last_error(void);
@@ -322,6 +312,20 @@ int swarm_allocate_indexed(swarm_ctx *ctx, int64_t n, const int32_t *ids, const 
                            double hysteresis, double u_scale, int32_t *winner, double *util,
                            int32_t *won, const int32_t *id_to_index, int64_t id_span,
                            int64_t *nclaim, int64_t *nmsg, swarm_alloc_stats *stats, void *stream);
+
+/* swarm_allocate_indexed with flags (same results):
+ *   SWARM_ALLOC_TRUST_INDEX   the caller vouches that apos are the positions swarm_cell_index indexed
+ *                             (unchanged since): no device staleness check (never SWARM_ERR_STALE)
+ *   SWARM_ALLOC_FRESH_CLAIMS  no claim table: winner / util are outputs only, initialised on the
+ *                             device to -1 / 0.0 (what an empty agent.py task_claims table means) */
+#define SWARM_ALLOC_TRUST_INDEX 1
+#define SWARM_ALLOC_FRESH_CLAIMS 2
+int swarm_allocate_indexed_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos,
+                              const uint32_t *acaps, const swarm_grid *grid, const uint32_t *cell_off,
+                              int64_t t, const double *tpos, const int8_t *treq, double claim_thr,
+                              double hysteresis, double u_scale, int32_t flags, int32_t *winner, double *util,
+                              int32_t *won, const int32_t *id_to_index, int64_t id_span,
+                              int64_t *nclaim, int64_t *nmsg, swarm_alloc_stats *stats, void *stream);
 
 /*
  * Exact fp64 utility for m (agent, task) pairs (agent.py:338-347), GPU arithmetic.

@@ -1,11 +1,16 @@
-"""The HIP sharded path across PROCESSES on one GPU (VERDICT r2 item 5).
+"""The HIP sharded path across PROCESSES on one GPU (VERDICT r2 item 5, r3 item 1).
 
 Two (or three) processes share cuda:0 over gloo: each is one rank with the product backend
-(GpuBackend: libswarm's frontier stepper, ghost and allocation kernels), the halo staged through
-host memory (gloo cannot move device tensors; RCCL refuses two ranks on one device, so the native
-RCCL loop is covered by tests/test_native_halo_multigpu.py where >= 2 GPUs exist).  Every rank's
-leaders, rounds and per-round global change counts, and the sharded allocation (winners, claim
-values, conflicts, won counts), must equal the oracle over the union swarm.
+(GpuBackend: libswarm's frontier stepper, ghost and allocation kernels).  RCCL refuses two ranks on
+one device, so the ranks talk through host memory, in two ways:
+  transport "shm"     libswarm's NATIVE sharded C loops (swarm_elect_sharded, swarm_auction_sharded)
+                      over its shared-memory transport (SWARM_COMM_SHM): the batching, the counter
+                      all-reduce, the ghost application order and the convergence decision of the
+                      code that runs over RCCL on a multi-GPU node;
+  transport "python"  SWARM_NATIVE_HALO=0: ShardedSwarm's Python stepper, halo over gloo.
+Every rank's leaders, rounds and per-round global change counts, the sharded allocation (winners,
+claim values, conflicts, won counts) and -- native -- the sharded auction (owners, prices, per-round
+bidders) must equal the oracle over the union swarm.
 """
 import os
 import socket
@@ -34,11 +39,20 @@ def _inputs(kind, world):
     return d
 
 
-def _worker(rank, world, port, out_q, kind, depth):
+def _auction_tasks(kind, world):
+    """The task list every rank passes to the sharded auction (tasks are replicated): all of them."""
+    d = _inputs(kind, world)
+    if kind == "shards":
+        return tuple(np.concatenate([e[k] for e in d]) for k in ("tx", "ty", "treq"))
+    return d["tx"], d["ty"], d["treq"]
+
+
+def _worker(rank, world, port, out_q, kind, depth, transport):
     import sys
     for p in (PKG, ROOT, os.path.join(ROOT, "tests")):
         sys.path.insert(0, p)
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      SWARM_NATIVE_HALO="1" if transport == "shm" else "0")
     import torch
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -60,23 +74,34 @@ def _worker(rank, world, port, out_q, kind, depth):
             tasks = k
         assert isinstance(sh.backend, GpuBackend) and sh.halo.host_staged
         r = sh.elect(check_every=16)
+        native = getattr(sh, "_native", None) is not None
+        assert native == (transport == "shm") and (not native or sh.backend.comm_kind == "shm")
         sh._check_ghosts(sh.leaders[r.rounds_exec & 1])
         res, won, gst = sh.allocate(tx, ty, tq)
+        auc = None
+        if native:  # the native sharded auction over the same transport: agents sharded, tasks replicated
+            a = sh.auction(*_auction_tasks(kind, world), native=True)
+            auc = dict(owner=a.owner_id.cpu().numpy(), price=a.price.cpu().numpy(), bidders=a.bidders,
+                       rounds=a.rounds_exec, ids=sh.ids.cpu().numpy(), assigned=a.assigned.cpu().numpy())
         torch.cuda.synchronize()
         out_q.put(dict(rank=rank, rounds=r.rounds_exec, changes=r.changes, ids=sh.ids.cpu().numpy(),
                        leader=r.leader.cpu().numpy(), state=r.state.cpu().numpy(), winner=res.winner.cpu().numpy(),
                        util=res.util.cpu().numpy(), nmsg=res.nmsg.cpu().numpy(), won=won.cpu().numpy(),
-                       gstats=gst, tasks=tasks, converged=r.converged, ghosts=sh.n_glo + sh.n_ghi))
+                       gstats=gst, tasks=tasks, converged=r.converged, ghosts=sh.n_glo + sh.n_ghi, native=native,
+                       auc=auc))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,kind,depth", [(2, "shards", 16), (2, "global", 4), (3, "global", 16)])
-def test_hip_sharded_processes_match_union_oracle(world, kind, depth, oracle_mod):
+@pytest.mark.parametrize("world,kind,depth,transport", [(2, "shards", 16, "python"), (2, "global", 4, "python"),
+                                                         (3, "global", 16, "python"), (2, "shards", 16, "shm"),
+                                                         (2, "global", 1, "shm"), (3, "global", 16, "shm"),
+                                                         (3, "shards", 4, "shm")])
+def test_hip_sharded_processes_match_union_oracle(world, kind, depth, transport, oracle_mod):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, kind, depth)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, kind, depth, transport)) for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -97,6 +122,7 @@ def test_hip_sharded_processes_match_union_oracle(world, kind, depth, oracle_mod
     lead, _, rounds, changes = oracle_mod.elect(rp, col, ids)
     want = dict(zip(ids.tolist(), lead.tolist()))
     for o in outs:
+        assert o["native"] == (transport == "shm")
         assert o["converged"] and o["rounds"] == rounds and o["ghosts"] > 0
         np.testing.assert_array_equal(o["changes"], changes)
         assert all(want[int(i)] == int(v) for i, v in zip(o["ids"], o["leader"]))
@@ -115,3 +141,15 @@ def test_hip_sharded_processes_match_union_oracle(world, kind, depth, oracle_mod
     for o in outs:
         assert all(won_want[int(i)] == int(w) for i, w in zip(o["ids"], o["won"]))
         assert o["gstats"]["n_claims"] == wa["n_claims"] and o["gstats"]["n_conflicts"] == wa["n_conflicts"]
+    if transport == "shm":  # the native sharded auction equals the one-GPU auction over the union
+        atx, aty, atq = _auction_tasks(kind, world)
+        w = oracle_mod.auction(ids, x, y, caps, atx, aty, atq)
+        own_w = np.where(w["owner"] >= 0, ids[np.maximum(w["owner"], 0)], -1)
+        for o in outs:
+            au = o["auc"]
+            assert au["rounds"] == w["rounds"]
+            np.testing.assert_array_equal(au["bidders"], w["bidders"][: w["rounds"]])
+            np.testing.assert_array_equal(au["owner"], own_w)
+            np.testing.assert_array_equal(au["price"].view(np.uint32), np.asarray(w["price"], np.float32).view(np.uint32))
+            by_id = dict(zip(ids.tolist(), w["assigned"].tolist()))
+            assert all(by_id[int(i)] == int(a) for i, a in zip(au["ids"], au["assigned"]))
