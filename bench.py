@@ -24,6 +24,7 @@ sys.path.insert(0, os.path.join(ROOT, "distributed-swarm-algorithm_amd"))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
+REF_PYTHON_RATE = 65_355.0  # agent-rounds/s, SURVEY.md §6 (reference Python, 1 core)
 
 
 def parse():
@@ -239,6 +240,11 @@ def main():
             # allocation's compulsory 24 B/agent + 36 B/task) over its time
             "hbm_frac_step": (r.bytes_total + 24 * n + 36 * args.tasks)
             / ((t_elect_ms + t_alloc_ms) * 1e-3) / (HBM_PEAK_GBS * 1e9),
+            # the same over SURVEY §8(d)'s per-unit bytes only (12 B per gathered agent + 8 B per edge in
+            # every executed round, dense rounds 12N + 8E + 4; no stamp scan, no second row offset):
+            # the step-level fraction of the north-star target
+            "hbm_frac_step_survey": survey_step_bytes(r, n, e, args.tasks)
+            / ((t_elect_ms + t_alloc_ms) * 1e-3) / (HBM_PEAK_GBS * 1e9),
             # SURVEY §8d's formula, which prices every executed round as a dense round
             # (12N + 8E + 4 bytes): > 1 because the frontier reads only the changing neighbourhoods
             "hbm_frac_step_dense_equivalent": (r.rounds_exec * bytes_round + 24 * n + 36 * args.tasks)
@@ -258,6 +264,12 @@ def main():
                                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                                      "bytes_per_launch": bytes_round, "avg_launch_ms": dense_round_ms,
                                      "agent_rounds_per_s": n / (dense_round_ms * 1e-3)},
+            # the reference Python CPU path (agent.py:263-275 driven as contract E2, one core), as
+            # SURVEY §6 measured it in the build container: the reference does not ship to the GPU box
+            "reference_python": {"value": REF_PYTHON_RATE, "unit": "agent-rounds/s", "cores": 1,
+                                 "source": "SURVEY.md §6: reference election, N=100k RGG deg 15.9, 183 rounds, "
+                                           "280 s on 1 core of the build container (Xeon KVM)",
+                                 "gpu_over_reference_python": value / REF_PYTHON_RATE},
             "build": _lib.provenance(),
             "result_check": check,
             "elect_stats": {"rounds_launched": r.rounds_launched, "active_total": r.active_total,
@@ -651,6 +663,13 @@ def sharded_state_check(sh, r):
     assert fixed_point and state_ok, ("sharded election state is not a fixed point", fixed_point, state_ok)
     return {"fixed_point_all_ranks": fixed_point, "state_consistent_all_ranks": state_ok,
             "rounds_exec": r.rounds_exec, "converged": r.converged}
+
+
+def survey_step_bytes(r, n, e, tasks):
+    """SURVEY §8(d)'s algorithmic bytes of one step: every executed election round at 12 B per
+    gathered agent + 8 B per edge (a dense round gathers all n agents and E edges, + 4 B), and the
+    allocation's compulsory 24 B per agent + 36 B per task."""
+    return (12.0 * r.active_total + 8.0 * r.edges_total + 4.0 * r.dense_rounds + 24.0 * n + 36.0 * tasks)
 
 
 def sparse_round_bytes(active_total, edges_total, dense_rounds, rounds_exec, n, e, launches, compact):

@@ -680,7 +680,13 @@ __global__ __launch_bounds__(kBlock) void k_alloc_dense_tiles(
     if (threadIdx.x == 0 && f) flush_stats(P, 0, 0, (unsigned long long)f, 0, 0);
 }
 
-// One wave per task: walk the record chain over the tile summaries.
+// One wave per task: walk the record chain over the tile summaries.  RESOLVE: the deferred tasks
+// (P.D.list[0, t_count)) with the host's libm decisions for their guard-band pairs (P.D.ov): the
+// claim count corrected by each override, tiles holding an overridden agent always scanned (their
+// summary was computed with the device's decision), the override applied inside them.  The chain
+// stays a walk over tile summaries, where the per-task wave pass over every agent (k_alloc_binned
+// SRC_ALL) would rescan all n agents per chain link once a task's claims overflow its LDS list.
+template <bool RESOLVE>
 __global__ __launch_bounds__(kBlock) void k_alloc_dense_chain(
     int64_t n, int64_t t_count, const double2 *__restrict__ tpos, const int8_t *__restrict__ treq,
     const int32_t *__restrict__ ids, const double2 *__restrict__ apos,
@@ -692,9 +698,10 @@ __global__ __launch_bounds__(kBlock) void k_alloc_dense_chain(
     const int64_t nwaves = (int64_t(gridDim.x) * kBlock) >> 6;
     BlockStats bs;
     __shared__ unsigned long long s_c[kBlock / kWave], s_m[kBlock / kWave], s_b[kBlock / kWave];
-    for (int64_t k = wave; k < t_count; k += nwaves) {
+    for (int64_t kk = wave; kk < t_count; kk += nwaves) {
+        const int64_t k = RESOLVE ? int64_t(P.D.list[kk]) : kk;
         const int rq = treq[k];
-        if (P.D.list && P.D.tflag[k]) {  // a guard-band pair: deferred to the libm pass (SRC_ALL)
+        if (!RESOLVE && P.D.list && P.D.tflag[k]) {  // a guard-band pair: deferred to the libm pass
             if (lane == 0) {
                 P.D.list[atomicAdd(P.D.count, 1ull)] = int32_t(k);
                 bs.bad += bad_req(rq) ? 1 : 0;
@@ -708,6 +715,29 @@ __global__ __launch_bounds__(kBlock) void k_alloc_dense_chain(
         const int *ck = tcnt + k * ntiles;
         long long nclaims = 0;
         for (int64_t a = lane; a < ntiles; a += 64) nclaims += ck[a];
+        uint32_t ov_a = 0, ov_b = 0;
+        int64_t ov_tile = -1;  // RESOLVE: the ID-order tile of override ov_a + lane (lanes < nov)
+        int nov = 0;
+        if (RESOLVE) {
+            ov_a = P.D.ov_off[kk];
+            ov_b = P.D.ov_off[kk + 1];
+            nov = int(ov_b - ov_a);
+            for (uint32_t q = ov_a + lane; q < ov_b; q += 64) {
+                const Override o = P.D.ov[q];
+                const double2 p = apos[o.agent];
+                const bool dev = utility(p.x, p.y, caps[o.agent], tp.x, tp.y, rq, P.u_scale) > P.thr;
+                nclaims += (o.claim ? 1 : 0) - (dev ? 1 : 0);
+                if (q == ov_a + lane) {  // its position in ID order: binary search of its ID
+                    const uint32_t id = uint32_t(ids[o.agent]);
+                    int64_t lo = 0, hi = n - 1;
+                    while (lo < hi) {
+                        const int64_t mid = (lo + hi) >> 1;
+                        if (sorted_ids[mid] < id) lo = mid + 1; else hi = mid;
+                    }
+                    ov_tile = lo / kTileA;
+                }
+            }
+        }
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) nclaims += __shfl_xor(nclaims, off, 64);
         // did the incumbent claim?  (binary search of w0 in the ID-sorted keys)
@@ -720,7 +750,11 @@ __global__ __launch_bounds__(kBlock) void k_alloc_dense_chain(
                 if (v == uint32_t(w0)) {
                     const int32_t i = order[mid];
                     const double2 p = apos[i];
-                    w0_claimed = utility(p.x, p.y, caps[i], tp.x, tp.y, rq, P.u_scale) > P.thr;
+                    const double U = utility(p.x, p.y, caps[i], tp.x, tp.y, rq, P.u_scale);
+                    bool cl = U > P.thr;
+                    float xw = float(U);
+                    if (RESOLVE && guard_flag(U, P.thr)) apply_override(P, ov_a, ov_b, i, cl, xw);
+                    w0_claimed = cl;
                     break;
                 }
                 if (v < uint32_t(w0)) lo = mid + 1; else hi = mid - 1;
@@ -738,7 +772,15 @@ __global__ __launch_bounds__(kBlock) void k_alloc_dense_chain(
             for (int64_t a0 = tstart; a0 < ntiles && found_tile < 0; a0 += 64) {
                 const int64_t a = a0 + lane;
                 const float m = a < ntiles ? mk[a] : -INFINITY;
-                const bool ok = a < ntiles && m != -INFINITY && (!has || double(m) > cur_u + P.h);
+                bool forced = false;  // RESOLVE: a tile with an overridden agent (more than 64: every tile)
+                if (RESOLVE && nov > 0) {
+                    if (nov > 64) {
+                        forced = true;
+                    } else {
+                        for (int q = 0; q < nov; ++q) forced = forced || __shfl(ov_tile, q, 64) == a;
+                    }
+                }
+                const bool ok = a < ntiles && ((m != -INFINITY && (!has || double(m) > cur_u + P.h)) || forced);
                 const unsigned long long b = __ballot(ok);
                 if (b) found_tile = a0 + __ffsll((long long)b) - 1;
             }
@@ -757,7 +799,9 @@ __global__ __launch_bounds__(kBlock) void k_alloc_dense_chain(
                     const double2 p = apos[i];
                     const double U = utility(p.x, p.y, caps[i], tp.x, tp.y, rq, P.u_scale);
                     x = float(U);
-                    ok = U > P.thr && (!has || double(x) > cur_u + P.h);
+                    bool cl = U > P.thr;
+                    if (RESOLVE && guard_flag(U, P.thr)) apply_override(P, ov_a, ov_b, i, cl, x);
+                    ok = cl && (!has || double(x) > cur_u + P.h);
                 }
                 const unsigned long long b = __ballot(ok);
                 if (b) {
@@ -823,6 +867,15 @@ static_assert(sizeof(swarm_grid) == sizeof(Grid), "swarm_grid mirrors the intern
 
 namespace {
 
+// The dense strategy's ID order and tile summaries (the deferred tasks' chains walk them too).
+struct DenseChain {
+    const int32_t *order = nullptr;
+    const uint32_t *sorted_ids = nullptr;
+    int64_t ntiles = 0;
+    const float *tmax = nullptr;
+    const int *tcnt = nullptr;
+};
+
 // A per-task pass's candidate source (SRC_* and what it reads).
 struct Cand {
     int src = SRC_ALL;
@@ -831,6 +884,7 @@ struct Cand {
     HashGrid hg{1.0, 0};
     Grid g{};
     double rp = 0.0;
+    DenseChain dense;  // SRC_ALL from the dense strategy: resolve through k_alloc_dense_chain<true>
 };
 
 template <int SRC, int PASS>
@@ -915,7 +969,15 @@ int resolve_deferred(swarm_ctx *ctx, Params P, const Cand &cand, int64_t deferre
         SW_HIP(hipMemcpyAsync(ob + off_bytes, ov.data(), ov.size() * sizeof(Override), hipMemcpyHostToDevice, s));
     P.D.ov_off = reinterpret_cast<const uint32_t *>(ob);
     P.D.ov = reinterpret_cast<const Override *>(ob + off_bytes);
-    SW_TRY(launch_tasks<PASS_RESOLVE>(cand, deferred, n, tpos, treq, ids, apos, acaps, P, s));
+    if (cand.dense.tmax) {
+        hipLaunchKernelGGL((k_alloc_dense_chain<true>), dim3(grid_for(deferred, kBlock / kWave, 1u << 20)), dim3(kBlock),
+                           0, s, n, deferred, reinterpret_cast<const double2 *>(tpos), treq, ids,
+                           reinterpret_cast<const double2 *>(apos), acaps, cand.dense.order, cand.dense.sorted_ids,
+                           cand.dense.ntiles, cand.dense.tmax, cand.dense.tcnt, P);
+        SW_LAUNCHED();
+    } else {
+        SW_TRY(launch_tasks<PASS_RESOLVE>(cand, deferred, n, tpos, treq, ids, apos, acaps, P, s));
+    }
     SW_HIP(hipStreamSynchronize(s));  // the host vectors above are the copies' sources
     return SWARM_OK;
 }
@@ -1057,15 +1119,17 @@ int alloc_impl(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos
                            reinterpret_cast<const double2 *>(tpos), treq,
                            reinterpret_cast<const double2 *>(apos), acaps, order, ntiles, tmax, tcnt, P);
         SW_LAUNCHED();
-        hipLaunchKernelGGL(k_alloc_dense_chain, dim3(grid_for(t, kBlock / kWave, 1u << 20)), dim3(kBlock), 0, s,
-                           n, t, reinterpret_cast<const double2 *>(tpos), treq, ids,
+        hipLaunchKernelGGL((k_alloc_dense_chain<false>), dim3(grid_for(t, kBlock / kWave, 1u << 20)), dim3(kBlock), 0,
+                           s, n, t, reinterpret_cast<const double2 *>(tpos), treq, ids,
                            reinterpret_cast<const double2 *>(apos), acaps, order, kout, ntiles, tmax,
                            tcnt, P);
         SW_LAUNCHED();
-        // deferred tasks: every agent is a candidate (no radius: rp2 = +inf keeps all finite ones,
-        // the tile kernel's NaN utilities never claim either)
+        // deferred tasks: their guard-band pairs collected over every agent (no radius: rp2 = +inf
+        // keeps all finite ones, the tile kernel's NaN utilities never claim either), then resolved
+        // by the chain kernel over the same tile summaries (k_alloc_dense_chain<true>)
         P.rp2 = INFINITY;
         cand = Cand{SRC_ALL, nullptr, nullptr, HashGrid{1.0, 0}, Grid{}, 0.0};
+        cand.dense = DenseChain{order, kout, ntiles, tmax, tcnt};
     }
     unsigned long long *hs = static_cast<unsigned long long *>(pinned(ctx, 128));
     if (!hs) return SWARM_ERR_OOM;

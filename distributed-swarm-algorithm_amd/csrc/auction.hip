@@ -30,8 +30,10 @@
 //                atomics: no kernel boundary per round.  Same rounds, same results.
 // Per-round bidder counts: 64-way sharded counters in a ring (multi-workgroup rounds), a log
 // written by the tail kernel; the host reads them every batch of rounds.
+#include <algorithm>
 #include <climits>
 #include <cmath>
+#include <cstring>
 #include <vector>
 
 #include "binning.h"
@@ -742,6 +744,104 @@ __global__ __launch_bounds__(kBlock) void k_auc_resolve_ids(AucState s, int worl
     }
 }
 
+// ---- sparse bid exchange of the sharded rounds (round 4).  Each rank's bids of a round travel as
+// a list, not as a dense t-key array: send buffer (u64 words) [0] = this rank's bidders (every
+// unassigned, active agent: the per-round log), [1] = its bids, then cap entries {key, task}.  One
+// all-gather of the (2 + 2 cap)-word buffers; every rank applies every rank's bids to its (zeroed)
+// key array and resolves exactly the tasks that were bid on -- the same keys, owners and prices
+// everywhere, as the dense MAX all-reduce gave.  cap (the host's bound on any rank's bids in a
+// round) is the global bidder count of the last round it read: the global count never grows (a
+// winner displaces at most the owner it replaces), so no rank can bid more.
+constexpr int kBidHdr = 2;
+
+__global__ __launch_bounds__(kBlock) void k_auc_bid_sparse(AucState s, int64_t r, unsigned long long *__restrict__ send,
+                                                          int64_t cap) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = int64_t(gridDim.x) * (kBlock / kWave);
+    unsigned long long nb = 0;
+    for (int64_t a = int64_t(blockIdx.x) * (kBlock / kWave) + (threadIdx.x >> 6); a < s.n; a += nw) {
+        if (s.assigned[a] >= 0 || s.out[a]) continue;  // wave-uniform
+        ++nb;
+        int32_t bk;
+        const unsigned long long kk = wave_bid(s, a, &bk);
+        if (lane == 0) {
+            if (kk == 0) {
+                s.out[a] = 1;
+            } else {
+                const unsigned long long slot = atomicAdd(send + 1, 1ull);
+                if (slot < (unsigned long long)cap) {
+                    send[kBidHdr + 2 * slot] = kk;
+                    send[kBidHdr + 2 * slot + 1] = (unsigned long long)uint32_t(bk);
+                }
+            }
+        }
+    }
+    __shared__ unsigned long long s_nb[kBlock / kWave];
+    if (lane == 0) s_nb[threadIdx.x >> 6] = nb;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long v = 0;
+        for (int w = 0; w < kBlock / kWave; ++w) v += s_nb[w];
+        if (v) atomicAdd(aslot(s.ring, r, blockIdx.x & (kAShards - 1)), v);
+    }
+}
+
+// send[0] <- this rank's bidders of round r (the ring slot, recycled)
+__global__ void k_auc_post_sparse(unsigned long long *ring, int64_t r, unsigned long long *send) {
+    unsigned long long *p = aslot(ring, r, threadIdx.x);
+    unsigned long long v = *p;
+    *p = 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (threadIdx.x == 0) send[0] = v;
+}
+
+// Every rank's bids (recv: world buffers of `words` u64) onto the key array; log[r] = global bidders.
+__global__ __launch_bounds__(kBlock) void k_auc_apply_bids(AucState s, const unsigned long long *__restrict__ recv,
+                                                          int world, int64_t words, int64_t cap, int64_t r,
+                                                          int64_t *__restrict__ log, unsigned *__restrict__ err) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        unsigned long long tot = 0;
+        for (int q = 0; q < world; ++q) tot += recv[q * words];
+        log[r] = int64_t(tot);
+    }
+    for (int q = 0; q < world; ++q) {
+        const unsigned long long *b = recv + q * words;
+        const unsigned long long nb = b[1];
+        if (nb > (unsigned long long)cap) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(err, 1u);
+            continue;
+        }
+        for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < int64_t(nb); i += int64_t(gridDim.x) * kBlock)
+            atomicMax(&s.key[b[kBidHdr + 2 * i + 1]], b[kBidHdr + 2 * i]);
+    }
+}
+
+// Resolve exactly the tasks bid on: the first entry of a task to take its key (atomicExch) resolves
+// it, as k_auc_resolve_ids does for every task; the key array is left zeroed.
+__global__ __launch_bounds__(kBlock) void k_auc_resolve_bids(AucState s, const unsigned long long *__restrict__ recv,
+                                                            int world, int64_t words, int64_t cap) {
+    for (int q = 0; q < world; ++q) {
+        const unsigned long long *b = recv + q * words;
+        const int64_t nb = int64_t(b[1] < (unsigned long long)cap ? b[1] : (unsigned long long)cap);
+        for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < nb; i += int64_t(gridDim.x) * kBlock) {
+            const int64_t k = int64_t(b[kBidHdr + 2 * i + 1]);
+            const unsigned long long kk = atomicExch(&s.key[k], 0ull);
+            if (!kk) continue;
+            const uint32_t w = 0xFFFFFFFFu - static_cast<uint32_t>(kk & 0xFFFFFFFFull);
+            const int32_t prev = s.owner[k];
+            if (prev >= 0) {
+                const int32_t pi = local_index(s, uint32_t(prev));
+                if (pi >= 0) s.assigned[pi] = -1;
+            }
+            s.owner[k] = int32_t(w);
+            const int32_t wi = local_index(s, w);
+            if (wi >= 0) s.assigned[wi] = int32_t(k);
+            s.price[k] = __uint_as_float(static_cast<uint32_t>(kk >> 32));
+        }
+    }
+}
+
 AucState auc_from_ctx(const swarm_ctx *ctx) {
     const AucPersist &p = ctx->auc;
     AucState st{};
@@ -1089,23 +1189,77 @@ int swarm_auction_sharded(swarm_ctx *ctx, swarm_comm *comm, int64_t n, const int
     constexpr int kMaxBatch = 256;
     int64_t *h = static_cast<int64_t *>(pinned(ctx, size_t(kMaxBatch) * 8 + 64));
     if (!h) return SWARM_ERR_OOM;
+    // SWARM_AUCTION_EXCHANGE=dense: the round-3 exchange (one MAX all-reduce of all t task keys per
+    // round); default: the round's bids as lists (k_auc_bid_sparse, one all-gather; see above)
+    static const bool dense_x = [] {
+        const char *e = getenv("SWARM_AUCTION_EXCHANGE");
+        return e && strcmp(e, "dense") == 0;
+    }();
+    unsigned long long *send = nullptr, *recv = nullptr;
+    unsigned *xerr = nullptr;
+    int64_t cap = 0, cap0 = 0;
+    AucState xs{};
+    if (!dense_x) {
+        // the first rounds' bound: the largest shard (a rank bids at most once per agent)
+        unsigned long long *w;
+        SW_ALLOC(w, ctx, S_TMP0, 64);
+        const unsigned long long nn = (unsigned long long)n;
+        SW_HIP(hipMemcpyAsync(w, &nn, 8, hipMemcpyHostToDevice, s));
+        if (int rc = comm_allreduce_max_u64(comm, w, 1, s)) return rc;
+        SW_HIP(hipMemcpyAsync(h, w, 8, hipMemcpyDeviceToHost, s));
+        SW_HIP(hipStreamSynchronize(s));
+        cap0 = cap = std::max<int64_t>(1, h[0]);
+        const size_t words0 = size_t(kBidHdr + 2 * cap0);
+        uint8_t *xb;
+        SW_ALLOC(xb, ctx, S_AUC_LIST, (words0 * size_t(world + 1)) * 8 + 64);
+        send = reinterpret_cast<unsigned long long *>(xb);
+        recv = send + words0;
+        xerr = reinterpret_cast<unsigned *>(recv + words0 * size_t(world));
+        SW_HIP(hipMemsetAsync(xerr, 0, 4, s));
+        xs = auc_from_ctx(ctx);
+        xs.key = keys;
+        xs.owner = owner_id;
+        xs.price = price;
+        xs.assigned = assigned;
+    }
     int64_t r = 1, found = -1, launched = 0, total_bids = 0;
     int batch = 8;
     *rounds_exec = 0;
     while (r <= max_rounds && found < 0) {
         const int64_t rend = (max_rounds - r + 1 < batch) ? max_rounds : r + batch - 1;
+        const int64_t words = kBidHdr + 2 * cap;
         for (int64_t q = r; q <= rend; ++q) {
-            if (int rc = swarm_auction_bid(ctx, q, rank, world, reinterpret_cast<uint64_t *>(keys), price, assigned,
-                                           stream))
-                return rc;
-            if (int rc = comm_allreduce_max_u64(comm, keys, size_t(t + world), s)) return rc;
-            if (int rc = swarm_auction_resolve(ctx, q, world, reinterpret_cast<uint64_t *>(keys), owner_id, price,
-                                               assigned, dlog, stream))
-                return rc;
+            if (dense_x) {
+                if (int rc = swarm_auction_bid(ctx, q, rank, world, reinterpret_cast<uint64_t *>(keys), price,
+                                               assigned, stream))
+                    return rc;
+                if (int rc = comm_allreduce_max_u64(comm, keys, size_t(t + world), s)) return rc;
+                if (int rc = swarm_auction_resolve(ctx, q, world, reinterpret_cast<uint64_t *>(keys), owner_id, price,
+                                                   assigned, dlog, stream))
+                    return rc;
+                continue;
+            }
+            SW_HIP(hipMemsetAsync(send + 1, 0, 8, s));
+            hipLaunchKernelGGL(k_auc_bid_sparse, dim3(grid_for(xs.n, kBlock / kWave, 8192)), dim3(kBlock), 0, s, xs, q,
+                               send, cap);
+            SW_LAUNCHED();
+            hipLaunchKernelGGL(k_auc_post_sparse, dim3(1), dim3(kWave), 0, s, xs.ring, q, send);
+            SW_LAUNCHED();
+            if (int rc = comm_allgather_u64(comm, send, size_t(words), recv, s)) return rc;
+            const unsigned g = grid_for(cap, kBlock, 1024);
+            hipLaunchKernelGGL(k_auc_apply_bids, dim3(g), dim3(kBlock), 0, s, xs, recv, world, words, cap, q, dlog, xerr);
+            SW_LAUNCHED();
+            hipLaunchKernelGGL(k_auc_resolve_bids, dim3(g), dim3(kBlock), 0, s, xs, recv, world, words, cap);
+            SW_LAUNCHED();
         }
         launched = rend;
         SW_HIP(hipMemcpyAsync(h, dlog + r, size_t(rend - r + 1) * 8, hipMemcpyDeviceToHost, s));
+        if (xerr) SW_HIP(hipMemcpyAsync(h + kMaxBatch, xerr, 4, hipMemcpyDeviceToHost, s));
         SW_HIP(hipStreamSynchronize(s));
+        if (xerr && reinterpret_cast<const unsigned *>(h + kMaxBatch)[0]) {
+            set_error("sharded auction: a rank's bids exceeded the exchange bound %lld", (long long)cap);
+            return SWARM_ERR_HIP;
+        }
         for (int64_t q = r; q <= rend; ++q) {
             const int64_t nb = h[q - r];
             if (nb == 0) {
@@ -1115,6 +1269,8 @@ int swarm_auction_sharded(swarm_ctx *ctx, swarm_comm *comm, int64_t n, const int
             if (bidders_per_round) bidders_per_round[q - 1] = nb;
             total_bids += nb;
         }
+        // the global bidder count never grows: the last round read bounds every rank's bids from here
+        if (!dense_x && found < 0) cap = std::max<int64_t>(1, std::min<int64_t>(cap0, h[rend - r]));
         r = rend + 1;
         batch = batch < kMaxBatch ? batch * 2 : kMaxBatch;
     }

@@ -67,6 +67,7 @@ struct Rccl {
     ncclResult_t (*recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*allReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                               hipStream_t) = nullptr;
+    ncclResult_t (*allGather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*groupStart)() = nullptr;
     ncclResult_t (*groupEnd)() = nullptr;
     const char *(*errorString)(ncclResult_t) = nullptr;
@@ -89,11 +90,12 @@ const Rccl &rccl() {
         SW_SYM(send, "ncclSend");
         SW_SYM(recv, "ncclRecv");
         SW_SYM(allReduce, "ncclAllReduce");
+        SW_SYM(allGather, "ncclAllGather");
         SW_SYM(groupStart, "ncclGroupStart");
         SW_SYM(groupEnd, "ncclGroupEnd");
         SW_SYM(errorString, "ncclGetErrorString");
 #undef SW_SYM
-        x.ok = x.getUniqueId && x.commInitRank && x.commDestroy && x.send && x.recv && x.allReduce &&
+        x.ok = x.getUniqueId && x.commInitRank && x.commDestroy && x.send && x.recv && x.allReduce && x.allGather &&
                x.groupStart && x.groupEnd && x.errorString;
         return x;
     }();
@@ -191,6 +193,19 @@ int shm_allreduce_u64(swarm_comm *c, unsigned long long *buf, size_t count, bool
     return SWARM_OK;
 }
 
+int shm_allgather_u64(swarm_comm *c, const unsigned long long *send, size_t count, unsigned long long *recv,
+                      hipStream_t s) {
+    const uint64_t par = c->ops++ & 1;
+    SW_ARG(uint64_t(count) * 8 <= c->hdr->cap, "all-gather larger than the shared-memory mailboxes (raise SWARM_SHM_MB)");
+    SW_HIP(hipMemcpyAsync(shm_box(c, c->rank, par), send, count * 8, hipMemcpyDeviceToHost, s));
+    SW_HIP(hipStreamSynchronize(s));
+    if (int rc = shm_barrier(c)) return rc;
+    for (int r = 0; r < c->nranks; ++r)
+        SW_HIP(hipMemcpyAsync(recv + size_t(r) * count, shm_box(c, r, par), count * 8, hipMemcpyHostToDevice, s));
+    SW_HIP(hipStreamSynchronize(s));
+    return SWARM_OK;
+}
+
 int shm_create(swarm_comm *c, const char *name) {
     const char *mb = getenv("SWARM_SHM_MB");
     const char *to = getenv("SWARM_SHM_TIMEOUT_S");
@@ -275,6 +290,23 @@ int comm_allreduce_max_u64(swarm_comm *comm, unsigned long long *buf, size_t cou
     if (comm->nranks <= 1 || count == 0) return SWARM_OK;
     if (comm->kind == SWARM_COMM_SHM) return shm_allreduce_u64(comm, buf, count, true, s);
     SW_NCCL(rccl().allReduce(buf, buf, count, ncclUint64, ncclMax, comm->comm, s));
+    return SWARM_OK;
+}
+
+// recv[r * count ...] <- rank r's send buffer of count u64 words, for every rank r (device stream).
+int comm_allgather_u64(swarm_comm *comm, const unsigned long long *send, size_t count, unsigned long long *recv,
+                       hipStream_t s) {
+    if (comm == nullptr) {
+        set_error("NULL communicator");
+        return SWARM_ERR_ARG;
+    }
+    if (count == 0) return SWARM_OK;
+    if (comm->nranks <= 1) {
+        SW_HIP(hipMemcpyAsync(recv, send, count * 8, hipMemcpyDeviceToDevice, s));
+        return SWARM_OK;
+    }
+    if (comm->kind == SWARM_COMM_SHM) return shm_allgather_u64(comm, send, count, recv, s);
+    SW_NCCL(rccl().allGather(send, recv, count, ncclUint64, comm->comm, s));
     return SWARM_OK;
 }
 

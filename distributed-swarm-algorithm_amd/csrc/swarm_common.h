@@ -98,6 +98,8 @@ struct swarm_ctx {
 namespace swarm {
 
 int comm_allreduce_max_u64(swarm_comm *comm, unsigned long long *buf, size_t count, hipStream_t s);
+int comm_allgather_u64(swarm_comm *comm, const unsigned long long *send, size_t count, unsigned long long *recv,
+                       hipStream_t s);
 int comm_rank(const swarm_comm *comm, int *rank, int *nranks);
 
 // Returns a device buffer of at least `bytes` for `s` (nullptr + error on failure: the ctx

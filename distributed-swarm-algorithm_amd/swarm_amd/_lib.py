@@ -21,6 +21,7 @@ ERR_ARG, ERR_HIP, ERR_OOM, ERR_RANGE, ERR_STALE = -1, -2, -3, -4, -5
 FOLLOWER, ELECTION_WAIT, LEADER = 1, 2, 3
 ELECT_DENSE, ELECT_FRONTIER, ELECT_TIMED = 0, 1, 0x100
 COMM_RCCL, COMM_SHM = 0, 1  # swarm_comm_create_kind transports
+ALLOC_TRUST_INDEX, ALLOC_FRESH_CLAIMS = 1, 2  # swarm_allocate_indexed_ex flags
 ALLOC_AUTO, ALLOC_BINNED, ALLOC_DENSE = 0, 1, 2
 
 # every symbol include/swarm.h declares (tests/test_capi.py checks the two agree)
@@ -34,7 +35,7 @@ EXPORTS = ("swarm_last_error", "swarm_version", "swarm_ctx_create", "swarm_ctx_d
            "swarm_auction_bid", "swarm_auction_resolve", "swarm_auction_sharded", "swarm_cell_index",
            "swarm_allocate_indexed", "swarm_graph_compact", "swarm_elect_compact",
            "swarm_elect_compact_i64", "swarm_frontier_begin_range", "swarm_frontier_set_compact",
-           "swarm_comm_unique_id_kind", "swarm_comm_create_kind", "swarm_comm_kind")
+           "swarm_comm_unique_id_kind", "swarm_comm_create_kind", "swarm_comm_kind", "swarm_allocate_indexed_ex")
 
 
 class SwarmError(RuntimeError):
@@ -117,6 +118,8 @@ def load(path: str = LIB_PATH):
         L.swarm_utility.argtypes = [P, i64, P, P, P, P, d, P, P]
         L.swarm_cell_index.argtypes = [P, i64, P, d, ctypes.POINTER(Grid), P, i64, ctypes.POINTER(i64), P]
         L.swarm_allocate_indexed.argtypes = [P, i64, P, P, P, ctypes.POINTER(Grid), P, i64, P, P, d, d, d, P, P, P,
+                                             P, i64, P, P, P, P]
+        L.swarm_allocate_indexed_ex.argtypes = [P, i64, P, P, P, ctypes.POINTER(Grid), P, i64, P, P, d, d, d, i32, P, P, P,
                                              P, i64, P, P, P, P]
         L.swarm_build_rgg.argtypes = [P, i64, P, d, P, P, i64, ctypes.POINTER(i64), P]
         L.swarm_cell_order.argtypes = [P, i64, P, d, P, P]

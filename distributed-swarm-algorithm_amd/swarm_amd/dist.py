@@ -112,6 +112,10 @@ def partition(x, y, world: int, rank: int, *, ty=None, min_height: float = 0.0, 
         ids = np.asarray(ids, np.int64)
         icut = id_cuts(ids, world)
         who = np.searchsorted(icut, ids, side="right")
+        counts = np.bincount(who, minlength=world)
+        if world > 1 and (counts == 0).any():
+            raise ValueError(f"ID ranges of equal agent count leave rank(s) {np.nonzero(counts == 0)[0].tolist()} "
+                             f"without agents ({len(ids)} agents, world {world}; repeated IDs?)")
         cuts = np.array([y[who == k].min() for k in range(1, world)], np.float64) if world > 1 else np.zeros(0)
         if not np.array_equal(np.searchsorted(cuts, y, side="right"), who):
             raise ValueError("the ID ranges are not horizontal strips (every agent of range k must lie below every "
@@ -306,8 +310,8 @@ class GpuBackend:
         import sys
         import zlib
         L = self.L
-        if os.environ.get("SWARM_NATIVE_HALO", "1") == "0" or halo.world < 2:
-            return None
+        if os.environ.get("SWARM_NATIVE_HALO", "1") == "0" or halo.world < 2 or not isinstance(halo, Halo):
+            return None  # (test doubles that exchange in-process have no torch.distributed group)
         kind = L.COMM_SHM if halo.host_staged else L.COMM_RCCL
         dev = "cpu" if halo.host_staged else self.device
         avail = 1 if (kind == L.COMM_SHM or L.lib().swarm_comm_available()) else 0

@@ -348,6 +348,7 @@ class Swarm:
                 return None
             _lib.check(rc)
             self._cindex = (g, off)
+            self._cindex_key = pos_key  # the positions it indexed (allocate trusts it while unchanged)
         return self._cindex
 
     def allocate(self, tx, ty, treq, *, winner=None, util=None, claim_thr: float = 20.0,
@@ -357,9 +358,11 @@ class Swarm:
         tpos = self._task_pos(tx, ty)
         tq = _to(treq, torch.int8, dev)
         t = tq.numel()
-        w = (torch.full((t,), -1, dtype=torch.int32, device=dev) if winner is None
+        # no claim table: winner / util are outputs only (the indexed call initialises them on the device)
+        fresh = winner is None and util is None
+        w = (torch.empty(t, dtype=torch.int32, device=dev) if winner is None
              else _to(winner, torch.int32, dev).clone())
-        u = (torch.zeros(t, dtype=torch.float64, device=dev) if util is None
+        u = (torch.empty(t, dtype=torch.float64, device=dev) if util is None
              else _to(util, torch.float64, dev).clone())
         # libswarm zeroes won and writes nclaim / nmsg for every task (one buffer for both)
         won = torch.empty(self.n, dtype=torch.int32, device=dev)
@@ -374,14 +377,18 @@ class Swarm:
         with torch.cuda.device(dev):
             ci = self._cell_index() if self._indexable(mode, claim_thr, u_scale) else None
             rc = _lib.ERR_STALE
-            if ci is not None:  # spatial storage order: no binning pass (swarm_allocate_indexed)
-                # the claim table is updated in place: keep the caller's for a stale-index retry
-                w0 = None if winner is None else w.clone()
-                u0 = None if util is None else u.clone()
-                rc = L.swarm_allocate_indexed(
+            if ci is not None:  # spatial storage order: no binning pass (swarm_allocate_indexed_ex)
+                # the index is trusted while self.pos is the tensor and version it was built from (the
+                # device staleness check runs otherwise); the claim table is updated in place: keep
+                # the caller's for a stale-index retry
+                trusted = getattr(self, "_cindex_key", None) == (self.pos.data_ptr(), self.pos._version)
+                flags = (_lib.ALLOC_TRUST_INDEX if trusted else 0) | (_lib.ALLOC_FRESH_CLAIMS if fresh else 0)
+                w0 = None if winner is None or trusted else w.clone()
+                u0 = None if util is None or trusted else u.clone()
+                rc = L.swarm_allocate_indexed_ex(
                     _lib.ctx(), self.n, p(self.ids), p(self.pos), p(self.caps),
                     ctypes.byref(ci[0]), p(ci[1]), t, p(tpos), p(tq), float(claim_thr),
-                    float(hysteresis), float(u_scale), p(w), p(u), p(won), p(idx),
+                    float(hysteresis), float(u_scale), flags, p(w), p(u), p(won), p(idx),
                     0 if idx is None else idx.numel(), p(nclaim), p(nmsg), ctypes.byref(st),
                     _lib.stream())
                 if rc == _lib.ERR_STALE:  # positions moved since the index: bin them this call
@@ -391,6 +398,9 @@ class Swarm:
                 else:
                     _lib.check(rc)
             if rc == _lib.ERR_STALE:
+                if ci is None and fresh:
+                    w.fill_(-1)
+                    u.zero_()
                 _lib.check(L.swarm_allocate(
                     _lib.ctx(), self.n, p(self.ids), p(self.pos), p(self.caps), t,
                     p(tpos), p(tq), float(claim_thr), float(hysteresis), float(u_scale), m,

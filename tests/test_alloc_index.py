@@ -170,3 +170,52 @@ def test_task_positions_cache_follows_in_place_writes(mods, oracle_mod):
     want = _oracle_now(oracle_mod, s, tx.cpu().numpy(), d["ty"], d["treq"])
     np.testing.assert_array_equal(b.winner.cpu().numpy(), want["winner"])
     assert not np.array_equal(a.winner.cpu().numpy(), b.winner.cpu().numpy())
+
+
+def test_trusted_index_and_fresh_claims_flags(mods, oracle_mod):
+    """swarm_allocate_indexed_ex: SWARM_ALLOC_TRUST_INDEX (no device staleness check) and
+    SWARM_ALLOC_FRESH_CLAIMS (winner / util initialised on the device, whatever the buffers held)
+    give the results of the plain indexed call, and of the oracle; Swarm.allocate trusts its index
+    only while self.pos is the tensor and version it was built from."""
+    swm, _lib, gen = mods
+    d = gen.swarm_inputs(60_000, 31, t=3_000)
+    s = swm.Swarm(d["ids"], d["x"], d["y"], d["caps"], device="cuda")
+    a0 = s.allocate(d["tx"], d["ty"], d["treq"])  # builds the index
+    assert s._cindex_key == (s.pos.data_ptr(), s.pos._version)
+    g, off = s._cindex
+    L = _lib.lib()
+    t = len(d["tx"])
+    tpos = torch.stack([torch.as_tensor(d["tx"]), torch.as_tensor(d["ty"])], 1).cuda().contiguous()
+    tq = torch.as_tensor(d["treq"]).cuda()
+    outs = {}
+    for flags in (0, _lib.ALLOC_TRUST_INDEX, _lib.ALLOC_FRESH_CLAIMS, _lib.ALLOC_TRUST_INDEX | _lib.ALLOC_FRESH_CLAIMS):
+        if flags & _lib.ALLOC_FRESH_CLAIMS:  # garbage the device must overwrite
+            w = torch.randint(-5, 1000, (t,), dtype=torch.int32, device="cuda")
+            u = torch.rand(t, dtype=torch.float64, device="cuda") * 1e3
+        else:
+            w = torch.full((t,), -1, dtype=torch.int32, device="cuda")
+            u = torch.zeros(t, dtype=torch.float64, device="cuda")
+        won = torch.empty(s.n, dtype=torch.int32, device="cuda")
+        nc = torch.empty((2, t), dtype=torch.int64, device="cuda")
+        st = _lib.AllocStats()
+        _lib.check(L.swarm_allocate_indexed_ex(
+            _lib.ctx(), s.n, _lib.ptr(s.ids), _lib.ptr(s.pos), _lib.ptr(s.caps), ctypes.byref(g), _lib.ptr(off), t,
+            _lib.ptr(tpos), _lib.ptr(tq), 20.0, 5.0, 100.0, flags, _lib.ptr(w), _lib.ptr(u), _lib.ptr(won), None, 0,
+            _lib.ptr(nc[0]), _lib.ptr(nc[1]), ctypes.byref(st), _lib.stream()))
+        outs[flags] = (w.cpu().numpy(), u.cpu().numpy(), won.cpu().numpy(), nc.cpu().numpy(), st.n_claims)
+    for flags, o in outs.items():
+        for a, b in zip(o[:4], outs[0][:4]):
+            np.testing.assert_array_equal(a, b, err_msg=str(flags))
+        assert o[4] == outs[0][4]
+    want = _oracle_now(oracle_mod, s, d["tx"], d["ty"], d["treq"])
+    np.testing.assert_array_equal(outs[0][0], want["winner"])
+    np.testing.assert_array_equal(a0.winner.cpu().numpy(), want["winner"])
+    np.testing.assert_array_equal(a0.util.cpu().numpy(), want["util"])
+    # an in-place write moves the version: the next call checks on the device and rebins
+    i = int(torch.argmax(s.pos[:, 1]))
+    s.pos[i, 1] += 50.0
+    assert s._cindex_key != (s.pos.data_ptr(), s.pos._version)
+    b = s.allocate(d["tx"], d["ty"], d["treq"])
+    want = _oracle_now(oracle_mod, s, d["tx"], d["ty"], d["treq"])
+    np.testing.assert_array_equal(b.winner.cpu().numpy(), want["winner"])
+    np.testing.assert_array_equal(b.won.cpu().numpy(), want["won"])

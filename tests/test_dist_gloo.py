@@ -289,3 +289,13 @@ def test_partition_cuts():
         assert (y[p.agents] >= p.strip[0]).all() and (y[p.agents] <= p.strip[1]).all()
     with pytest.raises(ValueError):
         partition(np.zeros(8), np.arange(8.0), 4, 0, min_height=5.0)
+
+
+def test_partition_by_id_empty_range_is_a_clear_error():
+    """More ranks than distinct IDs leaves an ID range empty: a ValueError that says so,
+    not numpy's bare 'zero-size array' error."""
+    from swarm_amd.dist import partition
+    ids = np.array([5, 5, 5, 5, 9, 9], np.int64)
+    y = np.array([0.0, 0.1, 0.2, 0.3, 5.0, 5.1])
+    with pytest.raises(ValueError, match="without agents"):
+        partition(np.zeros_like(y), y, 3, 0, by="id", ids=ids)

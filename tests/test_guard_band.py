@@ -88,3 +88,34 @@ def test_flagged_claims_with_prior_claim_table(case, oracle_mod, sw):
     np.testing.assert_array_equal(r.util.cpu().numpy().view(np.uint64), want["util"].view(np.uint64))
     np.testing.assert_array_equal(r.nmsg.cpu().numpy(), want["nmsg"])
     np.testing.assert_array_equal(s.to_input_order(r.won), want["won"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("h", [5.0, 0.0])
+def test_dense_deferred_tasks_with_crowded_claims(case, oracle_mod, sw, h):
+    """Dense strategy, deferred tasks whose claims overflow the per-task LDS list (> 512 claimants):
+    700 extra agents inside the claim radius of every task.  The deferred tasks are resolved by the
+    chain walk over the dense tile summaries with the host's decisions patched in (the
+    per-task wave pass rescanned every agent per chain link there)."""
+    d = case
+    g = np.random.default_rng(11)
+    tx, ty = np.asarray(d["tx"]), np.asarray(d["ty"])
+    m = 700
+    r_ = 3.5 * np.sqrt(g.random((len(tx), m)))
+    th = g.uniform(0, 2 * np.pi, (len(tx), m))
+    ex = (tx[:, None] + r_ * np.cos(th)).ravel()
+    ey = (ty[:, None] + r_ * np.sin(th)).ravel()
+    ids = np.concatenate([d["ids"], int(np.max(d["ids"])) + 1 + g.permutation(ex.size)]).astype(np.int32)
+    x = np.concatenate([d["x"], ex])
+    y = np.concatenate([d["y"], ey])
+    caps = np.concatenate([d["caps"], np.full(ex.size, 15, np.uint32)]).astype(np.uint32)
+    s = sw.Swarm(ids, x, y, caps, device="cuda")
+    r = s.allocate(tx, ty, d["treq"], mode="dense", hysteresis=h)
+    want = oracle_mod.allocate(ids, x, y, caps, tx, ty, d["treq"], hysteresis=h, use_pow=True)
+    assert r.stats["mode_used"] == 2 and r.stats["n_resolved"] > 0, r.stats
+    assert want["nclaim"].max() > 512
+    np.testing.assert_array_equal(r.winner.cpu().numpy(), want["winner"])
+    np.testing.assert_array_equal(r.util.cpu().numpy().view(np.uint64), want["util"].view(np.uint64))
+    np.testing.assert_array_equal(r.nclaim.cpu().numpy(), want["nclaim"])
+    np.testing.assert_array_equal(r.nmsg.cpu().numpy(), want["nmsg"])
+    np.testing.assert_array_equal(s.to_input_order(r.won), want["won"])
