@@ -620,6 +620,8 @@ def sharded(args, rank, world, dev):
                                       "rounds (ghosts that deep, stepped locally)"},
             "alloc_stats": a[2],
             "result_check": check,
+            "reference_python": {"value": REF_PYTHON_RATE, "unit": "agent-rounds/s", "cores": 1,
+                                 "source": "SURVEY.md §6 (reference election on 1 core of the build container)"},
             "roofline": dict(dom, frac_max_over_ranks=float(fr[0]), frac_min_over_ranks=-float(fr[1]),
                              note="rank 0's k_sparse_block over its shard graph (owned + ghost rows), HIP events "
                                   "on libswarm's stream, one instrumented election of that graph"),
@@ -628,7 +630,7 @@ def sharded(args, rank, world, dev):
         if args.cpu_baseline:
             out["cpu_baseline"] = shard_cpu_baseline(sh, tx, ty, tq)
     # C4 on N GPUs beside the headline: 100k agents split over the ranks, 100k tasks replicated,
-    # the native sharded auction (one RCCL MAX all-reduce of the task keys per round)
+    # the native sharded auction (the round's bids exchanged by one all-gather per round)
     if args.rows:
         c4 = sharded_auction_row(args, rank, world, dev)
         if rank == 0:
