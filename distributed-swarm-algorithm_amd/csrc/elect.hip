@@ -444,23 +444,6 @@ constexpr int kG = 4;                    // lanes per marked agent
 constexpr int kKs = 8;                   // loads in flight per lane
 constexpr int kListCap = 4096;           // marked agents listed in LDS per workgroup (16 KiB)
 
-// Work stealing in busy sparse rounds (round 4).  The marked agents per workgroup are Poisson-like
-// (32-agent blocks dealt over 2 048 workgroups): the round waits for the heaviest list, 2-3x the
-// mean.  A workgroup whose final list has more than `keep` + 1 passes of 64 agents keeps the first
-// `keep` passes, copies the rest to its global slot and announces itself in the round's heavy list;
-// every workgroup, once its own passes are done, claims donated passes 64 agents at a time
-// (atomicAdd on the donor's pass counter) -- the donor first, then up to `tries` other donors.
-// Hand-off: the list copy stored sc1 and drained before the announcement (an atomic), read sc1.
-struct Steal {
-    int32_t *glist;    // [grid][kListCap] donated list copies
-    int32_t *gcount;   // [grid] a donor's list length this round
-    unsigned *pc;      // [grid] passes claimed from a donor's donated part
-    unsigned *hcnt;    // [2] donors of the round (by round parity)
-    int32_t *hlist;    // [2][grid] their indices (-1: announced slot not written yet)
-    int keep;          // passes a donor keeps; 0: no stealing this round
-    int tries;         // donors a thief tries besides itself
-};
-
 struct Frontier {
     int32_t *L[2];
     uint8_t *act[2];         // stamps, sm.M << sm.cshift bytes each (stamp_slot layout)
@@ -472,7 +455,6 @@ struct Frontier {
     int64_t c_lo, n_count;   // rows [c_lo, n_count) are owned: only their changes are counted
     StampMap sm, wsm;
     const int16_t *c16;      // Col16 columns of the same graph (swarm_graph_compact), or nullptr
-    Steal st;                // busy rounds: work stealing (k_sparse_block STEAL), zero when unused
 };
 
 // Max over the G lanes of an agent's group (G = 4: a quad) through DPP quad permutes -- register
@@ -632,8 +614,7 @@ __device__ __forceinline__ void flush_counts(unsigned long long *ring, int t, lo
 
 // One workgroup per chunk of kBlock * S agents: S stamps per thread, the chunk's marked agents
 // compacted in LDS and gathered by the whole workgroup.
-template <typename Off, int S = kScan, bool DIR = false, typename CT = Col32, int G = kG, int K = kKs,
-          bool STEAL = false>
+template <typename Off, int S = kScan, bool DIR = false, typename CT = Col32, int G = kG, int K = kKs>
 __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_block(
     const Off *__restrict__ rp, CT cols, Frontier f, int t, int guard,
     const Off *__restrict__ hrp = nullptr, const int32_t *__restrict__ hcol = nullptr) {
@@ -649,11 +630,6 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
     unsigned long long ph_stamps = 0, ph_listed = 0, ph_gathered = 0;
 #endif
     bookkeeping_last(f.ring, f.tot, t);
-    if (STEAL && blockIdx.x == gridDim.x - 1) {  // the next round's donor list: empty
-        const int np = (t + 1) & 1;
-        if (threadIdx.x == 0) f.st.hcnt[np] = 0;
-        for (int i = threadIdx.x; i < int(gridDim.x); i += kBlock) f.st.hlist[np * int(gridDim.x) + i] = -1;
-    }
     // single-GPU runs: round t-2 changed nothing => round t-1 had no marked agent => neither t.
     // Loaded here, tested only once the first stamp words are in flight (no dependent load in
     // front of the round's own chain).
@@ -736,77 +712,9 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
 #ifdef SWARM_PHASES
     ph_listed = wall_clock64();
 #endif
-    if constexpr (STEAL) {
-        __shared__ int s_steal[2];
-        const int par = t & 1, b = int(blockIdx.x), NGi = int(gridDim.x);
-        const int npass = (listed + 63) >> 6, keep = f.st.keep;
-        const bool donor = npass > keep + 1;
-        if (donor) {  // donate passes [keep, npass): list copy, length, counter, then the announcement
-            int32_t *gl = f.st.glist + int64_t(b) * kListCap;
-            for (int i = keep * 64 + threadIdx.x; i < listed; i += kBlock)
-                __hip_atomic_store(gl + i, s_list[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (threadIdx.x == 0) {
-                __hip_atomic_store(f.st.gcount + b, listed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                atomicExch(f.st.pc + b, 0u);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                const unsigned slot = atomicAdd(f.st.hcnt + par, 1u);
-                __hip_atomic_store(f.st.hlist + par * NGi + int(slot), b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        const int own = donor ? keep * 64 : listed;
-        if (own > 0)
-            gather_listed<Off, G, K, DIR>(rp, cols, hrp, hcol, P, Q, aw, f.wsm, sw, s_list, own, wid * (64 / G),
-                                          kBlock / G, f.c_lo, f.n_count, my_chg, my_act, my_edges);
-        // help: this workgroup's own donated passes first (if any), then other donors'
-        int vtry = donor ? -1 : 0, vcur = donor ? b : -1, vlen = donor ? listed : 0;
-        unsigned nh = 0;
-        for (;;) {
-            __syncthreads();  // s_list free
-            if (threadIdx.x == 0) {
-                int got = -1;
-                while (got < 0) {
-                    if (vcur >= 0) {
-                        const unsigned q = atomicAdd(f.st.pc + vcur, 1u);
-                        const int pass = keep + int(q);
-                        if (pass * 64 < vlen) {
-                            got = pass;
-                            break;
-                        }
-                        vcur = -1;
-                    }
-                    // next donor: up to `tries` of them, spread by workgroup index
-                    if (vtry < 0) vtry = 0;
-                    if (vtry == 0) nh = __hip_atomic_load(f.st.hcnt + par, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (vtry >= f.st.tries || unsigned(vtry) >= nh) break;
-                    const int v = __hip_atomic_load(f.st.hlist + par * NGi + int((unsigned(b) + unsigned(vtry)) % nh),
-                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ++vtry;
-                    if (v < 0 || v == b) continue;
-                    vcur = v;
-                    vlen = __hip_atomic_load(f.st.gcount + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                s_steal[0] = got;
-                s_steal[1] = vcur;
-            }
-            __syncthreads();
-            const int pass = s_steal[0], v = s_steal[1];
-            if (pass < 0) break;
-            const int glen = __hip_atomic_load(f.st.gcount + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int cnt = glen - pass * 64 < 64 ? glen - pass * 64 : 64;
-            if (threadIdx.x < cnt)
-                s_list[threadIdx.x] = __hip_atomic_load(f.st.glist + int64_t(v) * kListCap + pass * 64 + threadIdx.x,
-                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __syncthreads();
-            gather_listed<Off, G, K, DIR>(rp, cols, hrp, hcol, P, Q, aw, f.wsm, sw, s_list, cnt, wid * (64 / G),
-                                          kBlock / G, f.c_lo, f.n_count, my_chg, my_act, my_edges);
-        }
-    } else if (listed > 0) {
+    if (listed > 0)
         gather_listed<Off, G, K, DIR>(rp, cols, hrp, hcol, P, Q, aw, f.wsm, sw, s_list, listed, wid * (64 / G),
                                       kBlock / G, f.c_lo, f.n_count, my_chg, my_act, my_edges);
-    }
 #ifdef SWARM_PHASES
     ph_gathered = wall_clock64() + (my_chg & 0);
 #endif
@@ -922,20 +830,11 @@ struct Tuning {
     int dense_flat = 1;       // dense rounds gather leaders 64 consecutive edges per load (FLAT)
     int dense_vec = 1;        // FLAT with 16-bit columns: 8 columns per lane per 16-byte load
     int use_c16 = 1;          // swarm_elect_compact reads the 16-bit columns (0: its int32 ones; A/B aid)
-    int steal = 1;            // work stealing in busy sparse rounds (Steal; 16-bit-column elections)
-    int steal_keep = 2;       // passes of 64 agents a donor keeps
-    int steal_tries = 4;      // donors a thief tries besides itself
-    int64_t steal_min = -1;   // stealing while the last read round changed >= this (-1: the interleaved
-                              // layout's threshold); once below, off for the rest of the election
     int il_min_changes = -1;   // interleaved stamp layout while the last read round changed >= this
                                // (-1: 8e-4 x agents, measured best at 100k, 1M and 10M agents)
     Tuning() {
         il_min_changes = env_int("SWARM_IL_MIN_CHANGES", -1);
         use_c16 = env_int("SWARM_C16", 1);
-        steal = env_int("SWARM_STEAL", 1);
-        steal_keep = std::max(1, env_int("SWARM_STEAL_KEEP", 2));
-        steal_tries = std::max(0, env_int("SWARM_STEAL_TRIES", 4));
-        if (const char *e = getenv("SWARM_STEAL_MIN")) steal_min = atoll(e);
         dense_flat = env_int("SWARM_DENSE_FLAT", 1);
         dense_vec = env_int("SWARM_DENSE_VEC", 1);
         stamp_bshift = env_int("SWARM_STAMP_BSHIFT", 5);
@@ -1098,12 +997,6 @@ int launch_frontier_round(const Off *rp, const int32_t *col, const Frontier &f, 
         hipLaunchKernelGGL((k_sparse_block<Off, 2, true>), grid, dim3(kBlock), 0, s, rp, c32, f, t, guard, hrp, hcol);
     else if (hrp)
         hipLaunchKernelGGL((k_sparse_block<Off, kScan, true>), grid, dim3(kBlock), 0, s, rp, c32, f, t, guard, hrp, hcol);
-    else if (f.c16 && f.st.keep > 0 && small)
-        hipLaunchKernelGGL((k_sparse_block<Off, 2, false, Col16, kG, kKs, true>), grid, dim3(kBlock), 0, s, rp,
-                           Col16{f.c16}, f, t, guard, nullptr, nullptr);
-    else if (f.c16 && f.st.keep > 0)
-        hipLaunchKernelGGL((k_sparse_block<Off, kScan, false, Col16, kG, kKs, true>), grid, dim3(kBlock), 0, s, rp,
-                           Col16{f.c16}, f, t, guard, nullptr, nullptr);
     else if (f.c16 && small)
         hipLaunchKernelGGL((k_sparse_block<Off, 2, false, Col16>), grid, dim3(kBlock), 0, s, rp, Col16{f.c16}, f, t,
                            guard, nullptr, nullptr);
@@ -1175,20 +1068,6 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         if (rc0) return rc0;
         ring = f.ring;
         f.c16 = c16;
-        if (tuning().steal && c16 && !hrp) {  // work stealing scratch: donated lists, counters, donor lists
-            const int64_t grid = grid_for(f.sm.M, 1, unsigned(tuning().sparse_blocks));
-            uint8_t *sb;
-            const size_t lists = size_t(grid) * kListCap * 4, per = size_t(grid) * 4;
-            SW_ALLOC(sb, ctx, S_STEAL, lists + 2 * per + 64 + 2 * per);
-            f.st.glist = reinterpret_cast<int32_t *>(sb);
-            f.st.gcount = reinterpret_cast<int32_t *>(sb + lists);
-            f.st.pc = reinterpret_cast<unsigned *>(sb + lists + per);
-            f.st.hcnt = reinterpret_cast<unsigned *>(sb + lists + 2 * per);
-            f.st.hlist = reinterpret_cast<int32_t *>(sb + lists + 2 * per + 64);
-            SW_HIP(hipMemsetAsync(f.st.hcnt, 0, 64, s));
-            SW_HIP(hipMemsetAsync(f.st.hlist, 0xFF, 2 * per, s));
-            f.st.tries = tuning().steal_tries;
-        }
     } else {
         SW_ALLOC(ring, ctx, S_CHANGES, ring_bytes());
         SW_HIP(hipMemsetAsync(ring, 0, ring_bytes(), s));
@@ -1208,8 +1087,6 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     const int64_t il_min = tuning().il_min_changes >= 0 ? tuning().il_min_changes
                                                         : std::max<int64_t>(1, int64_t(8e-4 * double(n)));
     StampMap rd_map = il_map;
-    const int64_t steal_min = tuning().steal_min >= 0 ? tuning().steal_min : il_min;
-    bool steal_on = true;
     int64_t act_sum = 0, edge_sum = 0, chg_sum = 0, dense_rounds = 0, sp_launches = 0;
     double bytes = 0.0, sp_bytes = 0.0, sp_ms = 0.0;
     std::vector<RoundKind> kinds(kMaxBatch);
@@ -1307,9 +1184,6 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
                 // order once they are sparse (locality of the few gathers)
                 f.sm = rd_map;
                 f.wsm = (hist.empty() || hist.back() >= il_min) ? il_map : ag_map;
-                // work stealing while rounds are busy; off for good once a read round changed fewer
-                if (steal_on && !hist.empty() && hist.back() < steal_min) steal_on = false;
-                f.st.keep = (steal_on && f.st.glist) ? tuning().steal_keep : 0;
                 rc = launch_frontier_round<Off>(rp, col, f, r, kinds[r - t], 1, s, hrp, hcol);
                 rd_map = f.wsm;
             }

@@ -54,7 +54,6 @@ enum Slot {
     S_DEFER,          // allocation: guard-band tasks deferred to the libm pass (list + per-task flags)
     S_FPAIRS,         // allocation: the deferred tasks' guard-band pairs (device -> host)
     S_OVR,            // allocation: host libm decisions for those pairs (host -> device)
-    S_STEAL,          // election: work stealing's donated lists, counters, donor lists
     S_NUM
 };
 
