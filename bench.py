@@ -511,21 +511,27 @@ def rows_bench(sw, dev, args):
     off = (np.arange(n, dtype=np.int64) * 7919 % 40).astype(np.int32)
     ticks = 200
 
-    def run_fsm():
+    def run_fsm(traffic=False):
         sw.protocol_reset(tick_off=off, last_hb=-(off * 0.1))
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        c = sw.protocol_run(ticks, kill_ticks=(80, 150), seed=5)
+        c = sw.protocol_run(ticks, kill_ticks=(80, 150), seed=5, traffic=traffic)  # hybrid: storm ticks pull
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) * 1e3, c
     run_fsm()
     ms, c = run_fsm()
+    run_fsm(traffic=True)  # what the ticks touched (an untimed replay: the counters add atomics)
+    fb = fsm_bytes(sw.fsm_traffic, n, ticks)
     rows["f2_protocol_ticks"] = {"agents": n, "ticks": ticks, "ms_per_tick": ms / ticks,
                                  "agent_ticks_per_s": n * ticks / (ms * 1e-3),
                                  "leaders_final": int(c[-1, 0]), "heartbeats": int(c[:, 3].sum()),
-                                 "roofline": _roof(12.0 * n, ms / ticks, "k_compact + k_receive + k_sweep", "k_sweep",
-                                                   note="sweep bytes only (alive, state, outbox r/w, 8-B timer per "
-                                                        "agent); receivers' rows not counted: a lower bound")}
+                                 "traffic": [int(v) for v in sw.fsm_traffic],
+                                 "roofline": _roof(fb / ticks, ms / ticks, "k_compact + k_receive + k_sweep + k_mail",
+                                                   "k_sweep",
+                                                   note="every tick's algorithmic bytes (fsm_bytes: the sweep's 15 B "
+                                                        "per agent, the mail bitmap, each receiver's fields, 5 B per "
+                                                        "row edge walked, 8 B per sender + 6 B per hearer mailed), "
+                                                        "from the run's traffic counters; storm ticks pulled")}
     if cpu:
         dq = gen.swarm_inputs(1_000_000, args.seed + 7)
         rpq, colq = oracle.rgg_csr(dq["x"], dq["y"], 1.0)
@@ -672,6 +678,18 @@ def survey_step_bytes(r, n, e, tasks):
     gathered agent + 8 B per edge (a dense round gathers all n agents and E edges, + 4 B), and the
     allocation's compulsory 24 B per agent + 36 B per task."""
     return (12.0 * r.active_total + 8.0 * r.edges_total + 4.0 * r.dense_rounds + 24.0 * n + 36.0 * tasks)
+
+
+def fsm_bytes(tr, n, ticks):
+    """Algorithmic bytes of `ticks` protocol ticks from swarm_protocol_run_ex's traffic counters
+    (DESIGN.md §4e): the sweep reads 15 B per agent per tick (alive, outbox, state, tick phase, 8-B
+    timer); a mailed tick's compaction reads the 1-bit mail map and writes / reads a 4-B list entry
+    per receiver; a receiver served by its single sender reads / writes ~36 B of fields, one that
+    walks its row ~31 B plus 5 B per row edge (column, sender's outbox); a sender mails for 8 B
+    (row offsets) + 6 B per hearer (column, the 64-bit mail word per few hearers)."""
+    single, multi, edges, senders, hear, _, pulled_agents, pulled_ticks = (float(v) for v in tr)
+    return (15.0 * n * ticks + (ticks - pulled_ticks) * n / 8.0 + 8.0 * (single + multi) + 36.0 * single
+            + 31.0 * (multi + pulled_agents) + 5.0 * edges + 8.0 * senders + 6.0 * hear)
 
 
 def sparse_round_bytes(active_total, edges_total, dense_rounds, rounds_exec, n, e, launches, compact):

@@ -23,8 +23,11 @@
 //              segment: no global atomics), per-tick counters;
 //   k_mail     per segment, mail bits for the hearers of every sender (64-bit atomicOr,
 //              combined per word, all hearer loads in flight).
-// A quiet agent costs ~12 B (alive, state, outbox byte, its 8-byte timer); only receivers pay
-// for their rows.  Pull mode (no hearers CSR): one fused launch in which every agent walks
+// A quiet agent costs ~15 B (alive, state, outbox byte, tick phase, its 8-byte timer); only receivers
+// pay for their rows.  Storm ticks (round 4): when a tick's senders exceed pull_frac x n (a timeout
+// wave: thousands of ACCLAIMs at once), k_mail skips the mail atomics and the next tick's k_receive
+// pulls instead -- every alive agent walks its own row, as pull mode does -- and k_compact has
+// nothing to compact.  Same results: an agent without a sender in its row hears nothing either way.  Pull mode (no hearers CSR): one fused launch in which every agent walks
 // its row -- the cross-check.  Both are latency-bound gathers, no arithmetic worth the name.
 // Agents killed at a kill tick (every alive LEADER then) stop receiving and sending.
 #include <cmath>
@@ -160,6 +163,14 @@ __device__ __forceinline__ uint8_t timers(int64_t i, uint8_t &st, bool heard, in
 // every workgroup's 4 atomics queue on the same 4 addresses: ~50 us per tick at 4 096
 // workgroups, ~470 us at one agent per thread (measured).
 constexpr int kShards = 64;
+constexpr int kTraffic = 8;  // traffic counters (swarm_protocol_run_ex), sharded like the tick counts
+
+// Per-workgroup traffic counts into one of kShards copies (one atomic per nonzero value).
+__device__ __forceinline__ void add_traffic(unsigned long long *tr, int k, unsigned long long v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if (tr && (threadIdx.x & 63) == 0 && v) atomicAdd(&tr[(blockIdx.x & (kShards - 1)) * kTraffic + k], v);
+}
 
 __device__ __forceinline__ void add_counts(unsigned c0, unsigned c1, unsigned c2, unsigned c3, unsigned *s_cnt,
                                            unsigned long long *counts) {
@@ -289,9 +300,10 @@ __global__ __launch_bounds__(kBlock) void k_mail_from_outbox(int64_t n, const ui
 constexpr uint32_t kMulti = 0x80000000u;
 
 __global__ __launch_bounds__(kBlock) void k_compact(int64_t n_words, Mail mail, int32_t *__restrict__ list,
-                                                   unsigned *__restrict__ n_list) {
+                                                   unsigned *__restrict__ n_list, const unsigned *__restrict__ pull) {
     __shared__ unsigned s_wave[kBlock / kWave];
     __shared__ unsigned s_base;
+    if (*pull) return;  // a storm tick: nothing was mailed, the receivers pull
     const unsigned lane = threadIdx.x & (kWave - 1);
     const int wv = threadIdx.x / kWave;
     for (int64_t base = int64_t(blockIdx.x) * kBlock; base < n_words; base += int64_t(gridDim.x) * kBlock) {
@@ -341,29 +353,42 @@ __global__ __launch_bounds__(kBlock) void k_receive(int64_t t, const int32_t *__
                                                    const int32_t *__restrict__ rp, const int32_t *__restrict__ col,
                                                    const int32_t *__restrict__ tick_off, Fsm f,
                                                    const uint8_t *__restrict__ ob_in, uint8_t *__restrict__ ob_out,
-                                                   double dt) {
+                                                   double dt, const unsigned *__restrict__ pull, int64_t n,
+                                                   unsigned long long *__restrict__ tr) {
     if (blockIdx.x == 0 && threadIdx.x == 0) *n_next = 0;  // the next tick's list counter
-    const int64_t m = *n_list;
+    const bool pulled = *pull != 0;  // a storm tick: every alive agent walks its row
+    const int64_t m = pulled ? n : int64_t(*n_list);
     const double now = double(t) * dt;
+    unsigned long long c_single = 0, c_multi = 0, c_edges = 0;
     for (int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x; q < m; q += int64_t(gridDim.x) * kBlock) {
-        const uint32_t entry = uint32_t(list[q]);
+        const uint32_t entry = pulled ? (uint32_t(q) | kMulti) : uint32_t(list[q]);
         const int32_t i = int32_t(entry & ~kMulti);
         if (!f.alive[i]) continue;
         const uint8_t st0 = f.state[i];
         Heard h{st0, 0, false, false, 0, -1};
         const int32_t me = ids[i];
         const bool hb_tick = ((t + tick_off[i]) % 10) == 0;
-        if (entry & kMulti) {  // several senders: the row, in CSR order
-            receive_row(rp[i], rp[i + 1], col, ob_in, ids, me, hb_tick, h);
+        if (entry & kMulti) {  // several senders (or a pulled tick): the row, in CSR order
+            const int32_t b = rp[i], e = rp[i + 1];
+            receive_row(b, e, col, ob_in, ids, me, hb_tick, h);
+            ++c_multi;
+            c_edges += uint64_t(e - b);
         } else {  // exactly one sender: no row walk
             const int32_t j = from[i];
             const uint8_t o = ob_in[j] & (kAcclaim | kHeartbeat);
             if (o) hear(h, o, ids[j], j, me, hb_tick);
+            ++c_single;
         }
         apply_heard(i, h, now, pos, f);
         if (h.st != st0) f.state[i] = h.st;
         if (h.lead_set) f.leader[i] = h.lead;
         ob_out[i] = uint8_t(kFresh | h.ob | (h.live ? kHeard : 0));
+    }
+    if (tr) {
+        add_traffic(tr, pulled ? 5 : 0, pulled ? 0ull : c_single);
+        add_traffic(tr, pulled ? 6 : 1, c_multi);
+        add_traffic(tr, 2, c_edges);
+        if (pulled && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&tr[7], 1ull);  // pulled ticks
     }
 }
 
@@ -449,16 +474,51 @@ __global__ __launch_bounds__(kBlock) void k_sweep(int64_t n, int64_t t, const in
     if (threadIdx.x == 0) seg_count[blockIdx.x] = s_ns;
 }
 
-// Mail for the hearers of every sender the sweep listed: workgroup b walks segment b.
+// Mail for the hearers of every sender the sweep listed: workgroup b walks segment b.  A storm tick
+// (this tick's senders -- ACCLAIM + HEARTBEAT counts, an agent sending both counted twice -- above
+// thr) mails nothing and flags the next tick's receive as a pull; every workgroup decides the same.
 __global__ __launch_bounds__(kBlock) void k_mail(const int32_t *__restrict__ senders, int64_t seg_cap,
                                                 const int32_t *__restrict__ seg_count,
                                                 const int32_t *__restrict__ trp, const int32_t *__restrict__ tcol,
-                                                Mail mail) {
+                                                Mail mail, const unsigned long long *__restrict__ cnt_t,
+                                                unsigned long long thr, unsigned *__restrict__ pull_next,
+                                                unsigned long long *__restrict__ tr) {
+    __shared__ unsigned long long s_tot;
+    if (thr != ~0ull) {
+        if (threadIdx.x < kWave) {
+            unsigned long long v = cnt_t[threadIdx.x * 4 + 2] + cnt_t[threadIdx.x * 4 + 3];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+            if (threadIdx.x == 0) s_tot = v;
+        }
+        __syncthreads();
+        const bool storm = s_tot > thr;
+        if (blockIdx.x == 0 && threadIdx.x == 0) *pull_next = storm ? 1u : 0u;
+        if (storm) return;
+    } else if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *pull_next = 0;
+    }
     const int m = seg_count[blockIdx.x];
     const int32_t *seg = senders + int64_t(blockIdx.x) * seg_cap;
+    unsigned long long c_edges = 0;
     for (int q = threadIdx.x; q < m; q += kBlock) {
         const int32_t i = seg[q];
-        mail_hearers(trp[i], trp[i + 1], tcol, mail, i);
+        const int32_t b = trp[i], e = trp[i + 1];
+        mail_hearers(b, e, tcol, mail, i);
+        c_edges += uint64_t(e - b);
+    }
+    if (tr) {
+        add_traffic(tr, 3, threadIdx.x < unsigned(m) ? uint64_t((m - int(threadIdx.x) + kBlock - 1) / kBlock) : 0ull);
+        add_traffic(tr, 4, c_edges);
+    }
+}
+
+// traffic shards -> out[kTraffic]
+__global__ void k_sum_traffic(const unsigned long long *__restrict__ tr, unsigned long long *__restrict__ out) {
+    if (threadIdx.x < kTraffic) {
+        unsigned long long v = 0;
+        for (int sh = 0; sh < kShards; ++sh) v += tr[sh * kTraffic + threadIdx.x];
+        out[threadIdx.x] = v;
     }
 }
 
@@ -472,6 +532,15 @@ int swarm_protocol_run(swarm_ctx *ctx, int64_t n, const int32_t *ids, const doub
                        const int32_t *tick_off, const swarm_fsm *fsm, int64_t t0, int32_t ticks,
                        double dt, double timeout, double jitter, uint64_t seed, const int64_t *kill_ticks,
                        int32_t n_kill, int64_t *counts, void *stream) {
+    return swarm_protocol_run_ex(ctx, n, ids, pos, row_ptr, col, hear_row_ptr, hear_col, tick_off, fsm, t0, ticks, dt,
+                                 timeout, jitter, seed, kill_ticks, n_kill, -1.0, counts, nullptr, stream);
+}
+
+int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *pos, const int32_t *row_ptr,
+                          const int32_t *col, const int32_t *hear_row_ptr, const int32_t *hear_col,
+                          const int32_t *tick_off, const swarm_fsm *fsm, int64_t t0, int32_t ticks,
+                          double dt, double timeout, double jitter, uint64_t seed, const int64_t *kill_ticks,
+                          int32_t n_kill, double pull_frac, int64_t *counts, int64_t *traffic, void *stream) {
     using namespace swarm;
     SW_ARG(ctx != nullptr && fsm != nullptr, "NULL argument");
     SW_ARG(n >= 0 && n < (int64_t(1) << 31) && ticks >= 0 && t0 >= 0 && n_kill >= 0, "sizes out of range");
@@ -482,6 +551,8 @@ int swarm_protocol_run(swarm_ctx *ctx, int64_t n, const int32_t *ids, const doub
                       fsm->wait_start && fsm->delay && fsm->leader_pos && fsm->has_leader_pos && fsm->alive &&
                       fsm->outbox),
            "NULL agent array");
+    SW_ARG(!std::isnan(pull_frac), "pull_frac is NaN");
+    if (traffic) for (int q = 0; q < kTraffic; ++q) traffic[q] = 0;
     if (n == 0 || ticks == 0) {
         if (counts) for (int64_t q = 0; q < int64_t(ticks) * 4; ++q) counts[q] = 0;
         return SWARM_OK;
@@ -489,9 +560,15 @@ int swarm_protocol_run(swarm_ctx *ctx, int64_t n, const int32_t *ids, const doub
     hipStream_t s = static_cast<hipStream_t>(stream);
     unsigned long long *d_cnt;  // per tick: kShards x 4 partial counters, then the 4 sums
     const size_t part_bytes = size_t(ticks) * kShards * 4 * 8;
-    SW_ALLOC(d_cnt, ctx, S_TMP0, part_bytes + size_t(ticks) * 4 * 8);
+    const size_t tr_bytes = size_t(kShards) * kTraffic * 8;
+    SW_ALLOC(d_cnt, ctx, S_TMP0, part_bytes + size_t(ticks) * 4 * 8 + tr_bytes + kTraffic * 8);
     SW_HIP(hipMemsetAsync(d_cnt, 0, part_bytes, s));
     unsigned long long *d_sum = d_cnt + size_t(ticks) * kShards * 4;
+    unsigned long long *d_tr = traffic ? d_sum + size_t(ticks) * 4 : nullptr;
+    if (d_tr) SW_HIP(hipMemsetAsync(d_tr, 0, tr_bytes, s));
+    // storm threshold on a tick's senders (pull_frac < 0: never; the pull-mode entry has no mail at all)
+    const unsigned long long thr = pull_frac < 0.0 ? ~0ull
+                                   : (unsigned long long)std::min(pull_frac * double(n), 1.8e19);
     const Fsm f{fsm->state, fsm->leader, fsm->last_hb, fsm->wait_start, fsm->delay,
                 reinterpret_cast<float2 *>(fsm->leader_pos), fsm->has_leader_pos, fsm->alive};
     const unsigned grid = grid_for(n, kBlock, 4096);
@@ -503,7 +580,7 @@ int swarm_protocol_run(swarm_ctx *ctx, int64_t n, const int32_t *ids, const doub
     Mail mail{};
     int32_t *list = nullptr, *senders = nullptr, *seg_count = nullptr;
     int64_t seg_cap = 0;
-    unsigned *n_list = nullptr;
+    unsigned *n_list = nullptr, *pullf = nullptr;
     if (push) {  // mail bitmap + the two list counters (tick parity) after it
         unsigned long long *mw;  // mail bits, multi-sender bits, then the two list counters
         SW_ALLOC(mw, ctx, S_FSM_MAIL, size_t(n_words) * 16 + 64);
@@ -518,6 +595,7 @@ int swarm_protocol_run(swarm_ctx *ctx, int64_t n, const int32_t *ids, const doub
         SW_ALLOC(senders, ctx, S_FSM_SEND, size_t(seg_cap) * grid * 4 + size_t(grid) * 4);
         seg_count = senders + seg_cap * grid;
         n_list = reinterpret_cast<unsigned *>(mw + 2 * n_words);
+        pullf = n_list + 2;  // [2] by tick parity: the tick's receive pulls (zeroed with the bitmap)
         SW_HIP(hipMemsetAsync(mw, 0, size_t(n_words) * 16 + 64, s));
         hipLaunchKernelGGL(k_mail_from_outbox, dim3(grid), dim3(kBlock), 0, s, n,
                            fsm->outbox + size_t(t0 & 1) * size_t(n), hear_row_ptr, hear_col, mail);
@@ -536,23 +614,33 @@ int swarm_protocol_run(swarm_ctx *ctx, int64_t n, const int32_t *ids, const doub
         if (push) {
             unsigned *nl = n_list + (t & 1), *nl_next = n_list + ((t + 1) & 1);
             hipLaunchKernelGGL(k_compact, dim3(grid_for(n_words, kBlock, 2048)), dim3(kBlock), 0, s, n_words, mail,
-                               list, nl);
+                               list, nl, pullf + (t & 1));
             SW_LAUNCHED();
             hipLaunchKernelGGL(k_receive, dim3(2048), dim3(kBlock), 0, s, t, list, mail.from, nl, nl_next, ids,
-                               reinterpret_cast<const double2 *>(pos), row_ptr, col, tick_off, f, ob_in, ob_out, dt);
+                               reinterpret_cast<const double2 *>(pos), row_ptr, col, tick_off, f, ob_in, ob_out, dt,
+                               pullf + (t & 1), n, d_tr);
             SW_LAUNCHED();
             hipLaunchKernelGGL(k_sweep, dim3(grid), dim3(kBlock), 0, s, n, t, ids, tick_off, f, ob_out, senders,
                                seg_cap, seg_count, dt, timeout, jitter, seed, cnt,
                                int(vec && (reinterpret_cast<uintptr_t>(ob_out) & 3) == 0));
             SW_LAUNCHED();
             hipLaunchKernelGGL(k_mail, dim3(grid), dim3(kBlock), 0, s, senders, seg_cap, seg_count, hear_row_ptr,
-                               hear_col, mail);
+                               hear_col, mail, cnt, thr, pullf + ((t + 1) & 1), d_tr);
         } else {
             hipLaunchKernelGGL(k_tick_pull, dim3(grid), dim3(kBlock), 0, s, n, t, ids,
                                reinterpret_cast<const double2 *>(pos), row_ptr, col, tick_off, f, ob_in, ob_out, dt,
                                timeout, jitter, seed, cnt);
         }
         SW_LAUNCHED();
+    }
+    if (d_tr) {  // pull-mode runs: every tick walks every row (the receivers are all agents)
+        unsigned long long *hs = static_cast<unsigned long long *>(pinned(ctx, kTraffic * 8));
+        if (!hs) return SWARM_ERR_OOM;
+        hipLaunchKernelGGL(k_sum_traffic, dim3(1), dim3(kWave), 0, s, d_tr, d_tr + size_t(kShards) * kTraffic);
+        SW_LAUNCHED();
+        SW_HIP(hipMemcpyAsync(hs, d_tr + size_t(kShards) * kTraffic, kTraffic * 8, hipMemcpyDeviceToHost, s));
+        SW_HIP(hipStreamSynchronize(s));
+        for (int q = 0; q < kTraffic; ++q) traffic[q] = int64_t(hs[q]);
     }
     if (counts) {
         hipLaunchKernelGGL(k_sum_counts, dim3(grid_for(int64_t(ticks) * 4, kBlock, 256)), dim3(kBlock), 0, s,

@@ -35,7 +35,8 @@ EXPORTS = ("swarm_last_error", "swarm_version", "swarm_ctx_create", "swarm_ctx_d
            "swarm_auction_bid", "swarm_auction_resolve", "swarm_auction_sharded", "swarm_cell_index",
            "swarm_allocate_indexed", "swarm_graph_compact", "swarm_elect_compact",
            "swarm_elect_compact_i64", "swarm_frontier_begin_range", "swarm_frontier_set_compact",
-           "swarm_comm_unique_id_kind", "swarm_comm_create_kind", "swarm_comm_kind", "swarm_allocate_indexed_ex")
+           "swarm_comm_unique_id_kind", "swarm_comm_create_kind", "swarm_comm_kind", "swarm_allocate_indexed_ex",
+           "swarm_protocol_run_ex")
 
 
 class SwarmError(RuntimeError):
@@ -142,6 +143,8 @@ def load(path: str = LIB_PATH):
         L.swarm_codec_decode.argtypes = [P, i64, P, i64, P, i32, P, P, P, P, P, P, P, P, P, P]
         L.swarm_protocol_run.argtypes = [P, i64, P, P, P, P, P, P, P, ctypes.POINTER(Fsm), i64, i32, d, d, d,
                                          ctypes.c_uint64, P, i32, P, P]
+        L.swarm_protocol_run_ex.argtypes = [P, i64, P, P, P, P, P, P, P, ctypes.POINTER(Fsm), i64, i32, d, d, d,
+                                            ctypes.c_uint64, P, i32, d, P, P, P]
         L.swarm_auction_begin.argtypes = [P, i64, P, P, P, i64, P, P, d, d, ctypes.c_float, P, P, P, P, P]
         L.swarm_auction_bid.argtypes = [P, i64, i32, i32, P, P, P, P]
         L.swarm_auction_resolve.argtypes = [P, i64, i32, P, P, P, P, P, P]

@@ -530,13 +530,16 @@ class Swarm:
         return self
 
     def protocol_run(self, ticks: int, *, kill_ticks=(), dt: float = 0.1, timeout: float = 3.0,
-                     jitter: float = 0.2, seed: int = 0, mode: str = "push") -> np.ndarray:
+                     jitter: float = 0.2, seed: int = 0, mode: str = "hybrid", pull_frac: float = 0.125,
+                     traffic: bool = False) -> np.ndarray:
         """Advance the timer FSM + election handlers `ticks` ticks under contract T1
         (swarm_protocol_run; agent.py:66-80, 217-289), messages along the neighbour graph.
         kill_ticks: absolute ticks at whose start every alive LEADER dies.  Returns counts
         (ticks x 4): alive LEADERs, alive ELECTION_WAITs, ACCLAIM senders, HEARTBEAT senders.
         mode "push": senders mark their hearers and only marked agents scan their row; "pull":
-        every agent scans its row every tick (same results)."""
+        every agent scans its row every tick; "hybrid": push, but a tick whose senders exceed
+        pull_frac x n (a timeout wave) has the next tick pull (swarm_protocol_run_ex).  Same results.
+        traffic: count what the ticks touched (self.fsm_traffic: 8 int64, see include/swarm.h)."""
         if self.row_ptr is None:
             raise RuntimeError("no neighbour graph: call build_graph() or set_graph()")
         if not hasattr(self, "fsm"):
@@ -546,20 +549,24 @@ class Swarm:
                         (self.state, self.leader, f["last_hb"], f["wait_start"], f["delay"], f["leader_pos"],
                          f["has_leader_pos"], f["alive"], f["outbox"])])
         kt = np.ascontiguousarray(np.asarray(kill_ticks, np.int64))
-        if mode not in ("push", "pull"):
+        if mode not in ("push", "pull", "hybrid"):
             raise ValueError(f"unknown mode {mode!r}")
         h = getattr(self, "_hear", None) or (self.row_ptr, self.col)
         hear = (None, None) if mode == "pull" or self.n == 0 else \
             (_lib.ptr(h[0], torch.int32), _lib.ptr(h[1], torch.int32) if h[1].numel() else None)
         counts = np.zeros((int(ticks), 4), np.int64)
+        tr = np.zeros(8, np.int64)
         with torch.cuda.device(self.device):
-            _lib.check(_lib.lib().swarm_protocol_run(
+            _lib.check(_lib.lib().swarm_protocol_run_ex(
                 _lib.ctx(), self.n, _lib.ptr(self.ids) if self.n else None, _lib.ptr(self.pos) if self.n else None,
                 _lib.ptr(self.row_ptr, torch.int32), _lib.ptr(self.col, torch.int32) if self.n_edges else None,
                 *hear, _lib.ptr(self.tick_off) if self.n else None, ctypes.byref(fs), self.fsm_tick, int(ticks),
                 float(dt), float(timeout), float(jitter), ctypes.c_uint64(int(seed)),
                 kt.ctypes.data_as(ctypes.c_void_p) if kt.size else None, kt.size,
-                counts.ctypes.data_as(ctypes.c_void_p), _lib.stream()))
+                float(pull_frac) if mode == "hybrid" else -1.0, counts.ctypes.data_as(ctypes.c_void_p),
+                tr.ctypes.data_as(ctypes.c_void_p) if traffic else None, _lib.stream()))
+        if traffic:
+            self.fsm_traffic = tr
         self.fsm_tick += int(ticks)
         return counts
 

@@ -506,6 +506,20 @@ int swarm_protocol_run(swarm_ctx *ctx, int64_t n, const int32_t *ids, const doub
                        double dt, double timeout, double jitter, uint64_t seed, const int64_t *kill_ticks,
                        int32_t n_kill, int64_t *counts, void *stream);
 
+/* swarm_protocol_run with storm ticks pulled and the traffic counted (same results):
+ * pull_frac (push mode): when a tick's senders (ACCLAIM + HEARTBEAT counts) exceed pull_frac x n, the
+ *   next tick's receivers walk their own rows instead of being mailed (a timeout wave makes most
+ *   agents send at once: mailing every hearer costs more than every agent pulling); < 0: never.
+ * traffic (host, 8 int64, may be NULL; synchronises): summed over the run -- [0] receivers served by
+ *   their single sender, [1] receivers that walked their row (several senders), [2] row edges walked
+ *   (those and pulled ticks), [3] senders mailed, [4] hearer edges mailed, [5] 0, [6] agents that
+ *   walked their row in pulled ticks, [7] pulled ticks.  Pull mode (hear_row_ptr NULL) counts nothing. */
+int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *pos, const int32_t *row_ptr,
+                          const int32_t *col, const int32_t *hear_row_ptr, const int32_t *hear_col,
+                          const int32_t *tick_off, const swarm_fsm *fsm, int64_t t0, int32_t ticks,
+                          double dt, double timeout, double jitter, uint64_t seed, const int64_t *kill_ticks,
+                          int32_t n_kill, double pull_frac, int64_t *counts, int64_t *traffic, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

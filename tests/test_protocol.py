@@ -103,7 +103,8 @@ def _gpu_state(s):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", FSM)
-@pytest.mark.parametrize("layout,mode", [("spatial", "push"), ("input", "push"), ("spatial", "pull")])
+@pytest.mark.parametrize("layout,mode", [("spatial", "push"), ("input", "push"), ("spatial", "pull"),
+                                         ("spatial", "hybrid")])
 def test_gpu_matches_reference_fixture(name, layout, mode):
     g = load_golden(name)
     s = _gpu_swarm(g, layout)
@@ -214,3 +215,28 @@ def test_gpu_sweep_unaligned_arrays_match_oracle(oracle_mod, n):
     for k in OUT:
         np.testing.assert_array_equal(got[k], want[k], err_msg=k)
     np.testing.assert_array_equal(counts, want["counts"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pull_frac", [0.0, 0.02, 0.125])
+def test_gpu_hybrid_storm_ticks_match_oracle(oracle_mod, pull_frac):
+    """Hybrid mode (swarm_protocol_run_ex): a tick whose senders exceed pull_frac x n has the next
+    tick pull (every alive agent walks its row, no mail); pull_frac 0 pulls after every tick with a
+    sender.  States, timers, leader positions and per-tick counts equal the oracle's, in two chunks
+    (a pulled tick at a chunk boundary), and the traffic counters add up."""
+    g = _random_case(20000, 5, 50.0)
+    g["ticks"], g["kill_ticks"] = np.int64(150), np.array([60, 110], np.int64)
+    want = _run_oracle(oracle_mod, g)
+    s = _gpu_swarm(g)
+    c1 = s.protocol_run(64, kill_ticks=g["kill_ticks"], seed=5, mode="hybrid", pull_frac=pull_frac, traffic=True)
+    t1 = s.fsm_traffic.copy()
+    c2 = s.protocol_run(86, kill_ticks=g["kill_ticks"], seed=5, mode="hybrid", pull_frac=pull_frac, traffic=True)
+    tr = t1 + s.fsm_traffic
+    got = _gpu_state(s)
+    for k in OUT:
+        np.testing.assert_array_equal(got[k], want[k], err_msg=k)
+    np.testing.assert_array_equal(np.concatenate([c1, c2]), want["counts"])
+    if pull_frac == 0.0:  # every tick after one with a sender pulled: nothing was mailed
+        assert tr[7] > 0 and tr[6] > 0 and tr[3] == 0 and tr[0] == 0
+    senders = int((want["counts"][:, 2] + want["counts"][:, 3]).sum())
+    assert tr[3] <= senders

@@ -23,32 +23,24 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--agents", type=int, default=10_000_000)
 ap.add_argument("--ticks", type=int, default=200)
 ap.add_argument("--deg", type=float, default=16.0)
+ap.add_argument("--modes", default="push:0,hybrid:0.125,hybrid:0.05,hybrid:0.25,pull:0",
+                help="comma list of mode:pull_frac")
 a = ap.parse_args()
 d = gen.swarm_inputs(a.agents, 3, deg=a.deg)
 s = Swarm(d["ids"], d["x"], d["y"], device="cuda").build_graph(1.0)
 off = (np.arange(a.agents) * 7919 % 40).astype(np.int32)
-res = {}
-for rep in range(2):
-    s.protocol_reset(tick_off=off, last_hb=-(off * 0.1))
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    c = s.protocol_run(a.ticks, kill_ticks=(80, 150), seed=5)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-# per-chunk timing (10 ticks per call) to separate quiet ticks from election storms
-s.protocol_reset(tick_off=off, last_hb=-(off * 0.1))
-chunks = []
-for k in range(a.ticks // 10):
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    cc = s.protocol_run(10, kill_ticks=(80, 150), seed=5)
-    torch.cuda.synchronize()
-    chunks.append((round(1e3 * (time.perf_counter() - t1) / 10, 4), int(cc[:, 1].sum()), int(cc[:, 2].sum()),
-                   int(cc[:, 3].sum())))
-print(json.dumps(dict(chunk_ms_per_tick_waits_acclaims_hbs=chunks)))
-res = dict(agents=a.agents, edges=s.n_edges, ticks=a.ticks, ms_per_tick=1e3 * dt / a.ticks,
-           agent_ticks_per_s=a.agents * a.ticks / dt,
-           bytes_per_tick_est=a.agents * 26 + 5 * s.n_edges,
-           leaders_final=int(c[-1, 0]), waits=int(c[:, 1].sum()), hb=int(c[:, 3].sum()))
-res["gbs_est"] = res["bytes_per_tick_est"] / (res["ms_per_tick"] * 1e-3) / 1e9
-print(json.dumps(res))
+out = {}
+for mode, pf in ((m.split(":")[0], float(m.split(":")[1])) for m in a.modes.split(",")):
+    for rep in range(2):
+        s.protocol_reset(tick_off=off, last_hb=-(off * 0.1))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        c = s.protocol_run(a.ticks, kill_ticks=(80, 150), seed=5, mode=mode, pull_frac=pf, traffic=mode != "pull")
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    tr = getattr(s, "fsm_traffic", None) if mode != "pull" else None
+    out[f"{mode}_{pf}"] = dict(ms_per_tick=1e3 * dt / a.ticks, leaders_final=int(c[-1, 0]), hb=int(c[:, 3].sum()),
+                               counts_sum=int(c.sum()), traffic=None if tr is None else [int(v) for v in tr])
+    print(json.dumps({f"{mode}_{pf}": out[f"{mode}_{pf}"]}), flush=True)
+sums = {k: v["counts_sum"] for k, v in out.items()}
+print(json.dumps(dict(agents=a.agents, edges=s.n_edges, ticks=a.ticks, same_counts=len(set(sums.values())) == 1)))
