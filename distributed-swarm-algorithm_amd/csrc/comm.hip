@@ -330,6 +330,7 @@ int frontier_ghosts_both(swarm_ctx *ctx, int t, const int32_t *rp, const int32_t
                          const int32_t *in_lo, int64_t b_hi, int64_t n_hi, const int32_t *in_hi, int32_t *L0,
                          int32_t *L1, hipStream_t s);
 int frontier_round_totals(swarm_ctx *ctx, int t0, int t1, unsigned long long *dtot, hipStream_t s);
+int64_t frontier_il_min(int64_t n);
 }  // namespace swarm
 
 extern "C" {
@@ -456,8 +457,12 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sh,
     const int depth = sh->halo_depth > 1 ? sh->halo_depth : 1;
     int found = -1, t = 1, batch = 8;
     std::vector<int64_t> hist;
+    // the stamp layout: interleaved while rounds are busy, agent order in the tail (as swarm_elect),
+    // switched on the GLOBAL changes against the threshold for the global agent count
+    const int64_t il_min = frontier_il_min(sh->n_rows * int64_t(comm->nranks));
     while (t <= max_rounds && found < 0) {
         const int tend = std::min(max_rounds, t + batch - 1);
+        ctx->step_wr_agent = (!hist.empty() && hist.back() < il_min) ? 1 : 0;
         for (int r = t; r <= tend; ++r) {
             if ((rc = frontier_round_stepper(ctx, r, sh->row_ptr, sh->col, leader0, leader1, s))) return rc;
             if (r % depth) continue;  // deep halo: ghosts are stepped locally between exchanges

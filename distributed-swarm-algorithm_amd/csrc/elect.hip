@@ -937,7 +937,8 @@ int frontier_bind(swarm_ctx *ctx, int32_t *L0, int32_t *L1, Frontier *f) {
     uint8_t *a = static_cast<uint8_t *>(ctx->slot[S_ACT]);
     f->act[0] = a;
     f->act[1] = a + act_bytes(f->n_all);
-    f->sm = f->wsm = stamp_map(f->n_all);
+    f->sm = stamp_map(f->n_all, !ctx->step_rd_agent);
+    f->wsm = stamp_map(f->n_all, !ctx->step_wr_agent);
     f->ring = static_cast<unsigned long long *>(ctx->slot[S_CHANGES]);
     f->tot = f->ring + size_t(kRing) * kCounters * kRoundWords;
     return SWARM_OK;
@@ -956,6 +957,7 @@ int frontier_alloc(swarm_ctx *ctx, int64_t n_rows, int64_t n_all, int32_t *L0, i
     ctx->step_all = n_all;
     ctx->step_lo = 0;
     ctx->step_c16 = nullptr;
+    ctx->step_rd_agent = ctx->step_wr_agent = 0;
     int rc = frontier_bind(ctx, L0, L1, f);
     if (rc) return rc;
     SW_HIP(hipMemsetAsync(f->ring, 0, ring_bytes(), s));
@@ -1259,7 +1261,15 @@ int frontier_round_stepper(swarm_ctx *ctx, int t, const int32_t *rp, const int32
     int rc = frontier_bind(ctx, L0, L1, &f);
     if (rc) return rc;
     if (f.n_rows == 0) return SWARM_OK;
-    return launch_frontier_round<int32_t>(rp, col, f, t, plan_round(t), /*guard=*/0, s);
+    rc = launch_frontier_round<int32_t>(rp, col, f, t, plan_round(t), /*guard=*/0, s);
+    ctx->step_rd_agent = ctx->step_wr_agent;  // the marks this round wrote
+    return rc;
+}
+
+// The interleaved -> agent-order switch point of the stamp layout for an n-agent swarm (elect_impl's
+// il_min; the sharded C loop compares the global changes against it for the global agent count).
+int64_t frontier_il_min(int64_t n) {
+    return tuning().il_min_changes >= 0 ? tuning().il_min_changes : std::max<int64_t>(1, int64_t(8e-4 * double(n)));
 }
 
 int frontier_ghosts_both(swarm_ctx *ctx, int t, const int32_t *rp, const int32_t *col, int64_t b_lo, int64_t n_lo,
@@ -1273,6 +1283,7 @@ int frontier_ghosts_both(swarm_ctx *ctx, int t, const int32_t *rp, const int32_t
     };
     SW_ARG(outside(b_lo, n_lo) && outside(b_hi, n_hi), "ghost ranges must lie in [0, n_all) outside the owned rows");
     if (n_lo + n_hi == 0) return SWARM_OK;
+    f.wsm = f.sm;  // ghost rises mark for the next round, in the layout that round reads
     hipLaunchKernelGGL((k_frontier_ghosts<int32_t>), dim3(grid_for(n_lo + n_hi, kBlock / 8, 1024)), dim3(kBlock), 0,
                        s, rp, col, f, b_lo, n_lo, in_lo, b_hi, n_hi, in_hi, t);
     SW_LAUNCHED();

@@ -7,6 +7,8 @@ one device, so the ranks talk through host memory, in two ways:
                       over its shared-memory transport (SWARM_COMM_SHM): the batching, the counter
                       all-reduce, the ghost application order and the convergence decision of the
                       code that runs over RCCL on a multi-GPU node;
+  transport "shm-agent"  the same, with the tail's agent-order stamp layout forced from the second
+                      batch of rounds on (SWARM_IL_MIN_CHANGES): the layout switch of the native loop;
   transport "python"  SWARM_NATIVE_HALO=0: ShardedSwarm's Python stepper, halo over gloo.
 Every rank's leaders, rounds and per-round global change counts, the sharded allocation (winners,
 claim values, conflicts, won counts) and -- native -- the sharded auction (owners, prices, per-round
@@ -52,7 +54,9 @@ def _worker(rank, world, port, out_q, kind, depth, transport):
     for p in (PKG, ROOT, os.path.join(ROOT, "tests")):
         sys.path.insert(0, p)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-                      SWARM_NATIVE_HALO="1" if transport == "shm" else "0")
+                      SWARM_NATIVE_HALO="0" if transport == "python" else "1")
+    if transport == "shm-agent":  # the tail's agent-order stamp layout from the second batch on
+        os.environ["SWARM_IL_MIN_CHANGES"] = str(1 << 40)
     import torch
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -75,7 +79,7 @@ def _worker(rank, world, port, out_q, kind, depth, transport):
         assert isinstance(sh.backend, GpuBackend) and sh.halo.host_staged
         r = sh.elect(check_every=16)
         native = getattr(sh, "_native", None) is not None
-        assert native == (transport == "shm") and (not native or sh.backend.comm_kind == "shm")
+        assert native == (transport != "python") and (not native or sh.backend.comm_kind == "shm")
         sh._check_ghosts(sh.leaders[r.rounds_exec & 1])
         res, won, gst = sh.allocate(tx, ty, tq)
         auc = None
@@ -96,7 +100,8 @@ def _worker(rank, world, port, out_q, kind, depth, transport):
 @pytest.mark.parametrize("world,kind,depth,transport", [(2, "shards", 16, "python"), (2, "global", 4, "python"),
                                                          (3, "global", 16, "python"), (2, "shards", 16, "shm"),
                                                          (2, "global", 1, "shm"), (3, "global", 16, "shm"),
-                                                         (3, "shards", 4, "shm")])
+                                                         (3, "shards", 4, "shm"), (2, "global", 16, "shm-agent"),
+                                                         (3, "shards", 1, "shm-agent")])
 def test_hip_sharded_processes_match_union_oracle(world, kind, depth, transport, oracle_mod):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -122,7 +127,7 @@ def test_hip_sharded_processes_match_union_oracle(world, kind, depth, transport,
     lead, _, rounds, changes = oracle_mod.elect(rp, col, ids)
     want = dict(zip(ids.tolist(), lead.tolist()))
     for o in outs:
-        assert o["native"] == (transport == "shm")
+        assert o["native"] == (transport != "python")
         assert o["converged"] and o["rounds"] == rounds and o["ghosts"] > 0
         np.testing.assert_array_equal(o["changes"], changes)
         assert all(want[int(i)] == int(v) for i, v in zip(o["ids"], o["leader"]))
@@ -141,7 +146,7 @@ def test_hip_sharded_processes_match_union_oracle(world, kind, depth, transport,
     for o in outs:
         assert all(won_want[int(i)] == int(w) for i, w in zip(o["ids"], o["won"]))
         assert o["gstats"]["n_claims"] == wa["n_claims"] and o["gstats"]["n_conflicts"] == wa["n_conflicts"]
-    if transport == "shm":  # the native sharded auction equals the one-GPU auction over the union
+    if transport != "python":  # the native sharded auction equals the one-GPU auction over the union
         atx, aty, atq = _auction_tasks(kind, world)
         w = oracle_mod.auction(ids, x, y, caps, atx, aty, atq)
         own_w = np.where(w["owner"] >= 0, ids[np.maximum(w["owner"], 0)], -1)
