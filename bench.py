@@ -526,12 +526,12 @@ def rows_bench(sw, dev, args):
                                  "agent_ticks_per_s": n * ticks / (ms * 1e-3),
                                  "leaders_final": int(c[-1, 0]), "heartbeats": int(c[:, 3].sum()),
                                  "traffic": [int(v) for v in sw.fsm_traffic],
-                                 "roofline": _roof(fb / ticks, ms / ticks, "k_compact + k_receive + k_sweep + k_mail",
-                                                   "k_sweep",
+                                 "roofline": _roof(fb / ticks, ms / ticks, "k_tick + k_mail", "k_tick",
                                                    note="every tick's algorithmic bytes (fsm_bytes: the sweep's 15 B "
-                                                        "per agent, the mail bitmap, each receiver's fields, 5 B per "
-                                                        "row edge walked, 8 B per sender + 6 B per hearer mailed), "
-                                                        "from the run's traffic counters; storm ticks pulled")}
+                                                        "per agent, the mail bitmap read and cleared, each receiver's "
+                                                        "fields, 5 B per row edge walked, 8 B per sender + 6 B per "
+                                                        "hearer mailed), from the run's traffic counters; storm "
+                                                        "ticks pulled")}
     if cpu:
         dq = gen.swarm_inputs(1_000_000, args.seed + 7)
         rpq, colq = oracle.rgg_csr(dq["x"], dq["y"], 1.0)
@@ -683,12 +683,13 @@ def survey_step_bytes(r, n, e, tasks):
 def fsm_bytes(tr, n, ticks):
     """Algorithmic bytes of `ticks` protocol ticks from swarm_protocol_run_ex's traffic counters
     (DESIGN.md §4e): the sweep reads 15 B per agent per tick (alive, outbox, state, tick phase, 8-B
-    timer); a mailed tick's compaction reads the 1-bit mail map and writes / reads a 4-B list entry
-    per receiver; a receiver served by its single sender reads / writes ~36 B of fields, one that
-    walks its row ~31 B plus 5 B per row edge (column, sender's outbox); a sender mails for 8 B
-    (row offsets) + 6 B per hearer (column, the 64-bit mail word per few hearers)."""
+    timer); a mailed tick reads the 1-bit mail map and clears it; a receiver served by its single
+    sender reads / writes ~36 B of fields, one that walks its row ~31 B plus 5 B per row edge
+    (column, sender's outbox); a sender mails for 8 B (row offsets) + 6 B per hearer (column, the
+    64-bit mail word per few hearers).  (Round 4 counted a 4-B receiver list entry written and read,
+    8 B per receiver: the list was the implementation's, k_tick has none.)"""
     single, multi, edges, senders, hear, _, pulled_agents, pulled_ticks = (float(v) for v in tr)
-    return (15.0 * n * ticks + (ticks - pulled_ticks) * n / 8.0 + 8.0 * (single + multi) + 36.0 * single
+    return (15.0 * n * ticks + (ticks - pulled_ticks) * n / 4.0 + 36.0 * single
             + 31.0 * (multi + pulled_agents) + 5.0 * edges + 8.0 * senders + 6.0 * hear)
 
 

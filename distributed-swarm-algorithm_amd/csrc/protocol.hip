@@ -14,21 +14,25 @@
 //             ELECTION_WAIT past its delay -> LEADER + ELECTION_ACCLAIM + COORDINATOR;
 //   sends     into its outbox byte (tick-parity double buffer): bit 0 ACCLAIM+COORDINATOR,
 //             bit 1 HEARTBEAT -- exact, see swarm_oracle.c orc_protocol.
-// Push mode (the hearers CSR given), three launches per tick:
-//   k_compact  the mail bitmap (1 bit per agent, set by last tick's senders) -> a list of
-//              receivers (one workgroup-aggregated atomic per workgroup pass), words cleared;
-//   k_receive  one thread per listed receiver walks its CSR row (col / outbox loads in chunks
-//              of kRecv, all in flight) and applies the handlers in CSR order;
-//   k_sweep    one thread per agent: timers, sends (senders listed in the workgroup's own
-//              segment: no global atomics), per-tick counters;
-//   k_mail     per segment, mail bits for the hearers of every sender (64-bit atomicOr,
-//              combined per word, all hearer loads in flight).
-// A quiet agent costs ~15 B (alive, state, outbox byte, tick phase, its 8-byte timer); only receivers
-// pay for their rows.  Storm ticks (round 4): when a tick's senders exceed pull_frac x n (a timeout
-// wave: thousands of ACCLAIMs at once), k_mail skips the mail atomics and the next tick's k_receive
-// pulls instead -- every alive agent walks its own row, as pull mode does -- and k_compact has
-// nothing to compact.  Same results: an agent without a sender in its row hears nothing either way.  Pull mode (no hearers CSR): one fused launch in which every agent walks
-// its row -- the cross-check.  Both are latency-bound gathers, no arithmetic worth the name.
+// Push mode (the hearers CSR given), two launches per tick:
+//   k_tick   receive + timers, its workgroups in two roles: the receive role lists each 4 096-agent
+//            chunk's receivers (mail bit set: 1 bit per agent, set by last tick's senders) in LDS
+//            and serves them one per thread -- its one sender directly, or its CSR row in order
+//            (col / outbox loads in chunks of kRecv, all in flight) when it has several -- then
+//            their timers; the sweep role streams every other agent's timers (kSweepV agents per
+//            thread); sends are listed in the workgroup's own segment (no global atomics),
+//            per-tick counters;
+//   k_mail   clears the tick's mail words, then mails the hearers of every listed sender (64-bit
+//            atomicOr into the next tick's words, combined per word, all hearer loads in flight).
+// (Rounds 2-4 ran the receive as its own launch over a compacted receiver list, k_compact +
+// k_receive + k_sweep + k_mail: two more boundaries and the list round trip per tick.)
+// A quiet agent costs ~15 B (alive, state, outbox byte, tick phase, its 8-byte timer) plus its mail
+// bit; only receivers pay for their rows.  Storm ticks: when a tick's senders exceed pull_frac x n
+// (a timeout wave: thousands of ACCLAIMs at once), k_mail skips the mail atomics and the next tick
+// pulls instead -- every alive agent walks its own row, as pull mode does.  Same results: an agent
+// without a sender in its row hears nothing either way.  Pull mode (no hearers CSR): one fused
+// launch in which every agent walks its row -- the cross-check.  Both are latency-bound gathers, no
+// arithmetic worth the name.
 // Agents killed at a kill tick (every alive LEADER then) stop receiving and sending.
 #include <cmath>
 
@@ -239,8 +243,6 @@ __global__ __launch_bounds__(kBlock) void k_tick_pull(int64_t n, int64_t t, cons
 }
 
 // ---------------------------------------------------------------- push mode
-constexpr uint8_t kFresh = 0x80;  // outbox byte written by k_receive this tick
-constexpr uint8_t kHeard = 0x04;  // ... whose receiver got a liveness proof
 
 // Mail for the hearers of sender i: one bit per agent (one atomicOr per distinct 64-agent word).
 // The atomic returns the word's previous bits: a hearer whose bit was clear gets from[r] = i (its
@@ -252,22 +254,34 @@ struct Mail {
     int32_t *from;
 };
 
-__device__ __forceinline__ void mail_flush(const Mail &m, int32_t w, unsigned long long bits, int32_t sender) {
-    const unsigned long long old = atomicOr(&m.bits[w], bits);
-    const unsigned long long dup = old & bits;
-    if (dup) atomicOr(&m.multi[w], dup);
-    unsigned long long fresh = bits & ~old;
-    while (fresh) {
-        const int q = __ffsll((long long)fresh) - 1;
-        fresh &= fresh - 1;
-        m.from[int64_t(w) * 64 + q] = sender;
+// Up to kFlush word runs of one sender at once: every returning atomic in flight before the first
+// result is used (one after the other, a sender's ~3 words cost ~3 atomic round trips).
+constexpr int kFlush = 4;
+
+__device__ __forceinline__ void mail_flush(const Mail &m, const int32_t *pw, const unsigned long long *pb, int np,
+                                           int32_t sender) {
+    unsigned long long old[kFlush];
+#pragma unroll
+    for (int j = 0; j < kFlush; ++j) old[j] = j < np ? atomicOr(&m.bits[pw[j]], pb[j]) : 0ull;
+#pragma unroll
+    for (int j = 0; j < kFlush; ++j) {
+        if (j >= np) break;
+        const unsigned long long dup = old[j] & pb[j];
+        if (dup) atomicOr(&m.multi[pw[j]], dup);
+        unsigned long long fresh = pb[j] & ~old[j];
+        while (fresh) {
+            const int q = __ffsll((long long)fresh) - 1;
+            fresh &= fresh - 1;
+            m.from[int64_t(pw[j]) * 64 + q] = sender;
+        }
     }
 }
 
 __device__ __forceinline__ void mail_hearers(int32_t b, int32_t e, const int32_t *__restrict__ tcol, const Mail &m,
                                              int32_t sender) {
-    int32_t w = -1;
-    unsigned long long bits = 0;
+    int32_t w = -1, pw[kFlush];
+    unsigned long long bits = 0, pb[kFlush];
+    int np = 0;
     for (int32_t k0 = b; k0 < e; k0 += kRecv) {
         int32_t rr[kRecv];  // all hearer loads of the chunk in flight
 #pragma unroll
@@ -277,14 +291,29 @@ __device__ __forceinline__ void mail_hearers(int32_t b, int32_t e, const int32_t
             const int32_t r = rr[u];
             if (r < 0) continue;
             if ((r >> 6) != w) {
-                if (bits) mail_flush(m, w, bits, sender);
+                if (bits) {
+                    if (np == kFlush) {
+                        mail_flush(m, pw, pb, np, sender);
+                        np = 0;
+                    }
+                    pw[np] = w;
+                    pb[np++] = bits;
+                }
                 w = r >> 6;
                 bits = 0;
             }
             bits |= 1ull << (r & 63);
         }
     }
-    if (bits) mail_flush(m, w, bits, sender);
+    if (bits) {
+        if (np == kFlush) {
+            mail_flush(m, pw, pb, np, sender);
+            np = 0;
+        }
+        pw[np] = w;
+        pb[np++] = bits;
+    }
+    if (np) mail_flush(m, pw, pb, np, sender);
 }
 
 // Resumed run: mail for the receivers of tick t0's sends.
@@ -295,195 +324,244 @@ __global__ __launch_bounds__(kBlock) void k_mail_from_outbox(int64_t n, const ui
         if (ob[i]) mail_hearers(trp[i], trp[i + 1], tcol, m, int32_t(i));
 }
 
-// Mail bitmap -> receiver list, words cleared.  One atomicAdd per workgroup pass.
-// List entries carry the multi-sender flag in bit 31 (agent indices are < 2^31).
-constexpr uint32_t kMulti = 0x80000000u;
-
-__global__ __launch_bounds__(kBlock) void k_compact(int64_t n_words, Mail mail, int32_t *__restrict__ list,
-                                                   unsigned *__restrict__ n_list, const unsigned *__restrict__ pull) {
-    __shared__ unsigned s_wave[kBlock / kWave];
-    __shared__ unsigned s_base;
-    if (*pull) return;  // a storm tick: nothing was mailed, the receivers pull
-    const unsigned lane = threadIdx.x & (kWave - 1);
-    const int wv = threadIdx.x / kWave;
-    for (int64_t base = int64_t(blockIdx.x) * kBlock; base < n_words; base += int64_t(gridDim.x) * kBlock) {
-        const int64_t w = base + threadIdx.x;
-        unsigned long long bits = 0, multi = 0;
-        if (w < n_words) {
-            bits = mail.bits[w];
-            if (bits) {
-                mail.bits[w] = 0;
-                multi = mail.multi[w];
-                if (multi) mail.multi[w] = 0;
-            }
-        }
-        const unsigned c = unsigned(__popcll(bits));
-        unsigned incl = c;  // wave inclusive scan
-#pragma unroll
-        for (int off = 1; off < kWave; off <<= 1) {
-            const unsigned v = __shfl_up(incl, off, kWave);
-            if (lane >= unsigned(off)) incl += v;
-        }
-        if (lane == kWave - 1) s_wave[wv] = incl;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned tot = 0;
-            for (int q = 0; q < kBlock / kWave; ++q) {
-                const unsigned v = s_wave[q];
-                s_wave[q] = tot;
-                tot += v;
-            }
-            s_base = tot ? atomicAdd(n_list, tot) : 0u;
-        }
-        __syncthreads();
-        unsigned o = s_base + s_wave[wv] + incl - c;
-        while (bits) {
-            const int b = __ffsll((long long)bits) - 1;
-            bits &= bits - 1;
-            list[o++] = int32_t(uint32_t(w * 64 + b) | (((multi >> b) & 1ull) ? kMulti : 0u));
-        }
-        __syncthreads();
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void k_receive(int64_t t, const int32_t *__restrict__ list,
-                                                   const int32_t *__restrict__ from,
-                                                   const unsigned *__restrict__ n_list, unsigned *__restrict__ n_next,
-                                                   const int32_t *__restrict__ ids, const double2 *__restrict__ pos,
-                                                   const int32_t *__restrict__ rp, const int32_t *__restrict__ col,
-                                                   const int32_t *__restrict__ tick_off, Fsm f,
-                                                   const uint8_t *__restrict__ ob_in, uint8_t *__restrict__ ob_out,
-                                                   double dt, const unsigned *__restrict__ pull, int64_t n,
-                                                   unsigned long long *__restrict__ tr) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *n_next = 0;  // the next tick's list counter
-    const bool pulled = *pull != 0;  // a storm tick: every alive agent walks its row
-    const int64_t m = pulled ? n : int64_t(*n_list);
-    const double now = double(t) * dt;
-    unsigned long long c_single = 0, c_multi = 0, c_edges = 0;
-    for (int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x; q < m; q += int64_t(gridDim.x) * kBlock) {
-        const uint32_t entry = pulled ? (uint32_t(q) | kMulti) : uint32_t(list[q]);
-        const int32_t i = int32_t(entry & ~kMulti);
-        if (!f.alive[i]) continue;
-        const uint8_t st0 = f.state[i];
-        Heard h{st0, 0, false, false, 0, -1};
-        const int32_t me = ids[i];
-        const bool hb_tick = ((t + tick_off[i]) % 10) == 0;
-        if (entry & kMulti) {  // several senders (or a pulled tick): the row, in CSR order
-            const int32_t b = rp[i], e = rp[i + 1];
-            receive_row(b, e, col, ob_in, ids, me, hb_tick, h);
-            ++c_multi;
-            c_edges += uint64_t(e - b);
-        } else {  // exactly one sender: no row walk
-            const int32_t j = from[i];
-            const uint8_t o = ob_in[j] & (kAcclaim | kHeartbeat);
-            if (o) hear(h, o, ids[j], j, me, hb_tick);
-            ++c_single;
-        }
-        apply_heard(i, h, now, pos, f);
-        if (h.st != st0) f.state[i] = h.st;
-        if (h.lead_set) f.leader[i] = h.lead;
-        ob_out[i] = uint8_t(kFresh | h.ob | (h.live ? kHeard : 0));
-    }
-    if (tr) {
-        add_traffic(tr, pulled ? 5 : 0, pulled ? 0ull : c_single);
-        add_traffic(tr, pulled ? 6 : 1, c_multi);
-        add_traffic(tr, 2, c_edges);
-        if (pulled && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&tr[7], 1ull);  // pulled ticks
-    }
-}
-
-// kSweepV consecutive agents per thread: their byte fields (alive, outbox, state) as one 32-bit
-// word each, their timers (last_hb, tick_off) loaded up front with the bytes, so a thread has
-// every load of a pass in flight at once instead of a dependent chain per agent.
+// One launch per tick for receive + timers (push mode), its workgroups in two roles that run side
+// by side: the receivers' short dependent chains overlap the sweep's streaming instead of following
+// it.  (A single role -- each sweep wave serving its own receivers -- held every wave for its
+// receivers' chains: 0.170 vs 0.152 ms per tick with separate kernels.)
+//   sweep    (workgroups g_recv ..): kSweepV consecutive agents per thread, their byte fields
+//            (alive, outbox, state) as one 32-bit word each, their timers (last_hb, tick_off) and
+//            their 64-agent mail word loaded up front; agents with a mail bit are left to the
+//            receive role, the others tick their timers.
+//   receive  (workgroups 0 .. g_recv - 1; all of them on a pulled tick): chunks of 4 096 agents;
+//            the chunk's receivers (mail bit set; on a pulled tick every agent) are listed in LDS
+//            and served one per thread -- its one sender directly (from[]), or its CSR row in
+//            order when it has several (multi bit) or the tick is pulled -- then its timers run on
+//            the result.
+// Senders of both roles are listed in the workgroup's own segment for k_mail.  The mail words of
+// the tick are cleared by k_mail (both roles read them here).
 constexpr int kSweepV = 4;
+constexpr int kRecvChunk = 4096;  // agents per receive-role pass (64 mail words, 16 agents per thread;
+                                  // 2 048: 0.144 vs 0.138 ms per tick)
 
-__global__ __launch_bounds__(kBlock) void k_sweep(int64_t n, int64_t t, const int32_t *__restrict__ ids,
-                                                 const int32_t *__restrict__ tick_off, Fsm f,
-                                                 uint8_t *__restrict__ ob_out, int32_t *__restrict__ senders,
-                                                 int64_t seg_cap, int32_t *__restrict__ seg_count,
-                                                 double dt, double timeout, double jitter, uint64_t seed,
-                                                 unsigned long long *__restrict__ counts, int vec) {
+// Sender segments of k_tick's workgroups: the g_recv receive-role ones first (rcap entries each:
+// their chunks' agents), then the sweep-role ones (scap each: their agents, or their chunks' on a
+// pulled tick, when every workgroup receives).
+struct Segs {
+    int32_t *base;
+    int64_t rcap, scap;
+    int g_recv;
+    __device__ __forceinline__ int32_t *of(int b) const {
+        return b < g_recv ? base + int64_t(b) * rcap : base + int64_t(g_recv) * rcap + int64_t(b - g_recv) * scap;
+    }
+};
+
+// Exclusive prefix over the workgroup of c (0 <= c < 2^B) and the total (every thread gets it).
+template <int B>
+__device__ __forceinline__ int block_excl_scan(int c, int &total, int *s_wave) {
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    int ex = 0, tot = 0;
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        const unsigned long long m = __ballot((c >> b) & 1);
+        ex += int(__builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u))) << b;
+        tot += __popcll(m) << b;
+    }
+    if (lane == 0) s_wave[wid] = tot;
+    __syncthreads();
+    int off = 0, all = 0;
+#pragma unroll
+    for (int q = 0; q < kBlock / kWave; ++q) {
+        off += q < wid ? s_wave[q] : 0;
+        all += s_wave[q];
+    }
+    __syncthreads();  // s_wave read by all
+    total = all;
+    return off + ex;
+}
+
+struct TickCounts {
+    unsigned lead = 0, wait = 0, acc = 0, hb = 0;
+    unsigned long long single = 0, multi = 0, edges = 0;
+};
+
+// Timers and writes of alive agent i after what it heard (h), its sends listed.
+__device__ __forceinline__ void finish_agent(int64_t i, Heard &h, uint8_t st0, uint8_t prev, int64_t t, double now,
+                                             double timeout, double jitter, uint64_t seed,
+                                             const int32_t *__restrict__ ids, int32_t toff, double lhb, const Fsm &f,
+                                             uint8_t *__restrict__ ob_out, int32_t *seg, int *s_ns, TickCounts &c) {
+    uint8_t st = h.st;
+    const uint8_t ob = uint8_t(h.ob | timers(i, st, h.live, h.lead, h.lead_set, t, now, timeout, jitter, seed, ids,
+                                             toff, lhb, f));
+    if (st != st0) f.state[i] = st;
+    if (h.lead_set) f.leader[i] = h.lead;
+    if (ob != prev) ob_out[i] = ob;
+    if (ob) seg[atomicAdd(s_ns, 1)] = int32_t(i);  // this workgroup's sender segment (LDS counter)
+    c.lead += st == ST_L;
+    c.wait += st == ST_W;
+    c.acc += (ob & kAcclaim) != 0;
+    c.hb += (ob & kHeartbeat) != 0;
+}
+
+__global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int32_t *__restrict__ ids,
+                                                const double2 *__restrict__ pos, const int32_t *__restrict__ rp,
+                                                const int32_t *__restrict__ col, const int32_t *__restrict__ tick_off,
+                                                Fsm f, Mail mail, const uint8_t *__restrict__ ob_in,
+                                                uint8_t *__restrict__ ob_out, const unsigned *__restrict__ pull,
+                                                Segs segs, int32_t *__restrict__ seg_count, double dt, double timeout,
+                                                double jitter, uint64_t seed, unsigned long long *__restrict__ counts,
+                                                int vec, unsigned long long *__restrict__ tr) {
     __shared__ unsigned s_cnt[4];
     __shared__ int s_ns;
+    __shared__ int s_wave[kBlock / kWave];
+    __shared__ uint32_t s_list[kRecvChunk];  // receive role: the chunk's receivers (agent | multi bit 31)
+    static_assert(kRecvChunk % kBlock == 0 && kRecvChunk / kBlock <= 16, "receive slice: <= 16 bits of a word");
     if (threadIdx.x < 4) s_cnt[threadIdx.x] = 0;
     if (threadIdx.x == 0) s_ns = 0;
     __syncthreads();
-    int32_t *seg = senders + int64_t(blockIdx.x) * seg_cap;
+    int32_t *seg = segs.of(blockIdx.x);
+    const int g_recv = segs.g_recv;
+    // receive-role workgroups first: dispatched first, all their chains in flight at once (every
+    // R-th workgroup instead, the roles side by side: 0.151 vs 0.138 ms per tick)
+    const bool recv_role = int(blockIdx.x) < g_recv;
+    const int rank = recv_role ? int(blockIdx.x) : int(blockIdx.x) - g_recv;
     const double now = double(t) * dt;
-    unsigned c_lead = 0, c_wait = 0, c_acc = 0, c_hb = 0;
-    const int64_t ngroups = (n + kSweepV - 1) / kSweepV;
-    for (int64_t gi = int64_t(blockIdx.x) * kBlock + threadIdx.x; gi < ngroups; gi += int64_t(gridDim.x) * kBlock) {
-        const int64_t i0 = gi * kSweepV;
-        const bool full = vec && i0 + kSweepV <= n;
-        uint8_t al[kSweepV], pv[kSweepV], sv[kSweepV];
-        int32_t to[kSweepV];
-        double lh[kSweepV];
-        if (full) {  // vec: the host checked the alignments; i0 is a multiple of 4
-            const uint32_t wa = *reinterpret_cast<const uint32_t *>(f.alive + i0);
-            const uint32_t wp = *reinterpret_cast<const uint32_t *>(ob_out + i0);
-            const uint32_t ws = *reinterpret_cast<const uint32_t *>(f.state + i0);
-            const int4 tv = *reinterpret_cast<const int4 *>(tick_off + i0);
-            const double2 l0 = *reinterpret_cast<const double2 *>(f.last_hb + i0);
-            const double2 l1 = *reinterpret_cast<const double2 *>(f.last_hb + i0 + 2);
-#pragma unroll
-            for (int v = 0; v < kSweepV; ++v) {
-                al[v] = uint8_t(wa >> (8 * v));
-                pv[v] = uint8_t(wp >> (8 * v));
-                sv[v] = uint8_t(ws >> (8 * v));
+    const bool pulled = *pull != 0;
+    TickCounts c;
+    if (pulled || recv_role) {
+        // ---- receive role
+        const int64_t nrole = pulled ? int64_t(gridDim.x) : int64_t(g_recv);
+        const int64_t nchunks = (n + kRecvChunk - 1) / kRecvChunk;
+        for (int64_t ck = pulled ? int64_t(blockIdx.x) : int64_t(rank); ck < nchunks; ck += nrole) {
+            // thread: kPerT agents, a slice of mail word (ck * kRecvChunk + threadIdx.x * kPerT) / 64
+            constexpr int kPerT = kRecvChunk / kBlock;
+            const int64_t a0 = ck * kRecvChunk + int64_t(threadIdx.x) * kPerT;
+            unsigned b16 = 0, m16 = 0;
+            if (a0 < n) {
+                const unsigned valid = n - a0 >= kPerT ? (1u << kPerT) - 1u : ((1u << (n - a0)) - 1u);
+                if (pulled) {
+                    b16 = valid;  // every agent (the dead ones clear their outbox)
+                    m16 = valid;
+                } else {
+                    const int64_t w = a0 >> 6;
+                    const int sh = int(a0 & 63);
+                    b16 = unsigned(mail.bits[w] >> sh) & valid;
+                    if (b16) m16 = unsigned(mail.multi[w] >> sh) & b16;
+                }
             }
-            to[0] = tv.x; to[1] = tv.y; to[2] = tv.z; to[3] = tv.w;
-            lh[0] = l0.x; lh[1] = l0.y; lh[2] = l1.x; lh[3] = l1.y;
-        } else {
-#pragma unroll
-            for (int v = 0; v < kSweepV; ++v) {
-                const int64_t i = i0 + v < n ? i0 + v : n - 1;
-                al[v] = i0 + v < n ? f.alive[i] : 0;
-                pv[v] = ob_out[i];
-                sv[v] = f.state[i];
-                to[v] = tick_off[i];
-                lh[v] = f.last_hb[i];
+            int total;
+            int pos_ = block_excl_scan<5>(__popc(b16), total, s_wave);
+            while (b16) {
+                const int q = __ffs(b16) - 1;
+                b16 &= b16 - 1;
+                s_list[pos_++] = uint32_t(a0 + q) | (((m16 >> q) & 1u) ? 0x80000000u : 0u);
             }
+            __syncthreads();
+            for (int q = threadIdx.x; q < total; q += kBlock) {
+                const uint32_t entry = s_list[q];
+                const int64_t i = int32_t(entry & 0x7FFFFFFFu);
+                const uint8_t prev = ob_out[i];
+                if (!f.alive[i]) {
+                    if (prev) ob_out[i] = 0;
+                    continue;
+                }
+                const uint8_t st0 = f.state[i];
+                const int32_t toff = tick_off[i];
+                const double lhb = f.last_hb[i];
+                Heard h{st0, 0, false, false, 0, -1};
+                const int32_t me = ids[i];
+                const bool hb_tick = ((t + toff) % 10) == 0;
+                if (entry & 0x80000000u) {  // several senders (or a pull): the row, in CSR order
+                    const int32_t b = rp[i], e = rp[i + 1];
+                    receive_row(b, e, col, ob_in, ids, me, hb_tick, h);
+                    ++c.multi;
+                    c.edges += uint64_t(e - b);
+                } else {  // exactly one sender: no row walk
+                    const int32_t j = mail.from[i];
+                    const uint8_t o = ob_in[j] & (kAcclaim | kHeartbeat);
+                    if (o) hear(h, o, ids[j], j, me, hb_tick);
+                    ++c.single;
+                }
+                apply_heard(i, h, now, pos, f);
+                finish_agent(i, h, st0, prev, t, now, timeout, jitter, seed, ids, toff, lhb, f, ob_out, seg, &s_ns, c);
+            }
+            __syncthreads();  // the list is reused
         }
+    } else {
+        // ---- sweep role
+        const int64_t ngroups = (n + kSweepV - 1) / kSweepV;
+        const int64_t stride = int64_t(int(gridDim.x) - g_recv) * kBlock;
+        for (int64_t gi = int64_t(rank) * kBlock + threadIdx.x; gi < ngroups; gi += stride) {
+            const int64_t i0 = gi * kSweepV;
+            const bool full = vec && i0 + kSweepV <= n;
+            uint8_t al[kSweepV], pv[kSweepV], sv[kSweepV];
+            int32_t to[kSweepV];
+            double lh[kSweepV];
+            const unsigned mine = unsigned(mail.bits[i0 >> 6] >> (i0 & 63)) & ((1u << kSweepV) - 1u);
+            if (full) {  // vec: the host checked the alignments; i0 is a multiple of 4
+                const uint32_t wa = *reinterpret_cast<const uint32_t *>(f.alive + i0);
+                const uint32_t wp = *reinterpret_cast<const uint32_t *>(ob_out + i0);
+                const uint32_t ws = *reinterpret_cast<const uint32_t *>(f.state + i0);
+                const int4 tv = *reinterpret_cast<const int4 *>(tick_off + i0);
+                const double2 l0 = *reinterpret_cast<const double2 *>(f.last_hb + i0);
+                const double2 l1 = *reinterpret_cast<const double2 *>(f.last_hb + i0 + 2);
 #pragma unroll
-        for (int v = 0; v < kSweepV; ++v) {
-            const int64_t i = i0 + v;
-            const uint8_t prev = pv[v];  // this tick's receive result, or a stale tick t-2 byte
-            if (!al[v]) {
-                if (i < n && prev) ob_out[i] = 0;
-                continue;
+                for (int v = 0; v < kSweepV; ++v) {
+                    al[v] = uint8_t(wa >> (8 * v));
+                    pv[v] = uint8_t(wp >> (8 * v));
+                    sv[v] = uint8_t(ws >> (8 * v));
+                }
+                to[0] = tv.x; to[1] = tv.y; to[2] = tv.z; to[3] = tv.w;
+                lh[0] = l0.x; lh[1] = l0.y; lh[2] = l1.x; lh[3] = l1.y;
+            } else {
+#pragma unroll
+                for (int v = 0; v < kSweepV; ++v) {
+                    const int64_t i = i0 + v < n ? i0 + v : n - 1;
+                    al[v] = i0 + v < n ? f.alive[i] : 0;
+                    pv[v] = ob_out[i];
+                    sv[v] = f.state[i];
+                    to[v] = tick_off[i];
+                    lh[v] = f.last_hb[i];
+                }
             }
-            uint8_t st = sv[v];
-            const uint8_t rb = (prev & kFresh) ? prev : uint8_t(0);
-            const uint8_t st0 = st;
-            int32_t lead = 0;
-            bool lead_set = false;
-            const uint8_t ob = uint8_t((rb & (kAcclaim | kHeartbeat)) |
-                                       timers(i, st, (rb & kHeard) != 0, lead, lead_set, t, now, timeout, jitter,
-                                              seed, ids, to[v], lh[v], f));
-            if (st != st0) f.state[i] = st;
-            if (lead_set) f.leader[i] = lead;
-            if (ob != prev) ob_out[i] = ob;
-            if (ob) seg[atomicAdd(&s_ns, 1)] = int32_t(i);  // this workgroup's sender segment (LDS counter)
-            c_lead += st == ST_L;
-            c_wait += st == ST_W;
-            c_acc += (ob & kAcclaim) != 0;
-            c_hb += (ob & kHeartbeat) != 0;
+#pragma unroll
+            for (int v = 0; v < kSweepV; ++v) {
+                const int64_t i = i0 + v;
+                if ((mine >> v) & 1u) continue;  // a receiver: the receive role's
+                const uint8_t prev = pv[v];      // this slot's byte from tick t-2
+                if (!al[v]) {
+                    if (i < n && prev) ob_out[i] = 0;
+                    continue;
+                }
+                Heard h{sv[v], 0, false, false, 0, -1};
+                finish_agent(i, h, sv[v], prev, t, now, timeout, jitter, seed, ids, to[v], lh[v], f, ob_out, seg,
+                             &s_ns, c);
+            }
         }
     }
-    add_counts(c_lead, c_wait, c_acc, c_hb, s_cnt, counts);  // (ends with a barrier: s_ns is final)
+    if (tr) {
+        add_traffic(tr, pulled ? 5 : 0, pulled ? 0ull : c.single);
+        add_traffic(tr, pulled ? 6 : 1, c.multi);
+        add_traffic(tr, 2, c.edges);
+        if (pulled && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&tr[7], 1ull);  // pulled ticks
+    }
+    add_counts(c.lead, c.wait, c.acc, c.hb, s_cnt, counts);  // (ends with a barrier: s_ns is final)
     if (threadIdx.x == 0) seg_count[blockIdx.x] = s_ns;
 }
 
 // Mail for the hearers of every sender the sweep listed: workgroup b walks segment b.  A storm tick
 // (this tick's senders -- ACCLAIM + HEARTBEAT counts, an agent sending both counted twice -- above
 // thr) mails nothing and flags the next tick's receive as a pull; every workgroup decides the same.
-__global__ __launch_bounds__(kBlock) void k_mail(const int32_t *__restrict__ senders, int64_t seg_cap,
+__global__ __launch_bounds__(kBlock) void k_mail(Segs segs,
                                                 const int32_t *__restrict__ seg_count,
                                                 const int32_t *__restrict__ trp, const int32_t *__restrict__ tcol,
                                                 Mail mail, const unsigned long long *__restrict__ cnt_t,
                                                 unsigned long long thr, unsigned *__restrict__ pull_next,
-                                                unsigned long long *__restrict__ tr) {
+                                                unsigned long long *__restrict__ tr,
+                                                unsigned long long *__restrict__ clear, int64_t n_clear) {
     __shared__ unsigned long long s_tot;
+    // the tick's own mail words (bits and multi of the other parity), read by k_tick: cleared here
+    for (int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x; q < n_clear; q += int64_t(gridDim.x) * kBlock)
+        if (clear[q]) clear[q] = 0;
     if (thr != ~0ull) {
         if (threadIdx.x < kWave) {
             unsigned long long v = cnt_t[threadIdx.x * 4 + 2] + cnt_t[threadIdx.x * 4 + 3];
@@ -499,7 +577,7 @@ __global__ __launch_bounds__(kBlock) void k_mail(const int32_t *__restrict__ sen
         *pull_next = 0;
     }
     const int m = seg_count[blockIdx.x];
-    const int32_t *seg = senders + int64_t(blockIdx.x) * seg_cap;
+    const int32_t *seg = segs.of(blockIdx.x);
     unsigned long long c_edges = 0;
     for (int q = threadIdx.x; q < m; q += kBlock) {
         const int32_t i = seg[q];
@@ -578,27 +656,45 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
     const bool push = hear_row_ptr != nullptr;
     const int64_t n_words = (n + 63) / 64;
     Mail mail{};
-    int32_t *list = nullptr, *senders = nullptr, *seg_count = nullptr;
-    int64_t seg_cap = 0;
-    unsigned *n_list = nullptr, *pullf = nullptr;
-    if (push) {  // mail bitmap + the two list counters (tick parity) after it
-        unsigned long long *mw;  // mail bits, multi-sender bits, then the two list counters
-        SW_ALLOC(mw, ctx, S_FSM_MAIL, size_t(n_words) * 16 + 64);
-        mail.bits = mw;
-        mail.multi = mw + n_words;
+    int32_t *seg_count = nullptr;
+    Segs segs{};
+    unsigned *pullf = nullptr;
+    unsigned long long *mw = nullptr;  // by tick parity p: mail bits at mw + 2p n_words, multi bits after them
+    auto mail_of = [&](int64_t tick) {  // the mail a tick receives (parity of the tick)
+        Mail m = mail;
+        m.bits = mw + size_t(tick & 1) * 2 * size_t(n_words);
+        m.multi = m.bits + n_words;
+        return m;
+    };
+    // k_tick's receive role: a workgroup per 4 096-agent chunk, at most half the sweep grid (10M agents:
+    // 2 048 of 2 442 chunks' workgroups, 0.138 ms per tick; 1 500: 0.138, 512: 0.160, 256: 0.214;
+    // SWARM_FSM_RECV_WGS overrides, A/B aid)
+    static const int recv_env = [] {
+        const char *e = getenv("SWARM_FSM_RECV_WGS");
+        return e ? atoi(e) : 0;
+    }();
+    const int64_t nchunks_all = (n + kRecvChunk - 1) / kRecvChunk;
+    const int g_recv = int(std::max<int64_t>(
+        1, std::min<int64_t>(nchunks_all, recv_env > 0 ? recv_env : std::max<int64_t>(1, grid / 2))));
+    const unsigned tgrid = grid + unsigned(g_recv);  // k_tick / k_mail: both roles, interleaved
+    if (push) {  // mail bitmaps (two parities) + the pull flags (tick parity) after them
+        SW_ALLOC(mw, ctx, S_FSM_MAIL, size_t(n_words) * 32 + 64);
         SW_ALLOC(mail.from, ctx, S_FSM_FROM, size_t(n) * 4);
-        SW_ALLOC(list, ctx, S_FSM_LIST, size_t(n) * 4);
-        // per-workgroup sender segments of the sweep (grid-stride: each workgroup sees at most
-        // seg_cap agents), then their counts
-        const int64_t ngroups = (n + kSweepV - 1) / kSweepV;  // k_sweep: kSweepV agents per thread
-        seg_cap = (ngroups + int64_t(grid) * kBlock - 1) / (int64_t(grid) * kBlock) * kBlock * kSweepV;
-        SW_ALLOC(senders, ctx, S_FSM_SEND, size_t(seg_cap) * grid * 4 + size_t(grid) * 4);
-        seg_count = senders + seg_cap * grid;
-        n_list = reinterpret_cast<unsigned *>(mw + 2 * n_words);
-        pullf = n_list + 2;  // [2] by tick parity: the tick's receive pulls (zeroed with the bitmap)
-        SW_HIP(hipMemsetAsync(mw, 0, size_t(n_words) * 16 + 64, s));
+        // per-workgroup sender segments of k_tick (each workgroup lists at most the agents it sees:
+        // a grid-stride share of kSweepV-agent groups, or of 4 096-agent chunks), then their counts
+        const int64_t ngroups = (n + kSweepV - 1) / kSweepV;
+        const int64_t nchunks = (n + kRecvChunk - 1) / kRecvChunk;
+        segs.g_recv = g_recv;
+        segs.rcap = (nchunks + g_recv - 1) / g_recv * kRecvChunk;
+        segs.scap = std::max((ngroups + int64_t(grid) * kBlock - 1) / (int64_t(grid) * kBlock) * kBlock * kSweepV,
+                             (nchunks + tgrid - 1) / tgrid * kRecvChunk);
+        const size_t seg_total = size_t(g_recv) * segs.rcap + size_t(grid) * segs.scap;
+        SW_ALLOC(segs.base, ctx, S_FSM_SEND, seg_total * 4 + size_t(tgrid) * 4);
+        seg_count = segs.base + seg_total;
+        pullf = reinterpret_cast<unsigned *>(mw + 4 * n_words);  // [2] by tick parity: the tick pulls
+        SW_HIP(hipMemsetAsync(mw, 0, size_t(n_words) * 32 + 64, s));
         hipLaunchKernelGGL(k_mail_from_outbox, dim3(grid), dim3(kBlock), 0, s, n,
-                           fsm->outbox + size_t(t0 & 1) * size_t(n), hear_row_ptr, hear_col, mail);
+                           fsm->outbox + size_t(t0 & 1) * size_t(n), hear_row_ptr, hear_col, mail_of(t0 + 1));
         SW_LAUNCHED();
     }
     for (int64_t t = t0 + 1; t <= t0 + ticks; ++t) {
@@ -612,20 +708,14 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
         uint8_t *ob_out = fsm->outbox + size_t(t & 1) * size_t(n);
         unsigned long long *cnt = d_cnt + size_t(t - t0 - 1) * kShards * 4;
         if (push) {
-            unsigned *nl = n_list + (t & 1), *nl_next = n_list + ((t + 1) & 1);
-            hipLaunchKernelGGL(k_compact, dim3(grid_for(n_words, kBlock, 2048)), dim3(kBlock), 0, s, n_words, mail,
-                               list, nl, pullf + (t & 1));
+            hipLaunchKernelGGL(k_tick, dim3(tgrid), dim3(kBlock), 0, s, n, t, ids,
+                               reinterpret_cast<const double2 *>(pos), row_ptr, col, tick_off, f, mail_of(t), ob_in,
+                               ob_out, pullf + (t & 1), segs, seg_count, dt, timeout, jitter, seed, cnt,
+                               int(vec && (reinterpret_cast<uintptr_t>(ob_out) & 3) == 0), d_tr);
             SW_LAUNCHED();
-            hipLaunchKernelGGL(k_receive, dim3(2048), dim3(kBlock), 0, s, t, list, mail.from, nl, nl_next, ids,
-                               reinterpret_cast<const double2 *>(pos), row_ptr, col, tick_off, f, ob_in, ob_out, dt,
-                               pullf + (t & 1), n, d_tr);
-            SW_LAUNCHED();
-            hipLaunchKernelGGL(k_sweep, dim3(grid), dim3(kBlock), 0, s, n, t, ids, tick_off, f, ob_out, senders,
-                               seg_cap, seg_count, dt, timeout, jitter, seed, cnt,
-                               int(vec && (reinterpret_cast<uintptr_t>(ob_out) & 3) == 0));
-            SW_LAUNCHED();
-            hipLaunchKernelGGL(k_mail, dim3(grid), dim3(kBlock), 0, s, senders, seg_cap, seg_count, hear_row_ptr,
-                               hear_col, mail, cnt, thr, pullf + ((t + 1) & 1), d_tr);
+            hipLaunchKernelGGL(k_mail, dim3(tgrid), dim3(kBlock), 0, s, segs, seg_count, hear_row_ptr,
+                               hear_col, mail_of(t + 1), cnt, thr, pullf + ((t + 1) & 1), d_tr, mail_of(t).bits,
+                               2 * n_words);
         } else {
             hipLaunchKernelGGL(k_tick_pull, dim3(grid), dim3(kBlock), 0, s, n, t, ids,
                                reinterpret_cast<const double2 *>(pos), row_ptr, col, tick_off, f, ob_in, ob_out, dt,

@@ -16,8 +16,7 @@ sys.path.insert(0, os.path.join(ROOT, "distributed-swarm-algorithm_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from swarm_amd import gen  # noqa: E402
-from swarm_amd.swarm import Swarm  # noqa: E402
+from swarm_amd import _lib, gen  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--agents", type=int, default=10_000_000)
@@ -25,7 +24,10 @@ ap.add_argument("--ticks", type=int, default=200)
 ap.add_argument("--deg", type=float, default=16.0)
 ap.add_argument("--modes", default="push:0,hybrid:0.125,hybrid:0.05,hybrid:0.25,pull:0",
                 help="comma list of mode:pull_frac")
+ap.add_argument("--lib", default="libswarm.so", help="library under swarm_amd/ (A/B builds)")
 a = ap.parse_args()
+_lib.load(os.path.join(_lib.HERE, a.lib))
+from swarm_amd.swarm import Swarm  # noqa: E402
 d = gen.swarm_inputs(a.agents, 3, deg=a.deg)
 s = Swarm(d["ids"], d["x"], d["y"], device="cuda").build_graph(1.0)
 off = (np.arange(a.agents) * 7919 % 40).astype(np.int32)
@@ -43,4 +45,5 @@ for mode, pf in ((m.split(":")[0], float(m.split(":")[1])) for m in a.modes.spli
                                counts_sum=int(c.sum()), traffic=None if tr is None else [int(v) for v in tr])
     print(json.dumps({f"{mode}_{pf}": out[f"{mode}_{pf}"]}), flush=True)
 sums = {k: v["counts_sum"] for k, v in out.items()}
-print(json.dumps(dict(agents=a.agents, edges=s.n_edges, ticks=a.ticks, same_counts=len(set(sums.values())) == 1)))
+print(json.dumps(dict(lib=a.lib, agents=a.agents, edges=s.n_edges, ticks=a.ticks,
+                      same_counts=len(set(sums.values())) == 1, counts_sums=sorted(set(sums.values())))))
