@@ -429,12 +429,15 @@ __global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int
     TickCounts c;
     if (pulled || recv_role) {
         // ---- receive role
+        // a pulled tick: every workgroup, 1 024-agent units (every agent walks its row: 4x the units,
+        // a quarter of the row walks one after the other per thread)
         const int64_t nrole = pulled ? int64_t(gridDim.x) : int64_t(g_recv);
-        const int64_t nchunks = (n + kRecvChunk - 1) / kRecvChunk;
+        const int kPerT = pulled ? kRecvChunk / 4 / kBlock : kRecvChunk / kBlock;  // agents per thread
+        const int64_t unit = int64_t(kPerT) * kBlock;
+        const int64_t nchunks = (n + unit - 1) / unit;
         for (int64_t ck = pulled ? int64_t(blockIdx.x) : int64_t(rank); ck < nchunks; ck += nrole) {
-            // thread: kPerT agents, a slice of mail word (ck * kRecvChunk + threadIdx.x * kPerT) / 64
-            constexpr int kPerT = kRecvChunk / kBlock;
-            const int64_t a0 = ck * kRecvChunk + int64_t(threadIdx.x) * kPerT;
+            // thread: kPerT agents, a slice of mail word (ck * unit + threadIdx.x * kPerT) / 64
+            const int64_t a0 = ck * unit + int64_t(threadIdx.x) * kPerT;
             unsigned b16 = 0, m16 = 0;
             if (a0 < n) {
                 const unsigned valid = n - a0 >= kPerT ? (1u << kPerT) - 1u : ((1u << (n - a0)) - 1u);

@@ -240,3 +240,23 @@ def test_gpu_hybrid_storm_ticks_match_oracle(oracle_mod, pull_frac):
         assert tr[7] > 0 and tr[6] > 0 and tr[3] == 0 and tr[0] == 0
     senders = int((want["counts"][:, 2] + want["counts"][:, 3]).sum())
     assert tr[3] <= senders
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("recv_wgs", ["1", "3"])
+def test_gpu_few_receive_workgroups_match_oracle(recv_wgs):
+    """k_tick's receive role with 1 or 3 workgroups (SWARM_FSM_RECV_WGS), each serving many
+    4 096-agent units one after the other, beside the sweep role: the oracle's states, timers and
+    counts.  The tuning is read once per process: a child process."""
+    import json
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    p = subprocess.run([sys.executable, "-u", os.path.join(here, "protocol_env_case.py")],
+                       env=dict(os.environ, SWARM_FSM_RECV_WGS=recv_wgs), capture_output=True, text=True,
+                       timeout=300)
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert p.returncode == 0 and lines, (p.returncode, p.stdout[-2000:], p.stderr[-2000:])
+    res = json.loads(lines[-1])
+    assert res["ok"], (res["error"], [c for c in res["cases"] if c["bad"]])
