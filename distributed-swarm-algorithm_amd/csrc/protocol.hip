@@ -462,29 +462,37 @@ __global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int
             for (int q = threadIdx.x; q < total; q += kBlock) {
                 const uint32_t entry = s_list[q];
                 const int64_t i = int32_t(entry & 0x7FFFFFFFu);
-                const uint8_t prev = ob_out[i];
-                if (!f.alive[i]) {
+                const bool multi = (entry & 0x80000000u) != 0;
+                // the receiver's fields and its single sender, all loads at once (no load behind the
+                // alive test), then the sender's outbox, ID and position at once
+                const uint8_t prev = ob_out[i], al = f.alive[i], st0 = f.state[i];
+                const int32_t toff = tick_off[i], me = ids[i];
+                const double lhb = f.last_hb[i];
+                const int32_t j = multi ? 0 : mail.from[i];
+                if (!al) {
                     if (prev) ob_out[i] = 0;
                     continue;
                 }
-                const uint8_t st0 = f.state[i];
-                const int32_t toff = tick_off[i];
-                const double lhb = f.last_hb[i];
                 Heard h{st0, 0, false, false, 0, -1};
-                const int32_t me = ids[i];
                 const bool hb_tick = ((t + toff) % 10) == 0;
-                if (entry & 0x80000000u) {  // several senders (or a pull): the row, in CSR order
+                if (multi) {  // several senders (or a pull): the row, in CSR order
                     const int32_t b = rp[i], e = rp[i + 1];
                     receive_row(b, e, col, ob_in, ids, me, hb_tick, h);
                     ++c.multi;
                     c.edges += uint64_t(e - b);
+                    apply_heard(i, h, now, pos, f);
                 } else {  // exactly one sender: no row walk
-                    const int32_t j = mail.from[i];
                     const uint8_t o = ob_in[j] & (kAcclaim | kHeartbeat);
-                    if (o) hear(h, o, ids[j], j, me, hb_tick);
+                    const int32_t sid = ids[j];
+                    const double2 sp = pos[j];  // used when its heartbeat is accepted (hb_from = j)
+                    if (o) hear(h, o, sid, j, me, hb_tick);
                     ++c.single;
+                    if (h.live) f.last_hb[i] = now;
+                    if (h.hb_from >= 0) {
+                        f.lpos[i] = make_float2(float(sp.x), float(sp.y));
+                        f.has_lpos[i] = 1;
+                    }
                 }
-                apply_heard(i, h, now, pos, f);
                 finish_agent(i, h, st0, prev, t, now, timeout, jitter, seed, ids, toff, lhb, f, ob_out, seg, &s_ns, c);
             }
             __syncthreads();  // the list is reused
