@@ -86,6 +86,23 @@ def pmc_traffic(kernel_prefix):
     return None if best is None else (best[0], f"rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE, {best[1]}")
 
 
+def pmc_traffic_sum(names):
+    """Summed HBM bytes per dispatch of several kernels (exact names, e.g. the launches of one
+    protocol tick) from profiles/LATEST's PMC summary, or None when one of them is missing."""
+    latest = os.path.join(ROOT, "profiles", "LATEST")
+    if not os.path.exists(latest):
+        return None
+    path = os.path.join(ROOT, "profiles", open(latest).read().strip(), "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    if not all(isinstance(d.get(k), dict) for k in names):
+        return None
+    return (sum(d[k]["hbm_bytes_per_dispatch"] for k in names),
+            f"rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE, {os.path.relpath(path, ROOT)} ({' + '.join(names)})")
+
+
 def main():
     args = parse()
     import torch
@@ -387,7 +404,10 @@ def _roof(alg_bytes, ms, kernel, pmc_kernel=None, note=None):
     """Row roofline: algorithmic bytes of one unit of work over its measured time (device work
     of the unit, wall-clock around a synchronised call), traffic from the committed PMC summary."""
     gbs = alg_bytes / (ms * 1e-3) / 1e9
-    t = pmc_traffic(pmc_kernel) if pmc_kernel else None
+    if isinstance(pmc_kernel, (list, tuple)):
+        t = pmc_traffic_sum(pmc_kernel)
+    else:
+        t = pmc_traffic(pmc_kernel) if pmc_kernel else None
     out = {"bound": "hbm", "kernel": kernel, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": gbs / HBM_PEAK_GBS, "algorithmic_bytes": alg_bytes, "ms": ms,
            "traffic_per_dispatch": t[0] if t else None, "traffic_source": t[1] if t else None}
@@ -526,7 +546,7 @@ def rows_bench(sw, dev, args):
                                  "agent_ticks_per_s": n * ticks / (ms * 1e-3),
                                  "leaders_final": int(c[-1, 0]), "heartbeats": int(c[:, 3].sum()),
                                  "traffic": [int(v) for v in sw.fsm_traffic],
-                                 "roofline": _roof(fb / ticks, ms / ticks, "k_tick + k_mail", "k_tick",
+                                 "roofline": _roof(fb / ticks, ms / ticks, "k_tick + k_mail", ["k_tick", "k_mail"],
                                                    note="every tick's algorithmic bytes (fsm_bytes: the sweep's 15 B "
                                                         "per agent, the mail bitmap read and cleared, each receiver's "
                                                         "fields, 5 B per row edge walked, 8 B per sender + 6 B per "
