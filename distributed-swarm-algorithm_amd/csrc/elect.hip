@@ -501,26 +501,14 @@ __device__ __forceinline__ int wave_excl_scan(int c, int &total) {
 // `first`/`step` select this wave's share; risers mark themselves and their neighbours.  Lane
 // `sub` of an agent takes edges b + sub + G*j (interleaved: one load instruction covers G
 // consecutive edges of every agent it serves, so each touches one cache line per agent).
-// TAIL (k_elect_xcd): leaders are read with sc1 loads (other CUs of this XCD wrote them earlier in
-// the same launch; L1 is not coherent, the XCD's L2 is), stamps are in agent order (slot = agent)
-// and every mark also flags its 2^CS-agent chunk in dw (the next round scans flagged chunks only).
-template <bool TAIL>
-__device__ __forceinline__ int ld_leader(const int32_t *__restrict__ P, int32_t i) {
-    if constexpr (TAIL)
-        return __hip_atomic_load(const_cast<int32_t *>(P) + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-        return ld4(P, i);
-}
-
-template <typename Off, int G, int K, bool DIR, typename CT, bool TAIL = false, int CS = 11>
+template <typename Off, int G, int K, bool DIR, typename CT>
 __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, CT cols,
                                               const Off *__restrict__ hrp, const int32_t *__restrict__ hcol,
                                               const int32_t *__restrict__ P, int32_t *__restrict__ Q,
                                               uint8_t *__restrict__ aw, const StampMap &sm, uint8_t sw,
                                               const int *lst, int total, int first, int step, int64_t c_lo,
                                               int64_t n_count,
-                                              long long &my_chg, int &my_act, int &my_edges,
-                                              uint8_t *__restrict__ dw = nullptr) {
+                                              long long &my_chg, int &my_act, int &my_edges) {
     const int lane = threadIdx.x & 63, sub = lane & (G - 1);
     using Ix = Off;  // 32-bit offsets in the int32-CSR instantiation (host: < 2^30 agents and edges)
     if (first >= total) return;
@@ -528,7 +516,7 @@ __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, CT col
     // pass, so a pass's chain is columns -> leaders only
     int32_t nv = lst[first + lane / G < total ? first + lane / G : total - 1];
     Off nb = ld4(rp, Ix(nv)), ne = ld4(rp, Ix(nv + 1));
-    int nown = TAIL ? ld_leader<true>(P, nv) : ld4(P, Ix(nv));
+    int nown = ld4(P, Ix(nv));
     for (int base = first; base < total; base += step) {
         const int i = base + lane / G;
         const bool valid = i < total;
@@ -540,7 +528,7 @@ __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, CT col
             nv = lst[i2 < total ? i2 : total - 1];
             nb = ld4(rp, Ix(nv));
             ne = ld4(rp, Ix(nv + 1));
-            nown = TAIL ? ld_leader<true>(P, nv) : ld4(P, Ix(nv));
+            nown = ld4(P, Ix(nv));
         }
         int m = own;
         int c[K];
@@ -549,33 +537,14 @@ __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, CT col
             for (int j = 0; j < K; ++j) c[j] = cols.at32((k + G * j < e) ? k + G * j : e - 1, v & ~63);
             int val[K];
 #pragma unroll
-            for (int j = 0; j < K; ++j) val[j] = TAIL ? ld_leader<true>(P, c[j]) : ld4(P, Ix(c[j]));
+            for (int j = 0; j < K; ++j) val[j] = ld4(P, Ix(c[j]));
 #pragma unroll
             for (int j = 0; j < K; ++j) m = max(m, val[j]);
         }
         m = group_max<G>(m);
         const bool up = valid && m > own;
         if (valid && sub == 0) st4(Q, Ix(v), m);
-        if (TAIL && up) {  // agent-order stamps: slot = agent; flag the chunk of every mark
-            if (sub == 0) {
-                aw[v] = sw;
-                dw[v >> CS] = 1;
-            }
-            if (e - b <= G * K) {
-#pragma unroll
-                for (int j = 0; j < K; ++j)
-                    if (b + sub + G * j < e) {
-                        aw[c[j]] = sw;
-                        dw[c[j] >> CS] = 1;
-                    }
-            } else {
-                for (Off k = b + sub; k < e; k += G) {
-                    const int32_t cc = cols.at32(k, v & ~63);
-                    aw[cc] = sw;
-                    dw[cc >> CS] = 1;
-                }
-            }
-        } else if (up) {
+        if (up) {
             if (sub == 0) aw[stamp_slot(sm, v)] = sw;
             if (DIR) {  // the agents that hear v
                 mark_row<Off>(aw, sm, Col32{hcol}, 0, hrp[v] + sub, hrp[v + 1], Off(G), sw);
@@ -763,294 +732,6 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
 #endif
 }
 
-// ------------------------------------------------------------------ small swarms: one XCD
-// A small swarm's sparse rounds (C2: 100k agents, ~170 of them) are each a kernel boundary plus a
-// few dependent loads: ~6.8 us per round, almost all of it latency, on a chip 100x wider than the
-// work.  k_elect_xcd runs all of them in ONE launch on ONE XCD: 8 x kXcdPer workgroups are
-// launched; workgroup 0 names its XCD (hardware XCC_ID, checked, not assumed from the dispatch
-// order), the workgroups on it stay and count themselves in a census, every other one leaves.  The
-// stayers separate rounds with a flag barrier of their own: their loads and stores all meet in
-// that XCD's L2 -- stores plain (L1 is write-through), loads of data written in the launch sc1 (L1
-// bypass) -- so no release / acquire fence is needed (tools/xcd_barrier_bench: 0 stale hand-offs,
-// 1.0 us per barrier at any participant count).  The swarm's leaders, stamps and columns stay in
-// that L2 from round to round.  Marks flag their chunk, so a round reads the chunk flags, then the
-// stamp words of flagged chunks only, and consumes them (no stale stamp survives: no periodic
-// clears).  The first round with no change is the last one run (exact convergence stop).
-// Measured on large swarms' tails (tag r4-xcd-tail): one XCD's 32 CUs lose to the chip
-// once a round has more than ~2 000 changes.
-constexpr int kXcdPer = 128;  // participants requested per XCD: 4 per CU
-constexpr int kCtlLine = 32;  // u32 per control line
-struct XcdCtl {               // k_elect_xcd control lines, zeroed before every launch except `done`
-    unsigned chosen[kCtlLine], joined[kCtlLine], nonpart[16][kCtlLine],
-        gen[kCtlLine], err[kCtlLine];
-    unsigned flag[kBlock];        // arrival of participant r in round i: 2 (i + 1) + (it changed an agent)
-    unsigned cnt[2][kBlock][4];   // participant r's changes, marked agents, edges of a round (by parity)
-    unsigned done[kCtlLine];      // sticky: a round of an earlier launch changed nothing
-};
-
-__device__ __forceinline__ unsigned ld_sc1(const unsigned *p) {
-    return __hip_atomic_load(const_cast<unsigned *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1(unsigned *p, unsigned v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned xcc_id() {
-    unsigned x;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-    return x & 0xFu;
-}
-// Bounded wait (1 s) for *p >= want; on timeout or another workgroup's error: err set, false.
-__device__ bool xcd_wait(const unsigned *p, unsigned want, unsigned *err) {
-    const unsigned long long t0 = wall_clock64();
-    while (ld_sc1(p) < want) {
-        if (ld_sc1(err) || wall_clock64() - t0 > 100000000ull) {
-            atomicMax(err, 1u);
-            return false;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-    return true;
-}
-
-__device__ __forceinline__ uint2 ld_stamp_sc1(const uint2 *p) {
-    const unsigned long long v = __hip_atomic_load(reinterpret_cast<unsigned long long *>(const_cast<uint2 *>(p)),
-                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return make_uint2(unsigned(v), unsigned(v >> 32));
-}
-__device__ __forceinline__ uint16_t ld_stamp_sc1(const uint16_t *p) {
-    return __hip_atomic_load(const_cast<uint16_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void zero_stamp(uint2 *p) { *p = make_uint2(0u, 0u); }
-__device__ __forceinline__ void zero_stamp(uint16_t *p) { *p = 0; }
-
-// Rounds t0..t1 (agent-order stamps, chunks of kBlock x S agents, single GPU).  full: the first round
-// scans every chunk (the stamps were written by the dense marking round, which keeps no chunk flags).
-template <typename Off, typename CT, int S>
-__global__ __launch_bounds__(kBlock) void k_elect_xcd(const Off *__restrict__ rp, CT cols, Frontier f, int t0,
-                                                     int t1, int full, uint8_t *__restrict__ dirty, int64_t mpad,
-                                                     XcdCtl *c, int total, unsigned long long *herr) {
-    __shared__ int s_list[kListCap];
-    __shared__ int s_chunks[kBlock];
-    __shared__ int s_wave[kWavesPerBlock];
-    __shared__ long long s_red[3][kWavesPerBlock];
-    __shared__ int s_rank, s_P, s_ok, s_stop;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    using W = typename StampWord<S>::T;
-    constexpr int CS = S == 8 ? 11 : 9;           // log2 of a chunk (kBlock x S agents)
-    constexpr int kPx = kListCap / (kBlock * S);  // chunks whose stamp words are loaded at once
-    // census: workgroup 0 names its XCD; the workgroups on it are the participants (rank = arrival
-    // order among them), every other one counts itself on its own XCD's counter and leaves (a single
-    // counter for 1 024 arrivals costs ~12 us of serialised device-scope atomics)
-    if (threadIdx.x == 0) {
-        const unsigned x = xcc_id();
-        s_rank = -1;
-        s_ok = 1;
-        if (blockIdx.x == 0) st_sc1(c->chosen, x + 1);
-        if (xcd_wait(c->chosen, 1u, c->err) && ld_sc1(c->chosen) == x + 1)
-            s_rank = int(atomicAdd(c->joined, 1u));
-        else
-            atomicAdd(&c->nonpart[x][0], 1u);
-    }
-    __syncthreads();
-    if (threadIdx.x < kWave) {
-        if (s_rank >= 0) {  // wait until every workgroup is counted: P = joined
-            const unsigned long long w0 = wall_clock64();
-            for (;;) {
-                unsigned v = threadIdx.x < 16 ? ld_sc1(&c->nonpart[threadIdx.x][0])
-                                              : threadIdx.x == 16 ? ld_sc1(c->joined) : 0u;
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-                if (v >= unsigned(total)) break;
-                if (ld_sc1(c->err) || wall_clock64() - w0 > 100000000ull) {
-                    if (threadIdx.x == 0) {
-                        atomicMax(c->err, 1u);
-                        s_ok = 0;
-                    }
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            if (threadIdx.x == 0 && s_ok) {
-                s_P = int(ld_sc1(c->joined));
-                // one chunk flag per thread (too few participants) and one arrival flag per thread of rank 0
-                if ((f.sm.M + s_P - 1) / s_P > kBlock || s_P > kBlock) {
-                    atomicMax(c->err, 2u);
-                    s_ok = 0;
-                }
-                if (ld_sc1(c->done)) s_ok = 0;  // converged in an earlier launch
-            }
-        }
-    }
-    __syncthreads();
-    if (s_rank >= 0 && threadIdx.x == 0 && ld_sc1(c->err)) *herr = ld_sc1(c->err);  // to the host (mapped)
-    if (s_rank < 0 || !s_ok) return;
-    const int r = s_rank, P = s_P;
-    const int64_t n = f.n_rows, M = f.sm.M;
-    for (int t = t0, i = 0; t <= t1; ++t, ++i) {
-        const int32_t *__restrict__ Pl = f.L[(t - 1) & 1];
-        int32_t *__restrict__ Q = f.L[t & 1];
-        const uint8_t *ar = f.act[t & 1];
-        uint8_t *aw = f.act[(t + 1) & 1];
-        uint8_t *dr = dirty + (t & 1) * mpad, *dw = dirty + ((t + 1) & 1) * mpad;
-        const unsigned stamp4 = unsigned(stamp_of(t)) * 0x01010101u;
-        const uint8_t sw = stamp_of(t + 1);
-        long long my_chg = 0;
-        int my_act = 0, my_edges = 0;
-        // this round's chunks: r, r + P, ... (all of them in a full scan, else the flagged ones)
-        const int nmine = int((M - r + P - 1) / P);  // <= kBlock (host: M <= kBlock * P)
-        int nd = 0;
-        if (full && t == t0) {
-            nd = nmine;
-            for (int q = threadIdx.x; q < nmine; q += kBlock) s_chunks[q] = r + q * P;
-        } else {
-            const int64_t k = r + int64_t(threadIdx.x) * P;
-            int fl = 0;
-            if (threadIdx.x < nmine) {
-                fl = __hip_atomic_load(dr + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (fl) dr[k] = 0;  // consumed (re-flagged by round t+1's marks only)
-            }
-            int wtot;
-            const int ex = wave_excl_scan<1>(fl ? 1 : 0, wtot);
-            if (lane == 0) s_wave[wid] = wtot;
-            __syncthreads();
-            int off = 0;
-#pragma unroll
-            for (int w = 0; w < kWavesPerBlock; ++w) {
-                off += w < wid ? s_wave[w] : 0;
-                nd += s_wave[w];
-            }
-            if (fl) s_chunks[off + ex] = int(k);
-        }
-        __syncthreads();
-        int listed = 0;  // workgroup-uniform
-        for (int q = 0; q < nd; q += kPx) {
-            W wv[kPx];
-#pragma unroll
-            for (int p = 0; p < kPx; ++p) {
-                const int64_t k = s_chunks[q + p < nd ? q + p : q];
-                wv[p] = ld_stamp_sc1(reinterpret_cast<const W *>(ar + (k << CS)) + threadIdx.x);
-            }
-            unsigned mask = 0;
-#pragma unroll
-            for (int p = 0; p < kPx; ++p) {
-                if (q + p >= nd) break;
-                const int64_t k = s_chunks[q + p];
-                if (any_stamp(wv[p]))  // consumed: a round's stamps are read once
-                    zero_stamp(reinterpret_cast<W *>(const_cast<uint8_t *>(ar) + (k << CS)) + threadIdx.x);
-                const int64_t v0 = (k << CS) + threadIdx.x * S;
-                mask |= take_stamps<S>(v0, n, wv[p], stamp4) << (p * S);
-            }
-            const int cnt = __popc(mask);  // <= kPx * S <= 16
-            int wtot;
-            const int excl = wave_excl_scan<5>(cnt, wtot);
-            if (lane == 0) s_wave[wid] = wtot;
-            __syncthreads();
-            int off = 0, tot = 0;
-#pragma unroll
-            for (int w = 0; w < kWavesPerBlock; ++w) {
-                off += w < wid ? s_wave[w] : 0;
-                tot += s_wave[w];
-            }
-            if (tot == 0) {
-                __syncthreads();  // s_wave read by all
-                continue;
-            }
-            if (listed + tot > kListCap) {  // gather what is listed first (tot <= kPx * chunk <= kListCap)
-                gather_listed<Off, kG, kKs, false, CT, true, CS>(rp, cols, nullptr, nullptr, Pl, Q, aw, f.wsm, sw,
-                                                                 s_list, listed, wid * (64 / kG), kBlock / kG,
-                                                                 f.c_lo, f.n_count, my_chg, my_act, my_edges, dw);
-                listed = 0;
-                __syncthreads();  // the list is reused
-            }
-            int pos = listed + off + excl;
-            while (mask) {
-                const int bit = __ffs(mask) - 1;
-                mask &= mask - 1;
-                s_list[pos++] = (s_chunks[q + bit / S] << CS) + threadIdx.x * S + (bit % S);
-            }
-            listed += tot;
-            __syncthreads();  // list entries visible, s_wave read by all
-        }
-        if (listed > 0)
-            gather_listed<Off, kG, kKs, false, CT, true, CS>(rp, cols, nullptr, nullptr, Pl, Q, aw, f.wsm, sw, s_list,
-                                                             listed, wid * (64 / kG), kBlock / kG, f.c_lo, f.n_count,
-                                                             my_chg, my_act, my_edges, dw);
-        // Round end, with no atomics (tools/xcd_barrier_bench: a flag barrier on one XCD costs 1.0 us
-        // at any participant count, counter barriers 1.3 .. 3 us): the workgroup's counts go to its slot
-        // of parity t & 1, then -- once every store of the round is in L2 -- its arrival flag
-        // 2 (i + 1) + changed.  Rank 0 polls all flags, publishes gen = 2 (i + 1) + stop (stop: no
-        // workgroup changed anything), and only then sums the counts into the ring for the host.
-        my_act = wave_sum(my_act);
-        my_edges = wave_sum(my_edges);
-        if (lane == 0) {
-            s_red[0][wid] = my_chg;
-            s_red[1][wid] = my_act;
-            s_red[2][wid] = my_edges;
-        }
-        __syncthreads();
-        unsigned changed = 0;
-        if (threadIdx.x == 0) {
-            long long a[3] = {0, 0, 0};
-            for (int w = 0; w < kWavesPerBlock; ++w)
-                for (int k = 0; k < 3; ++k) a[k] += s_red[k][w];
-            c->cnt[t & 1][r][0] = unsigned(a[0]);
-            c->cnt[t & 1][r][1] = unsigned(a[1]);
-            c->cnt[t & 1][r][2] = unsigned(a[2]);
-            changed = a[0] != 0;
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's leaders, marks, flags and counts
-        __syncthreads();
-        if (threadIdx.x == 0) c->flag[r] = unsigned(2 * (i + 1)) + changed;
-        if (r == 0) {
-            unsigned any = 0;
-            if (threadIdx.x < P) {
-                const unsigned long long w0 = wall_clock64();
-                unsigned fv;
-                while ((fv = ld_sc1(&c->flag[threadIdx.x])) < unsigned(2 * (i + 1))) {
-                    if (ld_sc1(c->err) || wall_clock64() - w0 > 100000000ull) {
-                        atomicMax(c->err, 1u);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                any = fv & 1u;
-            }
-            any = __syncthreads_or(int(any));
-            if (threadIdx.x == 0) {
-                s_stop = any ? 0 : 1;
-                if (!any) c->done[0] = 1u;
-                c->gen[0] = unsigned(2 * (i + 1)) + (any ? 0u : 1u);
-                if (ld_sc1(c->err)) s_stop = 1;
-            }
-            // the round's totals (ring shard 0, the other shards stay zero) and the slots of t + kRing/2
-            unsigned long long v[3] = {0, 0, 0};
-            if (threadIdx.x < P)
-                for (int k = 0; k < 3; ++k) v[k] = ld_sc1(&c->cnt[t & 1][threadIdx.x][k]);
-            for (int k = 0; k < 3; ++k) {
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off, 64);
-            }
-            if (lane == 0)
-                for (int k = 0; k < 3; ++k) s_red[k][wid] = (long long)v[k];
-            __syncthreads();
-            if (threadIdx.x < 3) {
-                long long a = 0;
-                for (int w = 0; w < kWavesPerBlock; ++w) a += s_red[threadIdx.x][w];
-                *slot(f.ring, t, threadIdx.x, 0) = (unsigned long long)a;
-                if (threadIdx.x == C_CHG) f.tot[t % kRing] = (unsigned long long)a;
-            }
-            for (int q = threadIdx.x; q < kCounters * kShards; q += kBlock)
-                *slot(f.ring, t + kRing / 2, q / kShards, q % kShards) = 0;
-        } else if (threadIdx.x == 0) {
-            s_ok = xcd_wait(c->gen, unsigned(2 * (i + 1)), c->err);
-            s_stop = s_ok ? int(ld_sc1(c->gen) & 1u) : 1;
-        }
-        __syncthreads();
-        if (s_stop) break;
-    }
-    if (threadIdx.x == 0 && ld_sc1(c->err)) *herr = ld_sc1(c->err);
-}
-
 // Sharded runs: halo values for ghosts [b_lo, b_lo + n_lo) and [b_hi, b_hi + n_hi) after round
 // t.  A ghost whose leader rose is written to BOTH leader buffers (ghosts are never gathered)
 // and its local neighbours are marked for round t+1 (ghost rows of the local CSR list them).
@@ -1151,10 +832,7 @@ struct Tuning {
     int use_c16 = 1;          // swarm_elect_compact reads the 16-bit columns (0: its int32 ones; A/B aid)
     int il_min_changes = -1;   // interleaved stamp layout while the last read round changed >= this
                                // (-1: 8e-4 x agents, measured best at 100k, 1M and 10M agents)
-    int xcd_max_n = 300000;    // single-GPU elections of at most this many agents: sparse rounds on one
-                               // XCD (k_elect_xcd; 0: never)
     Tuning() {
-        xcd_max_n = env_int("SWARM_XCD_MAX_N", 300000);
         il_min_changes = env_int("SWARM_IL_MIN_CHANGES", -1);
         use_c16 = env_int("SWARM_C16", 1);
         dense_flat = env_int("SWARM_DENSE_FLAT", 1);
@@ -1401,12 +1079,9 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     // the per-round totals land in mapped host memory, written by k_batch_totals itself
     void *dmap = nullptr;
     unsigned long long *hbuf =
-        static_cast<unsigned long long *>(mapped(ctx, size_t(kCounters) * 8 * kMaxBatch + 8, &dmap));
+        static_cast<unsigned long long *>(mapped(ctx, size_t(kCounters) * 8 * kMaxBatch, &dmap));
     if (!hbuf) return SWARM_ERR_OOM;
     unsigned long long *dtot = static_cast<unsigned long long *>(dmap);
-    // k_elect_xcd's error word, after the per-round totals: read with them, no extra synchronisation
-    volatile unsigned long long *herr = hbuf + size_t(kCounters) * kMaxBatch;
-    *herr = 0;
 
     int found = -1, t = 1, batch = 8, launched = 0;
     std::vector<int64_t> hist;  // per-round change counts read so far (batch sizing, layout)
@@ -1441,21 +1116,6 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     // and enqueues it (no idle gap at a batch boundary).  Rounds launched past convergence are
     // guarded no-ops.  Per-round timing and the round log keep the plain read-at-the-end batches.
     const int kLook = (timed || rlog) ? 0 : 8;
-    // Small swarms: every sparse round in k_elect_xcd launches of up to kMaxBatch - kLook rounds
-    // (symmetric int32 CSR, agent-order stamps from the dense marking round on, no per-round log).
-    // The first batch is the dense rounds, every later one a single launch read when it ends.
-    const bool xcd_small = mode == SWARM_ELECT_FRONTIER && n <= tuning().xcd_max_n && !rlog && !hrp &&
-                           sizeof(Off) == 4 && ag_map.bshift == ag_map.cshift &&
-                           (ag_map.cshift == 11 || ag_map.cshift == 9) && int64_t(ag_map.M) <= int64_t(kBlock) * 32;
-    const int64_t mpad = (int64_t(ag_map.M) + 127) / 128 * 128;
-    uint8_t *xcd_dirty = nullptr;
-    XcdCtl *xcd_ctl = nullptr;
-    bool xcd_on = false;
-    if (xcd_small) {
-        SW_ALLOC(xcd_dirty, ctx, S_XCD, size_t(2 * mpad) + sizeof(XcdCtl));
-        xcd_ctl = reinterpret_cast<XcdCtl *>(xcd_dirty + 2 * mpad);
-        if (tuning().dense_rounds > 0) batch = tuning().dense_rounds;
-    }
     hipEvent_t ev_read;
     SW_HIP(hipEventCreateWithFlags(&ev_read, hipEventDisableTiming));
     struct EvReadFree {
@@ -1493,12 +1153,9 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     };
     while (read_upto < max_rounds && found < 0) {
         t = launched + 1;  // first round launched in this batch (> tend when only a read is left)
-        // a small swarm's sparse rounds: one k_elect_xcd launch per batch, read at its end
-        const bool xcd_batch = xcd_small && plan_round(t) == RK_SPARSE;
-        if (xcd_batch) batch = kMaxBatch - kLook;
         const int tend = std::min(max_rounds, launched + batch);
         // read rounds (read_upto, tread]: at least one (the first batches are shorter than kLook)
-        const int tread = (tend == max_rounds || xcd_batch) ? tend : std::max(read_upto + 1, tend - kLook);
+        const int tread = tend == max_rounds ? tend : std::max(read_upto + 1, tend - kLook);
         int rc = 0;
         // per-round totals of rounds (read_upto, tread], reduced on device into mapped host memory, an event
         auto enqueue_read = [&]() -> int {
@@ -1514,38 +1171,6 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         // durations are the reference for this figure)
         int seg_n = 0;  // sparse launches inside this batch's segment
         for (int r = t; r <= tend; ++r) {
-            if (xcd_batch) {  // rounds [t, tend] in one launch (r == t)
-                const int full = xcd_on ? 0 : 1;  // the first launch scans every chunk (no flags yet)
-                if (full) SW_HIP(hipMemsetAsync(xcd_dirty, 0, size_t(2 * mpad) + sizeof(XcdCtl), s));
-                else SW_HIP(hipMemsetAsync(xcd_ctl, 0, offsetof(XcdCtl, done), s));
-                xcd_on = true;
-                Frontier fx = f;
-                fx.sm = fx.wsm = ag_map;
-                const int total = 8 * kXcdPer;
-                unsigned long long *herr_d = dtot + size_t(kCounters) * kMaxBatch;
-                if (timed) SW_HIP(hipEventRecord(ev[2 * kMaxBatch], s));
-                if constexpr (sizeof(Off) == 4) {  // xcd_small: int32 CSR only
-                    const bool big = ag_map.cshift == 11;  // 2 048-agent chunks (8 stamps per thread), else 512
-                    if (f.c16 && big)
-                        hipLaunchKernelGGL((k_elect_xcd<Off, Col16, 8>), dim3(total), dim3(kBlock), 0, s, rp,
-                                           Col16{f.c16}, fx, t, tend, full, xcd_dirty, mpad, xcd_ctl, total, herr_d);
-                    else if (f.c16)
-                        hipLaunchKernelGGL((k_elect_xcd<Off, Col16, 2>), dim3(total), dim3(kBlock), 0, s, rp,
-                                           Col16{f.c16}, fx, t, tend, full, xcd_dirty, mpad, xcd_ctl, total, herr_d);
-                    else if (big)
-                        hipLaunchKernelGGL((k_elect_xcd<Off, Col32, 8>), dim3(total), dim3(kBlock), 0, s, rp,
-                                           Col32{col}, fx, t, tend, full, xcd_dirty, mpad, xcd_ctl, total, herr_d);
-                    else
-                        hipLaunchKernelGGL((k_elect_xcd<Off, Col32, 2>), dim3(total), dim3(kBlock), 0, s, rp,
-                                           Col32{col}, fx, t, tend, full, xcd_dirty, mpad, xcd_ctl, total, herr_d);
-                }
-                SW_LAUNCHED();
-                if (timed) seg_n += tend - t + 1;
-                for (int q = t; q <= tend; ++q) kinds[q - t] = RK_SPARSE;
-                rd_map = ag_map;
-                if ((rc = enqueue_read())) return rc;
-                break;
-            }
             const bool sparse = mode == SWARM_ELECT_FRONTIER && plan_round(r) == RK_SPARSE;
             const bool seg = timed && sparse && !rlog;
             if (seg && seg_n++ == 0) SW_HIP(hipEventRecord(ev[2 * kMaxBatch], s));
@@ -1560,7 +1185,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
                 // marks for round r+1: interleaved layout while rounds are busy (balance), agent
                 // order once they are sparse (locality of the few gathers)
                 f.sm = rd_map;
-                f.wsm = (!xcd_small && (hist.empty() || hist.back() >= il_min)) ? il_map : ag_map;
+                f.wsm = (hist.empty() || hist.back() >= il_min) ? il_map : ag_map;
                 rc = launch_frontier_round<Off>(rp, col, f, r, kinds[r - t], 1, s, hrp, hcol);
                 rd_map = f.wsm;
             }
@@ -1571,11 +1196,6 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         if (seg_n) SW_HIP(hipEventRecord(ev[2 * kMaxBatch + 1], s));
         launched = std::max(launched, tend);
         SW_HIP(hipEventSynchronize(ev_read));
-        if (*herr) {  // a census or barrier of the single-XCD tail timed out: its rounds are undone
-            set_error("single-XCD tail rounds failed (%s)",
-                      *herr == 2 ? "too few workgroups on one XCD" : "census or barrier timed out");
-            return SWARM_ERR_HIP;
-        }
         if (timed) {  // kLook == 0: this batch's rounds are exactly the rounds read
             SW_HIP(hipStreamSynchronize(s));
             for (int r = t; r <= tend; ++r) {  // every launched round's kernel time (rocprof's view)
@@ -1603,9 +1223,6 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         // a batch spans at most kRing/2 rounds of counter slots, look-ahead included (bookkeeping
         // recycles the slot of round t - kRing/2 in round t)
         batch = next_round_batch(hist.data(), hist.size(), batch, kMaxBatch - kLook);
-        if (getenv("SWARM_BATCH_LOG"))  // tuning aid: each batch's rounds, read point and the next size
-            fprintf(stderr, "batch %d..%d read %d next %d last_changes %lld\n", t, tend, tread, batch,
-                    (long long)(hist.empty() ? -1 : hist.back()));
     }
     const int last = found > 0 ? found : max_rounds;
     if (found < 0 && (last & 1)) {

@@ -103,25 +103,3 @@ def test_elect_int64_offsets(sw, oracle_mod, n, deg):
         assert not r.converged and r.rounds_exec == m
         np.testing.assert_array_equal(r.leader.cpu().numpy(), want[0])
         np.testing.assert_array_equal(r.changes, changes[:m])
-
-
-@pytest.mark.parametrize("env", [{"SWARM_XCD_MAX_N": "0"},
-                                 {"SWARM_XCD_MAX_N": "2000000", "SWARM_SMALL_CHUNKS": "0"},
-                                 {"SWARM_XCD_MAX_N": "2000000"}],
-                         ids=["chip-only", "one-xcd-2048-chunks", "one-xcd-up-to-1M"])
-def test_elect_paths_forced_match_oracle(env):
-    """Small swarms run their sparse rounds on one XCD (k_elect_xcd) by default; these cases force
-    the whole-chip rounds for them, the one-XCD rounds with 2 048-agent chunks, and the one-XCD rounds
-    up to 1M agents: leaders, states, rounds, per-round counts and cut runs (path graph: cuts on and
-    around the 248-round launch boundaries) as the oracle.  The tuning is read once per process."""
-    import json
-    import os
-    import subprocess
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    p = subprocess.run([sys.executable, "-u", os.path.join(here, "elect_env_case.py")],
-                       env=dict(os.environ, **env), capture_output=True, text=True, timeout=400)
-    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
-    assert p.returncode == 0 and lines, (p.returncode, p.stdout[-2000:], p.stderr[-2000:])
-    res = json.loads(lines[-1])
-    assert res["ok"], (res["error"], [c for c in res["cases"] if not c["ok"]])
