@@ -38,7 +38,6 @@
 
 #include "binning.h"
 #include "utility.h"
-#include "xcd.h"
 
 namespace swarm {
 namespace {
@@ -162,24 +161,7 @@ __device__ __forceinline__ Best combine(Best x, Best y) {
 // the task in *bk.
 // W lanes (a power of two <= 64, aligned within the wave) evaluate agent a together, U list
 // entries per lane per pass.
-// COH (k_auc_xcd): prices and the previous round's keys were written in the same launch by other
-// workgroups of this XCD: read with sc1 loads (L1 bypass).
-template <bool COH>
-__device__ __forceinline__ float ld_price(const float *p, int32_t k) {
-    if constexpr (COH)
-        return __hip_atomic_load(const_cast<float *>(p) + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-        return p[k];
-}
-template <bool COH>
-__device__ __forceinline__ unsigned long long ld_key(const unsigned long long *p, int32_t k) {
-    if constexpr (COH)
-        return __hip_atomic_load(const_cast<unsigned long long *>(p) + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-        return p[k];
-}
-
-template <int W, int U, bool COH = false>
+template <int W, int U>
 __device__ __forceinline__ unsigned long long group_bid(const AucState &s, int64_t a, int32_t *bk_out,
                                                         const unsigned long long *kprev = nullptr) {
     const int lane = threadIdx.x & (W - 1);
@@ -198,11 +180,11 @@ __device__ __forceinline__ unsigned long long group_bid(const AucState &s, int64
             vv[u] = p < e ? s.cv[p] : 0.0f;
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) pr[u] = kk[u] >= 0 ? ld_price<COH>(s.price, kk[u]) : 0.0f;
+        for (int u = 0; u < U; ++u) pr[u] = kk[u] >= 0 ? s.price[kk[u]] : 0.0f;
         if (kprev) {  // fused rounds: the price after the previous round = max(price, its winning bid)
             unsigned long long kp[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) kp[u] = kk[u] >= 0 ? ld_key<COH>(kprev, kk[u]) : 0ull;
+            for (int u = 0; u < U; ++u) kp[u] = kk[u] >= 0 ? kprev[kk[u]] : 0ull;
 #pragma unroll
             for (int u = 0; u < U; ++u) pr[u] = fmaxf(pr[u], __uint_as_float(static_cast<uint32_t>(kp[u] >> 32)));
         }
@@ -448,93 +430,6 @@ __global__ __launch_bounds__(kBlock) void k_auc_fused(AucState s, AucFused f, in
     }
 }
 
-// Fused rounds on ONE XCD (xcd.h): once a round has <= xcd_max bidders, a batch of rounds runs as ONE
-// launch of k_auc_xcd -- the same round as k_auc_fused (resolve entry i's bid of round q-1, bid for
-// the agent it yields), list entry i always on the same wave (P x 4 waves, entries dealt round
-// robin), rounds separated by the XCD's flag barrier instead of a kernel boundary.  The candidate
-// lists of the few bidders, the prices and the task keys stay in that XCD's L2 from round to round.
-// What other workgroups wrote in the launch -- prices, owners, the previous round's keys (atomics)
-// -- is read with sc1 loads; entry arrays are only ever touched by their own wave.  The first round
-// without a bidder is the last one run; the host reads the per-round bidder counts (ring shard 0,
-// written by rank 0) when the launch ends.
-__global__ __launch_bounds__(kBlock) void k_auc_xcd(AucState s, AucFused f, int64_t q0, int64_t q1, int first,
-                                                   xcd::Ctl *c, int total, unsigned long long *herr) {
-    int rank, P;
-    if (!xcd::census(c, total, &rank, &P)) {
-        if (rank >= 0 && threadIdx.x == 0 && xcd::ld_sc1(c->err)) *herr = xcd::ld_sc1(c->err);
-        return;
-    }
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int64_t m = *f.cnt;
-    const int64_t nw = int64_t(P) * (kBlock / kWave), gw = int64_t(rank) * (kBlock / kWave) + wid;
-    __shared__ unsigned long long s_nb[kBlock / kWave];
-    for (int64_t q = q0, i = 0; q <= q1; ++q, ++i) {
-        const int mode = (q == q0 && first) ? int(AF_FIRST) : int(AF_NORMAL);
-        unsigned long long *kcur = auc_kbuf(s, q), *kprev = auc_kbuf(s, q - 1), *kold = auc_kbuf(s, q + 1);
-        unsigned long long nb = 0;
-        for (int64_t e = gw; e < m; e += nw) {
-            int32_t app = -1;
-            if (lane == 0) {
-                const int32_t a = f.L[e];
-                if (mode == AF_FIRST) {
-                    app = a;
-                } else {
-                    const int32_t c2 = f.tclr[e], k1 = f.tgt[e];
-                    if (c2 >= 0) kold[c2] = 0ull;  // round q-2's bid: nobody reads buf(q-2) this round
-                    if (a >= 0 && k1 >= 0) {
-                        const unsigned long long top = ld_key<true>(kprev, k1);
-                        const int32_t prev = __hip_atomic_load(s.owner + k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (top == f.mykey[e]) {
-                            s.owner[k1] = a;
-                            s.assigned[a] = k1;
-                            s.price[k1] = __uint_as_float(static_cast<uint32_t>(top >> 32));
-                            if (prev >= 0) s.assigned[prev] = -1;
-                            app = prev;
-                        } else {
-                            app = a;
-                        }
-                    }
-                    f.tclr[e] = k1;
-                }
-            }
-            app = __shfl(app, 0, 64);
-            if (app < 0) {
-                if (lane == 0) {
-                    f.L[e] = -1;
-                    f.tgt[e] = -1;
-                }
-                continue;
-            }
-            ++nb;
-            int32_t bk;
-            const unsigned long long kk = group_bid<64, kBidU, true>(s, app, &bk, mode == AF_FIRST ? nullptr : kprev);
-            if (lane == 0) {
-                f.L[e] = app;
-                f.tgt[e] = kk ? bk : -1;
-                f.mykey[e] = kk;
-                if (kk) atomicMax(&kcur[bk], kk);
-                else s.out[app] = 1;
-            }
-        }
-        if (lane == 0) s_nb[wid] = nb;
-        __syncthreads();
-        unsigned long long wg_nb = 0;
-        for (int w = 0; w < kBlock / kWave; ++w) wg_nb += s_nb[w];
-        if (threadIdx.x == 0) c->cnt[i & 1][rank][0] = unsigned(wg_nb);
-        unsigned long long sum = 0;
-        const int res = xcd::barrier(c, int(i), rank, P, wg_nb != 0, &sum);
-        if (rank == 0) {  // round q's bidders for the host; recycle the slot round q + kARing/2 uses
-            if (threadIdx.x == 0) *aslot(s.ring, q, 0) = sum;
-            for (int k = threadIdx.x; k < kAShards; k += kBlock) {
-                *aslot(s.ring, q + kARing / 2, k) = 0;
-                if (k > 0) *aslot(s.ring, q, k) = 0;
-            }
-        }
-        if (res != 0) break;  // no bidder in round q (or an error)
-    }
-    if (threadIdx.x == 0 && xcd::ld_sc1(c->err)) *herr = xcd::ld_sc1(c->err);
-}
-
 // A fresh, compact list of the unassigned, active agents (every resolution done, keys zeroed).
 __global__ __launch_bounds__(kBlock) void k_auc_rebuild(AucState s, AucFused f) {
     const int lane = threadIdx.x & 63;
@@ -659,14 +554,6 @@ __global__ __launch_bounds__(kTailBlock) void k_auc_tail(AucState s, int64_t r0,
 
 // Fused rounds (one kernel per round) once a round had <= this many bidders (SWARM_AUCTION_FUSED,
 // read per call; 0 = never, tests use it to exercise both paths).
-// Fused rounds on one XCD (k_auc_xcd) once a round had <= this many bidders (SWARM_AUCTION_XCD,
-// read per call; 0 = never).
-int64_t auc_xcd_threshold() {
-    int64_t x = 1024;
-    if (const char *e = getenv("SWARM_AUCTION_XCD")) x = atoll(e);
-    return x < 0 ? 0 : x;
-}
-
 int64_t auc_fused_threshold() {
     int64_t f = 8192;  // C4 sweep (tail 32): 2048..32768 all within 0.3 ms
     if (const char *e = getenv("SWARM_AUCTION_FUSED")) f = atoll(e);
@@ -1057,11 +944,6 @@ int swarm_auction(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *a
     }
     const int64_t tail_thr = auc_tail_threshold();
     const int64_t fused_max = auc_fused_threshold();
-    const int64_t xcd_max = auc_xcd_threshold();
-    xcd::Ctl *xctl = nullptr;  // k_auc_xcd's control lines, then its error word
-    if (xcd_max > 0) SW_ALLOC(xctl, ctx, S_XCD, sizeof(xcd::Ctl) + 64);
-    unsigned long long *xerr_d = xctl ? reinterpret_cast<unsigned long long *>(xctl + 1) : nullptr;
-    if (xerr_d) SW_HIP(hipMemsetAsync(xerr_d, 0, 8, s));
     int64_t r = 1, found = -1, last_nb = n, launched = 0, tail_rounds = 0, total_bids = 0;
     int batch = 8;
     bool fused_mode = false;  // fused rounds have run (keys in three buffers, entries in af)
@@ -1104,11 +986,7 @@ int swarm_auction(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *a
             if (r <= max_rounds) found = r;  // round r had no bidder
             break;
         }
-        // one-XCD batches: one launch of up to kARing / 2 rounds (it stops at the first round without
-        // a bidder), so the batch is as long as the counter ring allows
-        const bool xcd_batch = r > 1 && last_nb <= fused_max && last_nb <= xcd_max;
-        const int64_t blen = xcd_batch ? int64_t(kARing / 2) : int64_t(batch);
-        const int64_t rend = (max_rounds - r + 1 < blen) ? max_rounds : r + blen - 1;
+        const int64_t rend = (max_rounds - r + 1 < batch) ? max_rounds : r + batch - 1;
         if (r > 1 && last_nb <= fused_max) {  // fused rounds: one kernel per round
             if (fused_mode) {
                 if (int rc = fused_flush(r)) return rc;
@@ -1119,19 +997,11 @@ int swarm_auction(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *a
             SW_HIP(hipMemsetAsync(af.cnt, 0, sizeof(unsigned), s));
             hipLaunchKernelGGL(k_auc_rebuild, dim3(grid_for(n, kBlock, 4096)), dim3(kBlock), 0, s, st, af);
             SW_LAUNCHED();
-            if (xcd_batch) {
-                SW_HIP(hipMemsetAsync(xctl, 0, sizeof(xcd::Ctl), s));
-                const int total = 8 * xcd::kXcdPer;
-                hipLaunchKernelGGL(k_auc_xcd, dim3(total), dim3(kBlock), 0, s, st, af, r, rend, 1, xctl, total,
-                                   xerr_d);
+            const unsigned fgrid = grid_for(last_nb, kBlock / kWave, 8192);  // an upper bound: lists never grow
+            for (int64_t q = r; q <= rend; ++q) {
+                hipLaunchKernelGGL(k_auc_fused, dim3(fgrid), dim3(kBlock), 0, s, st, af, q,
+                                   int(q == r ? AF_FIRST : AF_NORMAL));
                 SW_LAUNCHED();
-            } else {
-                const unsigned fgrid = grid_for(last_nb, kBlock / kWave, 8192);  // an upper bound: lists never grow
-                for (int64_t q = r; q <= rend; ++q) {
-                    hipLaunchKernelGGL(k_auc_fused, dim3(fgrid), dim3(kBlock), 0, s, st, af, q,
-                                       int(q == r ? AF_FIRST : AF_NORMAL));
-                    SW_LAUNCHED();
-                }
             }
             pending = true;
             launched = rend;
@@ -1139,13 +1009,7 @@ int swarm_auction(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *a
                                reinterpret_cast<unsigned long long *>(dlog));
             SW_LAUNCHED();
             SW_HIP(hipMemcpyAsync(h, dlog, size_t(rend - r + 1) * 8, hipMemcpyDeviceToHost, s));
-            if (xcd_batch) SW_HIP(hipMemcpyAsync(h + kMaxBatch, xerr_d, 8, hipMemcpyDeviceToHost, s));
             SW_HIP(hipStreamSynchronize(s));
-            if (xcd_batch && h[kMaxBatch]) {  // a census or barrier timed out: the batch's rounds are undone
-                set_error("one-XCD auction rounds failed (%s)",
-                          h[kMaxBatch] == 2 ? "too many workgroups on one XCD" : "census or barrier timed out");
-                return SWARM_ERR_HIP;
-            }
             for (int64_t q = r; q <= rend; ++q) {
                 const int64_t nb = int64_t(h[q - r]);
                 if (nb == 0) {

@@ -24,7 +24,7 @@ void set_error(const char *fmt, ...);
 enum Slot {
     S_LEADER_B = 0,   // election: second leader buffer (dense)
     S_ACT,            // election: per-agent append stamp (frontier)
-    S_XCD,            // one-XCD persistent rounds: control lines (xcd.h) + the error word
+    S_LIST,           // election: change lists, both round parities (frontier)
     S_CHANGES,        // election: per-round change counters (device)
     S_ESTATS,         // election: per-round active/edge counters (device)
     S_KEYS_IN,        // binning: cell keys

@@ -245,21 +245,17 @@ def test_gpu_auction_large_ids(oracle_mod):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("fused,tail,xcd", [("1000000000", "0", "0"), ("1000000000", "0", "1000000000"),
-                                            ("1000000000", "128", "1024"), ("0", "128", "0"), ("4096", "0", "0"),
-                                            ("4096", "0", "1024"), ("4096", "32", "300")])
+@pytest.mark.parametrize("fused,tail", [("1000000000", "0"), ("1000000000", "128"), ("0", "128"), ("4096", "0")])
 @pytest.mark.parametrize("n,seed", [(2000, 14), (20000, 15)])
-def test_gpu_auction_fused_rounds_match_oracle(oracle_mod, n, seed, fused, tail, xcd):
+def test_gpu_auction_fused_rounds_match_oracle(oracle_mod, n, seed, fused, tail):
     """Fused rounds (resolve round q-1 and bid round q in one kernel, keys over three buffers,
     a fresh list per batch) against the oracle, alone, beside the list-driven rounds and before
-    the one-workgroup tail; launched per round or as one-XCD batches (k_auc_xcd, once a round has
-    <= xcd bidders)."""
+    the one-workgroup tail."""
     from swarm_amd.swarm import Swarm
     d = _inputs(n, seed)
     want = oracle_mod.auction(d["ids"], d["x"], d["y"], d["caps"], d["tx"], d["ty"], d["treq"])
     os.environ["SWARM_AUCTION_TAIL"] = tail
     os.environ["SWARM_AUCTION_FUSED"] = fused
-    os.environ["SWARM_AUCTION_XCD"] = xcd
     try:
         s = Swarm(d["ids"], d["x"], d["y"], d["caps"], device="cuda")
         r = s.auction(d["tx"], d["ty"], d["treq"])
@@ -270,7 +266,6 @@ def test_gpu_auction_fused_rounds_match_oracle(oracle_mod, n, seed, fused, tail,
     finally:
         del os.environ["SWARM_AUCTION_TAIL"]
         del os.environ["SWARM_AUCTION_FUSED"]
-        del os.environ["SWARM_AUCTION_XCD"]
     assert r.converged and r.rounds_exec == want["rounds"]
     np.testing.assert_array_equal(r.bidders, want["bidders"])
     np.testing.assert_array_equal(r.price.cpu().numpy(), want["price"])
