@@ -273,6 +273,19 @@ __global__ __launch_bounds__(kBlock) void k_decode(int64_t m, const uint8_t *__r
 }  // namespace
 }  // namespace swarm
 
+namespace swarm {
+// Grid cap of the codec kernels (10M messages: 16 384 -> encode 0.419-0.433 ms, decode 0.153-0.155;
+// 4 096 -> 0.440-0.451 / 0.158-0.162; 1 024 -> 0.484-0.493 / 0.173-0.178, same box,
+// profiles/r4_d/physics_codec_grid_ab.log; SWARM_CODEC_WGS overrides, A/B aid).
+unsigned codec_grid_cap() {
+    static const unsigned cap = [] {
+        const char *e = getenv("SWARM_CODEC_WGS");
+        return e && atoi(e) > 0 ? unsigned(atoi(e)) : 16384u;
+    }();
+    return cap;
+}
+}  // namespace swarm
+
 extern "C" {
 
 int swarm_codec_encode(swarm_ctx *ctx, int64_t m, const int64_t *type, const int64_t *sender, const int64_t *tick,
@@ -292,7 +305,8 @@ int swarm_codec_encode(swarm_ctx *ctx, int64_t m, const int64_t *type, const int
     const EncIn in{type, sender, tick, task, winner, a, b};
     int64_t *len;
     SW_ALLOC(len, ctx, S_TMP1, size_t(m + 1) * 8);
-    const unsigned grid = grid_for(m, kBlock, 4096);
+    const unsigned codec_wgs = swarm::codec_grid_cap();
+    const unsigned grid = grid_for(m, kBlock, codec_wgs);
     hipLaunchKernelGGL(k_enc_len, dim3(grid), dim3(kBlock), 0, s, m, in, int(wide != 0), len, status);
     SW_LAUNCHED();
     SW_HIP(hipMemsetAsync(len + m, 0, 8, s));
@@ -308,7 +322,7 @@ int swarm_codec_encode(swarm_ctx *ctx, int64_t m, const int64_t *type, const int
         set_error("output buffer holds %lld bytes, the packets need %lld", (long long)cap, (long long)*total_bytes);
         return SWARM_ERR_RANGE;
     }
-    hipLaunchKernelGGL(k_enc_write, dim3(grid_for(m, kEncPer, 4096)), dim3(kBlock), 0, s, m, in, int(wide != 0),
+    hipLaunchKernelGGL(k_enc_write, dim3(grid_for(m, kEncPer, codec_wgs)), dim3(kBlock), 0, s, m, in, int(wide != 0),
                        offsets, status, out);
     SW_LAUNCHED();
     return SWARM_OK;
@@ -327,7 +341,7 @@ int swarm_codec_decode(swarm_ctx *ctx, int64_t m, const uint8_t *buf, int64_t bu
     if (m == 0) return SWARM_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const DecOut o{status, type, sender, tick, task, winner, a, b, has_pos};
-    hipLaunchKernelGGL(k_decode, dim3(grid_for(m, kEncPer, 4096)), dim3(kBlock), 0, s, m, buf, buf_len, offsets,
+    hipLaunchKernelGGL(k_decode, dim3(grid_for(m, kEncPer, codec_grid_cap())), dim3(kBlock), 0, s, m, buf, buf_len, offsets,
                        int(wide != 0), o);
     SW_LAUNCHED();
     return SWARM_OK;
