@@ -455,7 +455,6 @@ struct Frontier {
     int64_t c_lo, n_count;   // rows [c_lo, n_count) are owned: only their changes are counted
     StampMap sm, wsm;
     const int16_t *c16;      // Col16 columns of the same graph (swarm_graph_compact), or nullptr
-    const int16_t *ell;      // ELL rows of the same graph (swarm_graph_ell; with c16 only), or nullptr
 };
 
 // Max over the G lanes of an agent's group (G = 4: a quad) through DPP quad permutes -- register
@@ -565,88 +564,6 @@ __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, CT col
     }
 }
 
-// ELL rows: agent v's neighbours as kEllW 16-bit deltas from v & ~63 (the Col16 deltas) in one
-// 64-byte row, edge k in slot (k % 4) * 8 + k / 4, so that lane k % 4 of the agent's quad reads its
-// edges k % 4, k % 4 + 4, ... with one 16-byte load; unused slots hold kEllPad.  A row of more than
-// kEllW neighbours holds kEllLong in every slot and is walked through the CSR instead.  The sparse
-// gather then needs no row offsets: its chain is stamps -> row -> neighbour leaders, one dependent
-// load fewer than stamps -> row_ptr -> columns -> leaders.
-constexpr int kEllW = 32;
-constexpr int kEllPad = -32768, kEllLong = -32767;  // deltas the rows reserve (swarm_graph_ell)
-
-template <typename Off, int G, int K>
-__device__ __forceinline__ void gather_listed_ell(const Off *__restrict__ rp, Col16 cols,
-                                                  const int16_t *__restrict__ ell, const int32_t *__restrict__ P,
-                                                  int32_t *__restrict__ Q, uint8_t *__restrict__ aw,
-                                                  const StampMap &sm, uint8_t sw, const int *lst, int total,
-                                                  int first, int step, int64_t c_lo, int64_t n_count,
-                                                  long long &my_chg, int &my_act, int &my_edges) {
-    static_assert(G == 4 && K == 8 && G * K == kEllW, "a lane reads 8 slots (16 bytes) of its agent's row");
-    const int lane = threadIdx.x & 63, sub = lane & (G - 1);
-    if (first >= total) return;
-    // the next pass's agent and own leader are loaded during the current pass (its row is not: the
-    // row is the pass's first load, as the columns are in gather_listed)
-    int32_t nv = lst[first + lane / G < total ? first + lane / G : total - 1];
-    int nown = ld4(P, nv);
-    for (int base = first; base < total; base += step) {
-        const int i = base + lane / G;
-        const bool valid = i < total;
-        const int32_t v = nv;
-        const int own = nown;
-        // v < 2^26 (host): a 32-bit byte offset
-        const uint4 row = *reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(ell) +
-                                                           ((uint32_t(v) << 6) | (uint32_t(sub) << 4)));
-        {
-            const int i2 = base + step + lane / G;
-            nv = lst[i2 < total ? i2 : total - 1];
-            nown = ld4(P, nv);
-        }
-        const int32_t b16 = v & ~63;
-        const uint32_t w[4] = {row.x, row.y, row.z, row.w};
-        int c[K];
-        int cnt = 0;
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const int32_t d = (j & 1) ? int32_t(w[j >> 1]) >> 16 : int32_t(w[j >> 1] << 16) >> 16;
-            const bool ok = d > kEllLong;  // not a pad, not a long row's marker
-            c[j] = ok ? b16 + d : v;       // a pad gathers the agent's own leader: no effect
-            cnt += ok ? 1 : 0;
-        }
-        const bool lng = int32_t(row.x << 16) >> 16 == kEllLong;
-        int m = own;
-        {
-            int val[K];
-#pragma unroll
-            for (int j = 0; j < K; ++j) val[j] = ld4(P, c[j]);
-#pragma unroll
-            for (int j = 0; j < K; ++j) m = max(m, val[j]);
-        }
-        if (lng) {  // rare (> kEllW neighbours): the CSR row, interleaved over the quad
-            const Off b = ld4(rp, v), e = ld4(rp, v + 1);
-            cnt = sub == 0 ? int(e - b) : 0;
-            for (Off k = b + sub; k < e; k += G) m = max(m, ld4(P, cols.at32(k, b16)));
-        }
-        m = group_max<G>(m);
-        const bool up = valid && m > own;
-        if (valid && sub == 0) st4(Q, v, m);
-        if (up) {
-            if (sub == 0) aw[stamp_slot(sm, v)] = sw;
-            if (!lng) {
-#pragma unroll
-                for (int j = 0; j < K; ++j)
-                    if (c[j] != v) aw[stamp_slot(sm, c[j])] = sw;
-            } else {
-                mark_row<Off>(aw, sm, cols, b16, ld4(rp, v) + sub, ld4(rp, v + 1), Off(G), sw);
-            }
-        }
-        my_chg += __popcll(__ballot(up && sub == 0 && v >= c_lo && v < n_count));
-        if (valid) {
-            my_act += sub == 0 ? 1 : 0;
-            my_edges += cnt;
-        }
-    }
-}
-
 // S stamps per thread as one word: 8 (uint2, 2 048-agent chunks) or 2 (uint16, 512-agent chunks:
 // small swarms, whose 2 048-agent chunks would leave most CUs idle).
 template <int S> struct StampWord;
@@ -697,8 +614,7 @@ __device__ __forceinline__ void flush_counts(unsigned long long *ring, int t, lo
 
 // One workgroup per chunk of kBlock * S agents: S stamps per thread, the chunk's marked agents
 // compacted in LDS and gathered by the whole workgroup.
-template <typename Off, int S = kScan, bool DIR = false, typename CT = Col32, int G = kG, int K = kKs,
-          bool ELL = false>
+template <typename Off, int S = kScan, bool DIR = false, typename CT = Col32, int G = kG, int K = kKs>
 __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_block(
     const Off *__restrict__ rp, CT cols, Frontier f, int t, int guard,
     const Off *__restrict__ hrp = nullptr, const int32_t *__restrict__ hcol = nullptr) {
@@ -787,13 +703,8 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
             listed = listed + total < kListCap ? listed + total : kListCap;
             __syncthreads();  // list entries visible
             if (listed < kListCap) break;  // everything fitted
-            if constexpr (ELL)
-                gather_listed_ell<Off, G, K>(rp, cols, f.ell, P, Q, aw, f.wsm, sw, s_list, listed, wid * (64 / G),
-                                             kBlock / G, f.c_lo, f.n_count, my_chg, my_act, my_edges);
-            else
-                gather_listed<Off, G, K, DIR>(rp, cols, hrp, hcol, P, Q, aw, f.wsm, sw, s_list, listed,
-                                              wid * (64 / G), kBlock / G, f.c_lo, f.n_count, my_chg, my_act,
-                                              my_edges);
+            gather_listed<Off, G, K, DIR>(rp, cols, hrp, hcol, P, Q, aw, f.wsm, sw, s_list, listed, wid * (64 / G),
+                                          kBlock / G, f.c_lo, f.n_count, my_chg, my_act, my_edges);
             listed = 0;
             __syncthreads();  // the list is reused
         }
@@ -801,14 +712,9 @@ __global__ __launch_bounds__(kBlock, sizeof(Off) == 4 ? 8 : 6) void k_sparse_blo
 #ifdef SWARM_PHASES
     ph_listed = wall_clock64();
 #endif
-    if (listed > 0) {
-        if constexpr (ELL)
-            gather_listed_ell<Off, G, K>(rp, cols, f.ell, P, Q, aw, f.wsm, sw, s_list, listed, wid * (64 / G),
-                                         kBlock / G, f.c_lo, f.n_count, my_chg, my_act, my_edges);
-        else
-            gather_listed<Off, G, K, DIR>(rp, cols, hrp, hcol, P, Q, aw, f.wsm, sw, s_list, listed, wid * (64 / G),
-                                          kBlock / G, f.c_lo, f.n_count, my_chg, my_act, my_edges);
-    }
+    if (listed > 0)
+        gather_listed<Off, G, K, DIR>(rp, cols, hrp, hcol, P, Q, aw, f.wsm, sw, s_list, listed, wid * (64 / G),
+                                      kBlock / G, f.c_lo, f.n_count, my_chg, my_act, my_edges);
 #ifdef SWARM_PHASES
     ph_gathered = wall_clock64() + (my_chg & 0);
 #endif
@@ -882,28 +788,6 @@ __global__ __launch_bounds__(kBlock) void k_build_col16(const int32_t *__restric
     if (__ballot(out) && (threadIdx.x & 63) == 0) atomicOr(bad, 1);
 }
 
-// ELL rows of a Col16 graph (gather_listed_ell): one thread per (agent, slot); slot s holds edge
-// (s % 8) * 4 + s / 8.  *bad is set when a delta is one of the two reserved values.
-__global__ __launch_bounds__(kBlock) void k_build_ell(const int32_t *__restrict__ rp, const int16_t *__restrict__ c16,
-                                                      int64_t n, int16_t *__restrict__ ell, int *__restrict__ bad) {
-    int out = 0;
-    for (int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x; q < n * kEllW; q += int64_t(gridDim.x) * kBlock) {
-        const int64_t v = q / kEllW;
-        const int s = int(q % kEllW);
-        const int32_t b = rp[v], deg = rp[v + 1] - b;
-        const int k = (s & 7) * 4 + (s >> 3);
-        int32_t d = kEllPad;
-        if (deg > kEllW) {
-            d = kEllLong;
-        } else if (k < deg) {
-            d = c16[b + k];
-            out |= d <= kEllLong ? 1 : 0;
-        }
-        ell[q] = int16_t(d);
-    }
-    if (__ballot(out) && (threadIdx.x & 63) == 0) atomicOr(bad, 1);
-}
-
 __global__ __launch_bounds__(kBlock) void k_state(const int32_t *__restrict__ leader,
                                                  const int32_t *__restrict__ ids,
                                                  uint8_t *__restrict__ state, int64_t n) {
@@ -946,13 +830,11 @@ struct Tuning {
     int dense_flat = 1;       // dense rounds gather leaders 64 consecutive edges per load (FLAT)
     int dense_vec = 1;        // FLAT with 16-bit columns: 8 columns per lane per 16-byte load
     int use_c16 = 1;          // swarm_elect_compact reads the 16-bit columns (0: its int32 ones; A/B aid)
-    int use_ell = 1;          // swarm_elect_ell reads the ELL rows (0: its CSR; A/B aid)
     int il_min_changes = -1;   // interleaved stamp layout while the last read round changed >= this
                                // (-1: 8e-4 x agents, measured best at 100k, 1M and 10M agents)
     Tuning() {
         il_min_changes = env_int("SWARM_IL_MIN_CHANGES", -1);
         use_c16 = env_int("SWARM_C16", 1);
-        use_ell = env_int("SWARM_ELL", 1);
         dense_flat = env_int("SWARM_DENSE_FLAT", 1);
         dense_vec = env_int("SWARM_DENSE_VEC", 1);
         stamp_bshift = env_int("SWARM_STAMP_BSHIFT", 5);
@@ -1111,20 +993,12 @@ int launch_frontier_round(const Off *rp, const int32_t *col, const Frontier &f, 
     // recurs (take_stamps)
     if (t > 2 && ((t - 1) & 255) < 2) SW_HIP(hipMemsetAsync(f.act[(t + 1) & 1], 0, act_bytes(f.n_all), s));
     const bool small = f.sm.cshift == 9;  // small swarm: 512-agent chunks, 4x the workgroups
-    // SWARM_ELL=2 (A/B aid): the ELL rows only in the tail (agent-order stamps)
-    const bool ell = f.ell && (tuning().use_ell != 2 || f.sm.bshift == f.sm.cshift);
     const dim3 grid(grid_for(f.sm.M, 1, unsigned(tuning().sparse_blocks)));
     const Col32 c32{col};
     if (hrp && small)
         hipLaunchKernelGGL((k_sparse_block<Off, 2, true>), grid, dim3(kBlock), 0, s, rp, c32, f, t, guard, hrp, hcol);
     else if (hrp)
         hipLaunchKernelGGL((k_sparse_block<Off, kScan, true>), grid, dim3(kBlock), 0, s, rp, c32, f, t, guard, hrp, hcol);
-    else if (sizeof(Off) == 4 && ell && f.c16 && small)
-        hipLaunchKernelGGL((k_sparse_block<Off, 2, false, Col16, kG, kKs, sizeof(Off) == 4>), grid, dim3(kBlock), 0, s,
-                           rp, Col16{f.c16}, f, t, guard, nullptr, nullptr);
-    else if (sizeof(Off) == 4 && ell && f.c16)
-        hipLaunchKernelGGL((k_sparse_block<Off, kScan, false, Col16, kG, kKs, sizeof(Off) == 4>), grid, dim3(kBlock), 0,
-                           s, rp, Col16{f.c16}, f, t, guard, nullptr, nullptr);
     else if (f.c16 && small)
         hipLaunchKernelGGL((k_sparse_block<Off, 2, false, Col16>), grid, dim3(kBlock), 0, s, rp, Col16{f.c16}, f, t,
                            guard, nullptr, nullptr);
@@ -1153,7 +1027,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
                int32_t *leader, uint8_t *state, int32_t max_rounds, int32_t mode,
                int32_t *rounds_exec, int64_t *changes_host, swarm_elect_stats *st,
                void *stream, const Off *hrp = nullptr, const int32_t *hcol = nullptr,
-               const int16_t *c16 = nullptr, const int16_t *ell = nullptr) {
+               const int16_t *c16 = nullptr) {
     SW_ARG(ctx != nullptr, "ctx is NULL");
     SW_ARG(n >= 0, "n < 0");
     SW_ARG(n < (int64_t(1) << 31), "n must be < 2^31");
@@ -1196,7 +1070,6 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         if (rc0) return rc0;
         ring = f.ring;
         f.c16 = c16;
-        f.ell = c16 && n < (int64_t(1) << 26) ? ell : nullptr;
     } else {
         SW_ALLOC(ring, ctx, S_CHANGES, ring_bytes());
         SW_HIP(hipMemsetAsync(ring, 0, ring_bytes(), s));
@@ -1473,51 +1346,6 @@ int swarm_elect_compact(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const
     return swarm::elect_impl<int32_t>(ctx, n, row_ptr, col, ids, leader, state, max_rounds, mode, rounds_exec,
                                       changes_per_round, stats, stream, nullptr, nullptr,
                                       swarm::tuning().use_c16 ? col16 : nullptr);
-}
-
-int swarm_graph_ell(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int16_t *col16, int16_t *ell,
-                    void *stream) {
-    using namespace swarm;
-    SW_ARG(ctx != nullptr, "ctx is NULL");
-    if (!ctx_on_current_device(ctx)) return SWARM_ERR_ARG;
-    SW_ARG(n >= 0, "n < 0");
-    if (n == 0) return SWARM_OK;
-    if (n >= (int64_t(1) << 26)) {
-        set_error("ELL rows address with 32-bit offsets: fewer than 2^26 agents");
-        return SWARM_ERR_RANGE;
-    }
-    SW_ARG(row_ptr && ell, "NULL array");
-    SW_ARG((reinterpret_cast<uintptr_t>(ell) & 15) == 0, "ell must be 16-byte aligned");
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    int32_t e_total = 0;
-    SW_HIP(hipMemcpyAsync(&e_total, row_ptr + n, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    SW_HIP(hipStreamSynchronize(s));
-    SW_ARG(e_total >= 0, "row_ptr[n] < 0");
-    SW_ARG(e_total == 0 || col16 != nullptr, "col16 is NULL but the graph has edges");
-    int *bad;
-    SW_ALLOC(bad, ctx, S_TMP1, sizeof(int));
-    SW_HIP(hipMemsetAsync(bad, 0, sizeof(int), s));
-    hipLaunchKernelGGL(k_build_ell, dim3(grid_for(n * kEllW, kBlock, 16384)), dim3(kBlock), 0, s, row_ptr, col16, n,
-                       ell, bad);
-    SW_LAUNCHED();
-    int hbad = 0;
-    SW_HIP(hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, s));
-    SW_HIP(hipStreamSynchronize(s));
-    if (hbad) {
-        set_error("a 16-bit column delta is one of the two values ELL rows reserve (-32768, -32767)");
-        return SWARM_ERR_RANGE;
-    }
-    return SWARM_OK;
-}
-
-int swarm_elect_ell(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col, const int16_t *col16,
-                    const int16_t *ell, const int32_t *ids, int32_t *leader, uint8_t *state, int32_t max_rounds,
-                    int32_t mode, int32_t *rounds_exec, int64_t *changes_per_round, swarm_elect_stats *stats,
-                    void *stream) {
-    const bool c16 = swarm::tuning().use_c16 && col16;
-    return swarm::elect_impl<int32_t>(ctx, n, row_ptr, col, ids, leader, state, max_rounds, mode, rounds_exec,
-                                      changes_per_round, stats, stream, nullptr, nullptr, c16 ? col16 : nullptr,
-                                      c16 && swarm::tuning().use_ell ? ell : nullptr);
 }
 
 int swarm_elect_directed(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col,

@@ -36,7 +36,7 @@ EXPORTS = ("swarm_last_error", "swarm_version", "swarm_ctx_create", "swarm_ctx_d
            "swarm_allocate_indexed", "swarm_graph_compact", "swarm_elect_compact",
            "swarm_elect_compact_i64", "swarm_frontier_begin_range", "swarm_frontier_set_compact",
            "swarm_comm_unique_id_kind", "swarm_comm_create_kind", "swarm_comm_kind", "swarm_allocate_indexed_ex",
-           "swarm_protocol_run_ex", "swarm_graph_ell", "swarm_elect_ell")
+           "swarm_protocol_run_ex")
 
 
 class SwarmError(RuntimeError):
@@ -113,8 +113,6 @@ def load(path: str = LIB_PATH):
         L.swarm_elect_round.argtypes = [P, i64, P, P, P, P, P, P]
         L.swarm_graph_compact.argtypes = [P, i64, P, P, P, P]
         L.swarm_elect_compact.argtypes = [P, i64, P, P, P, P, P, P, i32, i32, ctypes.POINTER(i32), P, P, P]
-        L.swarm_graph_ell.argtypes = [P, i64, P, P, P, P]
-        L.swarm_elect_ell.argtypes = [P, i64, P, P, P, P, P, P, P, i32, i32, ctypes.POINTER(i32), P, P, P]
         L.swarm_elect_compact_i64.argtypes = [P, i64, P, P, P, P, P, P, i32, i32, ctypes.POINTER(i32), P, P, P]
         L.swarm_allocate.argtypes = [P, i64, P, P, P, i64, P, P, d, d, d, i32, P, P, P, P, i64,
                                      P, P, P, P]

@@ -219,28 +219,6 @@ class Swarm:
             self._c16 = cached = (key, c16)
         return cached[1]
 
-    def graph_ell(self) -> torch.Tensor | None:
-        """ELL rows of the (symmetric) neighbour graph (swarm_graph_ell: 32 16-bit deltas per agent,
-        64 B each), built from graph_compact's columns on first use and rebuilt with them; None when
-        there are no 16-bit columns, the swarm has 2^26 agents or more, or a delta is one the rows
-        reserve (the sparse rounds then read row_ptr + columns)."""
-        c16 = self.graph_compact()
-        if c16 is None or self.n >= (1 << 26):
-            return None
-        key = self._c16[0]
-        cached = getattr(self, "_ell", None)
-        if cached is None or cached[0] != key:
-            ell = torch.empty(self.n * 32, dtype=torch.int16, device=self.device)
-            with torch.cuda.device(self.device):
-                rc = _lib.lib().swarm_graph_ell(_lib.ctx(), self.n, _lib.ptr(self.row_ptr, torch.int32),
-                                                _lib.ptr(c16), _lib.ptr(ell), _lib.stream())
-            if rc == _lib.ERR_RANGE:
-                ell = None
-            else:
-                _lib.check(rc)
-            self._ell = cached = (key, ell)
-        return cached[1]
-
     def elect(self, mode: str = "frontier", max_rounds: int = 1 << 16, timed: bool = False,
               compact: bool = True, wide: bool | None = None) -> ElectResult:
         """Contract E2 to convergence on the GPU (swarm_elect_compact with the graph's 16-bit
@@ -263,14 +241,7 @@ class Swarm:
         hear = getattr(self, "_hear", None)
         with torch.cuda.device(self.device):
             c16 = self.graph_compact() if (compact and hear is None) else None
-            ell = self.graph_ell() if (c16 is not None and mode == "frontier") else None
-            if ell is not None:  # symmetric graph, 16-bit columns, ELL rows for the sparse rounds
-                rc = _lib.check(_lib.lib().swarm_elect_ell(
-                    _lib.ctx(), n, _lib.ptr(self.row_ptr, torch.int32), _lib.ptr(self.col, torch.int32),
-                    _lib.ptr(c16), _lib.ptr(ell), _lib.ptr(self.ids, torch.int32), _lib.ptr(self.leader, torch.int32),
-                    _lib.ptr(self.state, torch.uint8), cap, m, ctypes.byref(rounds),
-                    changes.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st), _lib.stream()))
-            elif c16 is not None:  # symmetric graph, 16-bit columns
+            if c16 is not None:  # symmetric graph, 16-bit columns
                 rc = _lib.check(_lib.lib().swarm_elect_compact(
                     _lib.ctx(), n, _lib.ptr(self.row_ptr, torch.int32), _lib.ptr(self.col, torch.int32),
                     _lib.ptr(c16), _lib.ptr(self.ids, torch.int32), _lib.ptr(self.leader, torch.int32),

@@ -144,23 +144,6 @@ int swarm_elect_compact(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const
                         const int32_t *ids, int32_t *leader, uint8_t *state, int32_t max_rounds, int32_t mode,
                         int32_t *rounds_exec, int64_t *changes_per_round, swarm_elect_stats *stats, void *stream);
 
-/* ELL rows of the graph for the sparse election rounds (round 4): 32 slots of 16-bit deltas per agent
- * (the col16 deltas, interleaved over the 4 lanes that gather an agent; a row of more than 32
- * neighbours is marked and walked through the CSR), so a sparse round's gather needs no row_ptr
- * load.  ell: device, n * 32 int16 (64 B per agent), 16-byte aligned, caller-allocated; n < 2^26.
- * SWARM_ERR_RANGE: n too large, or a delta equals one of the two reserved values (-32768, -32767).
- * Rebuild it whenever the graph changes. */
-int swarm_graph_ell(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int16_t *col16, int16_t *ell,
-                    void *stream);
-
-/* swarm_elect_compact whose sparse rounds gather through the ELL rows (swarm_graph_ell of the same
- * graph; NULL: same as swarm_elect_compact).  Same election (agent.py:263-275), same results and
- * stats. */
-int swarm_elect_ell(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col, const int16_t *col16,
-                    const int16_t *ell, const int32_t *ids, int32_t *leader, uint8_t *state, int32_t max_rounds,
-                    int32_t mode, int32_t *rounds_exec, int64_t *changes_per_round, swarm_elect_stats *stats,
-                    void *stream);
-
 /* Same with int64 row offsets: graphs with >= 2^30 edges or agents (the int32-CSR entry points
  * address with 32-bit byte offsets and reject them with SWARM_ERR_ARG). */
 int swarm_elect_i64(swarm_ctx *ctx, int64_t n, const int64_t *row_ptr, const int32_t *col,
