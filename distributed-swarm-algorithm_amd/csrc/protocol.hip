@@ -42,7 +42,14 @@ namespace swarm {
 namespace {
 
 constexpr uint8_t kAcclaim = 1, kHeartbeat = 2;
-constexpr int kRecv = 8;  // CSR entries loaded per receive chunk
+constexpr int kRecv = 8;  // CSR entries loaded per receive chunk (pull mode, hearer walks)
+// k_tick's row walks (75 VGPRs, 6 waves per SIMD; 4 entries per chunk: 63 VGPRs, 8 waves, but
+// 0.135 against 0.128 ms per tick -- the walks' chunks one after the other cost more than the
+// occupancy gains; SWARM_RECV_TICK: A/B builds)
+#ifndef SWARM_RECV_TICK
+#define SWARM_RECV_TICK 8
+#endif
+constexpr int kRecvTick = SWARM_RECV_TICK;
 constexpr uint8_t ST_F = SWARM_FOLLOWER, ST_W = SWARM_ELECTION_WAIT, ST_L = SWARM_LEADER;
 
 __device__ __forceinline__ double jitter_u(uint64_t seed, int32_t id, int64_t t) {
@@ -99,26 +106,27 @@ __device__ __forceinline__ void hear(Heard &h, uint8_t o, int32_t s, int32_t j, 
     }
 }
 
+template <int R>
 __device__ __forceinline__ void receive_row(int32_t b, int32_t e, const int32_t *__restrict__ col,
                                             const uint8_t *__restrict__ ob_in, const int32_t *__restrict__ ids,
                                             int32_t me, bool hb_tick, Heard &h) {
-    for (int32_t k0 = b; k0 < e; k0 += kRecv) {
-        int32_t jj[kRecv];
-        uint8_t oo[kRecv];
+    for (int32_t k0 = b; k0 < e; k0 += R) {
+        int32_t jj[R];
+        uint8_t oo[R];
 #pragma unroll
-        for (int u = 0; u < kRecv; ++u) jj[u] = k0 + u < e ? col[k0 + u] : -1;
+        for (int u = 0; u < R; ++u) jj[u] = k0 + u < e ? col[k0 + u] : -1;
         uint8_t any = 0;
 #pragma unroll
-        for (int u = 0; u < kRecv; ++u) {
+        for (int u = 0; u < R; ++u) {
             oo[u] = jj[u] >= 0 ? ob_in[jj[u]] : uint8_t(0);
             any |= oo[u];
         }
         if (!any) continue;
-        int32_t ss[kRecv];  // the senders' IDs, all loads in flight
+        int32_t ss[R];  // the senders' IDs, all loads in flight
 #pragma unroll
-        for (int u = 0; u < kRecv; ++u) ss[u] = oo[u] ? ids[jj[u]] : 0;
+        for (int u = 0; u < R; ++u) ss[u] = oo[u] ? ids[jj[u]] : 0;
 #pragma unroll
-        for (int u = 0; u < kRecv; ++u) {
+        for (int u = 0; u < R; ++u) {
             const uint8_t o = oo[u] & (kAcclaim | kHeartbeat);
             if (o) hear(h, o, ss[u], jj[u], me, hb_tick);
         }
@@ -227,7 +235,7 @@ __global__ __launch_bounds__(kBlock) void k_tick_pull(int64_t n, int64_t t, cons
         }
         const uint8_t st0 = f.state[i];
         Heard h{st0, 0, false, false, 0, -1};
-        receive_row(rp[i], rp[i + 1], col, ob_in, ids, ids[i], ((t + tick_off[i]) % 10) == 0, h);
+        receive_row<kRecv>(rp[i], rp[i + 1], col, ob_in, ids, ids[i], ((t + tick_off[i]) % 10) == 0, h);
         apply_heard(i, h, now, pos, f);
         const uint8_t ob = h.ob | timers(i, h.st, h.live, h.lead, h.lead_set, t, now, timeout, jitter, seed, ids,
                                          tick_off[i], f.last_hb[i], f);
@@ -381,7 +389,7 @@ __device__ __forceinline__ int block_excl_scan(int c, int &total, int *s_wave) {
 
 struct TickCounts {
     unsigned lead = 0, wait = 0, acc = 0, hb = 0;
-    unsigned long long single = 0, multi = 0, edges = 0;
+    unsigned single = 0, multi = 0, edges = 0;  // one thread's, one tick: < 2^32 (32-bit: VGPRs)
 };
 
 // Timers and writes of alive agent i after what it heard (h), its sends listed.
@@ -477,9 +485,9 @@ __global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int
                 const bool hb_tick = ((t + toff) % 10) == 0;
                 if (multi) {  // several senders (or a pull): the row, in CSR order
                     const int32_t b = rp[i], e = rp[i + 1];
-                    receive_row(b, e, col, ob_in, ids, me, hb_tick, h);
+                    receive_row<kRecvTick>(b, e, col, ob_in, ids, me, hb_tick, h);
                     ++c.multi;
-                    c.edges += uint64_t(e - b);
+                    c.edges += unsigned(e - b);
                     apply_heard(i, h, now, pos, f);
                 } else {  // exactly one sender: no row walk
                     const uint8_t o = ob_in[j] & (kAcclaim | kHeartbeat);
