@@ -546,7 +546,7 @@ def rows_bench(sw, dev, args):
                                  "agent_ticks_per_s": n * ticks / (ms * 1e-3),
                                  "leaders_final": int(c[-1, 0]), "heartbeats": int(c[:, 3].sum()),
                                  "traffic": [int(v) for v in sw.fsm_traffic],
-                                 "roofline": _roof(fb / ticks, ms / ticks, "k_tick + k_mail", ["k_tick", "k_mail"],
+                                 "roofline": _roof(fb / ticks, ms / ticks, "k_tick", ["k_tick"],
                                                    note="every tick's algorithmic bytes (fsm_bytes: the sweep's 15 B "
                                                         "per agent, the mail bitmap read and cleared, each receiver's "
                                                         "fields, 5 B per row edge walked, 8 B per sender + 6 B per "

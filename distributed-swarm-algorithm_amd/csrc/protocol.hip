@@ -14,22 +14,23 @@
 //             ELECTION_WAIT past its delay -> LEADER + ELECTION_ACCLAIM + COORDINATOR;
 //   sends     into its outbox byte (tick-parity double buffer): bit 0 ACCLAIM+COORDINATOR,
 //             bit 1 HEARTBEAT -- exact, see swarm_oracle.c orc_protocol.
-// Push mode (the hearers CSR given), two launches per tick:
+// Push mode (the hearers CSR given), one launch per tick:
 //   k_tick   receive + timers, its workgroups in two roles: the receive role lists each 4 096-agent
 //            chunk's receivers (mail bit set: 1 bit per agent, set by last tick's senders) in LDS
 //            and serves them one per thread -- its one sender directly, or its CSR row in order
 //            (col / outbox loads in chunks of kRecv, all in flight) when it has several -- then
 //            their timers; the sweep role streams every other agent's timers (kSweepV agents per
 //            thread); sends are listed in the workgroup's own segment (no global atomics),
-//            per-tick counters;
-//   k_mail   clears the tick's mail words, then mails the hearers of every listed sender (64-bit
-//            atomicOr into the next tick's words, combined per word, all hearer loads in flight).
-// (Rounds 2-4 ran the receive as its own launch over a compacted receiver list, k_compact +
-// k_receive + k_sweep + k_mail: two more boundaries and the list round trip per tick.)
+//            per-tick counters; then each workgroup mails the hearers of the senders it listed
+//            (64-bit atomicOr into the next tick's words, combined per word, all hearer loads in
+//            flight).  The words rotate over three buffers: tick t reads buf(t), mails into
+//            buf(t+1) and clears buf(t+2).
+// (Rounds 2-3 ran k_compact + k_receive + k_sweep + k_mail, round 4 first k_tick + k_mail: the
+// boundaries and the list round trips per tick.)
 // A quiet agent costs ~15 B (alive, state, outbox byte, tick phase, its 8-byte timer) plus its mail
-// bit; only receivers pay for their rows.  Storm ticks: when a tick's senders exceed pull_frac x n
-// (a timeout wave: thousands of ACCLAIMs at once), k_mail skips the mail atomics and the next tick
-// pulls instead -- every alive agent walks its own row, as pull mode does.  Same results: an agent
+// bit; only receivers pay for their rows.  Storm ticks: when a workgroup's senders exceed pull_frac x the
+// agents of its share (a timeout wave: thousands of ACCLAIMs at once), it skips the mail atomics
+// and the next tick pulls instead -- every alive agent walks its own row, as pull mode does.  Same results: an agent
 // without a sender in its row hears nothing either way.  Pull mode (no hearers CSR): one fused
 // launch in which every agent walks its row -- the cross-check.  Both are latency-bound gathers, no
 // arithmetic worth the name.
@@ -345,15 +346,14 @@ __global__ __launch_bounds__(kBlock) void k_mail_from_outbox(int64_t n, const ui
 //            and served one per thread -- its one sender directly (from[]), or its CSR row in
 //            order when it has several (multi bit) or the tick is pulled -- then its timers run on
 //            the result.
-// Senders of both roles are listed in the workgroup's own segment for k_mail.  The mail words of
-// the tick are cleared by k_mail (both roles read them here).
+// Senders of both roles are listed in the workgroup's own segment, then mailed by it.
 constexpr int kSweepV = 4;
 constexpr int kRecvChunk = 4096;  // agents per receive-role pass (64 mail words, 16 agents per thread;
                                   // 2 048: 0.144 vs 0.138 ms per tick)
 
-// Sender segments of k_tick's workgroups: the g_recv receive-role ones first (rcap entries each:
-// their chunks' agents), then the sweep-role ones (scap each: their agents, or their chunks' on a
-// pulled tick, when every workgroup receives).
+// Sender segments of k_tick's workgroups (each mails its own): the g_recv receive-role ones first
+// (rcap entries each: their chunks' agents), then the sweep-role ones (scap each: their agents, or
+// their chunks' on a pulled tick, when every workgroup receives).
 struct Segs {
     int32_t *base;
     int64_t rcap, scap;
@@ -392,6 +392,22 @@ struct TickCounts {
     unsigned single = 0, multi = 0, edges = 0;  // one thread's, one tick: < 2^32 (32-bit: VGPRs)
 };
 
+// k_tick's own mail: once a workgroup's agents are done it mails the hearers of the senders it
+// listed, into tick t+1's words; the words are rotated over three buffers (tick t reads buf(t),
+// mails into buf(t+1) and clears buf(t+2), read in tick t-1 and next mailed in tick t+1) and the
+// single-sender slots over two, so no workgroup of tick t touches what another one still reads.
+// Storms are decided per workgroup: more senders than frac x the agents of its share -> it mails
+// nothing and flags tick t+1 as pulled.  (Round 4's separate k_mail launch after k_tick, deciding
+// on the tick's total senders: 0.128 against 0.123 ms per tick, same box.)
+struct NextMail {
+    Mail next;                       // tick t+1's words and single-sender slots
+    unsigned long long *clear;       // buf(t+2), n_clear words
+    int64_t n_clear;
+    unsigned *pull_next, *pull_clear;
+    double frac;                     // < 0: never a storm
+    const int32_t *trp, *tcol;       // who hears each agent
+};
+
 // Timers and writes of alive agent i after what it heard (h), its sends listed.
 __device__ __forceinline__ void finish_agent(int64_t i, Heard &h, uint8_t st0, uint8_t prev, int64_t t, double now,
                                              double timeout, double jitter, uint64_t seed,
@@ -415,9 +431,9 @@ __global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int
                                                 const int32_t *__restrict__ col, const int32_t *__restrict__ tick_off,
                                                 Fsm f, Mail mail, const uint8_t *__restrict__ ob_in,
                                                 uint8_t *__restrict__ ob_out, const unsigned *__restrict__ pull,
-                                                Segs segs, int32_t *__restrict__ seg_count, double dt, double timeout,
+                                                Segs segs, double dt, double timeout,
                                                 double jitter, uint64_t seed, unsigned long long *__restrict__ counts,
-                                                int vec, unsigned long long *__restrict__ tr) {
+                                                int vec, unsigned long long *__restrict__ tr, NextMail im) {
     __shared__ unsigned s_cnt[4];
     __shared__ int s_ns;
     __shared__ int s_wave[kBlock / kWave];
@@ -435,6 +451,7 @@ __global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int
     const double now = double(t) * dt;
     const bool pulled = *pull != 0;
     TickCounts c;
+    int64_t span = 0;  // agents of this workgroup's share (the storm rule)
     if (pulled || recv_role) {
         // ---- receive role
         // a pulled tick: every workgroup, 1 024-agent units (every agent walks its row: 4x the units,
@@ -444,6 +461,7 @@ __global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int
         const int64_t unit = int64_t(kPerT) * kBlock;
         const int64_t nchunks = (n + unit - 1) / unit;
         for (int64_t ck = pulled ? int64_t(blockIdx.x) : int64_t(rank); ck < nchunks; ck += nrole) {
+            span += unit;
             // thread: kPerT agents, a slice of mail word (ck * unit + threadIdx.x * kPerT) / 64
             const int64_t a0 = ck * unit + int64_t(threadIdx.x) * kPerT;
             unsigned b16 = 0, m16 = 0;
@@ -509,6 +527,10 @@ __global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int
         // ---- sweep role
         const int64_t ngroups = (n + kSweepV - 1) / kSweepV;
         const int64_t stride = int64_t(int(gridDim.x) - g_recv) * kBlock;
+        {  // the workgroup's groups (uniform)
+            const int64_t g0 = int64_t(rank) * kBlock;
+            span = g0 < ngroups ? ((ngroups - g0 + stride - 1) / stride) * kBlock * kSweepV : 0;
+        }
         for (int64_t gi = int64_t(rank) * kBlock + threadIdx.x; gi < ngroups; gi += stride) {
             const int64_t i0 = gi * kSweepV;
             const bool full = vec && i0 + kSweepV <= n;
@@ -564,48 +586,24 @@ __global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int
         if (pulled && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&tr[7], 1ull);  // pulled ticks
     }
     add_counts(c.lead, c.wait, c.acc, c.hb, s_cnt, counts);  // (ends with a barrier: s_ns is final)
-    if (threadIdx.x == 0) seg_count[blockIdx.x] = s_ns;
-}
-
-// Mail for the hearers of every sender the sweep listed: workgroup b walks segment b.  A storm tick
-// (this tick's senders -- ACCLAIM + HEARTBEAT counts, an agent sending both counted twice -- above
-// thr) mails nothing and flags the next tick's receive as a pull; every workgroup decides the same.
-__global__ __launch_bounds__(kBlock) void k_mail(Segs segs,
-                                                const int32_t *__restrict__ seg_count,
-                                                const int32_t *__restrict__ trp, const int32_t *__restrict__ tcol,
-                                                Mail mail, const unsigned long long *__restrict__ cnt_t,
-                                                unsigned long long thr, unsigned *__restrict__ pull_next,
-                                                unsigned long long *__restrict__ tr,
-                                                unsigned long long *__restrict__ clear, int64_t n_clear) {
-    __shared__ unsigned long long s_tot;
-    // the tick's own mail words (bits and multi of the other parity), read by k_tick: cleared here
-    for (int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x; q < n_clear; q += int64_t(gridDim.x) * kBlock)
-        if (clear[q]) clear[q] = 0;
-    if (thr != ~0ull) {
-        if (threadIdx.x < kWave) {
-            unsigned long long v = cnt_t[threadIdx.x * 4 + 2] + cnt_t[threadIdx.x * 4 + 3];
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-            if (threadIdx.x == 0) s_tot = v;
-        }
-        __syncthreads();
-        const bool storm = s_tot > thr;
-        if (blockIdx.x == 0 && threadIdx.x == 0) *pull_next = storm ? 1u : 0u;
-        if (storm) return;
-    } else if (blockIdx.x == 0 && threadIdx.x == 0) {
-        *pull_next = 0;
+    for (int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x; q < im.n_clear; q += int64_t(gridDim.x) * kBlock)
+        if (im.clear[q]) im.clear[q] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *im.pull_clear = 0;
+    const int ns = s_ns;
+    if (im.frac >= 0.0 && double(ns) > im.frac * double(span)) {
+        if (threadIdx.x == 0) *im.pull_next = 1u;
+        return;
     }
-    const int m = seg_count[blockIdx.x];
-    const int32_t *seg = segs.of(blockIdx.x);
+    // the segment was written by this workgroup's threads before add_counts' barrier
     unsigned long long c_edges = 0;
-    for (int q = threadIdx.x; q < m; q += kBlock) {
+    for (int q = threadIdx.x; q < ns; q += kBlock) {
         const int32_t i = seg[q];
-        const int32_t b = trp[i], e = trp[i + 1];
-        mail_hearers(b, e, tcol, mail, i);
+        const int32_t b = im.trp[i], e = im.trp[i + 1];
+        mail_hearers(b, e, im.tcol, im.next, i);
         c_edges += uint64_t(e - b);
     }
     if (tr) {
-        add_traffic(tr, 3, threadIdx.x < unsigned(m) ? uint64_t((m - int(threadIdx.x) + kBlock - 1) / kBlock) : 0ull);
+        add_traffic(tr, 3, threadIdx.x < unsigned(ns) ? uint64_t((ns - int(threadIdx.x) + kBlock - 1) / kBlock) : 0ull);
         add_traffic(tr, 4, c_edges);
     }
 }
@@ -663,9 +661,6 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
     unsigned long long *d_sum = d_cnt + size_t(ticks) * kShards * 4;
     unsigned long long *d_tr = traffic ? d_sum + size_t(ticks) * 4 : nullptr;
     if (d_tr) SW_HIP(hipMemsetAsync(d_tr, 0, tr_bytes, s));
-    // storm threshold on a tick's senders (pull_frac < 0: never; the pull-mode entry has no mail at all)
-    const unsigned long long thr = pull_frac < 0.0 ? ~0ull
-                                   : (unsigned long long)std::min(pull_frac * double(n), 1.8e19);
     const Fsm f{fsm->state, fsm->leader, fsm->last_hb, fsm->wait_start, fsm->delay,
                 reinterpret_cast<float2 *>(fsm->leader_pos), fsm->has_leader_pos, fsm->alive};
     // the sweep role's grid: 2 048 workgroups at most (10M agents: 0.128 ms per tick with 1 280
@@ -681,14 +676,16 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
     const bool push = hear_row_ptr != nullptr;
     const int64_t n_words = (n + 63) / 64;
     Mail mail{};
-    int32_t *seg_count = nullptr;
     Segs segs{};
     unsigned *pullf = nullptr;
-    unsigned long long *mw = nullptr;  // by tick parity p: mail bits at mw + 2p n_words, multi bits after them
-    auto mail_of = [&](int64_t tick) {  // the mail a tick receives (parity of the tick)
+    constexpr int nbuf = 3;            // mail word buffers, rotated by tick (NextMail)
+    unsigned long long *mw = nullptr;  // buffer b: mail bits at mw + 2b n_words, multi bits after them
+    int32_t *from_base = nullptr;      // single-sender slots, two buffers by tick parity
+    auto mail_of = [&](int64_t tick) {  // the mail a tick receives
         Mail m = mail;
-        m.bits = mw + size_t(tick & 1) * 2 * size_t(n_words);
+        m.bits = mw + size_t(tick % nbuf) * 2 * size_t(n_words);
         m.multi = m.bits + n_words;
+        m.from = from_base + size_t(tick & 1) * size_t(n);
         return m;
     };
     // k_tick's receive role: a workgroup per 4 096-agent chunk, at most 5/8 of the sweep grid (10M
@@ -702,10 +699,10 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
     const int64_t nchunks_all = (n + kRecvChunk - 1) / kRecvChunk;
     const int g_recv = int(std::max<int64_t>(
         1, std::min<int64_t>(nchunks_all, recv_env > 0 ? recv_env : std::max<int64_t>(1, int64_t(grid) * 5 / 8))));
-    const unsigned tgrid = grid + unsigned(g_recv);  // k_tick / k_mail: both roles, interleaved
-    if (push) {  // mail bitmaps (two parities) + the pull flags (tick parity) after them
-        SW_ALLOC(mw, ctx, S_FSM_MAIL, size_t(n_words) * 32 + 64);
-        SW_ALLOC(mail.from, ctx, S_FSM_FROM, size_t(n) * 4);
+    const unsigned tgrid = grid + unsigned(g_recv);  // k_tick: both roles
+    if (push) {  // mail bitmaps (nbuf buffers) + the pull flags (by tick, nbuf) after them
+        SW_ALLOC(mw, ctx, S_FSM_MAIL, size_t(n_words) * 48 + 64);
+        SW_ALLOC(from_base, ctx, S_FSM_FROM, size_t(n) * 8);
         // per-workgroup sender segments of k_tick (each workgroup lists at most the agents it sees:
         // a grid-stride share of kSweepV-agent groups, or of 4 096-agent chunks), then their counts
         const int64_t ngroups = (n + kSweepV - 1) / kSweepV;
@@ -715,10 +712,9 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
         segs.scap = std::max((ngroups + int64_t(grid) * kBlock - 1) / (int64_t(grid) * kBlock) * kBlock * kSweepV,
                              (nchunks + tgrid - 1) / tgrid * kRecvChunk);
         const size_t seg_total = size_t(g_recv) * segs.rcap + size_t(grid) * segs.scap;
-        SW_ALLOC(segs.base, ctx, S_FSM_SEND, seg_total * 4 + size_t(tgrid) * 4);
-        seg_count = segs.base + seg_total;
-        pullf = reinterpret_cast<unsigned *>(mw + 4 * n_words);  // [2] by tick parity: the tick pulls
-        SW_HIP(hipMemsetAsync(mw, 0, size_t(n_words) * 32 + 64, s));
+        SW_ALLOC(segs.base, ctx, S_FSM_SEND, seg_total * 4);
+        pullf = reinterpret_cast<unsigned *>(mw + 6 * n_words);  // [nbuf] by tick: the tick pulls
+        SW_HIP(hipMemsetAsync(mw, 0, size_t(n_words) * 48 + 64, s));
         hipLaunchKernelGGL(k_mail_from_outbox, dim3(grid), dim3(kBlock), 0, s, n,
                            fsm->outbox + size_t(t0 & 1) * size_t(n), hear_row_ptr, hear_col, mail_of(t0 + 1));
         SW_LAUNCHED();
@@ -734,14 +730,19 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
         uint8_t *ob_out = fsm->outbox + size_t(t & 1) * size_t(n);
         unsigned long long *cnt = d_cnt + size_t(t - t0 - 1) * kShards * 4;
         if (push) {
+            NextMail im{};
+            im.next = mail_of(t + 1);
+            im.clear = mail_of(t + 2).bits;
+            im.n_clear = 2 * n_words;
+            im.pull_next = pullf + (t + 1) % nbuf;
+            im.pull_clear = pullf + (t + 2) % nbuf;
+            im.frac = pull_frac < 0.0 ? -1.0 : pull_frac;
+            im.trp = hear_row_ptr;
+            im.tcol = hear_col;
             hipLaunchKernelGGL(k_tick, dim3(tgrid), dim3(kBlock), 0, s, n, t, ids,
                                reinterpret_cast<const double2 *>(pos), row_ptr, col, tick_off, f, mail_of(t), ob_in,
-                               ob_out, pullf + (t & 1), segs, seg_count, dt, timeout, jitter, seed, cnt,
-                               int(vec && (reinterpret_cast<uintptr_t>(ob_out) & 3) == 0), d_tr);
-            SW_LAUNCHED();
-            hipLaunchKernelGGL(k_mail, dim3(tgrid), dim3(kBlock), 0, s, segs, seg_count, hear_row_ptr,
-                               hear_col, mail_of(t + 1), cnt, thr, pullf + ((t + 1) & 1), d_tr, mail_of(t).bits,
-                               2 * n_words);
+                               ob_out, pullf + t % nbuf, segs, dt, timeout, jitter, seed, cnt,
+                               int(vec && (reinterpret_cast<uintptr_t>(ob_out) & 3) == 0), d_tr, im);
         } else {
             hipLaunchKernelGGL(k_tick_pull, dim3(grid), dim3(kBlock), 0, s, n, t, ids,
                                reinterpret_cast<const double2 *>(pos), row_ptr, col, tick_off, f, ob_in, ob_out, dt,

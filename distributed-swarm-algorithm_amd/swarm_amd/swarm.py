@@ -537,8 +537,9 @@ class Swarm:
         kill_ticks: absolute ticks at whose start every alive LEADER dies.  Returns counts
         (ticks x 4): alive LEADERs, alive ELECTION_WAITs, ACCLAIM senders, HEARTBEAT senders.
         mode "push": senders mark their hearers and only marked agents scan their row; "pull":
-        every agent scans its row every tick; "hybrid": push, but a tick whose senders exceed
-        pull_frac x n (a timeout wave) has the next tick pull (swarm_protocol_run_ex).  Same results.
+        every agent scans its row every tick; "hybrid": push, but a tick in which a workgroup's
+        senders exceed pull_frac x its share of the agents (a timeout wave) has the next tick pull
+        (swarm_protocol_run_ex).  Same results.
         traffic: count what the ticks touched (self.fsm_traffic: 8 int64, see include/swarm.h)."""
         if self.row_ptr is None:
             raise RuntimeError("no neighbour graph: call build_graph() or set_graph()")

@@ -507,9 +507,10 @@ int swarm_protocol_run(swarm_ctx *ctx, int64_t n, const int32_t *ids, const doub
                        int32_t n_kill, int64_t *counts, void *stream);
 
 /* swarm_protocol_run with storm ticks pulled and the traffic counted (same results):
- * pull_frac (push mode): when a tick's senders (ACCLAIM + HEARTBEAT counts) exceed pull_frac x n, the
- *   next tick's receivers walk their own rows instead of being mailed (a timeout wave makes most
- *   agents send at once: mailing every hearer costs more than every agent pulling); < 0: never.
+ * pull_frac (push mode): when the senders of a tick's workgroup (its share of the agents: a grid-stride
+ *   set of 4-agent groups, or of 4 096-agent chunks) exceed pull_frac x its agents, the next tick's
+ *   receivers walk their own rows instead of being mailed (a timeout wave makes most agents send at
+ *   once: mailing every hearer costs more than every agent pulling); < 0: never.
  * traffic (host, 8 int64, may be NULL; synchronises): summed over the run -- [0] receivers served by
  *   their single sender, [1] receivers that walked their row (several senders), [2] row edges walked
  *   (those and pulled ticks), [3] senders mailed, [4] hearer edges mailed, [5] 0, [6] agents that
