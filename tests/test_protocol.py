@@ -220,9 +220,9 @@ def test_gpu_sweep_unaligned_arrays_match_oracle(oracle_mod, n):
 @pytest.mark.gpu
 @pytest.mark.parametrize("pull_frac", [0.0, 0.02, 0.125])
 def test_gpu_hybrid_storm_ticks_match_oracle(oracle_mod, pull_frac):
-    """Hybrid mode (swarm_protocol_run_ex): a tick whose senders exceed pull_frac x n has the next
-    tick pull (every alive agent walks its row, no mail); pull_frac 0 pulls after every tick with a
-    sender.  States, timers, leader positions and per-tick counts equal the oracle's, in two chunks
+    """Hybrid mode (swarm_protocol_run_ex): a tick in which a workgroup's senders exceed pull_frac x
+    its share of the agents has the next tick pull (every alive agent walks its row); pull_frac 0
+    pulls after every tick with a sender, and nothing is mailed.  States, timers, leader positions and per-tick counts equal the oracle's, in two chunks
     (a pulled tick at a chunk boundary), and the traffic counters add up."""
     g = _random_case(20000, 5, 50.0)
     g["ticks"], g["kill_ticks"] = np.int64(150), np.array([60, 110], np.int64)
