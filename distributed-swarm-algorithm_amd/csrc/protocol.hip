@@ -663,13 +663,15 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
     if (d_tr) SW_HIP(hipMemsetAsync(d_tr, 0, tr_bytes, s));
     const Fsm f{fsm->state, fsm->leader, fsm->last_hb, fsm->wait_start, fsm->delay,
                 reinterpret_cast<float2 *>(fsm->leader_pos), fsm->has_leader_pos, fsm->alive};
-    // the sweep role's grid: 2 048 workgroups at most (10M agents: 0.128 ms per tick with 1 280
-    // receive-role workgroups, 0.131 with 4 096 + 2 048; SWARM_FSM_SWEEP_WGS overrides, A/B aid)
+    // the sweep role's grid: 2 560 workgroups at most, with half as many in the receive role (10M
+    // agents, one-launch ticks, two boxes: 0.1208-0.1212 ms per tick against 0.1232-0.1234 for
+    // 2 048 + 1 280, 0.122 for 1 536 + 1 280, 2 560 + 1 536 and 3 072 + 1 280; the two-launch form
+    // had 2 048 + 1 280 at 0.128, 4 096 + 2 048 at 0.131; SWARM_FSM_SWEEP_WGS overrides, A/B aid)
     static const int sweep_env = [] {
         const char *e = getenv("SWARM_FSM_SWEEP_WGS");
         return e ? atoi(e) : 0;
     }();
-    const unsigned grid = grid_for(n, kBlock, sweep_env > 0 ? unsigned(sweep_env) : 2048u);
+    const unsigned grid = grid_for(n, kBlock, sweep_env > 0 ? unsigned(sweep_env) : 2560u);
     auto a16 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     // k_sweep's word loads: byte arrays 4-byte aligned (the tick's outbox half too), timers 16-byte
     const int vec = a16(fsm->alive) && a16(fsm->outbox) && a16(fsm->state) && a16(tick_off) && a16(fsm->last_hb);
@@ -688,9 +690,9 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
         m.from = from_base + size_t(tick & 1) * size_t(n);
         return m;
     };
-    // k_tick's receive role: a workgroup per 4 096-agent chunk, at most 5/8 of the sweep grid (10M
-    // agents: 1 280 of 2 442 chunks' workgroups; with the sweep grid 2 048: 1 280 -> 0.1279 ms per
-    // tick, 1 536 -> 0.1281, 2 048 -> 0.1298, 1 024 -> 0.1303; earlier, sweep grid 4 096: 2 048 ->
+    // k_tick's receive role: a workgroup per 4 096-agent chunk, at most half the sweep grid (10M
+    // agents: 1 280 of 2 442 chunks' workgroups; two-launch form, sweep grid 2 048: 1 280 -> 0.1279
+    // ms per tick, 1 536 -> 0.1281, 2 048 -> 0.1298, 1 024 -> 0.1303; sweep grid 4 096: 2 048 ->
     // 0.138, 512 -> 0.160, 256 -> 0.214; SWARM_FSM_RECV_WGS overrides, A/B aid)
     static const int recv_env = [] {
         const char *e = getenv("SWARM_FSM_RECV_WGS");
@@ -698,7 +700,7 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
     }();
     const int64_t nchunks_all = (n + kRecvChunk - 1) / kRecvChunk;
     const int g_recv = int(std::max<int64_t>(
-        1, std::min<int64_t>(nchunks_all, recv_env > 0 ? recv_env : std::max<int64_t>(1, int64_t(grid) * 5 / 8))));
+        1, std::min<int64_t>(nchunks_all, recv_env > 0 ? recv_env : std::max<int64_t>(1, int64_t(grid) / 2))));
     const unsigned tgrid = grid + unsigned(g_recv);  // k_tick: both roles
     if (push) {  // mail bitmaps (nbuf buffers) + the pull flags (by tick, nbuf) after them
         SW_ALLOC(mw, ctx, S_FSM_MAIL, size_t(n_words) * 48 + 64);
