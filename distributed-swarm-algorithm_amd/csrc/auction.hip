@@ -1209,7 +1209,10 @@ int swarm_auction_sharded(swarm_ctx *ctx, swarm_comm *comm, int64_t n, const int
         SW_HIP(hipMemcpyAsync(h, w, 8, hipMemcpyDeviceToHost, s));
         SW_HIP(hipStreamSynchronize(s));
         cap0 = cap = std::max<int64_t>(1, h[0]);
-        const size_t words0 = size_t(kBidHdr + 2 * cap0);
+        // a round whose bound gives lists longer than the dense key array (2 cap + 2 >= t + world words)
+        // takes the dense MAX all-reduce instead: the lists are only ever cap_list long
+        const int64_t cap_list = std::max<int64_t>(1, std::min<int64_t>(cap0, (t + world - kBidHdr - 1) / 2));
+        const size_t words0 = size_t(kBidHdr + 2 * cap_list);
         uint8_t *xb;
         SW_ALLOC(xb, ctx, S_AUC_LIST, (words0 * size_t(world + 1)) * 8 + 64);
         send = reinterpret_cast<unsigned long long *>(xb);
@@ -1228,8 +1231,9 @@ int swarm_auction_sharded(swarm_ctx *ctx, swarm_comm *comm, int64_t n, const int
     while (r <= max_rounds && found < 0) {
         const int64_t rend = (max_rounds - r + 1 < batch) ? max_rounds : r + batch - 1;
         const int64_t words = kBidHdr + 2 * cap;
+        const bool dense_batch = dense_x || words >= t + world;
         for (int64_t q = r; q <= rend; ++q) {
-            if (dense_x) {
+            if (dense_batch) {
                 if (int rc = swarm_auction_bid(ctx, q, rank, world, reinterpret_cast<uint64_t *>(keys), price,
                                                assigned, stream))
                     return rc;

@@ -112,14 +112,11 @@ const Rccl &rccl() {
         }                                                                                    \
     } while (0)
 
-// send buffers <- current leaders of the boundary agents (both borders in one launch)
-__global__ __launch_bounds__(kBlock) void k_pack(const int32_t *__restrict__ L, const int64_t *__restrict__ lo_idx,
-                                                int64_t n_lo, const int64_t *__restrict__ hi_idx, int64_t n_hi,
-                                                int32_t *__restrict__ lo_buf, int32_t *__restrict__ hi_buf) {
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n_lo + n_hi; i += int64_t(gridDim.x) * kBlock) {
-        if (i < n_lo) lo_buf[i] = L[lo_idx[i]];
-        else hi_buf[i - n_lo] = L[hi_idx[i - n_lo]];
-    }
+// send buffer <- current leaders of the rows every peer keeps as ghosts (one index list, peer after peer)
+__global__ __launch_bounds__(kBlock) void k_pack(const int32_t *__restrict__ L, const int64_t *__restrict__ rows,
+                                                int64_t n, int32_t *__restrict__ buf) {
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock)
+        buf[i] = L[rows[i]];
 }
 
 // ---- shared-memory transport
@@ -155,21 +152,42 @@ int shm_barrier(swarm_comm *c) {
     return SWARM_OK;
 }
 
-// Halo exchange over the mailboxes: this rank's to-lo buffer goes in the first half of its mailbox,
-// its to-hi buffer in the second; the ghosts from below are the lower peer's to-hi half.
-int shm_halo(swarm_comm *c, const int32_t *s_lo, int64_t n_s_lo, int peer_lo, int32_t *r_lo, int64_t n_r_lo,
-             const int32_t *s_hi, int64_t n_s_hi, int peer_hi, int32_t *r_hi, int64_t n_r_hi, hipStream_t s) {
+// A local error inside a shared-memory op: the peers' next barrier fails at once instead of timing out.
+int shm_fail(swarm_comm *c, int rc) {
+    if (c->hdr) c->hdr->abort.store(1, std::memory_order_relaxed);
+    return rc;
+}
+
+// Halo exchange over the mailboxes.  This rank's mailbox of the op's parity holds a table of
+// (offset, count) per destination rank, then its whole send buffer (the segments for its peers back to
+// back); a rank reads its ghosts from each peer's mailbox at the offset that peer's table gives it.
+// One device -> host copy of the send buffer, one host -> device copy per peer.
+int shm_halo(swarm_comm *c, const int32_t *send, const int64_t *soff, const int32_t *peers, int n_peers,
+             int32_t *recv, const int64_t *roff, hipStream_t s) {
     const uint64_t par = c->ops++ & 1;
-    const uint64_t half = c->hdr->cap / 2;
-    SW_ARG(uint64_t(std::max({n_s_lo, n_s_hi, n_r_lo, n_r_hi})) * 4 <= half,
-           "halo larger than the shared-memory mailboxes (raise SWARM_SHM_MB)");
+    const size_t tab = size_t(c->nranks) * 2 * 8;
     char *mine = shm_box(c, c->rank, par);
-    if (n_s_lo) SW_HIP(hipMemcpyAsync(mine, s_lo, size_t(n_s_lo) * 4, hipMemcpyDeviceToHost, s));
-    if (n_s_hi) SW_HIP(hipMemcpyAsync(mine + half, s_hi, size_t(n_s_hi) * 4, hipMemcpyDeviceToHost, s));
+    int64_t *t = reinterpret_cast<int64_t *>(mine);
+    for (int q = 0; q < 2 * c->nranks; ++q) t[q] = 0;
+    for (int j = 0; j < n_peers; ++j) {
+        t[2 * peers[j]] = soff[j];
+        t[2 * peers[j] + 1] = soff[j + 1] - soff[j];
+    }
+    if (soff[n_peers]) SW_HIP(hipMemcpyAsync(mine + tab, send, size_t(soff[n_peers]) * 4, hipMemcpyDeviceToHost, s));
     SW_HIP(hipStreamSynchronize(s));
     if (int rc = shm_barrier(c)) return rc;
-    if (n_r_lo) SW_HIP(hipMemcpyAsync(r_lo, shm_box(c, peer_lo, par) + half, size_t(n_r_lo) * 4, hipMemcpyHostToDevice, s));
-    if (n_r_hi) SW_HIP(hipMemcpyAsync(r_hi, shm_box(c, peer_hi, par), size_t(n_r_hi) * 4, hipMemcpyHostToDevice, s));
+    for (int j = 0; j < n_peers; ++j) {
+        const char *box = shm_box(c, peers[j], par);
+        const int64_t *pt = reinterpret_cast<const int64_t *>(box);
+        const int64_t off = pt[2 * c->rank], cnt = pt[2 * c->rank + 1];
+        if (cnt != roff[j + 1] - roff[j]) {
+            set_error("halo exchange: rank %d sends %lld ghosts to rank %d, which expects %lld", peers[j],
+                      (long long)cnt, c->rank, (long long)(roff[j + 1] - roff[j]));
+            return shm_fail(c, SWARM_ERR_ARG);
+        }
+        if (cnt) SW_HIP(hipMemcpyAsync(recv + roff[j], box + tab + size_t(off) * 4, size_t(cnt) * 4,
+                                       hipMemcpyHostToDevice, s));
+    }
     // the mailboxes of this parity are rewritten two ops later, after every rank has passed the
     // next op's barrier -- which this rank reaches only once its reads here are done
     SW_HIP(hipStreamSynchronize(s));
@@ -178,7 +196,10 @@ int shm_halo(swarm_comm *c, const int32_t *s_lo, int64_t n_s_lo, int peer_lo, in
 
 int shm_allreduce_u64(swarm_comm *c, unsigned long long *buf, size_t count, bool is_max, hipStream_t s) {
     const uint64_t par = c->ops++ & 1;
-    SW_ARG(uint64_t(count) * 8 <= c->hdr->cap, "all-reduce larger than the shared-memory mailboxes (raise SWARM_SHM_MB)");
+    if (uint64_t(count) * 8 > c->hdr->cap) {
+        set_error("all-reduce larger than the shared-memory mailboxes (raise SWARM_SHM_MB)");
+        return shm_fail(c, SWARM_ERR_ARG);
+    }
     SW_HIP(hipMemcpyAsync(shm_box(c, c->rank, par), buf, count * 8, hipMemcpyDeviceToHost, s));
     SW_HIP(hipStreamSynchronize(s));
     if (int rc = shm_barrier(c)) return rc;
@@ -196,7 +217,10 @@ int shm_allreduce_u64(swarm_comm *c, unsigned long long *buf, size_t count, bool
 int shm_allgather_u64(swarm_comm *c, const unsigned long long *send, size_t count, unsigned long long *recv,
                       hipStream_t s) {
     const uint64_t par = c->ops++ & 1;
-    SW_ARG(uint64_t(count) * 8 <= c->hdr->cap, "all-gather larger than the shared-memory mailboxes (raise SWARM_SHM_MB)");
+    if (uint64_t(count) * 8 > c->hdr->cap) {
+        set_error("all-gather larger than the shared-memory mailboxes (raise SWARM_SHM_MB)");
+        return shm_fail(c, SWARM_ERR_ARG);
+    }
     SW_HIP(hipMemcpyAsync(shm_box(c, c->rank, par), send, count * 8, hipMemcpyDeviceToHost, s));
     SW_HIP(hipStreamSynchronize(s));
     if (int rc = shm_barrier(c)) return rc;
@@ -421,40 +445,79 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sh,
                         void *stream) {
     using namespace swarm;
     SW_ARG(ctx && comm && sh && rounds_exec, "NULL argument");
-    SW_ARG(max_rounds >= 1, "max_rounds < 1");
-    SW_ARG(sh->n_rows >= 0 && sh->n_all >= sh->n_rows, "shard sizes");
-    SW_ARG(sh->own_begin >= 0 && sh->own_begin + sh->n_rows <= sh->n_all, "owned range out of [0, n_all)");
-    SW_ARG((sh->peer_lo >= 0 || (sh->n_send_lo == 0 && sh->n_ghost_lo == 0)) &&
-           (sh->peer_hi >= 0 || (sh->n_send_hi == 0 && sh->n_ghost_hi == 0)), "halo without a peer");
-    SW_ARG(sh->peer_lo < comm->nranks && sh->peer_hi < comm->nranks, "peer rank out of range");
-    // the ghost ranges are checked here, before any collective: a rank that failed inside the loop
-    // would leave its peers blocked in their next exchange
-    const auto outside = [&](int64_t b, int64_t c) {
-        return c == 0 || (b >= 0 && b + c <= sh->n_all && (b + c <= sh->own_begin || b >= sh->own_begin + sh->n_rows));
-    };
-    SW_ARG(outside(sh->ghost_lo_begin, sh->n_ghost_lo) && outside(sh->ghost_hi_begin, sh->n_ghost_hi),
-           "ghost ranges must lie in [0, n_all) outside the owned rows");
     hipStream_t s = static_cast<hipStream_t>(stream);
-    int rc = swarm_frontier_begin_range(ctx, sh->own_begin, sh->n_rows, sh->n_all, sh->init, leader0, leader1, stream);
-    if (rc) return rc;
-    if ((rc = swarm_frontier_set_compact(ctx, sh->col16))) return rc;
-    int32_t *bufs;
-    const size_t nb = size_t(sh->n_send_lo + sh->n_send_hi + sh->n_ghost_lo + sh->n_ghost_hi) + 4;
-    SW_ALLOC(bufs, ctx, S_TMP0, nb * 4);
-    int32_t *s_lo = bufs, *s_hi = s_lo + sh->n_send_lo, *r_lo = s_hi + sh->n_send_hi, *r_hi = r_lo + sh->n_ghost_lo;
-    constexpr int kMaxBatch = 256;
-    unsigned long long *dtot;
-    constexpr int kC = kElectCounters;
-    SW_ALLOC(dtot, ctx, S_ESTATS, size_t(kC) * 8 * kMaxBatch);
-    unsigned long long *h = static_cast<unsigned long long *>(pinned(ctx, size_t(kC) * 8 * kMaxBatch));
-    if (!h) return SWARM_ERR_OOM;
     const bool shm = comm->kind == SWARM_COMM_SHM;
     const Rccl &R = rccl();
     if (!shm && comm->nranks > 1 && !R.ok) {
         set_error("RCCL not found in the process");
         return SWARM_ERR_ARG;
     }
+    // Every check that one rank alone could fail is made here and agreed on by all ranks (one MAX
+    // all-reduce) before the round loop: a rank that left early would keep its peers waiting in their
+    // next exchange.
+    char why[256] = {};
+    const int np = sh->n_peers;
+    std::vector<int64_t> soff(size_t(std::max(np, 0)) + 1, 0), roff(size_t(std::max(np, 0)) + 1, 0);
+    int64_t below = 0;
+    {
+        auto bad = [&](const char *m) { if (!why[0]) snprintf(why, sizeof(why), "%s", m); };
+        if (max_rounds < 1) bad("max_rounds < 1");
+        if (sh->n_rows < 0 || sh->n_all < sh->n_rows) bad("shard sizes");
+        if (sh->own_begin < 0 || sh->own_begin + sh->n_rows > sh->n_all) bad("owned range out of [0, n_all)");
+        if (np < 0 || (np > 0 && (!sh->peers || !sh->send_count || !sh->ghost_count))) bad("peer list");
+        for (int j = 0; j < np && !why[0]; ++j) {
+            const int p = sh->peers[j];
+            if (p < 0 || p >= comm->nranks || p == comm->rank || (j && p <= sh->peers[j - 1]))
+                bad("peers must be ascending ranks of the communicator, other than this rank");
+            if (sh->send_count[j] < 0 || sh->ghost_count[j] < 0) bad("negative halo count");
+            soff[j + 1] = soff[j] + sh->send_count[j];
+            roff[j + 1] = roff[j] + sh->ghost_count[j];
+            if (p < comm->rank) below += sh->ghost_count[j];
+        }
+        if (!why[0] && soff[np] && !sh->send_rows) bad("send_rows is NULL");
+        // the ghosts of the peers below fill [0, own_begin), those of the peers above the rows after the owned
+        if (!why[0] && (below != sh->own_begin || roff[np] != sh->n_all - sh->n_rows))
+            bad("ghost rows must be [peers below | owned | peers above], ghost_count peer by peer");
+        if (!why[0] && shm && uint64_t(comm->nranks) * 16 + uint64_t(soff[np]) * 4 > comm->hdr->cap)
+            bad("halo larger than the shared-memory mailboxes (raise SWARM_SHM_MB)");
+    }
+    const size_t nsend = size_t(soff[np]), nrecv = size_t(roff[np]);
+    constexpr int kMaxBatch = 256;
+    constexpr int kC = kElectCounters;
+    unsigned long long *dtot;
+    SW_ALLOC(dtot, ctx, S_ESTATS, size_t(kC) * 8 * kMaxBatch);
+    unsigned long long *h = static_cast<unsigned long long *>(pinned(ctx, size_t(kC) * 8 * kMaxBatch));
+    if (!h) return SWARM_ERR_OOM;
     const int depth = sh->halo_depth > 1 ? sh->halo_depth : 1;
+    {
+        unsigned long long agree[3] = {why[0] ? 1ull : 0ull, (unsigned long long)depth,
+                                       (unsigned long long)(65536 - depth)};
+        SW_HIP(hipMemcpyAsync(dtot, agree, sizeof(agree), hipMemcpyHostToDevice, s));
+        if (comm->nranks > 1) {
+            if (int rc = comm_allreduce_max_u64(comm, dtot, 3, s)) return rc;
+        }
+        SW_HIP(hipMemcpyAsync(agree, dtot, sizeof(agree), hipMemcpyDeviceToHost, s));
+        SW_HIP(hipStreamSynchronize(s));
+        if (why[0]) {
+            set_error("swarm_elect_sharded: %s", why);
+            return SWARM_ERR_ARG;
+        }
+        if (agree[0]) {
+            set_error("swarm_elect_sharded: a peer rejected its shard (see its error)");
+            return SWARM_ERR_ARG;
+        }
+        if (int(agree[1]) != depth || int(65536 - agree[2]) != depth) {
+            set_error("swarm_elect_sharded: halo_depth differs between ranks (%d here)", depth);
+            return SWARM_ERR_ARG;
+        }
+    }
+    int rc = swarm_frontier_begin_range(ctx, sh->own_begin, sh->n_rows, sh->n_all, sh->init, leader0, leader1, stream);
+    if (rc) return rc;
+    if ((rc = swarm_frontier_set_compact(ctx, sh->col16))) return rc;
+    int32_t *sbuf;
+    SW_ALLOC(sbuf, ctx, S_TMP0, (nsend + nrecv + 4) * 4);
+    int32_t *rbuf = sbuf + nsend;
+    const int64_t own_end = sh->own_begin + sh->n_rows;
     int found = -1, t = 1, batch = 8;
     std::vector<int64_t> hist;
     // the stamp layout: interleaved while rounds are busy, agent order in the tail (as swarm_elect),
@@ -465,33 +528,29 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sh,
         ctx->step_wr_agent = (!hist.empty() && hist.back() < il_min) ? 1 : 0;
         for (int r = t; r <= tend; ++r) {
             if ((rc = frontier_round_stepper(ctx, r, sh->row_ptr, sh->col, leader0, leader1, s))) return rc;
-            if (r % depth) continue;  // deep halo: ghosts are stepped locally between exchanges
+            if (r % depth || comm->nranks == 1) continue;  // deep halo: ghosts are stepped locally between exchanges
+            // every rank takes part in every exchange, peers or not (the shared-memory ops are barriers)
             int32_t *Lcur = (r & 1) ? leader1 : leader0;
-            const int64_t ns = sh->n_send_lo + sh->n_send_hi;
-            if (ns) {
-                hipLaunchKernelGGL(k_pack, dim3(grid_for(ns, kBlock, 1024)), dim3(kBlock), 0, s, Lcur, sh->send_lo,
-                                   sh->n_send_lo, sh->send_hi, sh->n_send_hi, s_lo, s_hi);
+            if (nsend) {
+                hipLaunchKernelGGL(k_pack, dim3(grid_for(int64_t(nsend), kBlock, 1024)), dim3(kBlock), 0, s, Lcur,
+                                   sh->send_rows, int64_t(nsend), sbuf);
                 SW_LAUNCHED();
             }
             if (shm) {
-                if ((rc = shm_halo(comm, s_lo, sh->peer_lo >= 0 ? sh->n_send_lo : 0, sh->peer_lo, r_lo,
-                                   sh->peer_lo >= 0 ? sh->n_ghost_lo : 0, s_hi, sh->peer_hi >= 0 ? sh->n_send_hi : 0,
-                                   sh->peer_hi, r_hi, sh->peer_hi >= 0 ? sh->n_ghost_hi : 0, s)))
-                    return rc;
+                if ((rc = shm_halo(comm, sbuf, soff.data(), sh->peers, np, rbuf, roff.data(), s))) return rc;
             } else {
-            SW_NCCL(R.groupStart());
-            if (sh->peer_lo >= 0) {
-                if (sh->n_send_lo) SW_NCCL(R.send(s_lo, size_t(sh->n_send_lo), ncclInt32, sh->peer_lo, comm->comm, s));
-                if (sh->n_ghost_lo) SW_NCCL(R.recv(r_lo, size_t(sh->n_ghost_lo), ncclInt32, sh->peer_lo, comm->comm, s));
+                SW_NCCL(R.groupStart());
+                for (int j = 0; j < np; ++j) {
+                    if (sh->send_count[j])
+                        SW_NCCL(R.send(sbuf + soff[j], size_t(sh->send_count[j]), ncclInt32, sh->peers[j], comm->comm, s));
+                    if (sh->ghost_count[j])
+                        SW_NCCL(R.recv(rbuf + roff[j], size_t(sh->ghost_count[j]), ncclInt32, sh->peers[j], comm->comm, s));
+                }
+                SW_NCCL(R.groupEnd());
             }
-            if (sh->peer_hi >= 0) {
-                if (sh->n_send_hi) SW_NCCL(R.send(s_hi, size_t(sh->n_send_hi), ncclInt32, sh->peer_hi, comm->comm, s));
-                if (sh->n_ghost_hi) SW_NCCL(R.recv(r_hi, size_t(sh->n_ghost_hi), ncclInt32, sh->peer_hi, comm->comm, s));
-            }
-            SW_NCCL(R.groupEnd());
-            }
-            if ((rc = frontier_ghosts_both(ctx, r, sh->row_ptr, sh->col, sh->ghost_lo_begin, sh->n_ghost_lo, r_lo,
-                                           sh->ghost_hi_begin, sh->n_ghost_hi, r_hi, leader0, leader1, s)))
+            // the receive buffer is in row order: the lower ghost block, then the upper one
+            if (nrecv && (rc = frontier_ghosts_both(ctx, r, sh->row_ptr, sh->col, 0, sh->own_begin, rbuf, own_end,
+                                           sh->n_all - own_end, rbuf + sh->own_begin, leader0, leader1, s)))
                 return rc;
         }
         const int nr = tend - t + 1;

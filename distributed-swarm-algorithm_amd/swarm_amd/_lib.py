@@ -77,13 +77,28 @@ class Grid(ctypes.Structure):
 
 
 class Shard(ctypes.Structure):
+    """swarm_shard: one rank's rows and its peer list (the host arrays are kept alive by .keep)."""
     _fields_ = [("n_rows", ctypes.c_int64), ("n_all", ctypes.c_int64), ("row_ptr", ctypes.c_void_p),
-                ("col", ctypes.c_void_p), ("init", ctypes.c_void_p), ("send_lo", ctypes.c_void_p),
-                ("n_send_lo", ctypes.c_int64), ("send_hi", ctypes.c_void_p), ("n_send_hi", ctypes.c_int64),
-                ("ghost_lo_begin", ctypes.c_int64), ("n_ghost_lo", ctypes.c_int64),
-                ("ghost_hi_begin", ctypes.c_int64), ("n_ghost_hi", ctypes.c_int64),
-                ("peer_lo", ctypes.c_int32), ("peer_hi", ctypes.c_int32), ("halo_depth", ctypes.c_int32),
-                ("own_begin", ctypes.c_int64), ("col16", ctypes.c_void_p)]
+                ("col", ctypes.c_void_p), ("init", ctypes.c_void_p), ("own_begin", ctypes.c_int64),
+                ("halo_depth", ctypes.c_int32), ("n_peers", ctypes.c_int32), ("peers", ctypes.c_void_p),
+                ("send_count", ctypes.c_void_p), ("send_rows", ctypes.c_void_p),
+                ("ghost_count", ctypes.c_void_p), ("col16", ctypes.c_void_p)]
+
+
+def shard_desc(n_rows, n_all, row_ptr, col, init, own_begin, halo_depth, peers=(), send_count=(), send_rows=None,
+               ghost_count=(), col16=None) -> Shard:
+    """A Shard over device tensors (row_ptr, col, init, send_rows, col16) and host peer lists."""
+    import numpy as np
+    pe = np.ascontiguousarray(peers, np.int32)
+    sc = np.ascontiguousarray(send_count, np.int64)
+    gc = np.ascontiguousarray(ghost_count, np.int64)
+    z = ctypes.c_void_p(0)
+    hp = lambda a: a.ctypes.data_as(ctypes.c_void_p) if a.size else z  # noqa: E731
+    dp = lambda t: ptr(t) if t is not None and t.numel() else z  # noqa: E731
+    d = Shard(int(n_rows), int(n_all), dp(row_ptr), dp(col), dp(init), int(own_begin), int(halo_depth), len(pe),
+              hp(pe), hp(sc), dp(send_rows), hp(gc), dp(col16))
+    d.keep = (pe, sc, gc)
+    return d
 
 
 _lib = None

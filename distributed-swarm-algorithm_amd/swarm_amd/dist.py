@@ -1,40 +1,42 @@
 """Multi-GPU swarm step: agents sharded across ranks, one process per GPU.
 
-Partition.  The global square is cut into horizontal strips, one per rank (the agent storage
-order inside a shard is row-major cell order, so a strip is a contiguous range of the spatial
-order).  north_star partitions agents by ID range: with strip-major IDs (gen.strip_ids,
-gen.shard_inputs) each rank's contiguous ID range IS its strip, and partition(by="id") cuts by
-ID and checks exactly that.  Each rank owns the agents inside its strip and keeps *ghost* copies
-of the neighbouring ranks' agents within k radio radii of the shared border (k = halo depth).
+Partition.  Every rank owns a set of agents (north_star: a contiguous ID range) and knows, through
+a Layout, which of its agents every other rank needs: the agents within a given distance of that
+rank's region.  Layouts: StripChain (this rank's horizontal strip only; the neighbours are the ranks
+above and below -- gen.shard_inputs, strip-major IDs), Rects (every rank's axis-aligned region:
+strips cut from one global swarm, Morton blocks -- gen.shard_inputs(layout="blocks")), and Cells
+(any ownership at all, e.g. ID ranges of random or Morton IDs of one global swarm: each rank's
+occupied grid cells, dilated).  The agent storage order inside a shard is row-major cell order, and
+the shard's rows are [ghosts of the peers ranked below | owned | ghosts of the peers ranked above].
 
-Election (exact, contract E2).  Rounds run on every rank in lockstep through the frontier
-stepper (include/swarm.h: swarm_frontier_*): round t gathers owned AND ghost agents over the
-local graph; only owned changes are counted.  Every k-th round the owned agents within k radii
-of a border send their leaders to the neighbour rank (torch.distributed P2P -- RCCL over xGMI on
-GPUs, gloo in the CPU tests), where they overwrite the ghosts and activate their local
-neighbours for the next round.  Between exchanges a ghost near the halo's outer edge misses
-neighbours and may lag (a lower bound); that error starts one radius inside the outer edge and
-moves at most one radius per round, so after j <= k rounds it has not reached the border: owned
-agents are exact at every round, and so are the ghosts within one radius of the border.  Per-
-round owned change counts are summed over ranks with one all-reduce every `check_every` rounds;
-the first globally zero round ends the run and is rounds_exec (rounds after it are no-ops
-everywhere).  Result: the same leaders, rounds and per-round change counts as a single-GPU run
-on the union graph, with a halo exchange every k rounds instead of every round.
+Election (exact, contract E2).  Rounds run on every rank in lockstep through the frontier stepper
+(include/swarm.h: swarm_frontier_*): round t gathers owned AND ghost agents over the local graph;
+only owned changes are counted.  The ghosts are every other rank's agents within k radio radii of
+this rank's region (k = halo depth), i.e. at least every agent within k hops of an owned agent.
+Every k-th round each rank sends the leaders of the owned agents each peer keeps as ghosts to that
+peer (torch.distributed P2P, or libswarm's native loop over RCCL / shared memory), where they
+overwrite the ghosts and activate their local neighbours for the next round.  Between exchanges a
+ghost k hops out misses neighbours and may lag (a lower bound); that error moves at most one hop per
+round, so after j <= k rounds it has not reached an owned agent: owned agents are exact at every
+round, and so are the ghosts adjacent to one.  Per-round owned change counts are summed over ranks
+with one all-reduce every `check_every` rounds; the first globally zero round ends the run and is
+rounds_exec.  Result: the same leaders, rounds and per-round change counts as a single-GPU run on
+the union graph, with a halo exchange every k rounds instead of every round.
 
-Allocation (exact, contract A-H).  Each rank resolves the tasks inside its strip.  Every
-agent that can claim such a task lies within the claim radius Rp of it, so each rank first
-receives the neighbour ranks' agents within Rp of the border (positions, IDs, capabilities),
-runs swarm_allocate over owned + halo agents, and sends the halo agents' won counts back to
-their owners.  No data-path all-gather; one small all-reduce for the global counters.
+Allocation (exact, contract A-H).  Each rank resolves its own tasks.  Every agent that can claim a
+task lies within the claim radius Rp of it, so each rank first receives every peer's agents within
+Rp of its region (positions, IDs, capabilities), runs swarm_allocate over owned + halo agents, and
+sends the halo agents' won counts back to their owners.  No data-path all-gather; one small
+all-reduce for the global counters.
 
 Auction (exact, config C4 on several GPUs).  Tasks are replicated, agents stay partitioned:
 every round, each rank's bidders bid into the task-key array, one MAX all-reduce of the keys
 (+ one bidder-count word per rank) makes them global, and every rank resolves every task the
 same way (owners as agent IDs).  Same rounds, prices and owners as one GPU over all agents.
 
-Exchanges: one per k election rounds, 2 x (k-radius band x 4 B) per neighbour (10k-20k agents
-per radius of border at 10M agents per GPU and N = 2-8) -- latency-bound; the deep halo trades k
-times fewer RCCL round trips for stepping k x 10k-20k ghost rows per border locally.
+Exchanges: one per k election rounds, (agents within k radii of the border) x 4 B per peer (10k-20k
+agents per radius of border at 10M agents per GPU and N = 2-8) -- latency-bound; the deep halo
+trades k times fewer round trips for stepping k x 10k-20k ghost rows per border locally.
 """
 from __future__ import annotations
 
@@ -46,16 +48,147 @@ import torch
 import torch.distributed as dist
 
 
+# ------------------------------------------------------------------------------------------ layouts
+class StripChain:
+    """This rank's horizontal strip [y_lo, y_hi) of a chain of strips, rank k below rank k+1: the peers
+    are rank - 1 (agents within `width` of the lower border) and rank + 1 (of the upper border).  Only
+    the rank's own strip is known (gen.shard_inputs builds every rank's strip on its own), so a halo may
+    reach one strip only: the depth is capped below the strip height."""
+    kind = "strips (chain)"
+
+    def __init__(self, strip, rank: int, world: int):
+        self.strip = (float(strip[0]), float(strip[1]))
+        self.rank, self.world = rank, world
+
+    def depth_cap(self, radius):
+        return max(1, int(math.floor((self.strip[1] - self.strip[0]) / radius)) - 1)
+
+    def targets(self, x, y, width, purpose="elect"):
+        out = {}
+        if self.rank > 0:
+            out[self.rank - 1] = y <= self.strip[0] + width + 1e-9
+        if self.rank < self.world - 1:
+            out[self.rank + 1] = y >= self.strip[1] - width - 1e-9
+        return out
+
+    def min_extent(self):
+        return self.strip[1] - self.strip[0]
+
+
+class Rects:
+    """Every rank's axis-aligned region (world x [x0, x1, y0, y1]; regions may not overlap): rank p needs
+    the agents within `width` (Euclidean) of its rectangle.  Strips cut from one global swarm, Morton
+    blocks (gen.block_rects).  No depth cap: a deep halo reaches as many ranks as it covers."""
+    kind = "rectangles"
+
+    def __init__(self, rects, rank: int):
+        self.rects = np.asarray(rects, np.float64).reshape(-1, 4)
+        self.rank, self.world = rank, len(self.rects)
+
+    def depth_cap(self, radius):
+        return None
+
+    def targets(self, x, y, width, purpose="elect"):
+        out = {}
+        w2 = (width + 1e-9) ** 2
+        for p in range(self.world):
+            if p == self.rank:
+                continue
+            x0, x1, y0, y1 = self.rects[p]
+            dx = np.maximum(np.maximum(x0 - x, x - x1), 0.0)
+            dy = np.maximum(np.maximum(y0 - y, y - y1), 0.0)
+            m = dx * dx + dy * dy <= w2
+            if m.any():
+                out[p] = m
+        return out
+
+    def min_extent(self):
+        r = self.rects
+        return float(min((r[:, 1] - r[:, 0]).min(), (r[:, 3] - r[:, 2]).min()))
+
+
+def _dilate(occ: np.ndarray, k: int) -> np.ndarray:
+    """Boolean grid: cells within Chebyshev distance k of an occupied cell (box sum by integral image)."""
+    if k <= 0:
+        return occ.copy()
+    ny, nx = occ.shape
+    c = np.zeros((ny + 1, nx + 1), np.int64)
+    c[1:, 1:] = np.cumsum(np.cumsum(occ, 0, dtype=np.int64), 1)
+    y0 = np.clip(np.arange(ny) - k, 0, ny)
+    y1 = np.clip(np.arange(ny) + k + 1, 0, ny)
+    x0 = np.clip(np.arange(nx) - k, 0, nx)
+    x1 = np.clip(np.arange(nx) + k + 1, 0, nx)
+    s = c[y1][:, x1] - c[y0][:, x1] - c[y1][:, x0] + c[y0][:, x0]
+    return s > 0
+
+
+class Cells:
+    """Any ownership of the agents (e.g. ID ranges of random or Morton IDs of one global swarm): each
+    rank's occupied cells of a grid of side `cell` over the global square, for its agents ("elect") and
+    for its tasks ("alloc").  Rank p needs an agent iff the agent's cell lies within ceil(width / cell)
+    cells (Chebyshev) of a cell p occupies -- a superset of the agents within `width` of p's agents or
+    tasks, which is all exactness needs."""
+    kind = "cells"
+
+    def __init__(self, x, y, who, rank: int, world: int, cell: float, tx=None, ty=None, twho=None):
+        self.rank, self.world, self.cell = rank, world, float(cell)
+        x, y = np.asarray(x, np.float64), np.asarray(y, np.float64)
+        pts = [x, y] + ([np.asarray(tx, np.float64), np.asarray(ty, np.float64)] if tx is not None else [])
+        self.x0 = min(float(v.min()) for v in pts[0::2] if len(v)) if len(x) else 0.0
+        self.y0 = min(float(v.min()) for v in pts[1::2] if len(v)) if len(x) else 0.0
+        x1 = max(float(v.max()) for v in pts[0::2] if len(v)) if len(x) else 0.0
+        y1 = max(float(v.max()) for v in pts[1::2] if len(v)) if len(x) else 0.0
+        self.shape = (int((y1 - self.y0) // self.cell) + 1, int((x1 - self.x0) // self.cell) + 1)
+        self.occ = {"elect": self._occupancy(x, y, who)}
+        if tx is not None:
+            self.occ["alloc"] = self._occupancy(np.asarray(tx, np.float64), np.asarray(ty, np.float64), twho)
+        self._dil = {}
+
+    def _cells(self, x, y):
+        cy = np.clip(((y - self.y0) // self.cell).astype(np.int64), 0, self.shape[0] - 1)
+        cx = np.clip(((x - self.x0) // self.cell).astype(np.int64), 0, self.shape[1] - 1)
+        return cy, cx
+
+    def _occupancy(self, x, y, who):
+        occ = np.zeros((self.world,) + self.shape, bool)
+        cy, cx = self._cells(x, y)
+        occ[np.asarray(who, np.int64), cy, cx] = True
+        return occ
+
+    def depth_cap(self, radius):
+        return None
+
+    def targets(self, x, y, width, purpose="elect"):
+        occ = self.occ["alloc" if purpose == "alloc" and "alloc" in self.occ else "elect"]
+        k = int(math.ceil(width / self.cell - 1e-12))
+        cy, cx = self._cells(np.asarray(x, np.float64), np.asarray(y, np.float64))
+        out = {}
+        for p in range(self.world):
+            if p == self.rank:
+                continue
+            key = (purpose, p, k)
+            if key not in self._dil:
+                self._dil[key] = _dilate(occ[p], k)
+            m = self._dil[key][cy, cx]
+            if m.any():
+                out[p] = m
+        return out
+
+    def min_extent(self):
+        return math.inf
+
+
 @dataclass
 class Part:
     """One rank's share of a global swarm (partition()): indices into the global arrays."""
     rank: int
     world: int
-    strip: tuple             # (y_lo, y_hi) of this rank's strip
-    cuts: np.ndarray         # the world - 1 interior strip boundaries (the same on every rank)
+    strip: tuple             # (y_lo, y_hi) of this rank's strip (strip layouts), else the agents' y-range
+    cuts: np.ndarray         # the world - 1 interior strip boundaries (strip layouts), else empty
     agents: np.ndarray       # int64 indices of the owned agents, ascending
     tasks: np.ndarray        # int64 indices of the tasks this rank resolves, ascending
     id_range: tuple = None   # by="id": [lo, hi) of the IDs this rank owns
+    layout: object = None    # Rects (strips) or Cells (any other ID map): what ShardedSwarm exchanges by
 
 
 def strip_cuts(y, world: int) -> np.ndarray:
@@ -78,31 +211,39 @@ def id_cuts(ids, world: int) -> np.ndarray:
     return np.partition(ids, ks)[ks].astype(np.int64)
 
 
-def partition(x, y, world: int, rank: int, *, ty=None, min_height: float = 0.0, by: str = "y",
-              ids=None) -> Part:
-    """Split ONE global swarm (every rank passes the same arrays) into `world` horizontal strips
-    of equal agent count; rank `rank` owns the agents of strip `rank` and the tasks whose y falls
-    in it (tasks outside the agents' y-range go to the first / last strip).
+def _strip_rects(x, y, tx, ty, cuts):
+    pts_x = [np.asarray(x, np.float64)] + ([np.asarray(tx, np.float64)] if tx is not None else [])
+    pts_y = [np.asarray(y, np.float64)] + ([np.asarray(ty, np.float64)] if ty is not None else [])
+    big = 1e300
+    ylo = np.concatenate([[-big], cuts])
+    yhi = np.concatenate([cuts, [big]])
+    return np.stack([np.full(len(ylo), -big), np.full(len(ylo), big), ylo, yhi], 1)
 
-    by="id" (north_star / SURVEY §8e: "agents are partitioned by ID range"): rank k owns the
-    k-th of `world` contiguous ID ranges of equal agent count.  The halo machinery is a chain of
-    strips, so the ranges must BE strips -- every agent of range k below every agent of range
-    k + 1 in y (strip-major IDs: gen.strip_ids, gen.shard_inputs).  The strip cuts are then read
-    off the ranges (the lowest y of each range above the first), and the function checks that
-    cutting by those y values assigns every agent to its own ID range (ValueError otherwise:
-    random or Morton IDs give ranges with up to 8 spatial neighbours, not a chain).
 
-    Why the strips reproduce the single-swarm results: every agent is owned by
-    exactly one rank, every RGG edge joins agents of the same or of adjacent strips when strips
-    are taller than the radio radius (ShardedSwarm checks), and ShardedSwarm's deep halo and
-    claim-radius halo give each rank every neighbour / claimant of its owned agents and tasks --
-    so elect() and allocate() equal Swarm.elect() / Swarm.allocate() on the union, whatever the
-    cut positions (tests/test_dist_gloo.py: one global swarm through partition())."""
+def partition(x, y, world: int, rank: int, *, ty=None, tx=None, min_height: float = 0.0, by: str = "y",
+              ids=None, cell: float = 1.0) -> Part:
+    """Split ONE global swarm (every rank passes the same arrays) over `world` ranks; rank `rank`
+    owns part.agents and resolves part.tasks.
+
+    by="y": horizontal strips of equal agent count; a task goes to the strip its y falls in (outside
+    the agents' range: the first / last strip).  Layout Rects.
+    by="id" (north_star / SURVEY §8e: "agents are partitioned by ID range"): rank k owns the k-th of
+    `world` contiguous ID ranges of equal agent count, whatever the ID map.  When the ranges are
+    horizontal strips (strip-major IDs: gen.strip_ids) the layout is those strips (Rects, tasks by
+    strip); otherwise (random IDs, Morton IDs, ...) the layout is Cells and the tasks are dealt in
+    `world` contiguous index ranges.
+
+    Why the union of the shards reproduces the single-swarm results: every agent is owned exactly
+    once, every task resolved exactly once, and ShardedSwarm's deep halo and claim-radius halo give
+    each rank every agent within k hops of its owned agents and every claimant of its tasks -- so
+    elect() and allocate() equal Swarm.elect() / Swarm.allocate() on the union, whatever the cut
+    (tests/test_dist_gloo.py: one global swarm through partition())."""
     if not 0 <= rank < world:
         raise ValueError("rank out of range")
     x = np.asarray(x, np.float64)
     y = np.asarray(y, np.float64)
     id_range = None
+    strips = True
     if by == "y":
         cuts = strip_cuts(y, world)
         who = np.searchsorted(cuts, y, side="right")
@@ -117,9 +258,8 @@ def partition(x, y, world: int, rank: int, *, ty=None, min_height: float = 0.0, 
             raise ValueError(f"ID ranges of equal agent count leave rank(s) {np.nonzero(counts == 0)[0].tolist()} "
                              f"without agents ({len(ids)} agents, world {world}; repeated IDs?)")
         cuts = np.array([y[who == k].min() for k in range(1, world)], np.float64) if world > 1 else np.zeros(0)
-        if not np.array_equal(np.searchsorted(cuts, y, side="right"), who):
-            raise ValueError("the ID ranges are not horizontal strips (every agent of range k must lie below every "
-                             "agent of range k + 1): ID-range sharding needs strip-major IDs (gen.strip_ids)")
+        # strip-major IDs: the ID ranges ARE horizontal strips (every agent of range k below range k+1)
+        strips = bool(np.array_equal(np.searchsorted(cuts, y, side="right"), who))
         edges_id = np.concatenate([[ids.min() if len(ids) else 0], icut, [ids.max() + 1 if len(ids) else 0]])
         id_range = (int(edges_id[rank]), int(edges_id[rank + 1]))
     else:
@@ -127,30 +267,38 @@ def partition(x, y, world: int, rank: int, *, ty=None, min_height: float = 0.0, 
     agents = np.nonzero(who == rank)[0].astype(np.int64)
     lo = float(y.min()) if len(y) else 0.0
     hi = float(y.max()) if len(y) else 0.0
-    edges = np.concatenate([[lo], cuts, [hi]])
-    strip = (float(edges[rank]), float(edges[rank + 1]))
-    if world > 1 and np.diff(edges).min() <= min_height:
-        raise ValueError(f"strips of {world} equal agent counts are not taller than {min_height}: "
-                         "too few agents per rank for this radius")
     tasks = np.zeros(0, np.int64)
-    if ty is not None:
-        tw = np.searchsorted(cuts, np.asarray(ty, np.float64), side="right")
-        tasks = np.nonzero(tw == rank)[0].astype(np.int64)
-    return Part(rank, world, strip, cuts, agents, tasks, id_range)
-
-
-def _neighbors(rank, world):
-    return (rank - 1 if rank > 0 else None), (rank + 1 if rank < world - 1 else None)
+    if strips:
+        edges = np.concatenate([[lo], cuts, [hi]])
+        strip = (float(edges[rank]), float(edges[rank + 1]))
+        if world > 1 and np.diff(edges).min() <= min_height:
+            raise ValueError(f"strips of {world} equal agent counts are not taller than {min_height}: "
+                             "too few agents per rank for this radius")
+        tw = None
+        if ty is not None:
+            tw = np.searchsorted(cuts, np.asarray(ty, np.float64), side="right")
+            tasks = np.nonzero(tw == rank)[0].astype(np.int64)
+        layout = Rects(_strip_rects(x, y, tx, ty, cuts), rank)
+    else:
+        strip, cuts = (lo, hi), np.zeros(0)
+        twho = None
+        if ty is not None:
+            nt = len(ty)
+            twho = (np.arange(nt, dtype=np.int64) * world) // max(nt, 1)
+            tasks = np.nonzero(twho == rank)[0].astype(np.int64)
+        if ty is not None and tx is None:
+            raise ValueError('partition(by="id") with non-strip IDs needs the task x too (tx=) to place the tasks')
+        layout = Cells(x, y, who, rank, world, cell, tx=tx, ty=ty, twho=twho)
+    return Part(rank, world, strip, cuts, agents, tasks, id_range, layout)
 
 
 class Halo:
-    """Neighbour exchange along the strip chain (rank-1 <-> rank <-> rank+1)."""
+    """Point-to-point exchange with any set of peers over a torch.distributed group."""
 
     def __init__(self, group=None, device=None):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
-        self.lo, self.hi = _neighbors(self.rank, self.world)
         self.device = device
         # gloo cannot move device tensors: stage through host memory (tests / 1-GPU rehearsal)
         self.host_staged = dist.get_backend(group) == "gloo"
@@ -158,32 +306,36 @@ class Halo:
     def _peer(self, r):
         return dist.get_global_rank(self.group, r) if self.group is not None else r
 
-    def exchange(self, to_lo, to_hi, n_from_lo, n_from_hi, like):
-        """Send to_lo to rank-1 and to_hi to rank+1; receive n_from_lo / n_from_hi elements."""
-        if self.host_staged and like.is_cuda:
-            a, b = self._exchange(to_lo.cpu(), to_hi.cpu(), n_from_lo, n_from_hi, like.cpu()[:0])
-            return a.to(like.device), b.to(like.device)
-        return self._exchange(to_lo, to_hi, n_from_lo, n_from_hi, like)
-
-    def _exchange(self, to_lo, to_hi, n_from_lo, n_from_hi, like):
-        shape_tail = tuple(like.shape[1:])
-        from_lo = torch.empty((n_from_lo,) + shape_tail, dtype=like.dtype, device=like.device)
-        from_hi = torch.empty((n_from_hi,) + shape_tail, dtype=like.dtype, device=like.device)
+    def exchange_peers(self, sends: dict, recv_counts: dict, like):
+        """Send sends[p] to every peer p and receive recv_counts[p] elements (rows shaped like `like`)
+        from it, in one batch of P2P ops.  Returns {peer: tensor}."""
+        dev = like.device
+        staged = self.host_staged and like.is_cuda
+        tail = tuple(like.shape[1:])
+        tdev = "cpu" if staged else dev
+        out = {p: torch.empty((int(n),) + tail, dtype=like.dtype, device=tdev) for p, n in recv_counts.items()}
         ops = []
-        if self.lo is not None:
-            if to_lo.numel():
-                ops.append(dist.P2POp(dist.isend, to_lo.contiguous(), self._peer(self.lo), self.group))
-            if n_from_lo:
-                ops.append(dist.P2POp(dist.irecv, from_lo, self._peer(self.lo), self.group))
-        if self.hi is not None:
-            if to_hi.numel():
-                ops.append(dist.P2POp(dist.isend, to_hi.contiguous(), self._peer(self.hi), self.group))
-            if n_from_hi:
-                ops.append(dist.P2POp(dist.irecv, from_hi, self._peer(self.hi), self.group))
+        for p in sorted(set(sends) | set(recv_counts)):
+            t = sends.get(p)
+            if t is not None and t.numel():
+                t = t.contiguous().cpu() if staged else t.contiguous()
+                ops.append(dist.P2POp(dist.isend, t, self._peer(p), self.group))
+            if recv_counts.get(p, 0):
+                ops.append(dist.P2POp(dist.irecv, out[p], self._peer(p), self.group))
         if ops:
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
-        return from_lo, from_hi
+        return {p: v.to(dev) for p, v in out.items()} if staged else out
+
+    def count_matrix(self, counts):
+        """counts[p] = what this rank sends to p (world int64): every rank's row, all_gather."""
+        dev = "cpu" if self.host_staged else self.device
+        t = torch.as_tensor(np.asarray(counts, np.int64)).to(dev)
+        if self.world == 1:
+            return t.cpu().numpy().reshape(1, -1)
+        rows = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(rows, t, group=self.group)
+        return torch.stack(rows).cpu().numpy()
 
     def all_reduce_sum(self, arr):
         """Element-wise sum over ranks of a small int64 vector (host array in, host array out)."""
@@ -202,14 +354,6 @@ class Halo:
             else:
                 dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return t
-
-    def exchange_counts(self, n_to_lo, n_to_hi):
-        dev = "cpu" if self.host_staged else self.device
-        t = torch.tensor([n_to_lo], dtype=torch.int64, device=dev)
-        u = torch.tensor([n_to_hi], dtype=torch.int64, device=dev)
-        a, b = self.exchange(t if self.lo is not None else t[:0], u if self.hi is not None else u[:0],
-                             1 if self.lo is not None else 0, 1 if self.hi is not None else 0, t)
-        return (int(a.item()) if a.numel() else 0), (int(b.item()) if b.numel() else 0)
 
 
 @dataclass
@@ -346,14 +490,9 @@ class GpuBackend:
     def elect_sharded(self, comm, sh, max_rounds):
         import ctypes
         L = self.L
-        z = ctypes.c_void_p(0)
-        desc = L.Shard(sh.n_own, sh.all_ids.numel(), L.ptr(sh.row_ptr), L.ptr(sh.col) if sh.col.numel() else z,
-                       L.ptr(sh.all_ids), L.ptr(sh.send_lo_all) if sh.send_lo.numel() else z, sh.send_lo.numel(),
-                       L.ptr(sh.send_hi_all) if sh.send_hi.numel() else z, sh.send_hi.numel(),
-                       0, sh.n_glo, sh.n_glo + sh.n_own, sh.n_ghi,
-                       sh.halo.lo if sh.halo.lo is not None else -1,
-                       sh.halo.hi if sh.halo.hi is not None else -1, sh.halo_depth, sh.own_begin,
-                       L.ptr(sh.c16) if sh.c16 is not None else z)
+        desc = L.shard_desc(sh.n_own, sh.all_ids.numel(), sh.row_ptr, sh.col, sh.all_ids, sh.own_begin,
+                            sh.halo_depth, sh.peers, [sh.send_count[p] for p in sh.peers], sh.send_rows_all,
+                            [sh.ghost_count[p] for p in sh.peers], sh.c16)
         rounds = ctypes.c_int32(0)
         changes = np.zeros(max_rounds, np.int64)
         rc = L.check(L.lib().swarm_elect_sharded(self.ctx, comm, ctypes.byref(desc), L.ptr(sh.leaders[0]),
@@ -432,17 +571,22 @@ class GpuBackend:
 
 
 class ShardedSwarm:
-    """This rank's shard of a strip-partitioned swarm (see module docstring)."""
+    """This rank's shard of a partitioned swarm (see module docstring).
 
-    def __init__(self, ids, x, y, caps, strip, *, radius: float = 1.0, group=None, device=None,
+    region: this rank's strip (y_lo, y_hi) in a chain of strips (StripChain: gen.shard_inputs), or a
+    layout (StripChain / Rects / Cells) that says which of this rank's agents every other rank needs."""
+
+    def __init__(self, ids, x, y, caps, region, *, radius: float = 1.0, group=None, device=None,
                  backend=None, halo=None, halo_depth: int | None = None):
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.backend = backend if backend is not None else GpuBackend(self.device)
         self.halo = halo if halo is not None else Halo(group, self.device)
         self.radius = float(radius)
-        self.strip = (float(strip[0]), float(strip[1]))
-        if self.halo.world > 1 and self.strip[1] - self.strip[0] <= self.radius:
-            raise ValueError("strips must be taller than the radio radius")
+        rank, world = self.halo.rank, self.halo.world
+        self.layout = region if hasattr(region, "targets") else StripChain(region, rank, world)
+        self.strip = getattr(self.layout, "strip", None)
+        if world > 1 and self.layout.min_extent() <= self.radius:
+            raise ValueError("regions must be wider and taller than the radio radius")
         self.halo_depth = self._agree_depth(halo_depth)
         dev = self.device
         pos = torch.stack([torch.as_tensor(np.ascontiguousarray(x), dtype=torch.float64),
@@ -456,43 +600,74 @@ class ShardedSwarm:
         self.pos, self.ids, self.caps = take_rows(pos, perm), ids_t[perm].contiguous(), caps_t[perm].contiguous()
         self.perm = perm
         self.n_own = int(self.ids.numel())
-        # ghosts: neighbour ranks' agents within halo_depth radii of the shared borders
-        self.send_lo, self.send_hi = self._border(self.radius * self.halo_depth)
-        n_lo, n_hi = self.halo.exchange_counts(self.send_lo.numel(), self.send_hi.numel())
-        gp_lo, gp_hi = self.halo.exchange(self.pos[self.send_lo], self.pos[self.send_hi], n_lo, n_hi, self.pos)
-        gi_lo, gi_hi = self.halo.exchange(self.ids[self.send_lo], self.ids[self.send_hi], n_lo, n_hi, self.ids)
-        self.n_glo, self.n_ghi = n_lo, n_hi
-        # ghosts within one radius of the border: exact at every round (the end-of-run check)
-        self.inner_lo = gp_lo[:, 1] >= self.strip[0] - self.radius - 1e-9
-        self.inner_hi = gp_hi[:, 1] <= self.strip[1] + self.radius + 1e-9
-        # shard graph rows: [ghosts from below | owned | ghosts from above] -- each block in its owner's
-        # cell order, so the whole shard is in (near) row-major cell order and its 16-bit columns fit
-        self.own_begin = self.n_glo
-        self.all_pos = torch.cat([gp_lo, self.pos, gp_hi]).contiguous()
-        self.all_ids = torch.cat([gi_lo, self.ids, gi_hi]).contiguous()
-        self.send_lo_all = (self.send_lo + self.own_begin).contiguous()  # owned send rows as shard rows
-        self.send_hi_all = (self.send_hi + self.own_begin).contiguous()
+        hp = self.pos.cpu().numpy()
+        self._hx, self._hy = np.ascontiguousarray(hp[:, 0]), np.ascontiguousarray(hp[:, 1])
+        # ghosts: every peer's agents within halo_depth radii of this rank's region
+        send = self._targets(self.radius * self.halo_depth, "elect")
+        recv = self._recv_counts(send)
+        self.peers = sorted(p for p in set(send) | set(recv) if send.get(p, np.zeros(0)).size or recv.get(p, 0))
+        self.send_rows = {p: send.get(p, np.zeros(0, np.int64)) for p in self.peers}
+        self.send_count = {p: int(self.send_rows[p].size) for p in self.peers}
+        self.ghost_count = {p: int(recv.get(p, 0)) for p in self.peers}
+        self.lower = [p for p in self.peers if p < rank]
+        self.upper = [p for p in self.peers if p > rank]
+        rows_dev = {p: torch.as_tensor(v, device=dev) for p, v in self.send_rows.items()}
+        gp = self.halo.exchange_peers({p: self.pos[r] for p, r in rows_dev.items()}, self.ghost_count, self.pos)
+        gi = self.halo.exchange_peers({p: self.ids[r] for p, r in rows_dev.items()}, self.ghost_count, self.ids)
+        # shard graph rows: [ghosts of the peers below | owned | ghosts of the peers above] -- each block in
+        # its owner's cell order; with strips the whole shard is in (near) row-major cell order and its
+        # 16-bit columns fit
+        self.own_begin = sum(self.ghost_count[p] for p in self.lower)
+        self.all_pos = torch.cat([gp[p] for p in self.lower] + [self.pos] + [gp[p] for p in self.upper]).contiguous()
+        self.all_ids = torch.cat([gi[p] for p in self.lower] + [self.ids] + [gi[p] for p in self.upper]).contiguous()
+        self.send_rows_all = (torch.cat([rows_dev[p] for p in self.peers]) + self.own_begin).contiguous() \
+            if self.peers else torch.zeros(0, dtype=torch.int64, device=dev)
         self.row_ptr, self.col = self.backend.build_graph(self.all_pos, self.radius)
         self.c16 = self.backend.graph_compact(self.row_ptr, self.col) if hasattr(self.backend, "graph_compact") \
             else None
         self.leaders = (torch.empty(self.all_ids.numel(), dtype=torch.int32, device=dev),
                         torch.empty(self.all_ids.numel(), dtype=torch.int32, device=dev))
 
+    # the ghost blocks below / above the owned rows (the strip chain's names)
+    @property
+    def n_glo(self):
+        return self.own_begin
+
+    @property
+    def n_ghi(self):
+        return int(self.all_ids.numel()) - self.own_begin - self.n_own
+
+    def _targets(self, width, purpose):
+        """{peer: ascending storage indices of the owned agents it needs} at halo width `width`."""
+        t = self.layout.targets(self._hx, self._hy, width, purpose) if self.halo.world > 1 else {}
+        return {p: np.nonzero(m)[0].astype(np.int64) for p, m in t.items() if m.any()}
+
+    def _recv_counts(self, send):
+        """What every peer sends this rank, from one all_gather of the send counts."""
+        world, rank = self.halo.world, self.halo.rank
+        if world == 1:
+            return {}
+        row = np.zeros(world, np.int64)
+        for p, v in send.items():
+            row[p] = v.size
+        m = self.halo.count_matrix(row)
+        return {q: int(m[q, rank]) for q in range(world) if q != rank and m[q, rank]}
+
     @classmethod
-    def from_global(cls, ids, x, y, caps=None, *, ty=None, radius: float = 1.0, group=None, device=None,
+    def from_global(cls, ids, x, y, caps=None, *, ty=None, tx=None, radius: float = 1.0, group=None, device=None,
                     backend=None, halo=None, halo_depth: int | None = None, by: str = "y"):
         """This rank's shard of ONE global swarm (every rank passes the same arrays): strips of
-        equal agent count (partition(); by="id": contiguous ID ranges, which must be strips).
+        equal agent count, or (by="id") contiguous ID ranges of any ID map -- partition().
         self.part holds the global indices of the owned agents and of the tasks this rank
         resolves (allocate_global)."""
         if halo is not None:
             rank, world = halo.rank, halo.world
         else:
             rank, world = dist.get_rank(group), dist.get_world_size(group)
-        part = partition(x, y, world, rank, ty=ty, min_height=radius, by=by, ids=ids)
+        part = partition(x, y, world, rank, ty=ty, tx=tx, min_height=radius, by=by, ids=ids, cell=radius)
         a = part.agents
         caps_a = None if caps is None else np.asarray(caps)[a]
-        sh = cls(np.asarray(ids)[a], np.asarray(x)[a], np.asarray(y)[a], caps_a, part.strip, radius=radius,
+        sh = cls(np.asarray(ids)[a], np.asarray(x)[a], np.asarray(y)[a], caps_a, part.layout, radius=radius,
                  group=group, device=device, backend=backend, halo=halo, halo_depth=halo_depth)
         sh.part = part
         return sh
@@ -504,12 +679,12 @@ class ShardedSwarm:
         return self.allocate(np.asarray(tx)[k], np.asarray(ty)[k], np.asarray(treq)[k], **kw)
 
     def _agree_depth(self, want):
-        """Halo depth k, the same on every rank: the requested depth (SWARM_HALO_DEPTH, default 16)
-        capped so that a k-radius band stays inside the neighbour's strip."""
+        """Halo depth k, the same on every rank: the requested depth (SWARM_HALO_DEPTH, default 16),
+        capped (StripChain) so that a k-radius band stays inside the neighbour's strip."""
         import os
         k = int(want if want is not None else os.environ.get("SWARM_HALO_DEPTH", "16"))
-        h = self.strip[1] - self.strip[0]
-        k = max(1, min(k, int(math.floor(h / self.radius)) - 1))
+        cap = self.layout.depth_cap(self.radius)
+        k = max(1, k if cap is None else min(k, cap))
         if self.halo.world > 1:
             t = torch.tensor([-k], dtype=torch.int64)
             if not getattr(self.halo, "host_staged", True):
@@ -517,12 +692,18 @@ class ShardedSwarm:
             k = -int(self.halo.all_reduce_max_(t)[0])
         return k
 
-    def _border(self, width):
-        y = self.pos[:, 1]
-        lo = torch.nonzero(y <= self.strip[0] + width + 1e-9).flatten() if self.halo.lo is not None \
-            else torch.zeros(0, dtype=torch.long, device=self.device)
-        hi = torch.nonzero(y >= self.strip[1] - width - 1e-9).flatten() if self.halo.hi is not None \
-            else torch.zeros(0, dtype=torch.long, device=self.device)
+    def _exchange_leaders(self, cur):
+        """The current leaders of the rows every peer keeps as ghosts, sent; the ghosts' owners' values
+        received: (lower block, upper block) in row order."""
+        sends, off = {}, 0
+        for p in self.peers:
+            n = self.send_count[p]
+            sends[p] = cur[self.send_rows_all[off:off + n]]
+            off += n
+        got = self.halo.exchange_peers(sends, self.ghost_count, cur)
+        empty = cur[:0]
+        lo = torch.cat([got[p] for p in self.lower]) if self.lower else empty
+        hi = torch.cat([got[p] for p in self.upper]) if self.upper else empty
         return lo, hi
 
     # ------------------------------------------------------------------ election
@@ -547,10 +728,9 @@ class ShardedSwarm:
             tend = min(max_rounds, t + check_every - 1)
             for r in range(t, tend + 1):
                 be.step(r, rp, col, lead)
-                if r % self.halo_depth:
+                if r % self.halo_depth or h.world == 1:
                     continue  # ghosts stepped locally between exchanges
-                cur = lead[r & 1]  # state after round r
-                in_lo, in_hi = h.exchange(cur[self.send_lo_all], cur[self.send_hi_all], self.n_glo, self.n_ghi, cur)
+                in_lo, in_hi = self._exchange_leaders(lead[r & 1])  # state after round r
                 be.ghosts(r, g_lo, in_lo, rp, col, lead)
                 be.ghosts(r, g_hi, in_hi, rp, col, lead)
             glob = h.all_reduce_sum(be.changes(t, tend))
@@ -565,15 +745,27 @@ class ShardedSwarm:
         state = torch.where(own == self.ids, 3, 1).to(torch.uint8)
         return ShardElectResult(rounds, np.array(changes[:rounds], np.int64), own, state, found > 0)
 
+    def exact_ghosts(self):
+        """Ghost rows adjacent to an owned row (one hop from the owned agents): their values are exact
+        at every round, so after the run they must equal their owners' final leaders."""
+        if getattr(self, "_exact_ghosts", None) is None:
+            rp = self.row_ptr.cpu().numpy()
+            col = self.col.cpu().numpy()
+            ob, oe = self.own_begin, self.own_begin + self.n_own
+            c = col[int(rp[ob]):int(rp[oe])] if self.n_own else col[:0]
+            m = np.zeros(int(self.all_ids.numel()), bool)
+            m[c[(c < ob) | (c >= oe)]] = True
+            self._exact_ghosts = torch.as_tensor(m)
+        return self._exact_ghosts
+
     def _check_ghosts(self, cur):
-        """Every ghost within one radius of the border must hold its owner's final leader (cheap
-        end-to-end halo check; the deeper ghosts may lag between exchanges by design)."""
-        h = self.halo
-        in_lo, in_hi = h.exchange(cur[self.send_lo_all], cur[self.send_hi_all], self.n_glo, self.n_ghi, cur)
-        g_lo = cur[: self.n_glo]
-        g_hi = cur[self.own_begin + self.n_own:self.own_begin + self.n_own + self.n_ghi]
-        il, ih = self.inner_lo.to(cur.device), self.inner_hi.to(cur.device)
-        if not (torch.equal(in_lo[il], g_lo[il]) and torch.equal(in_hi[ih], g_hi[ih])):
+        """Every ghost adjacent to an owned agent must hold its owner's final leader (cheap end-to-end
+        halo check; the deeper ghosts may lag between exchanges by design)."""
+        in_lo, in_hi = self._exchange_leaders(cur)
+        oe = self.own_begin + self.n_own
+        m = self.exact_ghosts().to(cur.device)
+        if not (torch.equal(in_lo[m[:self.own_begin]], cur[:self.own_begin][m[:self.own_begin]])
+                and torch.equal(in_hi[m[oe:]], cur[oe:][m[oe:]])):
             raise RuntimeError("sharded election: ghost leaders disagree with their owners")
 
     # ------------------------------------------------------------------ auction (C4 sharded)
@@ -624,34 +816,39 @@ class ShardedSwarm:
     # ------------------------------------------------------------------ allocation
     def allocate(self, tx, ty, treq, *, claim_thr: float = 20.0, hysteresis: float = 5.0,
                  u_scale: float = 100.0, mode: str = "auto"):
-        """Resolve this rank's tasks (inside its strip) exactly; returns (AllocResult over the
-        owned tasks, won counts of the owned agents in storage order, global stats)."""
+        """Resolve this rank's tasks exactly; returns (AllocResult over the owned tasks, won counts of
+        the owned agents in storage order, global stats).  The tasks must lie in this rank's region
+        (StripChain / Rects) or be this rank's share of the global tasks (Cells: partition().tasks)."""
         h = self.halo
         rp_claim = (u_scale / claim_thr - 1.0) * (1 + 1e-9) + 1e-12 if claim_thr > 0 and u_scale > 0 else math.inf
         if math.isinf(rp_claim) and h.world > 1:
             raise ValueError("sharded allocation needs a finite claim radius (claim_thr > 0)")
-        if h.world > 1 and self.strip[1] - self.strip[0] <= rp_claim:
+        if h.world > 1 and isinstance(self.layout, StripChain) and self.layout.min_extent() <= rp_claim:
             raise ValueError("strips must be taller than the claim radius")
-        s_lo, s_hi = self._border(rp_claim if h.world > 1 else 0.0)
-        n_lo, n_hi = h.exchange_counts(s_lo.numel(), s_hi.numel())
-        hp = h.exchange(self.pos[s_lo], self.pos[s_hi], n_lo, n_hi, self.pos)
-        hi_ = h.exchange(self.ids[s_lo], self.ids[s_hi], n_lo, n_hi, self.ids)
-        hc = h.exchange(self.caps[s_lo], self.caps[s_hi], n_lo, n_hi, self.caps)
-        ids = torch.cat([self.ids, hi_[0], hi_[1]]).contiguous()
-        pos = torch.cat([self.pos, hp[0], hp[1]]).contiguous()
-        caps = torch.cat([self.caps, hc[0], hc[1]]).contiguous()
+        send = self._targets(rp_claim, "alloc")
+        recv = self._recv_counts(send)
+        peers = sorted(set(send) | set(recv))
+        rows = {p: torch.as_tensor(send[p], device=self.device) for p in send}
+        cnt = {p: int(recv.get(p, 0)) for p in peers}
+        hp = h.exchange_peers({p: self.pos[r] for p, r in rows.items()}, cnt, self.pos)
+        hi_ = h.exchange_peers({p: self.ids[r] for p, r in rows.items()}, cnt, self.ids)
+        hc = h.exchange_peers({p: self.caps[r] for p, r in rows.items()}, cnt, self.caps)
+        ids = torch.cat([self.ids] + [hi_[p] for p in peers]).contiguous()
+        pos = torch.cat([self.pos] + [hp[p] for p in peers]).contiguous()
+        caps = torch.cat([self.caps] + [hc[p] for p in peers]).contiguous()
         res = self.backend.allocate(ids, pos, caps, tx, ty, treq, claim_thr=claim_thr,
                                     hysteresis=hysteresis, u_scale=u_scale, mode=mode)
         won_all = res.won
         # halo agents' wins go back to their owners (reverse of the halo exchange)
-        w_lo = won_all[self.n_own:self.n_own + n_lo]
-        w_hi = won_all[self.n_own + n_lo:]
-        back_lo, back_hi = h.exchange(w_lo, w_hi, s_lo.numel(), s_hi.numel(), won_all)
+        back, off = {}, self.n_own
+        for p in peers:
+            back[p] = won_all[off:off + cnt[p]]
+            off += cnt[p]
+        got = h.exchange_peers(back, {p: int(rows[p].numel()) for p in rows}, won_all)
         won = won_all[: self.n_own].clone()
-        if back_lo.numel():
-            won.index_add_(0, s_lo, back_lo)
-        if back_hi.numel():
-            won.index_add_(0, s_hi, back_hi)
+        for p, v in got.items():
+            if v.numel():
+                won.index_add_(0, rows[p], v)
         keys = ("n_claims", "n_conflicts", "n_flagged", "n_candidates", "n_overflow", "n_resolved")
         st = h.all_reduce_sum([res.stats[k] for k in keys])
         gstats = dict(zip(keys, (int(v) for v in st)))

@@ -91,17 +91,59 @@ def feistel_ids(index: np.ndarray, total: int, seed: int, rounds: int = 4) -> np
     return out.astype(np.int64)
 
 
+def _morton2(bx: np.ndarray, by: np.ndarray) -> np.ndarray:
+    """Interleaved bits of small non-negative integers (x in the even bits)."""
+    code = np.zeros(len(bx), np.int64)
+    for b in range(16):
+        code |= ((np.asarray(bx, np.int64) >> b) & 1) << (2 * b)
+        code |= ((np.asarray(by, np.int64) >> b) & 1) << (2 * b + 1)
+    return code
+
+
+def block_rects(world: int, side: float) -> np.ndarray:
+    """`world` equal rectangles tiling the square [0, side)^2, a gx x gy grid (gx the largest divisor of
+    world <= sqrt(world)), numbered along a Morton curve over the block grid: rank k's block is row k,
+    [x0, x1, y0, y1].  With Morton IDs inside each block (shard_inputs(layout="blocks")), the contiguous
+    ID ranges of equal size ARE these blocks -- SURVEY §8e's C5 partition."""
+    gx = max(d for d in range(1, int(math.isqrt(world)) + 1) if world % d == 0)
+    gy = world // gx
+    bx, by = np.meshgrid(np.arange(gx), np.arange(gy), indexing="xy")
+    bx, by = bx.ravel(), by.ravel()
+    o = np.argsort(_morton2(bx, by), kind="stable")
+    bx, by = bx[o], by[o]
+    w, h = side / gx, side / gy
+    return np.stack([bx * w, (bx + 1) * w, by * h, (by + 1) * h], 1).astype(np.float64)
+
+
 def shard_inputs(n_per: int, seed: int, world: int, rank: int, deg: float = 16.0, t: int = 0,
-                 ids: str = "range"):
+                 ids: str = "range", layout: str = "strips"):
     """Rank `rank`'s part of a world-wide synthetic swarm of n_per*world agents: uniform
-    positions inside the rank's horizontal strip of the global square, tasks inside the strip.
-    ids="range" (north_star: agents partitioned by ID range): rank k owns exactly the contiguous
-    ID range [k n_per, (k+1) n_per), in a seeded random order inside its strip -- the ID range IS
-    the strip.  ids="global": one global seeded bijection (IDs unrelated to ranks)."""
+    positions inside the rank's region of the global square, tasks inside the region.
+    layout="strips": horizontal strips.  ids="range" (north_star: agents partitioned by ID range): rank k
+    owns exactly the contiguous ID range [k n_per, (k+1) n_per), in a seeded random order inside its
+    strip -- the ID range IS the strip.  ids="global": one global seeded bijection (IDs unrelated to ranks).
+    layout="blocks" (SURVEY §8e's C5 shape): rank k's Morton-ordered block (block_rects), IDs
+    k n_per + the Morton rank of the agent inside its block -- Morton IDs whose contiguous ranges are
+    the blocks, each with up to 8 neighbouring ranks."""
     total = n_per * world
     side = side_length(total, deg)
     h = side / world
     sseed = seed * 1000003 + rank
+    if layout == "blocks":
+        rects = block_rects(world, side)
+        x0, x1, y0, y1 = rects[rank]
+        x = x0 + uniform(sseed, TAG_X, n_per) * (x1 - x0)
+        y = y0 + uniform(sseed, TAG_Y, n_per) * (y1 - y0)
+        loc = morton_rank(x - x0, y - y0, max(x1 - x0, y1 - y0))
+        out = dict(n=n_per, total=total, seed=seed, deg=deg, side=side, rects=rects, rect=tuple(rects[rank]),
+                   strip=(y0, y1), x=x, y=y, ids=(loc.astype(np.int64) + np.int64(rank) * n_per).astype(np.int32),
+                   id_range=(rank * n_per, (rank + 1) * n_per), caps=capabilities(n_per, sseed))
+        if t:
+            tx, ty, treq = tasks(t, sseed, side)
+            out["tx"], out["ty"], out["treq"] = x0 + tx / side * (x1 - x0), y0 + ty / side * (y1 - y0), treq
+        return out
+    if layout != "strips":
+        raise ValueError(f"unknown layout {layout!r}")
     x = uniform(sseed, TAG_X, n_per) * side
     y = rank * h + uniform(sseed, TAG_Y, n_per) * h
     if ids == "range":

@@ -331,9 +331,8 @@ class Swarm:
         cells): allocate() then bins by hashed cells, and the index is tried again only after
         the positions change again (self._cindex = False marks 'not indexable' for the position
         tensor and version in self._cindex_bad)."""
-        pos_key = (self.pos.data_ptr(), self.pos._version)
         if self._cindex is False:
-            if getattr(self, "_cindex_bad", None) == pos_key:
+            if self._indexed_pos("_cindex_bad"):
                 return None
             self._cindex = None
         if self._cindex is None:
@@ -344,12 +343,19 @@ class Swarm:
             rc = L.swarm_cell_index(_lib.ctx(), self.n, _lib.ptr(self.pos), self.cell, ctypes.byref(g),
                                     _lib.ptr(off), off.numel(), ctypes.byref(nc), _lib.stream())
             if rc == _lib.ERR_ARG and "not in cell order" in _lib.last_error():
-                self._cindex, self._cindex_bad = False, pos_key
+                self._cindex, self._cindex_bad = False, (self.pos, self.pos._version)
                 return None
             _lib.check(rc)
             self._cindex = (g, off)
-            self._cindex_key = pos_key  # the positions it indexed (allocate trusts it while unchanged)
+            # the positions it indexed: the tensor object itself (held, so its storage cannot be handed to
+            # another tensor) and its version; allocate trusts the index while both are unchanged
+            self._cindex_key = (self.pos, self.pos._version)
         return self._cindex
+
+    def _indexed_pos(self, attr="_cindex_key") -> bool:
+        """self.pos is the very tensor, at the same version, that the key `attr` recorded."""
+        k = getattr(self, attr, None)
+        return k is not None and k[0] is self.pos and k[1] == self.pos._version
 
     def allocate(self, tx, ty, treq, *, winner=None, util=None, claim_thr: float = 20.0,
                  hysteresis: float = 5.0, u_scale: float = 100.0, mode: str = "auto") -> AllocResult:
@@ -381,7 +387,7 @@ class Swarm:
                 # the index is trusted while self.pos is the tensor and version it was built from (the
                 # device staleness check runs otherwise); the claim table is updated in place: keep
                 # the caller's for a stale-index retry
-                trusted = getattr(self, "_cindex_key", None) == (self.pos.data_ptr(), self.pos._version)
+                trusted = self._indexed_pos()
                 flags = (_lib.ALLOC_TRUST_INDEX if trusted else 0) | (_lib.ALLOC_FRESH_CLAIMS if fresh else 0)
                 w0 = None if winner is None or trusted else w.clone()
                 u0 = None if util is None or trusted else u.clone()

@@ -204,38 +204,41 @@ int swarm_frontier_changes(swarm_ctx *ctx, int32_t t0, int32_t t1, int64_t *out,
 
 /*
  * Multi-GPU election: the sharded round loop on the device stream.  Each round:
- * the frontier round over the owned rows, the owned boundary agents' leaders packed and sent
- * to the neighbour shards with RCCL point-to-point calls (ncclSend/ncclRecv in one group), the
- * received ghost leaders applied (swarm_frontier_ghosts semantics); every batch of rounds one
- * ncclAllReduce(sum) of the per-round owned change counts decides convergence.  Same results
- * as swarm_elect(FRONTIER) on the union graph.  RCCL is taken from the process at run time
- * (the instance torch loaded); swarm_comm_available() says whether it was found.
+ * the frontier round over every shard row; after every halo_depth-th round the owned rows each
+ * peer keeps as ghosts are packed and sent to it, and the ghosts are received from it (RCCL
+ * ncclSend/ncclRecv to EVERY peer in one group), and the received ghost leaders applied
+ * (swarm_frontier_ghosts semantics); every batch of rounds one ncclAllReduce(sum) of the
+ * per-round owned change counts decides convergence.  Same results as swarm_elect(FRONTIER) on
+ * the union graph, for any partition of the agents over the ranks (strips: 2 peers; ID ranges of
+ * Morton IDs: a compact region with up to 8; random IDs: every rank).  RCCL is taken from the
+ * process at run time (the instance torch loaded); swarm_comm_available() says whether it was found.
+ * Replaces: the reference's transport stub (agent.py:188-194) -- it has no multi-process path.
  */
 typedef struct swarm_comm swarm_comm;
 
+/* One rank's shard.  Rows: [ghosts of the peers below this rank | owned | ghosts of the peers above]:
+ * the ghosts received from peers[j] are the ghost_count[j] rows that follow those of peers[j-1], the
+ * peers ranked below this rank filling [0, own_begin) and the peers above [own_begin + n_rows, n_all)
+ * (checked).  The ghosts must contain every agent within halo_depth hops of an owned agent, with
+ * every edge among the shard's rows in the CSR (swarm_amd/dist.py: every agent within
+ * halo_depth radio radii of the owner's region).  A peer appears once even if the halo is empty in
+ * one direction; a peer with nothing either way may be left out. */
 typedef struct swarm_shard {
-    int64_t n_rows;          /* owned agents: rows [own_begin, own_begin + n_rows) */
-    int64_t n_all;           /* owned + ghost agents */
-    const int32_t *row_ptr;  /* CSR over all n_all rows (ghost rows list their local neighbours) */
+    int64_t n_rows;               /* owned agents: rows [own_begin, own_begin + n_rows) */
+    int64_t n_all;                /* owned + ghost agents */
+    const int32_t *row_ptr;       /* CSR over all n_all rows (ghost rows list their local neighbours) */
     const int32_t *col;
-    const int32_t *init;     /* initial leaders = IDs of all n_all agents */
-    const int64_t *send_lo;  /* owned agents the lower neighbour keeps as ghosts (device idx) */
-    int64_t n_send_lo;
-    const int64_t *send_hi;  /* owned agents the upper neighbour keeps as ghosts */
-    int64_t n_send_hi;
-    int64_t ghost_lo_begin;  /* ghosts received from the lower neighbour: [begin, begin + n) */
-    int64_t n_ghost_lo;
-    int64_t ghost_hi_begin;  /* ghosts received from the upper neighbour */
-    int64_t n_ghost_hi;
-    int32_t peer_lo;         /* RCCL rank of the lower / upper neighbour, -1 = none */
-    int32_t peer_hi;
-    int32_t halo_depth;      /* k >= 1 (0 = 1): the ghosts are every agent within k radii of the
-                                border; all n_all rows are stepped, the halo is exchanged after
-                                every k-th round only (owned rows stay exact: a wrong value
-                                starts at the halo's outer edge and moves one radius per round) */
-    int64_t own_begin;       /* first owned row (round 3: [ghosts lo | owned | ghosts hi] keeps the shard
-                                graph in spatial order, so its 16-bit columns fit) */
-    const int16_t *col16;    /* swarm_graph_compact of row_ptr / col, or NULL (int32 columns) */
+    const int32_t *init;          /* initial leaders = IDs of all n_all agents */
+    int64_t own_begin;            /* first owned row */
+    int32_t halo_depth;           /* k >= 1 (0 = 1): all n_all rows are stepped, the halo is exchanged
+                                     after every k-th round only (owned rows stay exact: a wrong value
+                                     starts at the halo's outer edge and moves one hop per round) */
+    int32_t n_peers;              /* ranks this shard exchanges with (0 = none) */
+    const int32_t *peers;         /* host [n_peers]: their ranks, ascending, none equal to this rank */
+    const int64_t *send_count;    /* host [n_peers]: owned rows sent to each peer */
+    const int64_t *send_rows;     /* device [sum send_count]: those shard rows, peer after peer */
+    const int64_t *ghost_count;   /* host [n_peers]: ghost rows received from each peer */
+    const int16_t *col16;         /* swarm_graph_compact of row_ptr / col, or NULL (int32 columns) */
 } swarm_shard;
 
 int swarm_comm_available(void);

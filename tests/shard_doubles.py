@@ -155,7 +155,7 @@ class NumpyBackend:
 
 
 class ThreadHalo:
-    """In-process strip chain for shards driven by threads (one per shard)."""
+    """In-process point-to-point hub for shards driven by threads (one per shard)."""
 
     def __init__(self, world):
         self.world = world
@@ -174,47 +174,37 @@ class ThreadHalo:
 
             def __init__(self):
                 self.rank = rank
-                self.lo = rank - 1 if rank > 0 else None
-                self.hi = rank + 1 if rank < hub.world - 1 else None
 
-            def exchange(self, to_lo, to_hi, n_from_lo, n_from_hi, like):
-                if self.lo is not None:
-                    hub.q[(rank, self.lo)].put(to_lo.clone())
-                if self.hi is not None:
-                    hub.q[(rank, self.hi)].put(to_hi.clone())
-                a = hub.q[(self.lo, rank)].get() if self.lo is not None else like[:0].clone()
-                b = hub.q[(self.hi, rank)].get() if self.hi is not None else like[:0].clone()
-                assert a.shape[0] == n_from_lo and b.shape[0] == n_from_hi
-                return a, b
+            def exchange_peers(self, sends, recv_counts, like):
+                for p, t in sends.items():
+                    if t.numel():  # an empty message is never sent (the receiver expects 0 rows)
+                        hub.q[(rank, p)].put(t.clone())
+                out = {}
+                for p, n in recv_counts.items():
+                    got = hub.q[(p, rank)].get() if n else like[:0].clone()
+                    assert got.shape[0] == n
+                    out[p] = got
+                return out
 
-            def exchange_counts(self, n_to_lo, n_to_hi):
-                t = torch.tensor([n_to_lo]), torch.tensor([n_to_hi])
-                a, b = self.exchange(t[0], t[1], 1 if self.lo is not None else 0, 1 if self.hi is not None else 0, t[0])
-                return (int(a[0]) if a.numel() else 0), (int(b[0]) if b.numel() else 0)
+            def _gather(self, key, arr):
+                with hub.lock:
+                    hub.sums.setdefault(key, {})[rank] = arr
+                hub.barrier.wait()
+                vals = [hub.sums[key][r] for r in range(hub.world)]
+                hub.barrier.wait()
+                with hub.lock:
+                    hub.sums.pop(key, None)
+                hub.barrier.wait()
+                return vals
+
+            def count_matrix(self, counts):
+                return np.stack(self._gather("counts", np.asarray(counts, np.int64)))
 
             def all_reduce_max_(self, t):
-                with hub.lock:
-                    hub.sums.setdefault("max", []).append(t.clone())
-                hub.barrier.wait()
-                t.copy_(torch.stack(hub.sums["max"]).max(0).values)
-                hub.barrier.wait()
-                with hub.lock:
-                    hub.sums.pop("max", None)
-                hub.barrier.wait()
+                t.copy_(torch.stack(self._gather("max", t.clone())).max(0).values)
                 return t
 
             def all_reduce_sum(self, arr):
-                arr = np.asarray(arr)
-                key = id(hub)
-                with hub.lock:
-                    hub.sums.setdefault("acc", []).append(arr)
-                hub.barrier.wait()
-                total = np.sum(hub.sums["acc"], axis=0)
-                hub.barrier.wait()
-                with hub.lock:
-                    hub.sums.pop("acc", None)
-                hub.barrier.wait()
-                del key
-                return total
+                return np.sum(self._gather("acc", np.asarray(arr)), axis=0)
 
         return Member()

@@ -181,7 +181,7 @@ def test_trusted_index_and_fresh_claims_flags(mods, oracle_mod):
     d = gen.swarm_inputs(60_000, 31, t=3_000)
     s = swm.Swarm(d["ids"], d["x"], d["y"], d["caps"], device="cuda")
     a0 = s.allocate(d["tx"], d["ty"], d["treq"])  # builds the index
-    assert s._cindex_key == (s.pos.data_ptr(), s.pos._version)
+    assert s._indexed_pos() and s._cindex_key[0] is s.pos
     g, off = s._cindex
     L = _lib.lib()
     t = len(d["tx"])
@@ -214,8 +214,32 @@ def test_trusted_index_and_fresh_claims_flags(mods, oracle_mod):
     # an in-place write moves the version: the next call checks on the device and rebins
     i = int(torch.argmax(s.pos[:, 1]))
     s.pos[i, 1] += 50.0
-    assert s._cindex_key != (s.pos.data_ptr(), s.pos._version)
+    assert not s._indexed_pos()
     b = s.allocate(d["tx"], d["ty"], d["treq"])
     want = _oracle_now(oracle_mod, s, d["tx"], d["ty"], d["treq"])
     np.testing.assert_array_equal(b.winner.cpu().numpy(), want["winner"])
     np.testing.assert_array_equal(b.won.cpu().numpy(), want["won"])
+
+
+def test_reassigned_positions_are_not_trusted(mods, oracle_mod):
+    """a NEW position tensor of the same shape (possibly at a recycled address, version 0) must
+    not inherit the trust of the index built for the old one: the allocation checks on the device and
+    gives the oracle's result for the new positions."""
+    swm, _lib, gen = mods
+    d = gen.swarm_inputs(40_000, 37, t=2_000)
+    s = swm.Swarm(d["ids"], d["x"], d["y"], d["caps"], device="cuda")
+    s.allocate(d["tx"], d["ty"], d["treq"])  # builds and trusts the index
+    assert s._indexed_pos()
+    new = s.pos.clone()
+    i = int(torch.argmax(new[:, 1]))
+    new[i, 1] += 60.0  # one agent leaves its cell: the old index is wrong for these positions
+    del_ptr = s.pos.data_ptr()
+    s.pos = new
+    assert not s._indexed_pos()
+    b = s.allocate(d["tx"], d["ty"], d["treq"])
+    want = _oracle_now(oracle_mod, s, d["tx"], d["ty"], d["treq"])
+    np.testing.assert_array_equal(b.winner.cpu().numpy(), want["winner"])
+    np.testing.assert_array_equal(b.won.cpu().numpy(), want["won"])
+    # the same holds when the new tensor reuses the old storage address
+    s.pos = s.pos.clone()
+    assert not s._indexed_pos() and del_ptr is not None

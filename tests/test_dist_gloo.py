@@ -24,7 +24,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_q, n_per, deg, check_every, halo_depth):
+def _worker(rank, world, port, out_q, n_per, deg, check_every, halo_depth, layout="strips"):
     import sys
     for p in (PKG, ROOT, os.path.join(ROOT, "tests")):
         sys.path.insert(0, p)
@@ -33,9 +33,10 @@ def _worker(rank, world, port, out_q, n_per, deg, check_every, halo_depth):
     try:
         from shard_doubles import NumpyBackend
         from swarm_amd import gen
-        from swarm_amd.dist import ShardedSwarm
-        d = gen.shard_inputs(n_per, SEED, world, rank, deg=deg, t=T_PER)
-        sh = ShardedSwarm(d["ids"], d["x"], d["y"], d["caps"], d["strip"], device="cpu", backend=NumpyBackend(),
+        from swarm_amd.dist import Rects, ShardedSwarm
+        d = gen.shard_inputs(n_per, SEED, world, rank, deg=deg, t=T_PER, layout=layout)
+        region = Rects(d["rects"], rank) if layout == "blocks" else d["strip"]
+        sh = ShardedSwarm(d["ids"], d["x"], d["y"], d["caps"], region, device="cpu", backend=NumpyBackend(),
                           halo_depth=halo_depth)
         r = sh.elect(check_every=check_every)
         sh._check_ghosts(sh.leaders[r.rounds_exec & 1])
@@ -45,16 +46,16 @@ def _worker(rank, world, port, out_q, n_per, deg, check_every, halo_depth):
                        leader=r.leader.numpy(), state=r.state.numpy(), winner=res.winner.numpy(),
                        util=res.util.numpy(), won=won.numpy(), gstats=gst,
                        winner0=res0.winner.numpy(), won0=won0.numpy(),
-                       n_ghost=(sh.n_glo, sh.n_ghi), depth=sh.halo_depth))
+                       n_ghost=(sh.n_glo, sh.n_ghi), depth=sh.halo_depth, peers=list(sh.peers)))
     finally:
         dist.destroy_process_group()
 
 
-def _run(world, n_per=N_PER, deg=16.0, check_every=7, halo_depth=1):
+def _run(world, n_per=N_PER, deg=16.0, check_every=7, halo_depth=1, layout="strips"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, n_per, deg, check_every, halo_depth))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, n_per, deg, check_every, halo_depth, layout))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -65,19 +66,21 @@ def _run(world, n_per=N_PER, deg=16.0, check_every=7, halo_depth=1):
     return sorted(outs, key=lambda o: o["rank"])
 
 
-def _union(world, n_per=N_PER, deg=16.0):
+def _union(world, n_per=N_PER, deg=16.0, layout="strips"):
     from swarm_amd import gen
-    ds = [gen.shard_inputs(n_per, SEED, world, r, deg=deg, t=T_PER) for r in range(world)]
+    ds = [gen.shard_inputs(n_per, SEED, world, r, deg=deg, t=T_PER, layout=layout) for r in range(world)]
     cat = lambda k: np.concatenate([d[k] for d in ds])  # noqa: E731
     return ds, cat
 
 
-@pytest.mark.parametrize("world,depth", [(2, 1), (2, 4), (3, 16)])
-def test_sharded_election_and_allocation_match_single_graph(world, depth, oracle_mod):
-    """depth: halo depth k (ghosts k radii deep, exchanged every k rounds); 16 is capped by the
-    strip height (the same cap on every rank)."""
-    outs = _run(world, halo_depth=depth)
-    ds, cat = _union(world)
+@pytest.mark.parametrize("world,depth,layout", [(2, 1, "strips"), (2, 4, "strips"), (3, 16, "strips"),
+                                                (2, 4, "blocks"), (3, 3, "blocks"), (4, 6, "blocks")])
+def test_sharded_election_and_allocation_match_single_graph(world, depth, layout, oracle_mod):
+    """depth: halo depth k (ghosts k radii deep, exchanged every k rounds); with strips 16 is capped by
+    the strip height (the same cap on every rank).  layout "blocks": Morton-ordered blocks with Morton
+    IDs (SURVEY §8e's C5 partition) -- up to 8 peers per rank, halos deeper than a block reach further."""
+    outs = _run(world, halo_depth=depth, layout=layout)
+    ds, cat = _union(world, layout=layout)
     x, y, ids, caps = cat("x"), cat("y"), cat("ids"), cat("caps")
     rp, col = oracle_mod.rgg_csr(x, y, 1.0)
     lead, state, rounds, changes = oracle_mod.elect(rp, col, ids)
@@ -90,6 +93,10 @@ def test_sharded_election_and_allocation_match_single_graph(world, depth, oracle
         assert ((o["state"] == 3) == (o["leader"] == o["ids"])).all()
         assert sum(o["n_ghost"]) > 0
         assert o["depth"] == outs[0]["depth"] and 1 <= o["depth"] <= depth
+        if layout == "blocks":
+            assert o["depth"] == depth  # no cap: the peer set grows instead
+    if layout == "blocks" and world == 4:
+        assert all(len(o["peers"]) == 3 for o in outs)  # a 2 x 2 grid: every block touches the other three
     assert sum(len(o["ids"]) for o in outs) == len(ids)
     # allocation: every rank resolves its own tasks; the union resolver must agree
     wa = oracle_mod.allocate(ids, x, y, caps, cat("tx"), cat("ty"), cat("treq"))
@@ -141,8 +148,15 @@ def test_partition_by_id_range_is_the_strip_partition(world):
         covered.append((lo, hi))
     assert covered[0][0] == 0 and covered[-1][1] == 6_000
     assert all(covered[k][1] == covered[k + 1][0] for k in range(world - 1))
-    with pytest.raises(ValueError, match="not horizontal strips"):
-        partition(d["x"], d["y"], world, 0, by="id", ids=d["ids"])  # random IDs
+    assert type(pi.layout).__name__ == "Rects"
+    # any other ID map: the ranges are not strips -> the cell layout, tasks dealt by index ranges
+    parts = [partition(d["x"], d["y"], world, r, tx=d["tx"], ty=d["ty"], by="id", ids=d["ids"]) for r in range(world)]
+    assert all(type(q.layout).__name__ == "Cells" for q in parts)
+    assert np.array_equal(np.sort(np.concatenate([q.agents for q in parts])), np.arange(6_000))
+    assert np.array_equal(np.sort(np.concatenate([q.tasks for q in parts])), np.arange(300))
+    for q in parts:
+        lo, hi = q.id_range
+        assert np.array_equal(np.sort(d["ids"][q.agents]), np.arange(lo, hi))
 
 
 # ----------------------------------------------------------------------------- sharded auction
@@ -203,15 +217,15 @@ def test_sharded_auction_matches_single_auction(world, check_every, oracle_mod):
 G_N, G_T = 4000, 150
 
 
-def _global_inputs(world, by):
+def _global_inputs(world, by, ids="strip"):
     from swarm_amd import gen
-    d = gen.swarm_inputs(G_N, SEED + 3, t=G_T)  # the same global arrays on every rank
-    if by == "id":
+    d = gen.swarm_inputs(G_N, SEED + 3, t=G_T, ids="morton" if ids == "morton" else "random")
+    if by == "id" and ids == "strip":
         d["ids"] = gen.strip_ids(d["y"], world, SEED + 3)
     return d
 
 
-def _global_worker(rank, world, port, out_q, depth, by="y"):
+def _global_worker(rank, world, port, out_q, depth, by="y", ids="strip"):
     import sys
     for p in (PKG, ROOT, os.path.join(ROOT, "tests")):
         sys.path.insert(0, p)
@@ -221,8 +235,8 @@ def _global_worker(rank, world, port, out_q, depth, by="y"):
         from shard_doubles import NumpyBackend
         from swarm_amd import gen
         from swarm_amd.dist import ShardedSwarm
-        d = _global_inputs(world, by)
-        sh = ShardedSwarm.from_global(d["ids"], d["x"], d["y"], d["caps"], ty=d["ty"], device="cpu",
+        d = _global_inputs(world, by, ids)
+        sh = ShardedSwarm.from_global(d["ids"], d["x"], d["y"], d["caps"], tx=d["tx"], ty=d["ty"], device="cpu",
                                       backend=NumpyBackend(), halo_depth=depth, by=by)
         r = sh.elect(check_every=5)
         res, won, gst = sh.allocate_global(d["tx"], d["ty"], d["treq"])
@@ -234,24 +248,28 @@ def _global_worker(rank, world, port, out_q, depth, by="y"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,depth,by", [(2, 4, "y"), (3, 16, "y"), (2, 4, "id"), (3, 16, "id")])
-def test_partitioned_global_swarm_matches_single_swarm(world, depth, by, oracle_mod):
-    """ShardedSwarm.from_global: one global input (tasks anywhere) cut into strips of equal agent
-    count on every rank -- by y with random IDs, or by contiguous ID range with strip-major IDs
-    (north_star's ID-range partition); the union of the shards' results equals the single-swarm
-    oracle (leaders, rounds, per-round changes, winners, claim values, conflicts, won counts)."""
+@pytest.mark.parametrize("world,depth,by,ids", [(2, 4, "y", "strip"), (3, 16, "y", "strip"), (2, 4, "id", "strip"),
+                                               (3, 16, "id", "strip"), (2, 3, "id", "morton"), (3, 5, "id", "morton"),
+                                               (4, 4, "id", "morton"), (2, 2, "id", "random"),
+                                               (3, 1, "id", "random"), (4, 3, "id", "random")])
+def test_partitioned_global_swarm_matches_single_swarm(world, depth, by, ids, oracle_mod):
+    """ShardedSwarm.from_global: one global input (tasks anywhere) cut on every rank -- by y into strips
+    with random IDs, or by contiguous ID range (north_star's ID-range partition) of strip-major IDs
+    (strips), of Morton IDs (compact regions with several neighbouring ranks) or of random IDs (every
+    rank a peer of every other); the union of the shards' results equals the single-swarm oracle
+    (leaders, rounds, per-round changes, winners, claim values, conflicts, won counts)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_global_worker, args=(r, world, port, q, depth, by)) for r in range(world)]
+    procs = [ctx.Process(target=_global_worker, args=(r, world, port, q, depth, by, ids)) for r in range(world)]
     for p in procs:
         p.start()
     outs = sorted([q.get(timeout=240) for _ in range(world)], key=lambda o: o["rank"])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    d = _global_inputs(world, by)
-    # every agent and every task owned exactly once, strips of near-equal size
+    d = _global_inputs(world, by, ids)
+    # every agent and every task owned exactly once, parts of near-equal size
     agents = np.concatenate([o["agents"] for o in outs])
     assert np.array_equal(np.sort(agents), np.arange(G_N))
     assert max(len(o["agents"]) for o in outs) - min(len(o["agents"]) for o in outs) <= 2

@@ -36,15 +36,20 @@ def _inputs(kind, world):
     from swarm_amd import gen
     if kind == "shards":  # weak-scaling inputs: rank k's strip holds the ID range [k n, (k+1) n)
         return [gen.shard_inputs(6_000, 41, world, r, t=120) for r in range(world)]
-    d = gen.swarm_inputs(12_000, 43, t=300)  # one global swarm, cut by ID range (strip-major IDs)
-    d["ids"] = gen.strip_ids(d["y"], world, 43)
+    if kind == "blocks":  # C5's shape: Morton blocks, Morton IDs, rank k's block = the ID range [k n, (k+1) n)
+        return [gen.shard_inputs(6_000, 47, world, r, t=120, layout="blocks") for r in range(world)]
+    # one global swarm, cut by ID range: strip-major IDs (strips), Morton IDs or random IDs (cells)
+    ids = {"global": "random", "global-morton": "morton", "global-random": "random"}[kind]
+    d = gen.swarm_inputs(12_000, 43, t=300, ids=ids)
+    if kind == "global":
+        d["ids"] = gen.strip_ids(d["y"], world, 43)
     return d
 
 
 def _auction_tasks(kind, world):
     """The task list every rank passes to the sharded auction (tasks are replicated): all of them."""
     d = _inputs(kind, world)
-    if kind == "shards":
+    if kind in ("shards", "blocks"):
         return tuple(np.concatenate([e[k] for e in d]) for k in ("tx", "ty", "treq"))
     return d["tx"], d["ty"], d["treq"]
 
@@ -62,16 +67,17 @@ def _worker(rank, world, port, out_q, kind, depth, transport):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
-        from swarm_amd.dist import GpuBackend, ShardedSwarm
+        from swarm_amd.dist import GpuBackend, Rects, ShardedSwarm
         dev = torch.device("cuda", 0)
-        if kind == "shards":
+        if kind in ("shards", "blocks"):
             d = _inputs(kind, world)[rank]
-            sh = ShardedSwarm(d["ids"], d["x"], d["y"], d["caps"], d["strip"], device=dev, halo_depth=depth)
+            region = Rects(d["rects"], rank) if kind == "blocks" else d["strip"]
+            sh = ShardedSwarm(d["ids"], d["x"], d["y"], d["caps"], region, device=dev, halo_depth=depth)
             tx, ty, tq = d["tx"], d["ty"], d["treq"]
             tasks = None
         else:
             d = _inputs(kind, world)
-            sh = ShardedSwarm.from_global(d["ids"], d["x"], d["y"], d["caps"], ty=d["ty"], device=dev,
+            sh = ShardedSwarm.from_global(d["ids"], d["x"], d["y"], d["caps"], tx=d["tx"], ty=d["ty"], device=dev,
                                           halo_depth=depth, by="id")
             k = sh.part.tasks
             tx, ty, tq = d["tx"][k], d["ty"][k], d["treq"][k]
@@ -92,7 +98,7 @@ def _worker(rank, world, port, out_q, kind, depth, transport):
                        leader=r.leader.cpu().numpy(), state=r.state.cpu().numpy(), winner=res.winner.cpu().numpy(),
                        util=res.util.cpu().numpy(), nmsg=res.nmsg.cpu().numpy(), won=won.cpu().numpy(),
                        gstats=gst, tasks=tasks, converged=r.converged, ghosts=sh.n_glo + sh.n_ghi, native=native,
-                       auc=auc))
+                       auc=auc, peers=list(sh.peers)))
     finally:
         dist.destroy_process_group()
 
@@ -101,7 +107,11 @@ def _worker(rank, world, port, out_q, kind, depth, transport):
                                                          (3, "global", 16, "python"), (2, "shards", 16, "shm"),
                                                          (2, "global", 1, "shm"), (3, "global", 16, "shm"),
                                                          (3, "shards", 4, "shm"), (2, "global", 16, "shm-agent"),
-                                                         (3, "shards", 1, "shm-agent")])
+                                                         (3, "shards", 1, "shm-agent"), (4, "blocks", 16, "shm"),
+                                                         (3, "blocks", 5, "shm"), (2, "blocks", 8, "python"),
+                                                         (3, "global-morton", 6, "shm"), (4, "global-morton", 16, "shm"),
+                                                         (2, "global-random", 2, "shm"), (4, "global-random", 3, "shm"),
+                                                         (3, "global-random", 2, "python")])
 def test_hip_sharded_processes_match_union_oracle(world, kind, depth, transport, oracle_mod):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -118,7 +128,7 @@ def test_hip_sharded_processes_match_union_oracle(world, kind, depth, transport,
                 p.kill()
     assert all(p.exitcode == 0 for p in procs)
     d = _inputs(kind, world)
-    if kind == "shards":
+    if kind in ("shards", "blocks"):
         cat = lambda k: np.concatenate([e[k] for e in d])  # noqa: E731
         ids, x, y, caps, tx, ty, tq = (cat(k) for k in ("ids", "x", "y", "caps", "tx", "ty", "treq"))
     else:
@@ -134,8 +144,10 @@ def test_hip_sharded_processes_match_union_oracle(world, kind, depth, transport,
         assert ((o["state"] == 3) == (o["leader"] == o["ids"])).all()
     assert sum(len(o["ids"]) for o in outs) == len(ids)
     wa = oracle_mod.allocate(ids, x, y, caps, tx, ty, tq)
+    if kind in ("blocks", "global-random"):
+        assert all(len(o["peers"]) >= min(world - 1, 2) for o in outs)  # multi-peer halos
     for key in ("winner", "util", "nmsg"):
-        if kind == "shards":
+        if kind in ("shards", "blocks"):
             got = np.concatenate([o[key] for o in outs])
         else:
             got = np.empty_like(wa[key])

@@ -385,8 +385,7 @@ def test_native_sharded_loop_single_rank_rccl(sw, oracle_mod):
         n = s.n
         l0 = torch.empty(n, dtype=torch.int32, device="cuda")
         l1 = torch.empty(n, dtype=torch.int32, device="cuda")
-        z = ctypes.c_void_p(0)
-        desc = L.Shard(n, n, L.ptr(s.row_ptr), L.ptr(s.col), L.ptr(s.ids), z, 0, z, 0, n, 0, n, 0, -1, -1)
+        desc = L.shard_desc(n, n, s.row_ptr, s.col, s.ids, 0, 1)
         rounds = ctypes.c_int32(0)
         ch = np.zeros(1 << 12, np.int64)
         L.check(L.lib().swarm_elect_sharded(L.ctx(), comm, ctypes.byref(desc), L.ptr(l0), L.ptr(l1), len(ch),

@@ -27,8 +27,7 @@ comm = ctypes.c_void_p()
 L.check(L.lib().swarm_comm_create(ctypes.byref(comm), 1, 0, ctypes.cast(uid, ctypes.c_void_p)))
 l0 = torch.empty(n, dtype=torch.int32, device="cuda")
 l1 = torch.empty(n, dtype=torch.int32, device="cuda")
-z = ctypes.c_void_p(0)
-desc = L.Shard(n, n, L.ptr(s.row_ptr), L.ptr(s.col), L.ptr(s.ids), z, 0, z, 0, n, 0, n, 0, -1, -1)
+desc = L.shard_desc(n, n, s.row_ptr, s.col, s.ids, 0, 1)
 rounds = ctypes.c_int32(0)
 ch = np.zeros(1 << 16, np.int64)
 ts = []
