@@ -46,12 +46,25 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--rows", type=int, default=1,
                     help="0 to skip the other SURVEY §8 rows (C2, C4 auction, physics, protocol, codec)")
+    ap.add_argument("--partition", choices=["strips", "blocks"], default="strips",
+                    help="N > 1: strips (strip-major IDs: 2 peers per rank, 16-bit columns) or blocks "
+                         "(SURVEY §8e's Morton IDs: Morton-ordered blocks, up to 8 peers per rank)")
+    ap.add_argument("--union-gpu", type=int, default=1,
+                    help="with --oracle-check: also elect the union swarm on rank 0's GPU (the model's N = 1 time)")
+    ap.add_argument("--model", type=int, default=1,
+                    help="N > 1: the election cost model (DESIGN §6) from this run's per-rank round counts and a "
+                         "calibration election of rank 0's shard alone")
+    ap.add_argument("--oracle-check", type=int, default=None,
+                    help="N > 1: compare every rank's leaders, rounds and per-round global changes with the C "
+                         "oracle (orc_elect_frontier) over the union swarm on rank 0's host (default: on for C5)")
     a = ap.parse_args()
     a.world_hint = int(os.environ.get("WORLD_SIZE", "1"))
     if a.agents is None:
         a.agents = 100_000_000 // a.world_hint if a.config == "C5" else 10_000_000
     if a.config == "C5":
         a.rows = 0  # the other §8 rows keep their own (C2 / C3-sized) workloads: not re-run at C5
+    if a.oracle_check is None:
+        a.oracle_check = 1 if a.config == "C5" else 0
     return a
 
 
@@ -190,6 +203,17 @@ def main():
         splits.append((ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])))
     t_elect_ms = float(np.median([x[0] for x in splits]))
     t_alloc_ms = float(np.median([x[1] for x in splits]))
+    # the allocation's cell index (swarm_cell_index over the spatial storage order): built once per
+    # position set, before the timed region -- the positions are static over the bench's steps
+    idx_ms = []
+    for _ in range(3):
+        sw._cindex, sw._again = None, None
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        sw._cell_index()
+        torch.cuda.synchronize()
+        idx_ms.append((time.perf_counter() - t1) * 1e3)
+    sw.allocate(tpos_x, tpos_y, treq)  # trusted again (the index above is the current one)
 
     # ---- per-kernel device time of the election (HIP events recorded by libswarm around every
     # launch on the stream it launches on), one instrumented replay.  The dominant kernel is the
@@ -251,8 +275,11 @@ def main():
                        % (args.config, n, args.deg, args.tasks),
                        "agents_per_gpu": n, "edges_per_gpu": e, "tasks": args.tasks,
                        "elect_mode": args.elect_mode, "alloc_mode": a.stats.get("mode_used"),
-                       "rounds_exec": r.rounds_exec, "parallelism": f"agents sharded x{world}"},
+                       "rounds_exec": r.rounds_exec, "parallelism": f"agents sharded x{world}",
+                       "alloc_index": "the cell index of the static positions is built once, outside the timed "
+                                      "steps (alloc_index_build_ms); a step that moves agents rebuilds it"},
             "breakdown_ms": {"elect": t_elect_ms, "alloc": t_alloc_ms},
+            "alloc_index_build_ms": float(np.median(idx_ms)),
             # the step's algorithmic bytes (the frontier's per-round counters, DESIGN §4, + the
             # allocation's compulsory 24 B/agent + 36 B/task) over its time
             "hbm_frac_step": (r.bytes_total + 24 * n + 36 * args.tasks)
@@ -577,15 +604,17 @@ def sharded(args, rank, world, dev):
     from swarm_amd import gen
     from swarm_amd.dist import ShardedSwarm
 
+    from swarm_amd.dist import Rects
     t0 = time.time()
-    d = gen.shard_inputs(args.agents, args.seed, world, rank, deg=args.deg, t=args.tasks)
-    sh = ShardedSwarm(d["ids"], d["x"], d["y"], d["caps"], d["strip"], device=dev)
+    d = gen.shard_inputs(args.agents, args.seed, world, rank, deg=args.deg, t=args.tasks, layout=args.partition)
+    region = Rects(d["rects"], rank) if args.partition == "blocks" else d["strip"]
+    sh = ShardedSwarm(d["ids"], d["x"], d["y"], d["caps"], region, device=dev)
     tx = torch.as_tensor(d["tx"], device=dev)
     ty = torch.as_tensor(d["ty"], device=dev)
     tq = torch.as_tensor(d["treq"], device=dev)
     torch.cuda.synchronize()
     log(f"[rank {rank}] setup {time.time() - t0:.1f}s: own={sh.n_own} ghosts={sh.n_glo + sh.n_ghi} "
-        f"E_local={sh.col.numel()}")
+        f"peers={sh.peers} E_local={sh.col.numel()} col16={sh.c16 is not None}")
 
     def step():
         r = sh.elect(check_every=128)
@@ -612,13 +641,17 @@ def sharded(args, rank, world, dev):
     elapsed = float(t[0])
     total_agents = args.agents * world
     check = sharded_state_check(sh, r)
+    if args.oracle_check:
+        check["union_oracle"] = union_oracle_check(args, sh, r, rank, world)
     # dominant kernel on every rank: k_sparse_block timed with HIP events over one instrumented
     # election of this rank's shard graph (owned + ghost rows) -- the kernel the sharded loop
     # launches every round, on the same graph; rank 0 reports its own, and the spread over ranks
     dom = shard_roofline(sh, dev)
     fr = torch.tensor([dom["frac"], -dom["frac"]], dtype=torch.float64, device=cdev)
     dist.all_reduce(fr, op=dist.ReduceOp.MAX)
+    model = sharded_model(args, sh, rank, world, check) if args.model and getattr(sh, "_native", None) else None
     path = _shard_path(sh)
+    staged = dist.get_backend() != "nccl"
     if rank == 0:
         out = {
             "metric": "agent-rounds/sec (election+allocation) at 10M agents; % of HBM roofline",
@@ -632,20 +665,31 @@ def sharded(args, rank, world, dev):
             "scaling": "strong" if args.config == "C5" else "weak",
             "vs_baseline": None,
             "dtype": "int32+f64",
-            "data": "synthetic (seeded RGG strips, SplitMix64; rank k owns the contiguous ID range "
-                    "[k n, (k+1) n), random order inside its strip)",
+            "data": ("synthetic (seeded RGG, SplitMix64; rank k owns the contiguous ID range [k n, (k+1) n): "
+                     + ("its horizontal strip, random order inside it)" if args.partition == "strips" else
+                        "its Morton-ordered block, Morton order inside it)")),
             "config": {"workload": ("C5: %d agents sharded by ID range over %d GPUs (%d per GPU)"
                                     % (total_agents, world, args.agents) if args.config == "C5" else
                                     "C3 per GPU x %d GPUs (weak scaling): %d agents/GPU" % (world, args.agents))
                        + ", deg %g, election to convergence + %d tasks/GPU allocation" % (args.deg, args.tasks),
                        "agents_total": total_agents, "tasks_total": args.tasks * world,
-                       "partition": "contiguous ID ranges = horizontal strips (gen.shard_inputs ids='range')",
+                       "partition": ("contiguous ID ranges = horizontal strips (gen.shard_inputs ids='range': strip-major "
+                                     "IDs, not a global random permutation)" if args.partition == "strips" else
+                                     "contiguous ID ranges of Morton IDs = Morton-ordered blocks "
+                                     "(gen.shard_inputs layout='blocks')"),
+                       "peers_rank0": list(sh.peers), "ghosts_rank0": int(sh.n_glo + sh.n_ghi),
+                       "columns_rank0": "int16 deltas" if sh.c16 is not None else "int32",
                        "rounds_exec": r.rounds_exec,
                        "halo_depth": sh.halo_depth,
                        "parallelism": f"strip-sharded x{world}: {path}; halo exchanged every {sh.halo_depth} "
                                       "rounds (ghosts that deep, stepped locally)"},
             "alloc_stats": a[2],
             "result_check": check,
+            "model": model,
+            **({"rehearsal": f"REHEARSAL, not a scaling figure: {world} ranks over the host-staged "
+                             f"{dist.get_backend()} group (native loop over the shared-memory transport) on "
+                             f"{torch.cuda.device_count()} GPU(s); every exchange goes through host memory"}
+               if staged else {}),
             "reference_python": {"value": REF_PYTHON_RATE, "unit": "agent-rounds/s", "cores": 1,
                                  "source": "SURVEY.md §6 (reference election on 1 core of the build container)"},
             "roofline": dict(dom, frac_max_over_ranks=float(fr[0]), frac_min_over_ranks=-float(fr[1]),
@@ -691,6 +735,248 @@ def sharded_state_check(sh, r):
     assert fixed_point and state_ok, ("sharded election state is not a fixed point", fixed_point, state_ok)
     return {"fixed_point_all_ranks": fixed_point, "state_consistent_all_ranks": state_ok,
             "rounds_exec": r.rounds_exec, "converged": r.converged}
+
+
+# ---- election cost model at N GPUs.  Assumed transport latencies (the pool's boxes have one
+# GPU: RCCL over xGMI was never measured here): one send/recv group to the peers, one small all-reduce
+# with its host read-back, and the per-peer xGMI bandwidth a halo message sees.
+ALPHA_P2P_US = 10.0
+ALPHA_AR_US = 20.0
+LINK_GBS = 100.0
+STAMP_US_PER_MB = 0.23  # the sparse round's stamp scan: 10 MB in ~2.3 us (per-workgroup clocks)
+EXCH_LAUNCH_US = 4.0    # the pack and ghost-apply kernels of an exchange
+
+
+def batch_schedule(changes, max_batch=256):
+    """The host batches of the sharded C loop (comm.hip + swarm_common.h next_round_batch) over the GLOBAL
+    per-round changes: how many counter all-reduces (host round trips) the election takes."""
+    hist, t, batch, n, R = [], 1, 8, 0, len(changes)
+    while t <= R:
+        tend = min(R, t + batch - 1)
+        n += 1
+        hist.extend(int(c) for c in changes[t - 1:tend])
+        t = tend + 1
+        b = min(batch * 2, max_batch)
+        if len(hist) >= 32:
+            slope = (hist[-32] - hist[-1]) / 31.0
+            if slope > 0:
+                rem = 1.25 * hist[-1] / slope + 4.0
+                p = 8 if rem < 8 else (max_batch if rem > max_batch else int(rem + 0.5))
+                b = min(b, p)
+        batch = b
+    return n
+
+
+def fit_round_cost(local, round_ms, n_rows, n_edges):
+    """Per-round device time of the frontier round on one rank as a function of its work, fitted on a
+    calibration election (round_ms from HIP events, local = per-round (changes, rows, edges)): sparse
+    rounds t = a + b * rows + c * edges (non-negative least squares), dense rounds t = d * (rows + edges)."""
+    from scipy.optimize import nnls
+    local = np.asarray(local, np.float64)
+    t = np.asarray(round_ms, np.float64) * 1e3  # us
+    dense = local[:, 2] < 0
+    sp = ~dense
+    A = np.stack([np.ones(sp.sum()), local[sp, 1], local[sp, 2]], 1)
+    coef, _ = nnls(A, t[sp])
+    pred = A @ coef
+    d = float(np.mean(t[dense] / (n_rows + n_edges))) if dense.any() else 0.0
+    return {"a_us": float(coef[0]), "b_us_per_row": float(coef[1]), "c_us_per_edge": float(coef[2]),
+            "dense_us_per_row_or_edge": d, "calib_rows": int(n_rows), "calib_edges": int(n_edges),
+            "sparse_rounds_fitted": int(sp.sum()), "fit_r2": float(1 - ((t[sp] - pred) ** 2).sum()
+                                                                   / max(((t[sp] - t[sp].mean()) ** 2).sum(), 1e-30)),
+            "fit_sum_ms": float(pred.sum() / 1e3 + t[dense].sum() / 1e3), "measured_sum_ms": float(t.sum() / 1e3)}
+
+
+def election_model(per_rank, shard_rows, shard_edges, send_bytes, changes, depth, cal, merge=1):
+    """Predicted time of one sharded election on N = len(per_rank) / merge GPUs: every merge consecutive
+    ranks of the run taken as one (Morton blocks and strips both merge into the N/2-rank partition; their
+    ghost rows are counted as owned work), per-round cost from the calibration fit, the ranks meeting at
+    every halo exchange (each window costs its slowest rank), plus the exchanges (alpha + kernels + the
+    largest per-peer message over one xGMI link) and the per-batch counter all-reduce."""
+    R = len(changes)
+    k = len(per_rank) // merge
+    rows = np.zeros((k, R))
+    edges = np.zeros((k, R))
+    n_all = np.zeros(k)
+    e_all = np.zeros(k)
+    for g in range(k):
+        for q in range(g * merge, (g + 1) * merge):
+            loc = np.asarray(per_rank[q], np.float64)[:R]
+            dense = loc[:, 2] < 0
+            rows[g] += loc[:, 1]
+            edges[g] += np.where(dense, shard_edges[q], loc[:, 2])
+            n_all[g] += shard_rows[q]
+            e_all[g] += shard_edges[q]
+    dense = np.asarray(per_rank[0], np.float64)[:R, 2] < 0
+    a0 = cal["a_us"] - STAMP_US_PER_MB * cal["calib_rows"] / 1e6
+    t = np.where(dense[None, :], cal["dense_us_per_row_or_edge"] * (n_all[:, None] + e_all[:, None]),
+                 a0 + STAMP_US_PER_MB * n_all[:, None] / 1e6 + cal["b_us_per_row"] * rows
+                 + cal["c_us_per_edge"] * edges)
+    if k == 1:
+        return {"n_gpus": 1, "ms": float(t.sum() / 1e3), "rounds": R, "exchanges": 0, "batches": 0}
+    d = max(1, int(depth))
+    wins = [np.arange(i, min(i + d, R)) for i in range(0, R, d)]
+    compute = sum(float(t[:, w].sum(1).max()) for w in wins)
+    n_exch = R // d
+    msg_us = max(send_bytes) * merge ** 0.5 / (LINK_GBS * 1e3)  # a merged region's border grows ~ sqrt
+    nb = batch_schedule(changes)
+    exch = n_exch * (ALPHA_P2P_US + EXCH_LAUNCH_US + msg_us)
+    ar = nb * ALPHA_AR_US
+    return {"n_gpus": k, "ms": (compute + exch + ar) / 1e3, "compute_ms": compute / 1e3, "exchange_ms": exch / 1e3,
+            "allreduce_ms": ar / 1e3, "rounds": R, "exchanges": n_exch, "batches": nb,
+            "imbalance": float(compute / max(t.sum(0).sum() / k, 1e-9))}
+
+
+def sharded_model(args, sh, rank, world, check):
+    """DESIGN §6's election cost model for this run: one more (untimed, identical) sharded election records
+    every rank's per-round work; rank 0 then elects its shard graph alone (the other ranks wait, the GPU is
+    rank 0's) with per-round HIP events, fits the per-round cost, and predicts the election on N, N/2, ...,
+    1 real GPUs (RCCL over xGMI, the ALPHA_* latencies assumed)."""
+    import torch.distributed as dist
+    rec = sh.elect(check_every=128, record=True)
+    info = dict(local=rec.local, rows=int(sh.all_ids.numel()), edges=int(sh.col.numel()),
+                send=4 * max([0] + list(sh.send_count.values())), changes=rec.changes, rounds=rec.rounds_exec)
+    allinfo = [None] * world
+    dist.all_gather_object(allinfo, info)
+    dist.barrier()
+    out = None
+    if rank == 0:
+        ra, loc, rms, wall = sh.elect_alone()
+        cal = fit_round_cost(loc, rms, info["rows"], info["edges"])
+        per_rank = [i["local"] for i in allinfo]
+        rows, edges, send = [i["rows"] for i in allinfo], [i["edges"] for i in allinfo], [i["send"] for i in allinfo]
+        table, m = [], 1
+        while m <= world:
+            if world % m == 0:
+                table.append(election_model(per_rank, rows, edges, send, rec.changes, sh.halo_depth, cal, merge=m))
+            m *= 2
+        by_n = {e["n_gpus"]: e for e in table}
+        out = {"calibration": dict(cal, rounds=int(ra), wall_ms=wall, shard_rows=info["rows"]),
+               "assumed": {"alpha_p2p_us": ALPHA_P2P_US, "alpha_allreduce_us": ALPHA_AR_US, "link_GBps": LINK_GBS,
+                           "stamp_us_per_MB": STAMP_US_PER_MB, "exchange_launch_us": EXCH_LAUNCH_US},
+               "table": table,
+               "note": "per-round work = this run's per-rank counts (exact, timing-free); N/2 ... 1 merge adjacent "
+                       "ranks; the election only (the allocation is ~0.2 ms)"}
+        t1 = (check.get("union_oracle") or {}).get("t1_gpu_ms")
+        if t1:
+            out["t1_measured_ms"] = t1
+            out["model_speedup"] = t1 / by_n[world]["ms"]
+            out["model_vs_measured_n1"] = by_n[1]["ms"] / t1
+        else:
+            out["model_speedup"] = by_n[1]["ms"] / by_n[world]["ms"]
+    dist.barrier()
+    return out
+
+
+def union_oracle_check(args, sh, r, rank, world):
+    """The sharded election against the C oracle over the UNION swarm (rank 0's host): every rank's
+    owned leaders (by agent ID), rounds_exec and every per-round GLOBAL change count must equal
+    orc_elect_frontier's on the union graph (regenerated from the same seeds, cell-ordered, radius-1
+    RGG by orc_rgg_csr).  The oracle is the checker here, never the measured path.  Prints progress
+    while it runs (one C call per stage)."""
+    import threading
+
+    import torch
+    import torch.distributed as dist
+    from swarm_amd import gen
+    cpu = torch.device("cpu")
+    ids_t = sh.ids.to(cpu).to(torch.int64)
+    lead_t = r.leader.to(cpu).to(torch.int64)
+    n_t = torch.tensor([ids_t.numel()], dtype=torch.int64)
+    counts = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    staged = dist.get_backend() != "nccl"
+    if staged:
+        dist.all_gather(counts, n_t)
+    else:  # nccl groups carry device tensors only
+        cd = [c.to(sh.device) for c in counts]
+        dist.all_gather(cd, n_t.to(sh.device))
+        counts = [c.cpu() for c in cd]
+    mx = int(max(int(c) for c in counts))
+    pad = lambda t: torch.cat([t, torch.full((mx - t.numel(),), -1, dtype=torch.int64)])  # noqa: E731
+    g_ids = [torch.empty(mx, dtype=torch.int64) for _ in range(world)] if rank == 0 else None
+    g_lead = [torch.empty(mx, dtype=torch.int64) for _ in range(world)] if rank == 0 else None
+    if staged:
+        dist.gather(pad(ids_t), g_ids, dst=0)
+        dist.gather(pad(lead_t), g_lead, dst=0)
+    else:
+        gi = [torch.empty(mx, dtype=torch.int64, device=sh.device) for _ in range(world)]
+        gl = [torch.empty(mx, dtype=torch.int64, device=sh.device) for _ in range(world)]
+        dist.all_gather(gi, pad(ids_t).to(sh.device))
+        dist.all_gather(gl, pad(lead_t).to(sh.device))
+        g_ids, g_lead = ([t.cpu() for t in gi], [t.cpu() for t in gl]) if rank == 0 else (None, None)
+    res = None
+    if rank == 0:
+        from oracle import oracle as orc
+        t0 = time.time()
+        ds = [gen.shard_inputs(args.agents, args.seed, world, q, deg=args.deg, layout=args.partition)
+              for q in range(world)]
+        x = np.concatenate([e["x"] for e in ds])
+        y = np.concatenate([e["y"] for e in ds])
+        ids = np.concatenate([e["ids"] for e in ds]).astype(np.int32)
+        del ds
+        perm = gen.cell_order(x, y, 1.0)  # locality for the oracle's gathers (results are order-free)
+        x, y, ids = x[perm], y[perm], ids[perm]
+        del perm
+        box = {}
+
+        def work():
+            orc.set_threads(_threads())
+            t1 = time.time()
+            rp, col = orc.rgg_csr(x, y, 1.0)
+            box["graph_s"] = time.time() - t1
+            box["edges"] = int(rp[-1])
+            t1 = time.time()
+            box["elect"] = orc.elect_frontier(rp, col, ids)
+            box["elect_s"] = time.time() - t1
+
+        th = threading.Thread(target=work)
+        th.start()
+        while th.is_alive():
+            th.join(30)
+            log(f"[rank 0] union oracle running {time.time() - t0:.0f}s")
+        lead, _, rounds, changes = box["elect"]
+        # the union on ONE GPU (this rank's; the others wait): the N = 1 time the model's speedup divides
+        t1_ms, gpu_equal = None, None
+        if args.union_gpu:
+            import torch
+            from swarm_amd.swarm import Swarm
+            su = Swarm(ids, x, y, device=sh.device).build_graph(1.0)
+            ru = su.elect()
+            ts = []
+            for _ in range(2):
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                ru = su.elect()
+                torch.cuda.synchronize()
+                ts.append((time.perf_counter() - t1) * 1e3)
+            t1_ms = min(ts)
+            gpu_equal = ru.rounds_exec == int(rounds) and bool(np.array_equal(np.asarray(ru.changes), np.asarray(changes)))
+            log(f"[rank 0] union on one GPU: {su.n} agents, {ru.rounds_exec} rounds, {t1_ms:.1f} ms")
+            del su, ru
+            torch.cuda.empty_cache()
+        want = np.full(int(ids.max()) + 1, -1, np.int64)
+        want[ids] = lead
+        ok_lead, n_checked = True, 0
+        for q in range(world):
+            k = int(counts[q])
+            gi, gl = g_ids[q][:k].numpy(), g_lead[q][:k].numpy()
+            ok_lead &= bool(np.array_equal(want[gi], gl))
+            n_checked += k
+        res = {"agents_union": int(len(ids)), "edges_union": box["edges"], "agents_checked": n_checked,
+               "rounds_oracle": int(rounds), "rounds_sharded": int(r.rounds_exec),
+               "rounds_equal": int(rounds) == int(r.rounds_exec),
+               "changes_equal": bool(np.array_equal(np.asarray(changes), r.changes)),
+               "leaders_equal": ok_lead and n_checked == len(ids),
+               "oracle": f"orc_elect_frontier over the {len(ids)}-agent union (orc_rgg_csr {box['graph_s']:.0f} s, "
+                         f"election {box['elect_s']:.0f} s, {_threads()} threads)"}
+        if t1_ms is not None:
+            res.update(t1_gpu_ms=t1_ms, t1_gpu_rounds_changes_equal=gpu_equal)
+        res["all_equal"] = res["rounds_equal"] and res["changes_equal"] and res["leaders_equal"]
+        log(f"[rank 0] union oracle: {res}")
+    dist.barrier()
+    if rank == 0:
+        assert res["all_equal"], ("sharded election differs from the union oracle", res)
+    return res
 
 
 def survey_step_bytes(r, n, e, tasks):

@@ -355,6 +355,7 @@ int frontier_ghosts_both(swarm_ctx *ctx, int t, const int32_t *rp, const int32_t
                          int32_t *L1, hipStream_t s);
 int frontier_round_totals(swarm_ctx *ctx, int t0, int t1, unsigned long long *dtot, hipStream_t s);
 int64_t frontier_il_min(int64_t n);
+bool frontier_round_dense(int t);
 }  // namespace swarm
 
 extern "C" {
@@ -443,8 +444,21 @@ int swarm_comm_destroy(swarm_comm *c) {
 int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sh, int32_t *leader0,
                         int32_t *leader1, int32_t max_rounds, int32_t *rounds_exec, int64_t *changes_host,
                         void *stream) {
+    return swarm_elect_sharded_ex(ctx, comm, sh, leader0, leader1, max_rounds, rounds_exec, changes_host, nullptr,
+                                  nullptr, stream);
+}
+
+int swarm_elect_sharded_ex(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sh, int32_t *leader0,
+                           int32_t *leader1, int32_t max_rounds, int32_t *rounds_exec, int64_t *changes_host,
+                           int64_t *local_counts, float *round_ms, void *stream) {
     using namespace swarm;
-    SW_ARG(ctx && comm && sh && rounds_exec, "NULL argument");
+    SW_ARG(ctx && sh && rounds_exec, "NULL argument");
+    swarm_comm solo;  // comm NULL: one rank, no peers (a shard graph stepped alone)
+    if (!comm) {
+        SW_ARG(sh->n_peers == 0, "a shard with peers needs a communicator");
+        solo.kind = SWARM_COMM_RCCL;
+        comm = &solo;
+    }
     hipStream_t s = static_cast<hipStream_t>(stream);
     const bool shm = comm->kind == SWARM_COMM_SHM;
     const Rccl &R = rccl();
@@ -486,8 +500,10 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sh,
     constexpr int kC = kElectCounters;
     unsigned long long *dtot;
     SW_ALLOC(dtot, ctx, S_ESTATS, size_t(kC) * 8 * kMaxBatch);
-    unsigned long long *h = static_cast<unsigned long long *>(pinned(ctx, size_t(kC) * 8 * kMaxBatch));
+    // pinned read-back: the batch's global counters, then (local_counts) this rank's own
+    unsigned long long *h = static_cast<unsigned long long *>(pinned(ctx, size_t(kC) * 16 * kMaxBatch));
     if (!h) return SWARM_ERR_OOM;
+    unsigned long long *hl = h + size_t(kC) * kMaxBatch;
     const int depth = sh->halo_depth > 1 ? sh->halo_depth : 1;
     {
         unsigned long long agree[3] = {why[0] ? 1ull : 0ull, (unsigned long long)depth,
@@ -518,6 +534,20 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sh,
     SW_ALLOC(sbuf, ctx, S_TMP0, (nsend + nrecv + 4) * 4);
     int32_t *rbuf = sbuf + nsend;
     const int64_t own_end = sh->own_begin + sh->n_rows;
+    // per-round device time of this rank's round launches (round_ms): an event pair per round of a batch
+    std::vector<hipEvent_t> ev;
+    struct EvFree {
+        std::vector<hipEvent_t> &v;
+        ~EvFree() { for (auto e : v) (void)hipEventDestroy(e); }
+    } ev_free{ev};
+    if (round_ms) {
+        ev.resize(2 * kMaxBatch);
+        for (auto &e : ev) SW_HIP(hipEventCreate(&e));
+    }
+    unsigned long long *lcnt = nullptr;  // this rank's counters of the batch, before the all-reduce
+    if (local_counts) {
+        SW_ALLOC(lcnt, ctx, S_TMP1, size_t(kC) * 8 * kMaxBatch);
+    }
     int found = -1, t = 1, batch = 8;
     std::vector<int64_t> hist;
     // the stamp layout: interleaved while rounds are busy, agent order in the tail (as swarm_elect),
@@ -527,7 +557,9 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sh,
         const int tend = std::min(max_rounds, t + batch - 1);
         ctx->step_wr_agent = (!hist.empty() && hist.back() < il_min) ? 1 : 0;
         for (int r = t; r <= tend; ++r) {
+            if (round_ms) SW_HIP(hipEventRecord(ev[2 * (r - t)], s));
             if ((rc = frontier_round_stepper(ctx, r, sh->row_ptr, sh->col, leader0, leader1, s))) return rc;
+            if (round_ms) SW_HIP(hipEventRecord(ev[2 * (r - t) + 1], s));
             if (r % depth || comm->nranks == 1) continue;  // deep halo: ghosts are stepped locally between exchanges
             // every rank takes part in every exchange, peers or not (the shared-memory ops are barriers)
             int32_t *Lcur = (r & 1) ? leader1 : leader0;
@@ -555,6 +587,10 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sh,
         }
         const int nr = tend - t + 1;
         if ((rc = frontier_round_totals(ctx, t, tend, dtot, s))) return rc;
+        if (lcnt) {
+            SW_HIP(hipMemcpyAsync(lcnt, dtot, size_t(nr) * kC * 8, hipMemcpyDeviceToDevice, s));
+            SW_HIP(hipMemcpyAsync(hl, lcnt, size_t(nr) * kC * 8, hipMemcpyDeviceToHost, s));
+        }
         if (shm) {
             if (comm->nranks > 1 && (rc = shm_allreduce_u64(comm, dtot, size_t(nr) * kC, false, s))) return rc;
         } else if (comm->nranks > 1 || comm->comm) {
@@ -563,6 +599,14 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sh,
         SW_HIP(hipMemcpyAsync(h, dtot, size_t(nr) * kC * 8, hipMemcpyDeviceToHost, s));
         SW_HIP(hipStreamSynchronize(s));
         for (int r = t; r <= tend; ++r) {
+            if (local_counts) {  // owned changes, gathered rows, gathered edges (a dense round: every row)
+                const unsigned long long *q = hl + size_t(r - t) * kC;
+                const bool dn = frontier_round_dense(r);
+                local_counts[size_t(r - 1) * 3 + 0] = int64_t(q[0]);
+                local_counts[size_t(r - 1) * 3 + 1] = dn ? sh->n_all : int64_t(q[1]);
+                local_counts[size_t(r - 1) * 3 + 2] = dn ? -1 : int64_t(q[2]);  // -1: all the shard's edges
+            }
+            if (round_ms) SW_HIP(hipEventElapsedTime(&round_ms[r - 1], ev[2 * (r - t)], ev[2 * (r - t) + 1]));
             const unsigned long long c = h[size_t(r - t) * kC];  // C_CHG: owned changes
             hist.push_back(int64_t(c));
             if (changes_host) changes_host[r - 1] = int64_t(c);

@@ -1266,6 +1266,9 @@ int frontier_round_stepper(swarm_ctx *ctx, int t, const int32_t *rp, const int32
     return rc;
 }
 
+// Whether round t of the frontier stepper is a dense sweep (its active / edge counters are not kept).
+bool frontier_round_dense(int t) { return plan_round(t) != RK_SPARSE; }
+
 // The interleaved -> agent-order switch point of the stamp layout for an n-agent swarm (elect_impl's
 // il_min; the sharded C loop compares the global changes against it for the global agent count).
 int64_t frontier_il_min(int64_t n) {

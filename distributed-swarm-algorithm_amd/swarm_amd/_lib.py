@@ -36,7 +36,7 @@ EXPORTS = ("swarm_last_error", "swarm_version", "swarm_ctx_create", "swarm_ctx_d
            "swarm_allocate_indexed", "swarm_graph_compact", "swarm_elect_compact",
            "swarm_elect_compact_i64", "swarm_frontier_begin_range", "swarm_frontier_set_compact",
            "swarm_comm_unique_id_kind", "swarm_comm_create_kind", "swarm_comm_kind", "swarm_allocate_indexed_ex",
-           "swarm_protocol_run_ex")
+           "swarm_protocol_run_ex", "swarm_elect_sharded_ex")
 
 
 class SwarmError(RuntimeError):
@@ -153,6 +153,7 @@ def load(path: str = LIB_PATH):
         L.swarm_comm_kind.argtypes = [P]
         L.swarm_comm_destroy.argtypes = [P]
         L.swarm_elect_sharded.argtypes = [P, P, ctypes.POINTER(Shard), P, P, i32, ctypes.POINTER(i32), P, P]
+        L.swarm_elect_sharded_ex.argtypes = [P, P, ctypes.POINTER(Shard), P, P, i32, ctypes.POINTER(i32), P, P, P, P]
         L.swarm_physics_step.argtypes = [P, i64, P, P, P, P, P, P, P, P, i64, P, P, P, d, d, ctypes.POINTER(i64), P]
         L.swarm_codec_encode.argtypes = [P, i64, P, P, P, P, P, P, P, i32, P, i64, P, P, ctypes.POINTER(i64), P]
         L.swarm_codec_decode.argtypes = [P, i64, P, i64, P, i32, P, P, P, P, P, P, P, P, P, P]

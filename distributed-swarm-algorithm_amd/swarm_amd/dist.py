@@ -487,18 +487,31 @@ class GpuBackend:
         self.comm_kind = "rccl" if kind == L.COMM_RCCL else "shm"
         return comm
 
-    def elect_sharded(self, comm, sh, max_rounds):
+    def elect_sharded(self, comm, sh, max_rounds, record=False, alone=False):
+        """The native sharded loop (swarm_elect_sharded_ex).  record: also this rank's per-round counts
+        (owned changes, rows and edges gathered) and per-round device times.  alone: the shard graph stepped
+        by itself, no peers and no communicator (the cost model's calibration run)."""
         import ctypes
         L = self.L
-        desc = L.shard_desc(sh.n_own, sh.all_ids.numel(), sh.row_ptr, sh.col, sh.all_ids, sh.own_begin,
-                            sh.halo_depth, sh.peers, [sh.send_count[p] for p in sh.peers], sh.send_rows_all,
-                            [sh.ghost_count[p] for p in sh.peers], sh.c16)
+        peers = [] if alone else sh.peers
+        n_all = sh.all_ids.numel()
+        # alone: every row counts as owned (no ghost blocks without peers)
+        desc = L.shard_desc(n_all if alone else sh.n_own, n_all, sh.row_ptr, sh.col, sh.all_ids,
+                            0 if alone else sh.own_begin,
+                            sh.halo_depth, peers, [sh.send_count[p] for p in peers],
+                            None if alone else sh.send_rows_all, [sh.ghost_count[p] for p in peers], sh.c16)
         rounds = ctypes.c_int32(0)
         changes = np.zeros(max_rounds, np.int64)
-        rc = L.check(L.lib().swarm_elect_sharded(self.ctx, comm, ctypes.byref(desc), L.ptr(sh.leaders[0]),
-                                                 L.ptr(sh.leaders[1]), max_rounds, ctypes.byref(rounds),
-                                                 changes.ctypes.data_as(ctypes.c_void_p), L.stream()))
+        local = np.zeros((max_rounds, 3), np.int64) if record else None
+        rms = np.zeros(max_rounds, np.float32) if record else None
+        hp = lambda a: a.ctypes.data_as(ctypes.c_void_p) if a is not None else None  # noqa: E731
+        rc = L.check(L.lib().swarm_elect_sharded_ex(self.ctx, None if alone else comm, ctypes.byref(desc),
+                                                    L.ptr(sh.leaders[0]), L.ptr(sh.leaders[1]), max_rounds,
+                                                    ctypes.byref(rounds), hp(changes), hp(local), hp(rms),
+                                                    L.stream()))
         r = rounds.value
+        if record:
+            return r, changes[:r].copy(), rc == L.OK, local[:r].copy(), rms[:r].copy()
         return r, changes[:r].copy(), rc == L.OK
 
     def changes(self, t0, t1):
@@ -707,17 +720,26 @@ class ShardedSwarm:
         return lo, hi
 
     # ------------------------------------------------------------------ election
-    def elect(self, max_rounds: int = 1 << 16, check_every: int = 64) -> ShardElectResult:
+    def elect(self, max_rounds: int = 1 << 16, check_every: int = 64, record: bool = False) -> ShardElectResult:
+        """The sharded election (contract E2).  record (native loop only): the result also carries this
+        rank's per-round counts (.local: owned changes, rows gathered, edges gathered; -1 edges = a dense
+        round over the whole shard graph) and per-round device times (.round_ms)."""
         be, h = self.backend, self.halo
         if getattr(self, "_native", "unset") == "unset":
             self._native = be.native_comm(h) if hasattr(be, "native_comm") else None
         own_sl = slice(self.own_begin, self.own_begin + self.n_own)
         if self._native is not None:
-            rounds, changes, conv = be.elect_sharded(self._native, self, max_rounds)
+            out = be.elect_sharded(self._native, self, max_rounds, record=record)
+            rounds, changes, conv = out[:3]
             own = self.leaders[rounds & 1][own_sl]
             self._check_ghosts(self.leaders[rounds & 1])
             state = torch.where(own == self.ids, 3, 1).to(torch.uint8)
-            return ShardElectResult(rounds, changes, own, state, conv)
+            res = ShardElectResult(rounds, changes, own, state, conv)
+            if record:
+                res.local, res.round_ms = out[3], out[4]
+            return res
+        if record:
+            raise RuntimeError("elect(record=True) needs the native sharded loop")
         rp, col, lead = self.row_ptr, self.col, self.leaders
         be.begin(self.own_begin, self.n_own, self.all_ids, lead, self.c16)
         g_lo, g_hi = 0, self.own_begin + self.n_own
@@ -744,6 +766,17 @@ class ShardedSwarm:
         own = lead[rounds & 1][own_sl]
         state = torch.where(own == self.ids, 3, 1).to(torch.uint8)
         return ShardElectResult(rounds, np.array(changes[:rounds], np.int64), own, state, found > 0)
+
+    def elect_alone(self, max_rounds: int = 1 << 16):
+        """This shard's graph elected by itself on this rank's GPU (no peers, no exchange): the calibration
+        run of the election cost model -- (rounds, per-round local counts, per-round device ms, wall ms)."""
+        import time
+        be = self.backend
+        torch.cuda.synchronize(self.device)
+        t0 = time.perf_counter()
+        r, _, _, local, rms = be.elect_sharded(None, self, max_rounds, record=True, alone=True)
+        torch.cuda.synchronize(self.device)
+        return r, local, rms, (time.perf_counter() - t0) * 1e3
 
     def exact_ghosts(self):
         """Ghost rows adjacent to an owned row (one hop from the owned agents): their values are exact

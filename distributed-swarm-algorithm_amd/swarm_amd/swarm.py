@@ -360,6 +360,10 @@ class Swarm:
     def allocate(self, tx, ty, treq, *, winner=None, util=None, claim_thr: float = 20.0,
                  hysteresis: float = 5.0, u_scale: float = 100.0, mode: str = "auto") -> AllocResult:
         """One allocation round over t tasks (swarm_allocate).  winner/util = existing claims."""
+        if winner is None and util is None and mode == "auto":
+            r = self._allocate_again(tx, ty, treq, claim_thr, hysteresis, u_scale)
+            if r is not None:
+                return r
         dev = self.device
         tpos = self._task_pos(tx, ty)
         tq = _to(treq, torch.int8, dev)
@@ -397,6 +401,18 @@ class Swarm:
                     float(hysteresis), float(u_scale), flags, p(w), p(u), p(won), p(idx),
                     0 if idx is None else idx.numel(), p(nclaim), p(nmsg), ctypes.byref(st),
                     _lib.stream())
+                if rc == _lib.OK and trusted and fresh and mode == "auto" and isinstance(treq, torch.Tensor) \
+                        and tq is treq:
+                    # the same call again (same task tensors and versions, same trusted index, same
+                    # swarm arrays) needs none of the above: _allocate_again replays it from here
+                    self._again = ((tx, ty, treq, (tx._version, ty._version, treq._version), self.pos,
+                                    self.pos._version, self.ids, self.caps, (claim_thr, hysteresis, u_scale),
+                                    torch.cuda.current_device()),
+                                   (self.n, self.ids.data_ptr(), self.pos.data_ptr(), self.caps.data_ptr(),
+                                    ctypes.byref(ci[0]), ci[1].data_ptr(), t, tpos.data_ptr(), tq.data_ptr(),
+                                    float(claim_thr), float(hysteresis), float(u_scale), flags),
+                                   (idx.data_ptr() if idx is not None else None, 0 if idx is None else idx.numel()),
+                                   (ci, tpos, idx))
                 if rc == _lib.ERR_STALE:  # positions moved since the index: bin them this call
                     self._cindex = None  # rebuilt next call if they are still in cell order
                     w.copy_(w0) if w0 is not None else w.fill_(-1)
@@ -415,6 +431,33 @@ class Swarm:
                     ctypes.byref(st), _lib.stream()))
         stats = {k: getattr(st, k) for k, _ in _lib.AllocStats._fields_}
         return AllocResult(w, u, won, nclaim, nmsg, stats)
+
+    def _allocate_again(self, tx, ty, treq, claim_thr, hysteresis, u_scale):
+        """The previous fresh, trusted-index allocation repeated (the same task tensors at the same
+        versions, the same swarm arrays and position version, the same thresholds, on the same device):
+        one libswarm call with its arguments kept from that call -- none of allocate()'s per-call Python
+        (task stacking, index checks, device context, pointer validation).  None when anything differs."""
+        c = getattr(self, "_again", None)
+        if c is None:
+            return None
+        k = c[0]
+        if not (k[0] is tx and k[1] is ty and k[2] is treq and k[4] is self.pos and k[6] is self.ids
+                and k[7] is self.caps and k[3] == (tx._version, ty._version, treq._version)
+                and k[5] == self.pos._version and k[8] == (claim_thr, hysteresis, u_scale)
+                and k[9] == torch.cuda.current_device() and c[3][0] is self._cindex
+                and c[3][2] is self._id_index):
+            return None
+        a = c[1]
+        t, dev = a[6], self.device
+        w = torch.empty(t, dtype=torch.int32, device=dev)
+        u = torch.empty(t, dtype=torch.float64, device=dev)
+        won = torch.empty(self.n, dtype=torch.int32, device=dev)
+        nc_nm = torch.empty((2, t), dtype=torch.int64, device=dev)
+        st = _lib.AllocStats()
+        pn = nc_nm.data_ptr()
+        _lib.check(_lib.lib().swarm_allocate_indexed_ex(_lib.ctx(), *a, w.data_ptr(), u.data_ptr(), won.data_ptr(),
+                                                        *c[2], pn, pn + 8 * t, ctypes.byref(st), _lib.stream()))
+        return AllocResult(w, u, won, nc_nm[0], nc_nm[1], {k_: getattr(st, k_) for k_, _ in _lib.AllocStats._fields_})
 
     def _task_pos(self, tx, ty) -> torch.Tensor:
         """(t, 2) float64 task positions on the device.  When tx / ty are float64 device tensors the

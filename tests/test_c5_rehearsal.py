@@ -1,0 +1,49 @@
+"""C5's shape through the bench's N > 1 path, scaled down to fit the GPU suite.
+
+bench.py --config C5 with EIGHT ranks sharing one GPU (SWARM_DIST_BACKEND=gloo: libswarm's native
+sharded loop over the shared-memory transport, 7 peers' worth of ranks), Morton blocks with Morton IDs
+(SURVEY §8e's C5 partition: contiguous ID ranges, up to 8 neighbouring ranks) and strips; the line's
+result_check.union_oracle compares every rank's leaders, rounds_exec and per-round global changes with
+the C oracle over the union swarm.  The full-size run (8 x 12.5M) is the same command without --agents
+(profiles/)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("partition,agents", [("blocks", 150_000), ("strips", 100_000)])
+def test_c5_bench_eight_ranks_one_gpu_matches_union_oracle(partition, agents):
+    env = dict(os.environ, SWARM_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "8", "--config", "C5", "--agents", str(agents), "--tasks", "200", "--steps", "1",
+           "--warmup", "0", "--cpu-baseline", "0", "--partition", partition]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    if p.returncode:
+        os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(ROOT, "gpurun_out", f"c5_rehearsal_{partition}.err"), "w") as f:
+            f.write(p.stderr)
+        keep = [q for q in p.stderr.splitlines() if "Error" in q or "error" in q or q.strip().startswith("File ")]
+        raise AssertionError("\n".join(keep[:80]))
+    line = [q for q in p.stdout.splitlines() if q.startswith("{")][-1]
+    out = json.loads(line)
+    u = out["result_check"]["union_oracle"]
+    assert u["all_equal"] and u["agents_checked"] == 8 * agents == u["agents_union"], u
+    assert out["n_gpus"] == 8 and out["scaling"] == "strong" and "REHEARSAL" in out["rehearsal"]
+    assert "shared-memory" in out["config"]["parallelism"]
+    if partition == "blocks":
+        assert len(out["config"]["peers_rank0"]) >= 2

@@ -44,3 +44,23 @@ tm("_lib.ctx()", _lib.ctx)
 tm("_lib.stream()", _lib.stream)
 tm("_fast_ptr x13", lambda: [_fast_ptr(sw.ids) for _ in range(13)])
 tm("allocate() total", lambda: sw.allocate(tx, ty, tq), reps=50)
+
+
+def slow():
+    sw._again = None  # the full prelude every call
+    return sw.allocate(tx, ty, tq)
+
+
+tm("allocate() slow path", slow, reps=50)
+sw.allocate(tx, ty, tq)
+tm("allocate() repeat (fast path)", lambda: sw.allocate(tx, ty, tq), reps=50)
+ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+xs = []
+for _ in range(50):
+    torch.cuda.synchronize()
+    ev[0].record()
+    sw.allocate(tx, ty, tq)
+    ev[1].record()
+    torch.cuda.synchronize()
+    xs.append(ev[0].elapsed_time(ev[1]))
+print(f"{'bench split (events)':28s} {np.median(xs) * 1e3:7.1f} us", flush=True)
