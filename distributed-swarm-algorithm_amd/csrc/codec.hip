@@ -7,8 +7,9 @@
 // winner (322, 325) -- and parses inbound packets in on_message_received (agent.py:197-214).
 // These kernels do both for a whole batch of messages (one thread per message / packet; a
 // byte-moving, HBM-bound job: no arithmetic worth the name):
-//   encode  status + length per message, an exclusive scan into packet offsets, then every
-//           thread writes its packet's bytes.  Errors as the reference raises them, payload
+//   encode  status + length per message, packets assembled per tile of 2 048 messages (the fields
+//           read once), tile bases by a scan of the tile totals, then each tile's bytes placed
+//           (k_enc_tile / k_enc_base / k_enc_place below).  Errors as the reference raises them, payload
 //           first (it packs the payload before _send_msg packs the header): an out-of-range
 //           integer field -> struct.error (status 1), a finite value beyond the f32 range ->
 //           OverflowError (status 2); an unknown type -> status 3.  Errored messages take no
@@ -21,8 +22,6 @@
 //           payload carries a position only when it is exactly 8 bytes (agent.py:256-258).
 //           A packet whose offsets fall outside [0, buf_len] or run backwards is not read
 //           (status 4).
-#include <hipcub/hipcub.hpp>
-
 #include <cmath>
 
 #include "swarm_common.h"
@@ -81,92 +80,197 @@ __device__ __forceinline__ uint32_t get_u32(const uint8_t *p) {
     return (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | uint32_t(p[3]);
 }
 
+// Exclusive prefix over the workgroup of c (0 <= c < 2^B) and the total (every thread gets it).
+template <int B>
+__device__ __forceinline__ int block_excl_scan(int c, int &total, int *s_wave) {
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    int ex = 0, tot = 0;
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        const unsigned long long mk = __ballot((c >> b) & 1);
+        ex += int(__builtin_amdgcn_mbcnt_hi(uint32_t(mk >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mk), 0u))) << b;
+        tot += __popcll(mk) << b;
+    }
+    if (lane == 0) s_wave[wid] = tot;
+    __syncthreads();
+    int off = 0, all = 0;
+#pragma unroll
+    for (int q = 0; q < kBlock / kWave; ++q) {
+        off += q < wid ? s_wave[q] : 0;
+        all += s_wave[q];
+    }
+    __syncthreads();  // s_wave read by all
+    total = all;
+    return off + ex;
+}
+
 struct EncIn {
     const int64_t *type, *sender, *tick, *task, *winner;
     const double *a, *b;
 };
 
-__global__ __launch_bounds__(kBlock) void k_enc_len(int64_t m, EncIn in, int wide, int64_t *__restrict__ len,
-                                                   int8_t *__restrict__ status) {
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < m; i += int64_t(gridDim.x) * kBlock) {
-        int l;
-        status[i] = int8_t(enc_status(in.type[i], in.sender[i], in.tick[i], in.a[i], in.b[i], in.task[i],
-                                      in.winner[i], wide, &l));
-        len[i] = l;
-    }
-}
-
-// Packet bytes of message i at p (status 0).
-__device__ __forceinline__ void write_packet(uint8_t *p, const EncIn &in, int64_t i, int wide) {
-    const int ty = int(in.type[i]);
+// Packet bytes of one message (status 0) at p, from its fields in registers.
+__device__ __forceinline__ void write_packet(uint8_t *p, int ty, int64_t snd, int64_t tick, double a, double b,
+                                             int64_t task, int64_t win, int wide) {
     p[0] = uint8_t(ty);
     int h;
     if (wide) {
-        put_u32(p + 1, uint32_t(in.sender[i]));
-        put_u32(p + 5, uint32_t(in.tick[i]));
+        put_u32(p + 1, uint32_t(snd));
+        put_u32(p + 5, uint32_t(tick));
         h = 9;
     } else {
-        p[1] = uint8_t(in.sender[i]);
-        put_u32(p + 2, uint32_t(in.tick[i]));
+        p[1] = uint8_t(snd);
+        put_u32(p + 2, uint32_t(tick));
         h = 6;
     }
     p += h;
     switch (ty) {
         case T_HB:
-            put_u32(p, __float_as_uint(float(in.a[i])));
-            put_u32(p + 4, __float_as_uint(float(in.b[i])));
+            put_u32(p, __float_as_uint(float(a)));
+            put_u32(p + 4, __float_as_uint(float(b)));
             break;
         case T_ACCLAIM:
-            if (wide) put_u32(p, uint32_t(in.sender[i]));
-            else p[0] = uint8_t(in.sender[i]);
+            if (wide) put_u32(p, uint32_t(snd));
+            else p[0] = uint8_t(snd);
             break;
         case T_CLAIM:
-            put_u32(p, uint32_t(in.task[i]));
-            put_u32(p + 4, __float_as_uint(float(in.a[i])));
+            put_u32(p, uint32_t(task));
+            put_u32(p + 4, __float_as_uint(float(a)));
             break;
         case T_CONFLICT:
-            put_u32(p, uint32_t(in.task[i]));
-            if (wide) put_u32(p + 4, uint32_t(in.winner[i]));
-            else p[4] = uint8_t(in.winner[i]);
+            put_u32(p, uint32_t(task));
+            if (wide) put_u32(p + 4, uint32_t(win));
+            else p[4] = uint8_t(win);
             break;
         default:
             break;
     }
 }
 
-// Messages [c0, c0 + kEncPer) per workgroup: packets are assembled in LDS at the same 16-byte
-// alignment they have in `out`, then the workgroup's contiguous output range is stored with
-// 16-byte vector stores (its partial first / last 16 bytes byte by byte: they share lines with
-// the neighbouring workgroups' packets).
-constexpr int kEncJ = 4, kEncPer = kBlock * kEncJ, kMaxPkt = 17;
-constexpr int kEncLds = (kEncPer * kMaxPkt + 32 + 15) / 16;  // uint4 words
+// Encode in tiles (round 5): every field is read ONCE.
+//   k_enc_tile   a workgroup per tile of kTile messages: status and length per message (kTileJ
+//                slabs of 256, each a block scan of the lengths), the packets assembled in LDS at their
+//                tile-relative offsets, then the tile's packed bytes stored to scratch (16-byte stores),
+//                its total, and each message's tile-relative offset (u16);
+//   k_enc_base   one workgroup: exclusive scan of the tile totals -> each tile's base, the total;
+//   k_enc_place  a workgroup per tile: the scratch bytes staged in LDS at the output's 16-byte
+//                phase, stored at base (16-byte stores, partial head / tail bytewise), and the int64
+//                offsets base + local.
+// Per message: fields 56 B read once, status 1 B, local offset 2 + 2 B, the packet 3 x ~10 B (scratch
+// write, scratch read, output), offsets 8 B.  (Rounds 1-4: k_enc_len + hipCUB scan + host sync +
+// k_enc_write, the fields read twice: 0.40 ms at 10M messages.  A single kernel with a decoupled
+// look-back over 1 024-message chunks: 0.43 ms, the look-back chain the bound.)
+constexpr int kTileJ = 8, kTile = kBlock * kTileJ, kMaxPkt = 17;
+constexpr int kTileBytes = kTile * kMaxPkt;             // scratch bytes per tile (wide worst case)
+constexpr int kTileLds = (kTileBytes + 16 + 15) / 16;   // uint4 words (+16: the output phase)
 
-__global__ __launch_bounds__(kBlock) void k_enc_write(int64_t m, EncIn in, int wide, const int64_t *__restrict__ off,
-                                                     const int8_t *__restrict__ status, uint8_t *__restrict__ out) {
-    __shared__ uint4 s_buf[kEncLds];
+__global__ __launch_bounds__(kBlock) void k_enc_tile(int64_t m, EncIn in, int wide, int8_t *__restrict__ status,
+                                                    uint16_t *__restrict__ loc, uint8_t *__restrict__ tmp,
+                                                    int64_t *__restrict__ tile_tot) {
+    __shared__ uint4 s_buf[kTileLds];
+    __shared__ int s_wave[kBlock / kWave];
     uint8_t *lb = reinterpret_cast<uint8_t *>(s_buf);
-    for (int64_t c0 = int64_t(blockIdx.x) * kEncPer; c0 < m; c0 += int64_t(gridDim.x) * kEncPer) {
-        const int64_t c1 = c0 + kEncPer < m ? c0 + kEncPer : m;
-        const int64_t base = off[c0], end = off[c1], abase = base & ~int64_t(15);
-#pragma unroll
-        for (int j = 0; j < kEncJ; ++j) {
+    const int64_t ntiles = (m + kTile - 1) / kTile;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t c0 = tile * kTile;
+        int run = 0;  // workgroup-uniform: bytes of the slabs before this one
+#pragma unroll 2
+        for (int j = 0; j < kTileJ; ++j) {
             const int64_t i = c0 + j * kBlock + threadIdx.x;
-            if (i < c1 && status[i] == 0) write_packet(lb + (off[i] - abase), in, i, wide);
+            const bool ok = i < m;
+            const int64_t ty = ok ? in.type[i] : 0, snd = ok ? in.sender[i] : 0, tk = ok ? in.tick[i] : 0;
+            const double fa = ok ? in.a[i] : 0.0, fb = ok ? in.b[i] : 0.0;
+            const int64_t task = ok ? in.task[i] : 0, win = ok ? in.winner[i] : 0;
+            int len = 0;
+            const int st = ok ? enc_status(ty, snd, tk, fa, fb, task, win, wide, &len) : 3;
+            int total;
+            const int pos = run + block_excl_scan<5>(len, total, s_wave);
+            if (ok) {
+                status[i] = int8_t(st);
+                loc[i] = uint16_t(pos);
+                if (st == 0) write_packet(lb + pos, int(ty), snd, tk, fa, fb, task, win, wide);
+            }
+            run += total;
+        }
+        __syncthreads();  // the tile's packets are in LDS
+        uint4 *dst = reinterpret_cast<uint4 *>(tmp + tile * int64_t(kTileBytes));
+        for (int q = threadIdx.x; q < (run + 15) / 16; q += kBlock) dst[q] = s_buf[q];
+        if (threadIdx.x == 0) tile_tot[tile] = run;
+        __syncthreads();  // s_buf reused by the next tile
+    }
+}
+
+// Exclusive scan of the tile totals (one workgroup): base[t], and base[ntiles] = the total.
+__global__ __launch_bounds__(1024) void k_enc_base(int64_t ntiles, const int64_t *__restrict__ tot,
+                                                  int64_t *__restrict__ base) {
+    __shared__ int64_t s_part[1024];
+    const int64_t per = (ntiles + 1023) / 1024, b = int64_t(threadIdx.x) * per;
+    int64_t sum = 0;
+    for (int64_t q = b; q < b + per && q < ntiles; ++q) sum += tot[q];
+    s_part[threadIdx.x] = sum;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scan of the 1 024 parts
+        const int64_t v = threadIdx.x >= unsigned(off) ? s_part[threadIdx.x - off] : 0;
+        __syncthreads();
+        s_part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    int64_t run = threadIdx.x ? s_part[threadIdx.x - 1] : 0;
+    for (int64_t q = b; q < b + per && q < ntiles; ++q) {
+        base[q] = run;
+        run += tot[q];
+    }
+    if (threadIdx.x == 1023) base[ntiles] = s_part[1023];
+}
+
+__global__ __launch_bounds__(kBlock) void k_enc_place(int64_t m, const uint8_t *__restrict__ tmp,
+                                                     const int64_t *__restrict__ tile_tot,
+                                                     const int64_t *__restrict__ base_of,
+                                                     const uint16_t *__restrict__ loc, int64_t cap,
+                                                     int64_t *__restrict__ off, uint8_t *__restrict__ out,
+                                                     unsigned *__restrict__ err) {
+    __shared__ uint4 s_buf[kTileLds];
+    uint8_t *lb = reinterpret_cast<uint8_t *>(s_buf);
+    const int64_t ntiles = (m + kTile - 1) / kTile;
+    if (base_of[ntiles] > cap) {  // the caller's buffer is too small: nothing is written
+        if (blockIdx.x == 0 && threadIdx.x == 0) *err = 1u;
+        return;
+    }
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t c0 = tile * kTile, base = base_of[tile], n = tile_tot[tile];
+        const int ph = int(base & 15);  // the output's 16-byte phase: LDS byte ph + x holds out[base + x]
+        const uint4 *src = reinterpret_cast<const uint4 *>(tmp + tile * int64_t(kTileBytes));
+        for (int q = threadIdx.x; q < (n + 15) / 16; q += kBlock) {
+            const uint4 w = src[q];
+            const uint32_t v[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int k = 0; k < 16; ++k) lb[ph + 16 * q + k] = uint8_t(v[k >> 2] >> (8 * (k & 3)));
+        }
+#pragma unroll 4
+        for (int j = 0; j < kTileJ; ++j) {
+            const int64_t i = c0 + j * kBlock + threadIdx.x;
+            if (i < m) off[i] = base + loc[i];
         }
         __syncthreads();
+        const int64_t end = base + n, abase = base - ph;
         const int64_t A = (base + 15) & ~int64_t(15), B = end & ~int64_t(15);
-        if (A >= B) {  // no whole 16-byte block: bytewise
+        if (A >= B) {
             for (int64_t x = base + threadIdx.x; x < end; x += kBlock) out[x] = lb[x - abase];
         } else {
             if (threadIdx.x < A - base) out[base + threadIdx.x] = lb[base + threadIdx.x - abase];
             if (threadIdx.x < end - B) out[B + threadIdx.x] = lb[B + threadIdx.x - abase];
             uint4 *dst = reinterpret_cast<uint4 *>(out + A);
-            const uint4 *src = s_buf + (A - abase) / 16;
-            for (int64_t q = threadIdx.x; q < (B - A) / 16; q += kBlock) dst[q] = src[q];
+            const uint4 *sb = s_buf + (A - abase) / 16;
+            for (int64_t q = threadIdx.x; q < (B - A) / 16; q += kBlock) dst[q] = sb[q];
         }
-        __syncthreads();  // s_buf reused by the next chunk
+        __syncthreads();  // s_buf reused by the next tile
     }
+    if (blockIdx.x == 0 && threadIdx.x == 0) off[m] = base_of[ntiles];
 }
+
+// decode: packets [c0, c0 + kEncPer) per workgroup (LDS staging below)
+constexpr int kEncJ = 4, kEncPer = kBlock * kEncJ;
+constexpr int kEncLds = (kEncPer * kMaxPkt + 32 + 15) / 16;  // uint4 words
 
 struct DecOut {
     int8_t *status;
@@ -303,28 +407,39 @@ int swarm_codec_encode(swarm_ctx *ctx, int64_t m, const int64_t *type, const int
         return SWARM_OK;
     }
     const EncIn in{type, sender, tick, task, winner, a, b};
-    int64_t *len;
-    SW_ALLOC(len, ctx, S_TMP1, size_t(m + 1) * 8);
+    const int64_t ntiles = (m + kTile - 1) / kTile;
+    uint8_t *tmp;
+    int64_t *tt;
+    SW_ALLOC(tmp, ctx, S_TMP0, size_t(ntiles) * kTileBytes);
+    SW_ALLOC(tt, ctx, S_TMP1, size_t(m) * 2 + size_t(2 * ntiles + 2) * 8 + 64);
+    int64_t *base = tt + ntiles;
+    unsigned *err = reinterpret_cast<unsigned *>(base + ntiles + 1);
+    uint16_t *loc = reinterpret_cast<uint16_t *>(err + 16);
     const unsigned codec_wgs = swarm::codec_grid_cap();
-    const unsigned grid = grid_for(m, kBlock, codec_wgs);
-    hipLaunchKernelGGL(k_enc_len, dim3(grid), dim3(kBlock), 0, s, m, in, int(wide != 0), len, status);
+    const unsigned grid = grid_for(ntiles, 1, codec_wgs);
+    hipLaunchKernelGGL(k_enc_tile, dim3(grid), dim3(kBlock), 0, s, m, in, int(wide != 0), status, loc, tmp, tt);
     SW_LAUNCHED();
-    SW_HIP(hipMemsetAsync(len + m, 0, 8, s));
-    size_t tmp_bytes = 0;
-    SW_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, len, offsets, int(m + 1), s));
-    void *tmp;
-    SW_ALLOC(tmp, ctx, S_CUB_TMP, tmp_bytes);
-    SW_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, len, offsets, int(m + 1), s));
-    SW_HIP(hipMemcpyAsync(total_bytes, offsets + m, 8, hipMemcpyDeviceToHost, s));
+    hipLaunchKernelGGL(k_enc_base, dim3(1), dim3(1024), 0, s, ntiles, tt, base);
+    SW_LAUNCHED();
+    int64_t *host = static_cast<int64_t *>(pinned(ctx, 16));
+    if (!host) return SWARM_ERR_OOM;
+    if (out == nullptr) {  // sizing call: the lengths only
+        SW_HIP(hipMemcpyAsync(host, base + ntiles, 8, hipMemcpyDeviceToHost, s));
+        SW_HIP(hipStreamSynchronize(s));
+        *total_bytes = host[0];
+        return SWARM_OK;
+    }
+    SW_HIP(hipMemsetAsync(err, 0, 4, s));
+    hipLaunchKernelGGL(k_enc_place, dim3(grid), dim3(kBlock), 0, s, m, tmp, tt, base, loc, cap, offsets, out, err);
+    SW_LAUNCHED();
+    SW_HIP(hipMemcpyAsync(host, base + ntiles, 8, hipMemcpyDeviceToHost, s));
+    SW_HIP(hipMemcpyAsync(host + 1, err, 4, hipMemcpyDeviceToHost, s));
     SW_HIP(hipStreamSynchronize(s));
-    if (out == nullptr) return SWARM_OK;  // sizing call
-    if (cap < *total_bytes) {
-        set_error("output buffer holds %lld bytes, the packets need %lld", (long long)cap, (long long)*total_bytes);
+    *total_bytes = host[0];
+    if (reinterpret_cast<const unsigned *>(host + 1)[0]) {
+        set_error("output buffer holds %lld bytes, the packets need %lld", (long long)cap, (long long)host[0]);
         return SWARM_ERR_RANGE;
     }
-    hipLaunchKernelGGL(k_enc_write, dim3(grid_for(m, kEncPer, codec_wgs)), dim3(kBlock), 0, s, m, in, int(wide != 0),
-                       offsets, status, out);
-    SW_LAUNCHED();
     return SWARM_OK;
 }
 

@@ -433,7 +433,7 @@ __global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int
                                                 uint8_t *__restrict__ ob_out, const unsigned *__restrict__ pull,
                                                 Segs segs, double dt, double timeout,
                                                 double jitter, uint64_t seed, unsigned long long *__restrict__ counts,
-                                                int vec, unsigned long long *__restrict__ tr, NextMail im) {
+                                                int vec, unsigned long long *__restrict__ tr, NextMail im, int xg) {
     __shared__ unsigned s_cnt[4];
     __shared__ int s_ns;
     __shared__ int s_wave[kBlock / kWave];
@@ -460,7 +460,22 @@ __global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int
         const int kPerT = pulled ? kRecvChunk / 4 / kBlock : kRecvChunk / kBlock;  // agents per thread
         const int64_t unit = int64_t(kPerT) * kBlock;
         const int64_t nchunks = (n + unit - 1) / unit;
-        for (int64_t ck = pulled ? int64_t(blockIdx.x) : int64_t(rank); ck < nchunks; ck += nrole) {
+        // xg > 0: groups of xg chunks (4 xg units on a pulled tick) dealt round robin to the 8 XCDs
+        // (workgroup r runs on XCD r % 8 under round-robin dispatch), so a receiver's neighbours -- in the
+        // chunks around its own -- are mostly fetched into the L2 of the XCD that serves it
+        const int64_t me = pulled ? int64_t(blockIdx.x) : int64_t(rank);
+        const int64_t gsz = pulled ? 4 * int64_t(xg) : int64_t(xg);
+        const int64_t nl = nrole / 8, xcd = me % 8, l = me / 8;
+        for (int64_t q = xg ? l : me;; q += xg ? nl : nrole) {
+            int64_t ck = q;
+            if (xg) {
+                const int64_t gi = xcd + 8 * (q / gsz);
+                if (gi * gsz >= nchunks) break;
+                ck = gi * gsz + q % gsz;
+                if (ck >= nchunks) continue;
+            } else if (ck >= nchunks) {
+                break;
+            }
             span += unit;
             // thread: kPerT agents, a slice of mail word (ck * unit + threadIdx.x * kPerT) / 64
             const int64_t a0 = ck * unit + int64_t(threadIdx.x) * kPerT;
@@ -702,6 +717,13 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
     const int g_recv = int(std::max<int64_t>(
         1, std::min<int64_t>(nchunks_all, recv_env > 0 ? recv_env : std::max<int64_t>(1, int64_t(grid) / 2))));
     const unsigned tgrid = grid + unsigned(g_recv);  // k_tick: both roles
+    // the receive role's XCD-grouped chunk order (SWARM_TICK_XCD_GROUP chunks per group, 0 = plain
+    // grid stride); only when both role grids split evenly over the 8 XCDs
+    static const int xg_env = [] {
+        const char *e = getenv("SWARM_TICK_XCD_GROUP");
+        return e ? atoi(e) : 0;
+    }();
+    const int xg = (xg_env > 0 && g_recv % 8 == 0 && tgrid % 8 == 0) ? xg_env : 0;
     if (push) {  // mail bitmaps (nbuf buffers) + the pull flags (by tick, nbuf) after them
         SW_ALLOC(mw, ctx, S_FSM_MAIL, size_t(n_words) * 48 + 64);
         SW_ALLOC(from_base, ctx, S_FSM_FROM, size_t(n) * 8);
@@ -713,6 +735,23 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
         segs.rcap = (nchunks + g_recv - 1) / g_recv * kRecvChunk;
         segs.scap = std::max((ngroups + int64_t(grid) * kBlock - 1) / (int64_t(grid) * kBlock) * kBlock * kSweepV,
                              (nchunks + tgrid - 1) / tgrid * kRecvChunk);
+        if (xg) {  // the grouped order may deal a workgroup more chunks than the grid stride: its segment holds them
+            auto most = [&](int64_t nch, int64_t g, int64_t nrole) {  // max chunks of one workgroup
+                const int64_t ngr = (nch + g - 1) / g;
+                int64_t worst = 0;
+                for (int64_t x = 0; x < 8; ++x) {
+                    const int64_t full = ngr > x ? (ngr - 1 - x) / 8 + 1 : 0;  // groups of XCD x
+                    int64_t cx = full * g;
+                    if (full && (x + 8 * (full - 1)) == ngr - 1) cx -= ngr * g - nch;  // its last group is partial
+                    worst = std::max(worst, (cx + nrole / 8 - 1) / (nrole / 8));
+                }
+                return worst;
+            };
+            segs.rcap = std::max(segs.rcap, most(nchunks, xg, g_recv) * kRecvChunk);
+            const int64_t unit = kRecvChunk / 4, nunits = (n + unit - 1) / unit;
+            segs.scap = std::max(segs.scap, most(nunits, 4 * int64_t(xg), tgrid) * unit);
+            segs.rcap = std::max(segs.rcap, segs.scap);  // a pulled tick: the receive-role workgroups too
+        }
         const size_t seg_total = size_t(g_recv) * segs.rcap + size_t(grid) * segs.scap;
         SW_ALLOC(segs.base, ctx, S_FSM_SEND, seg_total * 4);
         pullf = reinterpret_cast<unsigned *>(mw + 6 * n_words);  // [nbuf] by tick: the tick pulls
@@ -744,7 +783,7 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
             hipLaunchKernelGGL(k_tick, dim3(tgrid), dim3(kBlock), 0, s, n, t, ids,
                                reinterpret_cast<const double2 *>(pos), row_ptr, col, tick_off, f, mail_of(t), ob_in,
                                ob_out, pullf + t % nbuf, segs, dt, timeout, jitter, seed, cnt,
-                               int(vec && (reinterpret_cast<uintptr_t>(ob_out) & 3) == 0), d_tr, im);
+                               int(vec && (reinterpret_cast<uintptr_t>(ob_out) & 3) == 0), d_tr, im, xg);
         } else {
             hipLaunchKernelGGL(k_tick_pull, dim3(grid), dim3(kBlock), 0, s, n, t, ids,
                                reinterpret_cast<const double2 *>(pos), row_ptr, col, tick_off, f, ob_in, ob_out, dt,

@@ -112,6 +112,7 @@ def test_gpu_matches_oracle_random(oracle_mod, wide):
     e = codec.encode(*f, wide=wide, device="cuda")
     np.testing.assert_array_equal(e.status.cpu().numpy(), st)
     np.testing.assert_array_equal(e.buf.cpu().numpy(), np.frombuffer(b"".join(pk), np.uint8))
+    np.testing.assert_array_equal(e.offsets.cpu().numpy(), np.concatenate([[0], np.cumsum([len(p) for p in pk])]))
     # decode: the encoded packets with malformed ones spliced in
     rng = np.random.default_rng(5)
     pk = [p for p in pk if p]
@@ -172,3 +173,29 @@ def test_gpu_empty_and_errors():
                                        _lib.ptr(buf), 10, _lib.ptr(off), _lib.ptr(st), ctypes.byref(tot),
                                        _lib.stream())
     assert rc == _lib.ERR_RANGE and tot.value == 56
+
+
+@pytest.mark.gpu
+def test_gpu_encode_sizing_call_and_tile_edges(oracle_mod):
+    """swarm_codec_encode with out = NULL returns the byte count only; message counts around the encode
+    tile (2 048) give the oracle's bytes and offsets."""
+    import ctypes
+
+    import torch
+    from swarm_amd import _lib, codec
+    for m in (1, 2047, 2048, 2049, 4096 + 17):
+        f = _random_msgs(m, 100 + m)
+        st, pk = oracle_mod.codec_encode_py(*f)
+        want = np.frombuffer(b"".join(pk), np.uint8)
+        e = codec.encode(*f, device="cuda")
+        np.testing.assert_array_equal(e.status.cpu().numpy(), st)
+        np.testing.assert_array_equal(e.buf.cpu().numpy(), want)
+        np.testing.assert_array_equal(e.offsets.cpu().numpy(), np.concatenate([[0], np.cumsum([len(p) for p in pk])]))
+        cols = [torch.as_tensor(np.asarray(v), device="cuda") for v in f]
+        cols = [c.double() if k in (3, 4) else c.long() for k, c in enumerate(cols)]
+        off = torch.empty(m + 1, dtype=torch.int64, device="cuda")
+        stt = torch.empty(m, dtype=torch.int8, device="cuda")
+        tot = ctypes.c_int64(-1)
+        _lib.check(_lib.lib().swarm_codec_encode(_lib.ctx(), m, *[_lib.ptr(c) for c in cols], 0, None, 0,
+                                                 _lib.ptr(off), _lib.ptr(stt), ctypes.byref(tot), _lib.stream()))
+        assert tot.value == len(want)
