@@ -80,30 +80,6 @@ __device__ __forceinline__ uint32_t get_u32(const uint8_t *p) {
     return (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | uint32_t(p[3]);
 }
 
-// Exclusive prefix over the workgroup of c (0 <= c < 2^B) and the total (every thread gets it).
-template <int B>
-__device__ __forceinline__ int block_excl_scan(int c, int &total, int *s_wave) {
-    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-    int ex = 0, tot = 0;
-#pragma unroll
-    for (int b = 0; b < B; ++b) {
-        const unsigned long long mk = __ballot((c >> b) & 1);
-        ex += int(__builtin_amdgcn_mbcnt_hi(uint32_t(mk >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mk), 0u))) << b;
-        tot += __popcll(mk) << b;
-    }
-    if (lane == 0) s_wave[wid] = tot;
-    __syncthreads();
-    int off = 0, all = 0;
-#pragma unroll
-    for (int q = 0; q < kBlock / kWave; ++q) {
-        off += q < wid ? s_wave[q] : 0;
-        all += s_wave[q];
-    }
-    __syncthreads();  // s_wave read by all
-    total = all;
-    return off + ex;
-}
-
 struct EncIn {
     const int64_t *type, *sender, *tick, *task, *winner;
     const double *a, *b;
@@ -148,65 +124,96 @@ __device__ __forceinline__ void write_packet(uint8_t *p, int ty, int64_t snd, in
 }
 
 // Encode in tiles (round 5): every field is read ONCE.
-//   k_enc_tile   a workgroup per tile of kTile messages: status and length per message (kTileJ
-//                slabs of 256, each a block scan of the lengths), the packets assembled in LDS at their
-//                tile-relative offsets, then the tile's packed bytes stored to scratch (16-byte stores),
-//                its total, and each message's tile-relative offset (u16);
+//   k_enc_tile   a workgroup per tile of kTile messages, each wave its own 512 consecutive ones: status
+//                and length per message (8 slabs of 64, a wave scan each -- no workgroup barrier), the
+//                packets assembled in the wave's LDS region at wave-relative offsets, then each wave's
+//                packed bytes stored to its scratch segment (16-byte stores), the wave totals, and each
+//                message's tile-relative offset (u16) once the tile's wave offsets are known;
 //   k_enc_base   one workgroup: exclusive scan of the tile totals -> each tile's base, the total;
-//   k_enc_place  a workgroup per tile: the scratch bytes staged in LDS at the output's 16-byte
-//                phase, stored at base (16-byte stores, partial head / tail bytewise), and the int64
-//                offsets base + local.
+//   k_enc_place  a workgroup per tile: the four wave segments staged in LDS at their tile offsets and the
+//                output's 16-byte phase, stored at base (16-byte stores, partial head / tail bytewise),
+//                and the int64 offsets base + local.
 // Per message: fields 56 B read once, status 1 B, local offset 2 + 2 B, the packet 3 x ~10 B (scratch
 // write, scratch read, output), offsets 8 B.  (Rounds 1-4: k_enc_len + hipCUB scan + host sync +
 // k_enc_write, the fields read twice: 0.40 ms at 10M messages.  A single kernel with a decoupled
-// look-back over 1 024-message chunks: 0.43 ms, the look-back chain the bound.)
+// look-back over 1 024-message chunks: 0.43 ms, the look-back chain the bound.  Round 5's first tiled
+// form scanned each 256-message slab across the workgroup, 16 barriers per tile: 0.338 ms.)
 constexpr int kTileJ = 8, kTile = kBlock * kTileJ, kMaxPkt = 17;
-constexpr int kTileBytes = kTile * kMaxPkt;             // scratch bytes per tile (wide worst case)
-constexpr int kTileLds = (kTileBytes + 16 + 15) / 16;   // uint4 words (+16: the output phase)
+constexpr int kWaveMsgs = kWave * kTileJ;                // 512 consecutive messages per wave
+constexpr int kWaveBytes = kWaveMsgs * kMaxPkt;          // 8 704: its LDS region and scratch segment
+constexpr int kTileBytes = kTile * kMaxPkt;              // scratch bytes per tile (wide worst case)
+constexpr int kTileLds = (kTileBytes + 16 + 15) / 16;    // uint4 words (+16: the output phase)
+constexpr int kWavesT = kBlock / kWave;
 
 __global__ __launch_bounds__(kBlock) void k_enc_tile(int64_t m, EncIn in, int wide, int8_t *__restrict__ status,
                                                     uint16_t *__restrict__ loc, uint8_t *__restrict__ tmp,
-                                                    int64_t *__restrict__ tile_tot) {
+                                                    int32_t *__restrict__ wave_tot) {
     __shared__ uint4 s_buf[kTileLds];
-    __shared__ int s_wave[kBlock / kWave];
-    uint8_t *lb = reinterpret_cast<uint8_t *>(s_buf);
+    __shared__ int s_wt[kWavesT];
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    uint8_t *wl = reinterpret_cast<uint8_t *>(s_buf) + w * kWaveBytes;
     const int64_t ntiles = (m + kTile - 1) / kTile;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t c0 = tile * kTile;
-        int run = 0;  // workgroup-uniform: bytes of the slabs before this one
-#pragma unroll 2
+        const int64_t c0 = tile * kTile + int64_t(w) * kWaveMsgs;
+        int run = 0;  // wave-uniform: bytes of this wave's slabs so far
+        int wpos[kTileJ];
+#pragma unroll
         for (int j = 0; j < kTileJ; ++j) {
-            const int64_t i = c0 + j * kBlock + threadIdx.x;
+            const int64_t i = c0 + j * kWave + lane;
             const bool ok = i < m;
             const int64_t ty = ok ? in.type[i] : 0, snd = ok ? in.sender[i] : 0, tk = ok ? in.tick[i] : 0;
             const double fa = ok ? in.a[i] : 0.0, fb = ok ? in.b[i] : 0.0;
             const int64_t task = ok ? in.task[i] : 0, win = ok ? in.winner[i] : 0;
             int len = 0;
             const int st = ok ? enc_status(ty, snd, tk, fa, fb, task, win, wide, &len) : 3;
-            int total;
-            const int pos = run + block_excl_scan<5>(len, total, s_wave);
+            int total = 0, ex = 0;
+#pragma unroll
+            for (int b = 0; b < 5; ++b) {  // wave exclusive scan of len (< 32): ballots + mbcnt
+                const unsigned long long mk = __ballot((len >> b) & 1);
+                ex += int(__builtin_amdgcn_mbcnt_hi(uint32_t(mk >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mk), 0u))) << b;
+                total += __popcll(mk) << b;
+            }
+            wpos[j] = run + ex;
             if (ok) {
                 status[i] = int8_t(st);
-                loc[i] = uint16_t(pos);
-                if (st == 0) write_packet(lb + pos, int(ty), snd, tk, fa, fb, task, win, wide);
+                if (st == 0) write_packet(wl + run + ex, int(ty), snd, tk, fa, fb, task, win, wide);
             }
             run += total;
         }
-        __syncthreads();  // the tile's packets are in LDS
-        uint4 *dst = reinterpret_cast<uint4 *>(tmp + tile * int64_t(kTileBytes));
-        for (int q = threadIdx.x; q < (run + 15) / 16; q += kBlock) dst[q] = s_buf[q];
-        if (threadIdx.x == 0) tile_tot[tile] = run;
-        __syncthreads();  // s_buf reused by the next tile
+        __builtin_amdgcn_wave_barrier();  // the wave's packets are in its LDS region
+        uint4 *dst = reinterpret_cast<uint4 *>(tmp + tile * int64_t(kTileBytes) + w * kWaveBytes);
+        const uint4 *src = reinterpret_cast<const uint4 *>(wl);
+        for (int q = lane; q < (run + 15) / 16; q += kWave) dst[q] = src[q];
+        if (lane == 0) {
+            s_wt[w] = run;
+            wave_tot[tile * kWavesT + w] = run;
+        }
+        __syncthreads();
+        int wo = 0;
+#pragma unroll
+        for (int q = 0; q < kWavesT; ++q) wo += q < w ? s_wt[q] : 0;
+#pragma unroll
+        for (int j = 0; j < kTileJ; ++j) {
+            const int64_t i = c0 + j * kWave + lane;
+            if (i < m) loc[i] = uint16_t(wo + wpos[j]);
+        }
+        __syncthreads();  // s_buf / s_wt reused by the next tile
     }
 }
 
-// Exclusive scan of the tile totals (one workgroup): base[t], and base[ntiles] = the total.
-__global__ __launch_bounds__(1024) void k_enc_base(int64_t ntiles, const int64_t *__restrict__ tot,
+// Exclusive scan of the tile totals (one workgroup; a tile's total = its waves'): base[t], base[ntiles] = all.
+__global__ __launch_bounds__(1024) void k_enc_base(int64_t ntiles, const int32_t *__restrict__ wave_tot,
                                                   int64_t *__restrict__ base) {
     __shared__ int64_t s_part[1024];
+    auto tot = [&](int64_t q) {
+        int64_t v = 0;
+#pragma unroll
+        for (int w = 0; w < kWavesT; ++w) v += wave_tot[q * kWavesT + w];
+        return v;
+    };
     const int64_t per = (ntiles + 1023) / 1024, b = int64_t(threadIdx.x) * per;
     int64_t sum = 0;
-    for (int64_t q = b; q < b + per && q < ntiles; ++q) sum += tot[q];
+    for (int64_t q = b; q < b + per && q < ntiles; ++q) sum += tot(q);
     s_part[threadIdx.x] = sum;
     __syncthreads();
     for (int off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scan of the 1 024 parts
@@ -218,33 +225,45 @@ __global__ __launch_bounds__(1024) void k_enc_base(int64_t ntiles, const int64_t
     int64_t run = threadIdx.x ? s_part[threadIdx.x - 1] : 0;
     for (int64_t q = b; q < b + per && q < ntiles; ++q) {
         base[q] = run;
-        run += tot[q];
+        run += tot(q);
     }
     if (threadIdx.x == 1023) base[ntiles] = s_part[1023];
 }
 
 __global__ __launch_bounds__(kBlock) void k_enc_place(int64_t m, const uint8_t *__restrict__ tmp,
-                                                     const int64_t *__restrict__ tile_tot,
+                                                     const int32_t *__restrict__ wave_tot,
                                                      const int64_t *__restrict__ base_of,
                                                      const uint16_t *__restrict__ loc, int64_t cap,
                                                      int64_t *__restrict__ off, uint8_t *__restrict__ out,
                                                      unsigned *__restrict__ err) {
     __shared__ uint4 s_buf[kTileLds];
     uint8_t *lb = reinterpret_cast<uint8_t *>(s_buf);
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
     const int64_t ntiles = (m + kTile - 1) / kTile;
     if (base_of[ntiles] > cap) {  // the caller's buffer is too small: nothing is written
         if (blockIdx.x == 0 && threadIdx.x == 0) *err = 1u;
         return;
     }
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t c0 = tile * kTile, base = base_of[tile], n = tile_tot[tile];
-        const int ph = int(base & 15);  // the output's 16-byte phase: LDS byte ph + x holds out[base + x]
-        const uint4 *src = reinterpret_cast<const uint4 *>(tmp + tile * int64_t(kTileBytes));
-        for (int q = threadIdx.x; q < (n + 15) / 16; q += kBlock) {
-            const uint4 w = src[q];
-            const uint32_t v[4] = {w.x, w.y, w.z, w.w};
+        const int64_t c0 = tile * kTile, base = base_of[tile];
+        int wo = 0, n = 0, mine = 0;
 #pragma unroll
-            for (int k = 0; k < 16; ++k) lb[ph + 16 * q + k] = uint8_t(v[k >> 2] >> (8 * (k & 3)));
+        for (int q = 0; q < kWavesT; ++q) {
+            const int v = wave_tot[tile * kWavesT + q];
+            wo += q < w ? v : 0;
+            mine = q == w ? v : mine;
+            n += v;
+        }
+        // LDS byte ph + x holds out[base + x] (ph: the output's 16-byte phase); wave w stages its segment
+        const int ph = int(base & 15);
+        const uint4 *src = reinterpret_cast<const uint4 *>(tmp + tile * int64_t(kTileBytes) + w * kWaveBytes);
+        for (int q = lane; q < (mine + 15) / 16; q += kWave) {
+            const uint4 v4 = src[q];
+            const uint32_t v[4] = {v4.x, v4.y, v4.z, v4.w};
+            const int lim = mine - 16 * q < 16 ? mine - 16 * q : 16;
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (k < lim) lb[ph + wo + 16 * q + k] = uint8_t(v[k >> 2] >> (8 * (k & 3)));
         }
 #pragma unroll 4
         for (int j = 0; j < kTileJ; ++j) {
@@ -409,17 +428,17 @@ int swarm_codec_encode(swarm_ctx *ctx, int64_t m, const int64_t *type, const int
     const EncIn in{type, sender, tick, task, winner, a, b};
     const int64_t ntiles = (m + kTile - 1) / kTile;
     uint8_t *tmp;
-    int64_t *tt;
+    int32_t *wt;
     SW_ALLOC(tmp, ctx, S_TMP0, size_t(ntiles) * kTileBytes);
-    SW_ALLOC(tt, ctx, S_TMP1, size_t(m) * 2 + size_t(2 * ntiles + 2) * 8 + 64);
-    int64_t *base = tt + ntiles;
+    SW_ALLOC(wt, ctx, S_TMP1, size_t(m) * 2 + size_t(ntiles) * kWavesT * 4 + size_t(ntiles + 1) * 8 + 128);
+    int64_t *base = reinterpret_cast<int64_t *>(wt + ((size_t(ntiles) * kWavesT + 1) & ~size_t(1)));
     unsigned *err = reinterpret_cast<unsigned *>(base + ntiles + 1);
     uint16_t *loc = reinterpret_cast<uint16_t *>(err + 16);
     const unsigned codec_wgs = swarm::codec_grid_cap();
     const unsigned grid = grid_for(ntiles, 1, codec_wgs);
-    hipLaunchKernelGGL(k_enc_tile, dim3(grid), dim3(kBlock), 0, s, m, in, int(wide != 0), status, loc, tmp, tt);
+    hipLaunchKernelGGL(k_enc_tile, dim3(grid), dim3(kBlock), 0, s, m, in, int(wide != 0), status, loc, tmp, wt);
     SW_LAUNCHED();
-    hipLaunchKernelGGL(k_enc_base, dim3(1), dim3(1024), 0, s, ntiles, tt, base);
+    hipLaunchKernelGGL(k_enc_base, dim3(1), dim3(1024), 0, s, ntiles, wt, base);
     SW_LAUNCHED();
     int64_t *host = static_cast<int64_t *>(pinned(ctx, 16));
     if (!host) return SWARM_ERR_OOM;
@@ -430,7 +449,7 @@ int swarm_codec_encode(swarm_ctx *ctx, int64_t m, const int64_t *type, const int
         return SWARM_OK;
     }
     SW_HIP(hipMemsetAsync(err, 0, 4, s));
-    hipLaunchKernelGGL(k_enc_place, dim3(grid), dim3(kBlock), 0, s, m, tmp, tt, base, loc, cap, offsets, out, err);
+    hipLaunchKernelGGL(k_enc_place, dim3(grid), dim3(kBlock), 0, s, m, tmp, wt, base, loc, cap, offsets, out, err);
     SW_LAUNCHED();
     SW_HIP(hipMemcpyAsync(host, base + ntiles, 8, hipMemcpyDeviceToHost, s));
     SW_HIP(hipMemcpyAsync(host + 1, err, 4, hipMemcpyDeviceToHost, s));

@@ -26,12 +26,7 @@ namespace {
 
 constexpr int kObsLds = 1024;  // obstacles staged in LDS per pass (3 doubles each)
 constexpr int kNb = 4;         // neighbour positions gathered in flight per thread (8 waves/SIMD: 4 beats 8 at 4 waves)
-constexpr int kSortBins = 64;  // k_physics<SORT>: neighbour-count bins (longer rows share the last)
 
-// SORT: each workgroup's 256 agents are dealt to its lanes in order of their neighbour counts (an LDS
-// counting sort per tile), so a wave's rows have similar lengths and its row loop idles fewer lanes;
-// every agent's arithmetic is unchanged (bit-exact), only which lane runs it.
-template <bool SORT>
 __global__ __launch_bounds__(kBlock, 8) void k_physics(int64_t n, const int32_t *__restrict__ ids,
                                                    const uint8_t *__restrict__ state,
                                                    const int32_t *__restrict__ leader,
@@ -42,32 +37,9 @@ __global__ __launch_bounds__(kBlock, 8) void k_physics(int64_t n, const int32_t 
                                                    const int32_t *__restrict__ col, double dt, double max_speed,
                                                    unsigned long long *__restrict__ singular) {
     __shared__ double s_obs[kObsLds * 3];
-    __shared__ int s_hist[kSortBins], s_order[SORT ? kBlock : 1];
     unsigned long long sing = 0;
     for (int64_t base = int64_t(blockIdx.x) * kBlock; base < n; base += int64_t(gridDim.x) * kBlock) {
-        int64_t i = base + threadIdx.x;
-        if constexpr (SORT) {  // lane <- the agent of this tile with the threadIdx.x-th shortest row
-            if (threadIdx.x < kSortBins) s_hist[threadIdx.x] = 0;
-            __syncthreads();
-            const int deg = i < n ? rp[i + 1] - rp[i] : 0;
-            const int bin = deg < kSortBins ? deg : kSortBins - 1;
-            const int slot = atomicAdd(&s_hist[bin], 1);  // order within a bin is free
-            __syncthreads();
-            if (threadIdx.x < 64) {  // exclusive scan of the bins by one wave
-                int v = threadIdx.x < kSortBins ? s_hist[threadIdx.x] : 0;
-                int x = v;
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const int y = __shfl_up(x, o, 64);
-                    if ((threadIdx.x & 63) >= o) x += y;
-                }
-                if (threadIdx.x < kSortBins) s_hist[threadIdx.x] = x - v;
-            }
-            __syncthreads();
-            s_order[s_hist[bin] + slot] = int(threadIdx.x);
-            __syncthreads();
-            i = base + s_order[threadIdx.x];
-        }
+        const int64_t i = base + threadIdx.x;
         const bool valid = i < n;
         double px = 0, py = 0, frx = 0.0, fry = 0.0;
         bool moving = false;
@@ -189,12 +161,7 @@ int swarm_physics_step(swarm_ctx *ctx, int64_t n, const int32_t *ids, const uint
     unsigned long long *d_sing;
     SW_ALLOC(d_sing, ctx, S_TMP0, 64);
     SW_HIP(hipMemsetAsync(d_sing, 0, 8, s));
-    static const int sort = [] {  // SWARM_PHYSICS_SORT=0: lanes in storage order (A/B aid)
-        const char *e = getenv("SWARM_PHYSICS_SORT");
-        return e ? atoi(e) : 1;
-    }();
-    auto kern = sort ? k_physics<true> : k_physics<false>;
-    hipLaunchKernelGGL(kern, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, n, ids, state, leader_index,
+    hipLaunchKernelGGL(k_physics, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, n, ids, state, leader_index,
                        reinterpret_cast<const double2 *>(pos_in), reinterpret_cast<double2 *>(pos_out),
                        reinterpret_cast<double2 *>(vel), reinterpret_cast<double2 *>(target), has_target, m, obstacles,
                        row_ptr, col, dt, max_speed, d_sing);
