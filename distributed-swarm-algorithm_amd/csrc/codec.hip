@@ -39,7 +39,8 @@ __device__ __forceinline__ bool f32_ok(double v) { return !std::isfinite(v) || s
 __device__ __forceinline__ int enc_status(int64_t ty, int64_t snd, int64_t tick, double a, double b, int64_t task,
                                           int64_t win, int wide, int *len) {
     const int hdr = wide ? 9 : 6;
-    bool (*id_ok)(int64_t) = wide ? u32_ok : u8_ok;
+    const auto id_ok = [wide](int64_t v) { return wide ? u32_ok(v) : u8_ok(v); };  // (a function pointer here
+    // compiled to an indirect call: SGPR spills and no inlining in the encode kernels)
     int st = 0, pl = 0;
     switch (int(ty)) {
         case T_HB:  // payload '!ff' first
@@ -138,9 +139,12 @@ __device__ __forceinline__ void write_packet(uint8_t *p, int ty, int64_t snd, in
 // k_enc_write, the fields read twice: 0.40 ms at 10M messages.  A single kernel with a decoupled
 // look-back over 1 024-message chunks: 0.43 ms, the look-back chain the bound.  Round 5's first tiled
 // form scanned each 256-message slab across the workgroup, 16 barriers per tile: 0.338 ms.)
-constexpr int kTileJ = 8, kTile = kBlock * kTileJ, kMaxPkt = 17;
-constexpr int kWaveMsgs = kWave * kTileJ;                // 512 consecutive messages per wave
-constexpr int kWaveBytes = kWaveMsgs * kMaxPkt;          // 8 704: its LDS region and scratch segment
+#ifndef SWARM_ENC_TILEJ
+#define SWARM_ENC_TILEJ 4  // slabs of 64 per wave (A/B builds: -DSWARM_ENC_TILEJ=8, tools/build_variant.sh; profiles/r5/ab_r5g.log)
+#endif
+constexpr int kTileJ = SWARM_ENC_TILEJ, kTile = kBlock * kTileJ, kMaxPkt = 17;
+constexpr int kWaveMsgs = kWave * kTileJ;                // 256 consecutive messages per wave (kTileJ 4)
+constexpr int kWaveBytes = kWaveMsgs * kMaxPkt;          // 4 352: its LDS region and scratch segment
 constexpr int kTileBytes = kTile * kMaxPkt;              // scratch bytes per tile (wide worst case)
 constexpr int kTileLds = (kTileBytes + 16 + 15) / 16;    // uint4 words (+16: the output phase)
 constexpr int kWavesT = kBlock / kWave;

@@ -540,8 +540,10 @@ int swarm_elect_sharded_ex(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *
         std::vector<hipEvent_t> &v;
         ~EvFree() { for (auto e : v) (void)hipEventDestroy(e); }
     } ev_free{ev};
-    if (round_ms) {
-        ev.resize(2 * kMaxBatch);
+    if (round_ms) {  // one event before every round of a batch and one after its last: round r's time is the
+                     // device time from its start to the next round's (launch gaps included, no second
+                     // event inside the round)
+        ev.resize(kMaxBatch + 1);
         for (auto &e : ev) SW_HIP(hipEventCreate(&e));
     }
     unsigned long long *lcnt = nullptr;  // this rank's counters of the batch, before the all-reduce
@@ -557,9 +559,8 @@ int swarm_elect_sharded_ex(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *
         const int tend = std::min(max_rounds, t + batch - 1);
         ctx->step_wr_agent = (!hist.empty() && hist.back() < il_min) ? 1 : 0;
         for (int r = t; r <= tend; ++r) {
-            if (round_ms) SW_HIP(hipEventRecord(ev[2 * (r - t)], s));
+            if (round_ms) SW_HIP(hipEventRecord(ev[r - t], s));
             if ((rc = frontier_round_stepper(ctx, r, sh->row_ptr, sh->col, leader0, leader1, s))) return rc;
-            if (round_ms) SW_HIP(hipEventRecord(ev[2 * (r - t) + 1], s));
             if (r % depth || comm->nranks == 1) continue;  // deep halo: ghosts are stepped locally between exchanges
             // every rank takes part in every exchange, peers or not (the shared-memory ops are barriers)
             int32_t *Lcur = (r & 1) ? leader1 : leader0;
@@ -586,6 +587,7 @@ int swarm_elect_sharded_ex(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *
                 return rc;
         }
         const int nr = tend - t + 1;
+        if (round_ms) SW_HIP(hipEventRecord(ev[nr], s));
         if ((rc = frontier_round_totals(ctx, t, tend, dtot, s))) return rc;
         if (lcnt) {
             SW_HIP(hipMemcpyAsync(lcnt, dtot, size_t(nr) * kC * 8, hipMemcpyDeviceToDevice, s));
@@ -606,7 +608,7 @@ int swarm_elect_sharded_ex(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *
                 local_counts[size_t(r - 1) * 3 + 1] = dn ? sh->n_all : int64_t(q[1]);
                 local_counts[size_t(r - 1) * 3 + 2] = dn ? -1 : int64_t(q[2]);  // -1: all the shard's edges
             }
-            if (round_ms) SW_HIP(hipEventElapsedTime(&round_ms[r - 1], ev[2 * (r - t)], ev[2 * (r - t) + 1]));
+            if (round_ms) SW_HIP(hipEventElapsedTime(&round_ms[r - 1], ev[r - t], ev[r - t + 1]));
             const unsigned long long c = h[size_t(r - t) * kC];  // C_CHG: owned changes
             hist.push_back(int64_t(c));
             if (changes_host) changes_host[r - 1] = int64_t(c);

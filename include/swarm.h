@@ -263,8 +263,9 @@ int swarm_elect_sharded(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *sha
                         int32_t *rounds_exec, int64_t *changes_per_round, void *stream);
 /* swarm_elect_sharded with this rank's own per-round figures (each optional, host, capacity max_rounds):
  * local_counts[3 (r-1) + {0,1,2}] = round r's owned changes, rows gathered and edges gathered on this rank
- * (a dense round: n_all rows and -1 = every edge of the shard graph); round_ms[r-1] = the device time of
- * round r's launch on this rank (HIP events; the per-round cost model of DESIGN §6 is fitted from them).
+ * (a dense round: n_all rows and -1 = every edge of the shard graph); round_ms[r-1] = the device time from
+ * the start of round r to the start of round r+1 on this rank (one HIP event per round; the per-round cost
+ * model of DESIGN §6 is fitted from them).
  * comm may be NULL for a shard without peers (one rank: the shard graph stepped alone). */
 int swarm_elect_sharded_ex(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *shard,
                            int32_t *leader0, int32_t *leader1, int32_t max_rounds,

@@ -28,3 +28,19 @@ def test_headline_pmc_entry():
     assert got is not None
     assert got[0] == d[keys[0]]["hbm_bytes_per_dispatch"]
     assert latest in got[1]
+
+
+def test_c5_defaults(monkeypatch):
+    """C5: 100M agents split over the ranks, the union-oracle check on by default (a rehearsal or a real
+    N-GPU run prints whether every rank's result equals the oracle's), the other rows off; C3 leaves the
+    (slow) union check off."""
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--config", "C5"])
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    a = bench.parse()
+    assert a.agents == 12_500_000 and a.oracle_check == 1 and a.rows == 0 and a.model == 1
+    assert a.partition == "strips"
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--config", "C5", "--partition", "blocks"])
+    assert bench.parse().partition == "blocks"
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8"])
+    a = bench.parse()
+    assert a.agents == 10_000_000 and a.oracle_check == 0 and a.rows == 1
