@@ -443,6 +443,42 @@ def _roof(alg_bytes, ms, kernel, pmc_kernel=None, note=None):
     return out
 
 
+def _codec_abi_ms(f, enc, m, pk, dev):
+    """Best-of-5 wall ms of swarm_codec_encode and swarm_codec_decode through the C-ABI, outputs
+    preallocated; both results checked against the wrapper's."""
+    import ctypes
+
+    import torch
+    from swarm_amd import _lib
+    L, P = _lib.lib(), _lib.ptr
+    off = torch.empty(m + 1, dtype=torch.int64, device=dev)
+    st = torch.empty(m, dtype=torch.int8, device=dev)
+    buf = torch.empty(pk, dtype=torch.uint8, device=dev)
+    tot = ctypes.c_int64()
+    with torch.cuda.device(dev):
+        ms_e, _ = _timed(lambda: _lib.check(L.swarm_codec_encode(
+            _lib.ctx(), m, *[P(t) for t in f], 0, P(buf), pk, P(off), P(st), ctypes.byref(tot), _lib.stream())),
+            reps=5)
+        assert tot.value == pk and torch.equal(buf, enc.buf) and torch.equal(off, enc.offsets)
+        cols = {k: torch.empty(m, dtype=dt, device=dev) for k, dt in (
+            ("status", torch.int8), ("type", torch.int64), ("sender", torch.int64), ("tick", torch.int64),
+            ("a", torch.float32), ("b", torch.float32), ("task", torch.int64), ("winner", torch.int64),
+            ("has_pos", torch.uint8))}
+        ms_d, _ = _timed(lambda: _lib.check(L.swarm_codec_decode(
+            _lib.ctx(), m, P(buf), pk, P(off), 0, *[P(cols[k]) for k in (
+                "status", "type", "sender", "tick", "a", "b", "task", "winner", "has_pos")], _lib.stream())), reps=5)
+        assert torch.equal(cols["type"][st == 0], f[0][st == 0])
+    return ms_e, ms_d
+
+
+def _enc_kernels():
+    """The encode's kernels (label, PMC names): the one-pass form, or the three-launch form when
+    SWARM_ENC_PASSES=3 selects it."""
+    if os.environ.get("SWARM_ENC_PASSES") == "3":
+        return "k_enc_tile + k_enc_base + k_enc_place", ["k_enc_tile", "k_enc_base", "k_enc_place"]
+    return "k_enc_one (one pass, tile bases by decoupled look-back)", ["k_enc_one<2>"]
+
+
 def rows_bench(sw, dev, args):
     """One measurement per SURVEY §8 row beside the headline (C3): C2 election, C4 auction,
     f1 physics, f2 timer FSM ticks, f3 codec -- each with its roofline figure and its CPU
@@ -534,14 +570,19 @@ def rows_bench(sw, dev, args):
     ms_e, enc = _timed(lambda: codec.encode(*f, device=dev), reps=3)
     ms_d, _ = _timed(lambda: codec.decode(enc.buf, enc.offsets, device=dev), reps=3)
     pk = enc.total_bytes
-    rows["f3_codec"] = {"messages": m, "bytes": pk, "encode_ms": ms_e, "decode_ms": ms_d,
-                        "encode_msgs_per_s": m / (ms_e * 1e-3), "decode_msgs_per_s": m / (ms_d * 1e-3),
-                        "roofline_encode": _roof(65.0 * m + 8.0 + pk, ms_e, "k_enc_tile + k_enc_base + k_enc_place",
-                                                 ["k_enc_tile", "k_enc_base", "k_enc_place"],
+    # the C-ABI calls themselves (swarm_codec_encode / _decode into preallocated outputs: what a caller
+    # that keeps its buffers pays; the Python wrappers above add their allocations and argument checks)
+    ms_ec, ms_dc = _codec_abi_ms(f, enc, m, pk, dev)
+    rows["f3_codec"] = {"messages": m, "bytes": pk, "encode_ms": ms_ec, "decode_ms": ms_dc,
+                        "encode_ms_python": ms_e, "decode_ms_python": ms_d,
+                        "encode_msgs_per_s": m / (ms_ec * 1e-3), "decode_msgs_per_s": m / (ms_dc * 1e-3),
+                        "timing": "wall clock per synchronised C-ABI call into preallocated buffers, best of 5 "
+                                  "(*_ms_python: the swarm_amd.codec wrappers, which allocate their outputs)",
+                        "roofline_encode": _roof(65.0 * m + 8.0 + pk, ms_ec, *_enc_kernels(),
                                                  note="compulsory bytes only: the 7 fields read once (56 B), status 1 B "
                                                       "and the int64 offsets 8 B written per message, the packet "
                                                       "bytes written; the call's final host sync included"),
-                        "roofline_decode": _roof(66.0 * m + pk, ms_d, "k_decode", "k_decode",
+                        "roofline_decode": _roof(66.0 * m + pk, ms_dc, "k_decode", "k_decode",
                                                  note="offsets 16 B + fields written 50 B per packet + packet bytes")}
     if cpu:
         mc = 200_000

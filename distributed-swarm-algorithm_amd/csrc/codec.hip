@@ -7,9 +7,10 @@
 // winner (322, 325) -- and parses inbound packets in on_message_received (agent.py:197-214).
 // These kernels do both for a whole batch of messages (one thread per message / packet; a
 // byte-moving, HBM-bound job: no arithmetic worth the name):
-//   encode  status + length per message, packets assembled per tile of 2 048 messages (the fields
-//           read once), tile bases by a scan of the tile totals, then each tile's bytes placed
-//           (k_enc_tile / k_enc_base / k_enc_place below).  Errors as the reference raises them, payload
+//   encode  one pass (k_enc_one below): a workgroup per tile of 2 048 messages reads the fields once,
+//           computes status + length, finds the tile's byte offset by a decoupled look-back over the
+//           lower tiles' published counts, and stores packets, status and offsets (the three-launch
+//           tile / base / place form stays as SWARM_ENC_PASSES=3).  Errors as the reference raises them, payload
 //           first (it packs the payload before _send_msg packs the header): an out-of-range
 //           integer field -> struct.error (status 1), a finite value beyond the f32 range ->
 //           OverflowError (status 2); an unknown type -> status 3.  Errored messages take no
@@ -124,6 +125,44 @@ __device__ __forceinline__ void write_packet(uint8_t *p, int ty, int64_t snd, in
     }
 }
 
+// The same bytes from the fields already narrowed to their wire types (status 0: every value in range).
+__device__ __forceinline__ void write_packet_n(uint8_t *p, int ty, uint32_t snd, uint32_t tick, float a, float b,
+                                               uint32_t task, uint32_t win, int wide) {
+    p[0] = uint8_t(ty);
+    int h;
+    if (wide) {
+        put_u32(p + 1, snd);
+        put_u32(p + 5, tick);
+        h = 9;
+    } else {
+        p[1] = uint8_t(snd);
+        put_u32(p + 2, tick);
+        h = 6;
+    }
+    p += h;
+    switch (ty) {
+        case T_HB:
+            put_u32(p, __float_as_uint(a));
+            put_u32(p + 4, __float_as_uint(b));
+            break;
+        case T_ACCLAIM:
+            if (wide) put_u32(p, snd);
+            else p[0] = uint8_t(snd);
+            break;
+        case T_CLAIM:
+            put_u32(p, task);
+            put_u32(p + 4, __float_as_uint(a));
+            break;
+        case T_CONFLICT:
+            put_u32(p, task);
+            if (wide) put_u32(p + 4, win);
+            else p[4] = uint8_t(win);
+            break;
+        default:
+            break;
+    }
+}
+
 // Encode in tiles (round 5): every field is read ONCE.
 //   k_enc_tile   a workgroup per tile of kTile messages, each wave its own 512 consecutive ones: status
 //                and length per message (8 slabs of 64, a wave scan each -- no workgroup barrier), the
@@ -142,14 +181,19 @@ __device__ __forceinline__ void write_packet(uint8_t *p, int ty, int64_t snd, in
 #ifndef SWARM_ENC_TILEJ
 #define SWARM_ENC_TILEJ 4  // slabs of 64 per wave (A/B builds: -DSWARM_ENC_TILEJ=8, tools/build_variant.sh; profiles/r5/ab_r5g.log)
 #endif
-constexpr int kTileJ = SWARM_ENC_TILEJ, kTile = kBlock * kTileJ, kMaxPkt = 17;
+#ifndef SWARM_ENC_BLOCK
+#define SWARM_ENC_BLOCK 512  // threads per encode workgroup: 8 waves, 2 048-message tiles (A/B: -DSWARM_ENC_BLOCK=256)
+#endif
+constexpr int kEB = SWARM_ENC_BLOCK;
+constexpr int kTileJ = SWARM_ENC_TILEJ, kTile = kEB * kTileJ, kMaxPkt = 17;
 constexpr int kWaveMsgs = kWave * kTileJ;                // 256 consecutive messages per wave (kTileJ 4)
 constexpr int kWaveBytes = kWaveMsgs * kMaxPkt;          // 4 352: its LDS region and scratch segment
 constexpr int kTileBytes = kTile * kMaxPkt;              // scratch bytes per tile (wide worst case)
 constexpr int kTileLds = (kTileBytes + 16 + 15) / 16;    // uint4 words (+16: the output phase)
-constexpr int kWavesT = kBlock / kWave;
+constexpr int kWavesT = kEB / kWave;
+static_assert(kTileBytes < 65536, "tile-relative packet offsets are u16 (k_enc_tile)");
 
-__global__ __launch_bounds__(kBlock) void k_enc_tile(int64_t m, EncIn in, int wide, int8_t *__restrict__ status,
+__global__ __launch_bounds__(kEB) void k_enc_tile(int64_t m, EncIn in, int wide, int8_t *__restrict__ status,
                                                     uint16_t *__restrict__ loc, uint8_t *__restrict__ tmp,
                                                     int32_t *__restrict__ wave_tot) {
     __shared__ uint4 s_buf[kTileLds];
@@ -234,7 +278,7 @@ __global__ __launch_bounds__(1024) void k_enc_base(int64_t ntiles, const int32_t
     if (threadIdx.x == 1023) base[ntiles] = s_part[1023];
 }
 
-__global__ __launch_bounds__(kBlock) void k_enc_place(int64_t m, const uint8_t *__restrict__ tmp,
+__global__ __launch_bounds__(kEB) void k_enc_place(int64_t m, const uint8_t *__restrict__ tmp,
                                                      const int32_t *__restrict__ wave_tot,
                                                      const int64_t *__restrict__ base_of,
                                                      const uint16_t *__restrict__ loc, int64_t cap,
@@ -271,24 +315,277 @@ __global__ __launch_bounds__(kBlock) void k_enc_place(int64_t m, const uint8_t *
         }
 #pragma unroll 4
         for (int j = 0; j < kTileJ; ++j) {
-            const int64_t i = c0 + j * kBlock + threadIdx.x;
+            const int64_t i = c0 + j * kEB + threadIdx.x;
             if (i < m) off[i] = base + loc[i];
         }
         __syncthreads();
         const int64_t end = base + n, abase = base - ph;
         const int64_t A = (base + 15) & ~int64_t(15), B = end & ~int64_t(15);
         if (A >= B) {
-            for (int64_t x = base + threadIdx.x; x < end; x += kBlock) out[x] = lb[x - abase];
+            for (int64_t x = base + threadIdx.x; x < end; x += kEB) out[x] = lb[x - abase];
         } else {
             if (threadIdx.x < A - base) out[base + threadIdx.x] = lb[base + threadIdx.x - abase];
             if (threadIdx.x < end - B) out[B + threadIdx.x] = lb[B + threadIdx.x - abase];
             uint4 *dst = reinterpret_cast<uint4 *>(out + A);
             const uint4 *sb = s_buf + (A - abase) / 16;
-            for (int64_t q = threadIdx.x; q < (B - A) / 16; q += kBlock) dst[q] = sb[q];
+            for (int64_t q = threadIdx.x; q < (B - A) / 16; q += kEB) dst[q] = sb[q];
         }
         __syncthreads();  // s_buf reused by the next tile
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) off[m] = base_of[ntiles];
+}
+
+// One-pass encode (round 5): a workgroup per tile, the tile's base by a decoupled look-back.
+// The tile comes from a ticket (an atomic counter, reset by the workgroup that draws the last one), so
+// every lower tile belongs to a workgroup that is already running and publishes its byte count without
+// waiting for anything: the look-back always ends.
+// A tile's word, one 8-byte agent-scope atomic (no other data is handed over, so no fence):
+//   bits 63..40 epoch (the call), 39..38 state (1 = this tile's count, 2 = inclusive prefix), 37..0 value.
+// Order inside a workgroup: fields -> status + lengths (wave scans) -> the tile count published -> the
+// packets assembled in LDS at tile offsets (the fields narrowed to wire types, then dead) -> wave 0 walks
+// back while the others wait -> offsets, and the packets stored with 16-byte stores shifted to the output's
+// byte phase.  Per message the compulsory bytes only: fields once, status, the int64 offset, the packet
+// (PMC 760 MB at 10M messages against 754 MB compulsory, profiles/r5/codec_*).
+// Measured and kept at their defaults (profiles/r5/ab_r5k.log, ab_r5l.log, 10M messages): one look-back
+// word per lane and poll -- 4 or 8 (wider windows, contiguous or strided) were slower, 0.255-0.34 ms per
+// call against 0.218, each poll's extra agent-coherent loads costing more than the round trips they save;
+// the sleep between polls (1, 8, 32) makes no difference.  Tiles (ab_r5m.log, ab_r5n.log): 2 048 messages
+// on 8 waves 0.201-0.204 ms, 1 024 on 4 (or on 8) 0.217-0.219, 4 096 on 16 0.207, 512 on 4 0.29.
+#ifndef SWARM_ENC_LB_PER
+#define SWARM_ENC_LB_PER 1  // look-back words per lane and poll (A/B builds: -DSWARM_ENC_LB_PER=4)
+#endif
+#ifndef SWARM_ENC_LB_SLEEP
+#define SWARM_ENC_LB_SLEEP 1  // s_sleep between polls (units of 64 cycles)
+#endif
+constexpr int kLbShift = 40, kLbStateShift = 38, kLbPer = SWARM_ENC_LB_PER;
+constexpr unsigned long long kLbValue = (1ull << kLbStateShift) - 1;
+
+__device__ __forceinline__ unsigned long long lb_word(uint32_t epoch, unsigned state, unsigned long long v) {
+    return (static_cast<unsigned long long>(epoch) << kLbShift) |
+           (static_cast<unsigned long long>(state) << kLbStateShift) | v;
+}
+
+// P consecutive messages per lane and slab (P = 2: 16-byte field loads and offset stores, for 16-byte
+// aligned arrays; the 8-byte accesses of P = 1 move data at ~0.6x the 16-byte rate).
+#ifdef SWARM_ENC_WPE  // A/B builds: a minimum of waves per SIMD for the one-pass kernel
+#define SWARM_ENC_ATTR __attribute__((amdgpu_waves_per_eu(SWARM_ENC_WPE)))
+#else
+#define SWARM_ENC_ATTR
+#endif
+template <int P>
+__global__ __launch_bounds__(kEB) SWARM_ENC_ATTR void k_enc_one(int64_t m, EncIn in, int wide, int8_t *__restrict__ status,
+                                                   int64_t *__restrict__ off, uint8_t *__restrict__ out, int64_t cap,
+                                                   unsigned long long *__restrict__ lb, uint32_t epoch,
+                                                   int64_t *__restrict__ total,
+                                                   unsigned *__restrict__ err) {
+    constexpr int J = kTileJ / P;  // slabs per wave, kWave * P messages each
+    static_assert(J * P == kTileJ, "slabs");
+    __shared__ uint4 s_buf[kTileLds];
+    __shared__ int s_wt[kWavesT];
+    __shared__ int64_t s_base;
+    __shared__ uint32_t s_tile;
+    uint8_t *lbuf = reinterpret_cast<uint8_t *>(s_buf);
+    unsigned *ticket = reinterpret_cast<unsigned *>(lb);  // word 0: the ticket counter; words 1.. the tiles
+    unsigned long long *word = lb + 1;
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    const int64_t ntiles = (m + kTile - 1) / kTile;
+    if (threadIdx.x == 0) {
+        const unsigned t = atomicAdd(ticket, 1u);
+        if (t == unsigned(ntiles - 1))  // the last ticket: every other one is taken, so reset for the next call
+            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_tile = t;
+    }
+    __syncthreads();
+    const int64_t tile = s_tile;
+    const int64_t c0 = tile * kTile + int64_t(w) * kWaveMsgs + int64_t(lane) * P;
+    int64_t ty[J][P], snd[J][P], tk[J][P], task[J][P], win[J][P];
+    double fa[J][P], fb[J][P];
+    int wpos[J][P], st[J][P];
+    int run = 0;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int64_t i = c0 + j * kWave * P;
+        if (P == 2 && i + 1 < m) {
+            const auto l2 = [&](const int64_t *p, int64_t *d) {
+                const longlong2 v = *reinterpret_cast<const longlong2 *>(p + i);
+                d[0] = v.x;
+                d[P - 1] = v.y;
+            };
+            const auto d2 = [&](const double *p, double *d) {
+                const double2 v = *reinterpret_cast<const double2 *>(p + i);
+                d[0] = v.x;
+                d[P - 1] = v.y;
+            };
+            l2(in.type, ty[j]);
+            l2(in.sender, snd[j]);
+            l2(in.tick, tk[j]);
+            d2(in.a, fa[j]);
+            d2(in.b, fb[j]);
+            l2(in.task, task[j]);
+            l2(in.winner, win[j]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < P; ++k) {
+                const bool ok = i + k < m;
+                ty[j][k] = ok ? in.type[i + k] : 0;
+                snd[j][k] = ok ? in.sender[i + k] : 0;
+                tk[j][k] = ok ? in.tick[i + k] : 0;
+                fa[j][k] = ok ? in.a[i + k] : 0.0;
+                fb[j][k] = ok ? in.b[i + k] : 0.0;
+                task[j][k] = ok ? in.task[i + k] : 0;
+                win[j][k] = ok ? in.winner[i + k] : 0;
+            }
+        }
+    }
+    // what the packets need, narrowed once the status is known (the int64 / f64 fields die here: 7 registers
+    // per message across the look-back instead of 14)
+    uint32_t nty[J][P], nsnd[J][P], ntk[J][P], ntask[J][P], nwin[J][P];
+    float nfa[J][P], nfb[J][P];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int64_t i = c0 + j * kWave * P;
+        int len = 0;  // the lane's P packets
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            int l = 0;
+            st[j][k] = i + k < m ? enc_status(ty[j][k], snd[j][k], tk[j][k], fa[j][k], fb[j][k], task[j][k],
+                                              win[j][k], wide, &l)
+                                 : 3;
+            wpos[j][k] = len;
+            len += l;
+            nty[j][k] = uint32_t(ty[j][k]);
+            nsnd[j][k] = uint32_t(snd[j][k]);
+            ntk[j][k] = uint32_t(tk[j][k]);
+            ntask[j][k] = uint32_t(task[j][k]);
+            nwin[j][k] = uint32_t(win[j][k]);
+            nfa[j][k] = float(fa[j][k]);
+            nfb[j][k] = float(fb[j][k]);
+        }
+        int tot = 0, ex = 0;
+#pragma unroll
+        for (int b = 0; b < (P == 1 ? 5 : 6); ++b) {  // wave exclusive scan of len (< 32 P): ballots + mbcnt
+            const unsigned long long mk = __ballot((len >> b) & 1);
+            ex += int(__builtin_amdgcn_mbcnt_hi(uint32_t(mk >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(mk), 0u))) << b;
+            tot += __popcll(mk) << b;
+        }
+#pragma unroll
+        for (int k = 0; k < P; ++k) wpos[j][k] += run + ex;
+        if (P == 2 && i + 1 < m) {
+            *reinterpret_cast<uint16_t *>(status + i) = uint16_t(uint8_t(st[j][0]) | (uint8_t(st[j][P - 1]) << 8));
+        } else {
+#pragma unroll
+            for (int k = 0; k < P; ++k)
+                if (i + k < m) status[i + k] = int8_t(st[j][k]);
+        }
+        run += tot;
+    }
+    if (lane == 0) s_wt[w] = run;
+    __syncthreads();
+    int wo = 0, n = 0;
+#pragma unroll
+    for (int q = 0; q < kWavesT; ++q) {
+        wo += q < w ? s_wt[q] : 0;
+        n += s_wt[q];
+    }
+    if (w == 0 && lane == 0)  // this tile's count, before anything else: the look-backs of later tiles wait on it
+        __hip_atomic_store(&word[tile], lb_word(epoch, tile ? 1u : 2u, unsigned(n)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (out) {  // the packets into LDS at their tile offsets (16-byte phase 0; the stores below shift them)
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+#pragma unroll
+            for (int k = 0; k < P; ++k)
+                if (st[j][k] == 0)  // (3 beyond m)
+                    write_packet_n(lbuf + wo + wpos[j][k], int(nty[j][k]), nsnd[j][k], ntk[j][k], nfa[j][k],
+                                   nfb[j][k], ntask[j][k], nwin[j][k], wide);
+    }
+    if (w == 0) {
+        int64_t excl = 0;
+        // a poll reads tiles j - L - 64 q (lane L, q = 0 .. kLbPer-1): each load instruction covers 64
+        // consecutive words (4 lines); the nearest inclusive word ends the walk
+        for (int64_t j = tile - 1; j >= 0;) {
+            unsigned long long v[kLbPer], incb[kLbPer];
+            unsigned okm = 0;  // bit q: word q valid
+#pragma unroll
+            for (int q = 0; q < kLbPer; ++q) {
+                const int64_t k = j - lane - int64_t(kWave) * q;
+                v[q] = k >= 0 ? __hip_atomic_load(&word[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : lb_word(epoch, 2u, 0);
+            }
+#pragma unroll
+            for (int q = 0; q < kLbPer; ++q) {
+                const unsigned sv = unsigned(v[q] >> kLbStateShift) & 3u;
+                const bool valid = uint32_t(v[q] >> kLbShift) == epoch && sv != 0;
+                okm |= unsigned(valid) << q;
+                incb[q] = __ballot(valid && sv == 2u);
+            }
+            int qq = kLbPer;  // the first q holding an inclusive word, and its nearest lane p
+#pragma unroll
+            for (int q = kLbPer - 1; q >= 0; --q)
+                if (incb[q]) qq = q;
+            const int p = qq < kLbPer ? __ffsll(static_cast<long long>(incb[qq])) - 1 : kWave - 1;
+            unsigned needm = 0;
+#pragma unroll
+            for (int q = 0; q < kLbPer; ++q)
+                needm |= unsigned(q < qq || (q == qq && lane <= p)) << q;
+            if (__ballot((okm & needm) != needm)) {  // a needed tile has not published yet
+                __builtin_amdgcn_s_sleep(SWARM_ENC_LB_SLEEP);
+                continue;
+            }
+            long long add = 0;
+#pragma unroll
+            for (int q = 0; q < kLbPer; ++q) add += (needm >> q) & 1u ? static_cast<long long>(v[q] & kLbValue) : 0;
+#pragma unroll
+            for (int d = 1; d < kWave; d <<= 1) add += __shfl_xor(add, d);
+            excl += add;
+            if (qq < kLbPer) break;
+            j -= int64_t(kWave) * kLbPer;
+        }
+        if (lane == 0) {
+            if (tile) __hip_atomic_store(&word[tile], lb_word(epoch, 2u, static_cast<unsigned long long>(excl + n)),
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_base = excl;
+            if (tile == ntiles - 1) {
+                *total = excl + n;
+                off[m] = excl + n;
+                *err = out && excl + n > cap ? 1u : 0u;
+            }
+        }
+    }
+    __syncthreads();
+    const int64_t base = s_base;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int64_t i = c0 + j * kWave * P;
+        if (P == 2 && i + 1 < m) {
+            *reinterpret_cast<longlong2 *>(off + i) = longlong2{base + wo + wpos[j][0], base + wo + wpos[j][P - 1]};
+        } else {
+#pragma unroll
+            for (int k = 0; k < P; ++k)
+                if (i + k < m) off[i + k] = base + wo + wpos[j][k];
+        }
+    }
+    if (!out || base + n > cap) return;  // sizing call, or a buffer too small (err set by the last tile)
+    // out[base + x] = lbuf[x]: bytewise head and tail, 16-byte stores between, each composed from five
+    // LDS dwords shifted by the tile's byte phase
+    const int64_t end = base + n;
+    const int64_t A = (base + 15) & ~int64_t(15), B = end & ~int64_t(15);
+    if (A >= B) {
+        for (int64_t x = base + threadIdx.x; x < end; x += kEB) out[x] = lbuf[x - base];
+        return;
+    }
+    if (threadIdx.x < A - base) out[base + threadIdx.x] = lbuf[threadIdx.x];
+    if (threadIdx.x < end - B) out[B + threadIdx.x] = lbuf[B - base + threadIdx.x];
+    const int s0 = int(A - base), r = s0 & 3;
+    const uint32_t *ld = reinterpret_cast<const uint32_t *>(s_buf) + (s0 >> 2);
+    uint4 *dst = reinterpret_cast<uint4 *>(out + A);
+    for (int q = threadIdx.x; q < int(B - A) / 16; q += kEB) {
+        const uint32_t *d = ld + 4 * q;
+        const uint32_t d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3], d4 = d[4];
+        dst[q] = r == 0 ? uint4{d0, d1, d2, d3}
+                        : uint4{__builtin_amdgcn_alignbyte(d1, d0, r), __builtin_amdgcn_alignbyte(d2, d1, r),
+                                __builtin_amdgcn_alignbyte(d3, d2, r), __builtin_amdgcn_alignbyte(d4, d3, r)};
+    }
 }
 
 // decode: packets [c0, c0 + kEncPer) per workgroup (LDS staging below)
@@ -404,6 +701,24 @@ namespace swarm {
 // Grid cap of the codec kernels (10M messages: 16 384 -> encode 0.419-0.433 ms, decode 0.153-0.155;
 // 4 096 -> 0.440-0.451 / 0.158-0.162; 1 024 -> 0.484-0.493 / 0.173-0.178, same box,
 // profiles/r4_d/physics_codec_grid_ab.log; SWARM_CODEC_WGS overrides, A/B aid).
+// Encode form: 1 = one pass (k_enc_one, the default), 3 = tile / base / place (SWARM_ENC_PASSES=3, A/B aid).
+int enc_passes() {
+    static const int p = [] {
+        const char *e = getenv("SWARM_ENC_PASSES");
+        return e && atoi(e) == 3 ? 3 : 1;
+    }();
+    return p;
+}
+
+// One-pass encode, two messages per lane when the arrays allow 16-byte accesses (SWARM_ENC_PAIR=0: one, A/B aid).
+bool enc_pair() {
+    static const bool p = [] {
+        const char *e = getenv("SWARM_ENC_PAIR");
+        return !(e && atoi(e) == 0);
+    }();
+    return p;
+}
+
 unsigned codec_grid_cap() {
     static const unsigned cap = [] {
         const char *e = getenv("SWARM_CODEC_WGS");
@@ -431,6 +746,36 @@ int swarm_codec_encode(swarm_ctx *ctx, int64_t m, const int64_t *type, const int
     }
     const EncIn in{type, sender, tick, task, winner, a, b};
     const int64_t ntiles = (m + kTile - 1) / kTile;
+    if (enc_passes() == 1) {
+        unsigned long long *lb;
+        SW_ALLOC(lb, ctx, S_ENC_FLAGS, size_t(ntiles + 1) * 8 + 64);
+        void *mdev = nullptr;  // the total and the error flag, written by the last tile into mapped host memory
+        volatile int64_t *host = static_cast<volatile int64_t *>(mapped(ctx, 16, &mdev));
+        if (!host) return SWARM_ERR_OOM;
+        int64_t *dev_tot = static_cast<int64_t *>(mdev);
+        unsigned *err = reinterpret_cast<unsigned *>(dev_tot + 1);
+        if (ctx->enc_flags != lb || ctx->enc_cap != ctx->cap[S_ENC_FLAGS] || ctx->enc_epoch >= (1u << 24) - 1) {
+            SW_HIP(hipMemsetAsync(lb, 0, ctx->cap[S_ENC_FLAGS], s));  // a new buffer, or the epoch tags used up
+            ctx->enc_flags = lb;
+            ctx->enc_cap = ctx->cap[S_ENC_FLAGS];
+            ctx->enc_epoch = 0;
+        }
+        const uint32_t epoch = ++ctx->enc_epoch;
+        SW_ARG(ntiles < (int64_t(1) << 31), "m out of range");
+        const auto al16 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+        const bool pair = enc_pair() && al16(type) && al16(sender) && al16(tick) && al16(a) && al16(b) &&
+                          al16(task) && al16(winner) && al16(offsets) && (reinterpret_cast<uintptr_t>(status) & 1) == 0;
+        hipLaunchKernelGGL(pair ? k_enc_one<2> : k_enc_one<1>, dim3(unsigned(ntiles)), dim3(kEB), 0, s, m, in,
+                           int(wide != 0), status, offsets, out, out ? cap : int64_t(0), lb, epoch, dev_tot, err);
+        SW_LAUNCHED();
+        SW_HIP(hipStreamSynchronize(s));
+        *total_bytes = host[0];
+        if (reinterpret_cast<volatile const unsigned *>(host + 1)[0]) {
+            set_error("output buffer holds %lld bytes, the packets need %lld", (long long)cap, (long long)host[0]);
+            return SWARM_ERR_RANGE;
+        }
+        return SWARM_OK;
+    }
     uint8_t *tmp;
     int32_t *wt;
     SW_ALLOC(tmp, ctx, S_TMP0, size_t(ntiles) * kTileBytes);
@@ -440,7 +785,7 @@ int swarm_codec_encode(swarm_ctx *ctx, int64_t m, const int64_t *type, const int
     uint16_t *loc = reinterpret_cast<uint16_t *>(err + 16);
     const unsigned codec_wgs = swarm::codec_grid_cap();
     const unsigned grid = grid_for(ntiles, 1, codec_wgs);
-    hipLaunchKernelGGL(k_enc_tile, dim3(grid), dim3(kBlock), 0, s, m, in, int(wide != 0), status, loc, tmp, wt);
+    hipLaunchKernelGGL(k_enc_tile, dim3(grid), dim3(kEB), 0, s, m, in, int(wide != 0), status, loc, tmp, wt);
     SW_LAUNCHED();
     hipLaunchKernelGGL(k_enc_base, dim3(1), dim3(1024), 0, s, ntiles, wt, base);
     SW_LAUNCHED();
@@ -453,7 +798,7 @@ int swarm_codec_encode(swarm_ctx *ctx, int64_t m, const int64_t *type, const int
         return SWARM_OK;
     }
     SW_HIP(hipMemsetAsync(err, 0, 4, s));
-    hipLaunchKernelGGL(k_enc_place, dim3(grid), dim3(kBlock), 0, s, m, tmp, wt, base, loc, cap, offsets, out, err);
+    hipLaunchKernelGGL(k_enc_place, dim3(grid), dim3(kEB), 0, s, m, tmp, wt, base, loc, cap, offsets, out, err);
     SW_LAUNCHED();
     SW_HIP(hipMemcpyAsync(host, base + ntiles, 8, hipMemcpyDeviceToHost, s));
     SW_HIP(hipMemcpyAsync(host + 1, err, 4, hipMemcpyDeviceToHost, s));

@@ -54,6 +54,7 @@ enum Slot {
     S_DEFER,          // allocation: guard-band tasks deferred to the libm pass (list + per-task flags)
     S_FPAIRS,         // allocation: the deferred tasks' guard-band pairs (device -> host)
     S_OVR,            // allocation: host libm decisions for those pairs (host -> device)
+    S_ENC_FLAGS,      // codec: tile ticket + per-tile look-back words (kept across calls, tagged by epoch)
     S_NUM
 };
 
@@ -95,6 +96,9 @@ struct swarm_ctx {
     int step_wr_agent = 0;         // ... and the next round writes its marks in agent order (the tail)
     hipStream_t side = nullptr;    // a second stream for work that overlaps the caller's (side_stream)
     hipEvent_t side_ev[2] = {};    // fork / join events
+    void *enc_flags = nullptr;     // codec one-pass encode: the S_ENC_FLAGS buffer last zeroed ...
+    size_t enc_cap = 0;            // ... and its size
+    uint32_t enc_epoch = 0;        // ... the epoch tag of the last call (look-back words carry it)
 };
 
 namespace swarm {

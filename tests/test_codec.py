@@ -177,13 +177,13 @@ def test_gpu_empty_and_errors():
 
 @pytest.mark.gpu
 def test_gpu_encode_sizing_call_and_tile_edges(oracle_mod):
-    """swarm_codec_encode with out = NULL returns the byte count only; message counts around the encode
-    tile (2 048) give the oracle's bytes and offsets."""
+    """swarm_codec_encode with out = NULL returns the byte count; message counts around the encode tile
+    (2 048 messages: 8 waves x 256, slabs of 128) give the oracle's bytes and offsets."""
     import ctypes
 
     import torch
     from swarm_amd import _lib, codec
-    for m in (1, 2047, 2048, 2049, 4096 + 17):
+    for m in (1, 127, 255, 257, 1024, 2047, 2048, 2049, 4096 + 17, 70_001):
         f = _random_msgs(m, 100 + m)
         st, pk = oracle_mod.codec_encode_py(*f)
         want = np.frombuffer(b"".join(pk), np.uint8)
@@ -199,3 +199,44 @@ def test_gpu_encode_sizing_call_and_tile_edges(oracle_mod):
         _lib.check(_lib.lib().swarm_codec_encode(_lib.ctx(), m, *[_lib.ptr(c) for c in cols], 0, None, 0,
                                                  _lib.ptr(off), _lib.ptr(stt), ctypes.byref(tot), _lib.stream()))
         assert tot.value == len(want)
+
+
+@pytest.mark.gpu
+def test_gpu_encode_unaligned_columns_and_sizing_offsets(oracle_mod):
+    """Columns that are views at an odd element offset (8-byte, not 16-byte aligned) take the one-message-
+    per-lane form of the one-pass encode; the result is the same, and the sizing call (out = NULL) fills
+    status and offsets too."""
+    import ctypes
+
+    import torch
+    from swarm_amd import _lib
+    for m in (3, 1025, 5000):
+        f = _random_msgs(m, 7 + m)
+        st, pk = oracle_mod.codec_encode_py(*f)
+        want = np.frombuffer(b"".join(pk), np.uint8)
+        want_off = np.concatenate([[0], np.cumsum([len(p) for p in pk])])
+        cols = []
+        for k, v in enumerate(f):
+            dt = torch.float64 if k in (3, 4) else torch.int64
+            big = torch.zeros(m + 1, dtype=dt, device="cuda")
+            big[1:] = torch.as_tensor(np.asarray(v), dtype=dt, device="cuda")
+            cols.append(big[1:])  # data_ptr % 16 == 8
+        assert all(c.data_ptr() % 16 == 8 for c in cols)
+        off_big = torch.full((m + 2,), -1, dtype=torch.int64, device="cuda")
+        off = off_big[1:]
+        stt = torch.full((m,), -1, dtype=torch.int8, device="cuda")
+        buf = torch.zeros(max(len(want), 1), dtype=torch.uint8, device="cuda")
+        tot = ctypes.c_int64(-1)
+        _lib.check(_lib.lib().swarm_codec_encode(_lib.ctx(), m, *[_lib.ptr(c) for c in cols], 0, _lib.ptr(buf),
+                                                 buf.numel(), _lib.ptr(off), _lib.ptr(stt), ctypes.byref(tot),
+                                                 _lib.stream()))
+        assert tot.value == len(want)
+        np.testing.assert_array_equal(buf.cpu().numpy()[:len(want)], want)
+        np.testing.assert_array_equal(off.cpu().numpy(), want_off)
+        np.testing.assert_array_equal(stt.cpu().numpy(), st)
+        off.fill_(-1)
+        stt.fill_(-1)
+        _lib.check(_lib.lib().swarm_codec_encode(_lib.ctx(), m, *[_lib.ptr(c) for c in cols], 0, None, 0,
+                                                 _lib.ptr(off), _lib.ptr(stt), ctypes.byref(tot), _lib.stream()))
+        np.testing.assert_array_equal(off.cpu().numpy(), want_off)
+        np.testing.assert_array_equal(stt.cpu().numpy(), st)

@@ -33,3 +33,10 @@ for rep in range(4):
 pk = e.total_bytes
 print(f"m={m} wide={wide} bytes={pk} encode {best_e * 1e3:.3f} ms ({(146 * m + pk) / best_e / 1e9:.0f} GB/s alg) "
       f"decode {best_d * 1e3:.3f} ms ({(66 * m + pk) / best_d / 1e9:.0f} GB/s alg)")
+sys.path.insert(0, ".")
+import bench  # noqa: E402
+
+if not wide:
+    ms_ec, ms_dc = bench._codec_abi_ms(f, e, m, pk, torch.device("cuda"))
+    print(f"C-ABI calls, preallocated outputs: encode {ms_ec:.3f} ms ({(65 * m + pk) / ms_ec / 1e6:.0f} GB/s compulsory) "
+          f"decode {ms_dc:.3f} ms ({(66 * m + pk) / ms_dc / 1e6:.0f} GB/s)")
