@@ -373,43 +373,40 @@ def cpu_baseline_step(h, d, r, args):
     """The C3 step on the host: the oracle's frontier election (orc_elect_frontier) and binned
     allocation (orc_allocate_binned) -- the same algorithms the GPU runs, restated in C with
     OpenMP -- over the same swarm (storage order), all host threads, measured whole (no
-    extrapolation).  One thread: the first rounds of the election and a task sample, scaled by
-    the agents recomputed (per round, from the full run) and by the task count."""
+    extrapolation), then again on one thread (round 4's one-thread figure was extrapolated from
+    the first 40 rounds and 1 000 tasks)."""
     from oracle import oracle
     threads = _threads()
     rp, col, ids, x, y, caps = h["rp"], h["col"], h["ids"], h["x"], h["y"], h["caps"]
     n = len(ids)
     oracle.set_threads(threads)
     t1 = time.perf_counter()
-    lead, _, rounds, _, active = oracle.elect_frontier(rp, col, ids, with_active=True)
+    lead, _, rounds, _ = oracle.elect_frontier(rp, col, ids)
     t_el = time.perf_counter() - t1
     t1 = time.perf_counter()
     al = oracle.allocate_binned(ids, x, y, caps, d["tx"], d["ty"], d["treq"], use_pow=False)
     t_al = time.perf_counter() - t1
     same = (rounds == r.rounds_exec and bool(np.array_equal(lead, h["leader"]))
             and bool(np.array_equal(al["winner"], h["winner"])))
-    # one thread: the first k rounds (the heaviest) and a task sample
+    # one thread: the same step again, whole (~20 s on the GPU box's host)
     oracle.set_threads(1)
-    k = min(rounds, 40)
     t1 = time.perf_counter()
-    oracle.elect_frontier(rp, col, ids, max_rounds=k)
-    t_k = time.perf_counter() - t1
-    ts = min(len(d["tx"]), 1000)
+    lead1, _, rounds1, _ = oracle.elect_frontier(rp, col, ids)
+    t_el1 = time.perf_counter() - t1
     t1 = time.perf_counter()
-    oracle.allocate_binned(ids, x, y, caps, d["tx"][:ts], d["ty"][:ts], d["treq"][:ts], use_pow=False)
-    t_ts = time.perf_counter() - t1
+    al1 = oracle.allocate_binned(ids, x, y, caps, d["tx"], d["ty"], d["treq"], use_pow=False)
+    t_al1 = time.perf_counter() - t1
     oracle.set_threads(threads)
-    t1_est = t_k * float(active.sum()) / float(active[:k].sum()) + t_ts * len(d["tx"]) / ts
+    same1 = rounds1 == rounds and bool(np.array_equal(lead1, lead)) and bool(np.array_equal(al1["winner"], al["winner"]))
     return {"value": n * rounds / (t_el + t_al), "unit": "agent-rounds/s", "cores": threads, "kind": "port",
-            "value_1core": n * rounds / t1_est,
-            "value_1core_kind": f"ESTIMATE, not a measurement: one thread timed on rounds 1-{k} and {ts} tasks, "
-                                f"scaled by the agents recomputed per round and by the task count",
-            "elect_s": t_el, "alloc_s": t_al, "same_result_as_gpu": same,
+            "value_1core": n * rounds / (t_el1 + t_al1),
+            "value_1core_kind": "measured: the whole step on one host thread",
+            "elect_s": t_el, "alloc_s": t_al, "elect_s_1core": t_el1, "alloc_s_1core": t_al1,
+            "same_result_as_gpu": same and same1,
             "sample": f"C oracle, the GPU's algorithms (orc_elect_frontier + orc_allocate_binned), the whole C3 step "
                       f"on the same {n}-agent swarm: election {rounds} rounds {t_el:.2f} s + {len(d['tx'])}-task "
-                      f"allocation {t_al:.2f} s on {threads} threads (measured, not extrapolated); 1 thread: "
-                      f"rounds 1-{k} ({t_k:.1f} s) + {ts} tasks ({t_ts:.1f} s), scaled by recomputed agents and "
-                      f"tasks to {t1_est:.0f} s"}
+                      f"allocation {t_al:.2f} s on {threads} threads; on 1 thread {t_el1:.1f} s + {t_al1:.1f} s "
+                      f"(both measured whole, not extrapolated)"}
 
 
 def _timed(fn, reps=1):
