@@ -240,3 +240,32 @@ def test_gpu_encode_unaligned_columns_and_sizing_offsets(oracle_mod):
                                                  _lib.ptr(off), _lib.ptr(stt), ctypes.byref(tot), _lib.stream()))
         np.testing.assert_array_equal(off.cpu().numpy(), want_off)
         np.testing.assert_array_equal(stt.cpu().numpy(), st)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wide", [False, True])
+def test_gpu_encode_large_matches_oracle_on_a_sample(oracle_mod, wide):
+    """6M messages with errors mixed in (~3 000 encode tiles, so the tile offsets come out of long
+    look-back walks): every packet length follows from its status and type, the offsets are their
+    running sum, and 30 000 sampled messages' statuses and packet bytes equal the oracle's."""
+    from swarm_amd import codec
+    m = 6_000_000
+    f = _random_msgs(m, 31 + wide, wide=wide)
+    e = codec.encode(*f, wide=wide, device="cuda")
+    st = e.status.cpu().numpy()
+    off = e.offsets.cpu().numpy()
+    buf = e.buf.cpu().numpy()
+    hdr = 9 if wide else 6
+    lut = np.zeros(16, np.int64)
+    lut[[1, 2, 3, 4, 5]] = [8, 4 if wide else 1, 0, 8, 8 if wide else 5]  # payload bytes by type
+    ty = np.asarray(f[0])
+    want_len = np.where(st == 0, hdr + lut[np.clip(ty, 0, 15)], 0)
+    np.testing.assert_array_equal(np.diff(off), want_len)
+    assert off[0] == 0 and off[-1] == e.total_bytes == len(buf)
+    assert {0, 1, 3} <= set(np.unique(st))
+    idx = np.sort(np.random.default_rng(3).choice(m, 30_000, replace=False))
+    sub = [np.asarray(v)[idx] for v in f]
+    ost, opk = oracle_mod.codec_encode_py(*sub, wide=wide)
+    np.testing.assert_array_equal(st[idx], ost)
+    for k, i in enumerate(idx):
+        assert bytes(buf[off[i]:off[i + 1]]) == opk[k], int(i)
