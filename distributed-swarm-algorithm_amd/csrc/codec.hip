@@ -358,6 +358,7 @@ __global__ __launch_bounds__(kEB) void k_enc_place(int64_t m, const uint8_t *__r
 #define SWARM_ENC_LB_SLEEP 1  // s_sleep between polls (units of 64 cycles)
 #endif
 constexpr int kLbShift = 40, kLbStateShift = 38, kLbPer = SWARM_ENC_LB_PER;
+constexpr unsigned kLbMaxPolls = 1u << 22;  // seconds of polling: only a broken call gets there
 constexpr unsigned long long kLbValue = (1ull << kLbStateShift) - 1;
 
 __device__ __forceinline__ unsigned long long lb_word(uint32_t epoch, unsigned state, unsigned long long v) {
@@ -377,7 +378,7 @@ __global__ __launch_bounds__(kEB) SWARM_ENC_ATTR void k_enc_one(int64_t m, EncIn
                                                    int64_t *__restrict__ off, uint8_t *__restrict__ out, int64_t cap,
                                                    unsigned long long *__restrict__ lb, uint32_t epoch,
                                                    int64_t *__restrict__ total,
-                                                   unsigned *__restrict__ err) {
+                                                   unsigned *__restrict__ err, unsigned *__restrict__ fail) {
     constexpr int J = kTileJ / P;  // slabs per wave, kWave * P messages each
     static_assert(J * P == kTileJ, "slabs");
     __shared__ uint4 s_buf[kTileLds];
@@ -397,6 +398,10 @@ __global__ __launch_bounds__(kEB) SWARM_ENC_ATTR void k_enc_one(int64_t m, EncIn
     }
     __syncthreads();
     const int64_t tile = s_tile;
+    if (tile >= ntiles) {  // only if another call shares this ctx's counter at the same time (not supported)
+        if (threadIdx.x == 0) *fail = 2u;
+        return;
+    }
     const int64_t c0 = tile * kTile + int64_t(w) * kWaveMsgs + int64_t(lane) * P;
     int64_t ty[J][P], snd[J][P], tk[J][P], task[J][P], win[J][P];
     double fa[J][P], fb[J][P];
@@ -501,6 +506,7 @@ __global__ __launch_bounds__(kEB) SWARM_ENC_ATTR void k_enc_one(int64_t m, EncIn
     }
     if (w == 0) {
         int64_t excl = 0;
+        unsigned polls = 0;  // bounded: a walk that never ends (a broken call) gives up and reports it
         // a poll reads tiles j - L - 64 q (lane L, q = 0 .. kLbPer-1): each load instruction covers 64
         // consecutive words (4 lines); the nearest inclusive word ends the walk
         for (int64_t j = tile - 1; j >= 0;) {
@@ -529,6 +535,10 @@ __global__ __launch_bounds__(kEB) SWARM_ENC_ATTR void k_enc_one(int64_t m, EncIn
             for (int q = 0; q < kLbPer; ++q)
                 needm |= unsigned(q < qq || (q == qq && lane <= p)) << q;
             if (__ballot((okm & needm) != needm)) {  // a needed tile has not published yet
+                if (++polls > kLbMaxPolls) {
+                    if (lane == 0) *fail = 1u;  // (mapped host memory: a plain store, no atomics)
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(SWARM_ENC_LB_SLEEP);
                 continue;
             }
@@ -750,10 +760,12 @@ int swarm_codec_encode(swarm_ctx *ctx, int64_t m, const int64_t *type, const int
         unsigned long long *lb;
         SW_ALLOC(lb, ctx, S_ENC_FLAGS, size_t(ntiles + 1) * 8 + 64);
         void *mdev = nullptr;  // the total and the error flag, written by the last tile into mapped host memory
-        volatile int64_t *host = static_cast<volatile int64_t *>(mapped(ctx, 16, &mdev));
+        volatile int64_t *host = static_cast<volatile int64_t *>(mapped(ctx, 24, &mdev));
         if (!host) return SWARM_ERR_OOM;
         int64_t *dev_tot = static_cast<int64_t *>(mdev);
         unsigned *err = reinterpret_cast<unsigned *>(dev_tot + 1);
+        unsigned *fail = reinterpret_cast<unsigned *>(dev_tot + 2);
+        reinterpret_cast<volatile unsigned *>(host + 2)[0] = 0u;  // (no kernel of this ctx is running: calls sync)
         if (ctx->enc_flags != lb || ctx->enc_cap != ctx->cap[S_ENC_FLAGS] || ctx->enc_epoch >= (1u << 24) - 1) {
             SW_HIP(hipMemsetAsync(lb, 0, ctx->cap[S_ENC_FLAGS], s));  // a new buffer, or the epoch tags used up
             ctx->enc_flags = lb;
@@ -766,10 +778,16 @@ int swarm_codec_encode(swarm_ctx *ctx, int64_t m, const int64_t *type, const int
         const bool pair = enc_pair() && al16(type) && al16(sender) && al16(tick) && al16(a) && al16(b) &&
                           al16(task) && al16(winner) && al16(offsets) && (reinterpret_cast<uintptr_t>(status) & 1) == 0;
         hipLaunchKernelGGL(pair ? k_enc_one<2> : k_enc_one<1>, dim3(unsigned(ntiles)), dim3(kEB), 0, s, m, in,
-                           int(wide != 0), status, offsets, out, out ? cap : int64_t(0), lb, epoch, dev_tot, err);
+                           int(wide != 0), status, offsets, out, out ? cap : int64_t(0), lb, epoch, dev_tot, err,
+                           fail);
         SW_LAUNCHED();
         SW_HIP(hipStreamSynchronize(s));
         *total_bytes = host[0];
+        if (const unsigned fl = reinterpret_cast<volatile const unsigned *>(host + 2)[0]) {
+            set_error("encode: tile offsets lost (%s); concurrent encode calls on one ctx are not supported",
+                      fl & 2u ? "a tile ticket out of range" : "a look-back walk gave up");
+            return SWARM_ERR_HIP;
+        }
         if (reinterpret_cast<volatile const unsigned *>(host + 1)[0]) {
             set_error("output buffer holds %lld bytes, the packets need %lld", (long long)cap, (long long)host[0]);
             return SWARM_ERR_RANGE;
