@@ -158,6 +158,16 @@ int shm_fail(swarm_comm *c, int rc) {
     return rc;
 }
 
+// A HIP call inside a shared-memory op: on failure the peers are told (abort) before this rank returns.
+#define SW_SHM_HIP(c, call)                                                                  \
+    do {                                                                                     \
+        hipError_t e_ = (call);                                                              \
+        if (e_ != hipSuccess) {                                                              \
+            swarm::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #call, hipGetErrorString(e_)); \
+            return shm_fail(c, SWARM_ERR_HIP);                                               \
+        }                                                                                    \
+    } while (0)
+
 // Halo exchange over the mailboxes.  This rank's mailbox of the op's parity holds a table of
 // (offset, count) per destination rank, then its whole send buffer (the segments for its peers back to
 // back); a rank reads its ghosts from each peer's mailbox at the offset that peer's table gives it.
@@ -173,8 +183,8 @@ int shm_halo(swarm_comm *c, const int32_t *send, const int64_t *soff, const int3
         t[2 * peers[j]] = soff[j];
         t[2 * peers[j] + 1] = soff[j + 1] - soff[j];
     }
-    if (soff[n_peers]) SW_HIP(hipMemcpyAsync(mine + tab, send, size_t(soff[n_peers]) * 4, hipMemcpyDeviceToHost, s));
-    SW_HIP(hipStreamSynchronize(s));
+    if (soff[n_peers]) SW_SHM_HIP(c, hipMemcpyAsync(mine + tab, send, size_t(soff[n_peers]) * 4, hipMemcpyDeviceToHost, s));
+    SW_SHM_HIP(c, hipStreamSynchronize(s));
     if (int rc = shm_barrier(c)) return rc;
     for (int j = 0; j < n_peers; ++j) {
         const char *box = shm_box(c, peers[j], par);
@@ -185,12 +195,12 @@ int shm_halo(swarm_comm *c, const int32_t *send, const int64_t *soff, const int3
                       (long long)cnt, c->rank, (long long)(roff[j + 1] - roff[j]));
             return shm_fail(c, SWARM_ERR_ARG);
         }
-        if (cnt) SW_HIP(hipMemcpyAsync(recv + roff[j], box + tab + size_t(off) * 4, size_t(cnt) * 4,
+        if (cnt) SW_SHM_HIP(c, hipMemcpyAsync(recv + roff[j], box + tab + size_t(off) * 4, size_t(cnt) * 4,
                                        hipMemcpyHostToDevice, s));
     }
     // the mailboxes of this parity are rewritten two ops later, after every rank has passed the
     // next op's barrier -- which this rank reaches only once its reads here are done
-    SW_HIP(hipStreamSynchronize(s));
+    SW_SHM_HIP(c, hipStreamSynchronize(s));
     return SWARM_OK;
 }
 
@@ -200,8 +210,8 @@ int shm_allreduce_u64(swarm_comm *c, unsigned long long *buf, size_t count, bool
         set_error("all-reduce larger than the shared-memory mailboxes (raise SWARM_SHM_MB)");
         return shm_fail(c, SWARM_ERR_ARG);
     }
-    SW_HIP(hipMemcpyAsync(shm_box(c, c->rank, par), buf, count * 8, hipMemcpyDeviceToHost, s));
-    SW_HIP(hipStreamSynchronize(s));
+    SW_SHM_HIP(c, hipMemcpyAsync(shm_box(c, c->rank, par), buf, count * 8, hipMemcpyDeviceToHost, s));
+    SW_SHM_HIP(c, hipStreamSynchronize(s));
     if (int rc = shm_barrier(c)) return rc;
     std::vector<unsigned long long> acc(count);
     memcpy(acc.data(), shm_box(c, 0, par), count * 8);
@@ -209,8 +219,8 @@ int shm_allreduce_u64(swarm_comm *c, unsigned long long *buf, size_t count, bool
         const unsigned long long *q = reinterpret_cast<const unsigned long long *>(shm_box(c, r, par));
         for (size_t i = 0; i < count; ++i) acc[i] = is_max ? std::max(acc[i], q[i]) : acc[i] + q[i];
     }
-    SW_HIP(hipMemcpyAsync(buf, acc.data(), count * 8, hipMemcpyHostToDevice, s));
-    SW_HIP(hipStreamSynchronize(s));
+    SW_SHM_HIP(c, hipMemcpyAsync(buf, acc.data(), count * 8, hipMemcpyHostToDevice, s));
+    SW_SHM_HIP(c, hipStreamSynchronize(s));
     return SWARM_OK;
 }
 
@@ -221,12 +231,12 @@ int shm_allgather_u64(swarm_comm *c, const unsigned long long *send, size_t coun
         set_error("all-gather larger than the shared-memory mailboxes (raise SWARM_SHM_MB)");
         return shm_fail(c, SWARM_ERR_ARG);
     }
-    SW_HIP(hipMemcpyAsync(shm_box(c, c->rank, par), send, count * 8, hipMemcpyDeviceToHost, s));
-    SW_HIP(hipStreamSynchronize(s));
+    SW_SHM_HIP(c, hipMemcpyAsync(shm_box(c, c->rank, par), send, count * 8, hipMemcpyDeviceToHost, s));
+    SW_SHM_HIP(c, hipStreamSynchronize(s));
     if (int rc = shm_barrier(c)) return rc;
     for (int r = 0; r < c->nranks; ++r)
-        SW_HIP(hipMemcpyAsync(recv + size_t(r) * count, shm_box(c, r, par), count * 8, hipMemcpyHostToDevice, s));
-    SW_HIP(hipStreamSynchronize(s));
+        SW_SHM_HIP(c, hipMemcpyAsync(recv + size_t(r) * count, shm_box(c, r, par), count * 8, hipMemcpyHostToDevice, s));
+    SW_SHM_HIP(c, hipStreamSynchronize(s));
     return SWARM_OK;
 }
 
