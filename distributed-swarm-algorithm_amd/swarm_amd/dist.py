@@ -487,7 +487,7 @@ class GpuBackend:
         self.comm_kind = "rccl" if kind == L.COMM_RCCL else "shm"
         return comm
 
-    def elect_sharded(self, comm, sh, max_rounds, record=False, alone=False):
+    def elect_sharded(self, comm, sh, max_rounds, record=False, alone=False, timed=True):
         """The native sharded loop (swarm_elect_sharded_ex).  record: also this rank's per-round counts
         (owned changes, rows and edges gathered) and per-round device times.  alone: the shard graph stepped
         by itself, no peers and no communicator (the cost model's calibration run)."""
@@ -503,7 +503,7 @@ class GpuBackend:
         rounds = ctypes.c_int32(0)
         changes = np.zeros(max_rounds, np.int64)
         local = np.zeros((max_rounds, 3), np.int64) if record else None
-        rms = np.zeros(max_rounds, np.float32) if record else None
+        rms = np.zeros(max_rounds, np.float32) if record and timed else None
         hp = lambda a: a.ctypes.data_as(ctypes.c_void_p) if a is not None else None  # noqa: E731
         rc = L.check(L.lib().swarm_elect_sharded_ex(self.ctx, None if alone else comm, ctypes.byref(desc),
                                                     L.ptr(sh.leaders[0]), L.ptr(sh.leaders[1]), max_rounds,
@@ -511,7 +511,7 @@ class GpuBackend:
                                                     L.stream()))
         r = rounds.value
         if record:
-            return r, changes[:r].copy(), rc == L.OK, local[:r].copy(), rms[:r].copy()
+            return r, changes[:r].copy(), rc == L.OK, local[:r].copy(), rms[:r].copy() if rms is not None else None
         return r, changes[:r].copy(), rc == L.OK
 
     def changes(self, t0, t1):
@@ -767,14 +767,15 @@ class ShardedSwarm:
         state = torch.where(own == self.ids, 3, 1).to(torch.uint8)
         return ShardElectResult(rounds, np.array(changes[:rounds], np.int64), own, state, found > 0)
 
-    def elect_alone(self, max_rounds: int = 1 << 16):
+    def elect_alone(self, max_rounds: int = 1 << 16, timed: bool = True):
         """This shard's graph elected by itself on this rank's GPU (no peers, no exchange): the calibration
-        run of the election cost model -- (rounds, per-round local counts, per-round device ms, wall ms)."""
+        run of the election cost model -- (rounds, per-round local counts, per-round device ms, wall ms).
+        timed=False: no per-round events (rms None), the wall time of the plain loop."""
         import time
         be = self.backend
         torch.cuda.synchronize(self.device)
         t0 = time.perf_counter()
-        r, _, _, local, rms = be.elect_sharded(None, self, max_rounds, record=True, alone=True)
+        r, _, _, local, rms = be.elect_sharded(None, self, max_rounds, record=True, alone=True, timed=timed)
         torch.cuda.synchronize(self.device)
         return r, local, rms, (time.perf_counter() - t0) * 1e3
 
