@@ -460,7 +460,10 @@ int swarm_physics_step(swarm_ctx *ctx, int64_t n, const int32_t *ids, const uint
  * value beyond f32), 3 unknown type -- payload checked before header, as the reference packs
  * them; an errored message takes no bytes.  offsets (device, m+1) = packet offsets into out,
  * offsets[m] = *total_bytes (host).  out == NULL: sizing call (status/offsets/total only);
- * otherwise cap must be >= the total (SWARM_ERR_RANGE).  Synchronises the stream (total_bytes).
+ * otherwise cap must be >= the total (SWARM_ERR_RANGE: nothing past cap is written).  Synchronises
+ * the stream (total_bytes).  One pass: tiles of 2 048 messages take their byte offsets from the lower
+ * tiles' published counts (a ticket counter and look-back words in the ctx), so encode calls on one
+ * ctx must not overlap (SWARM_ERR_HIP if they did and a look-back gave up).
  */
 int swarm_codec_encode(swarm_ctx *ctx, int64_t m, const int64_t *type, const int64_t *sender, const int64_t *tick,
                        const double *a, const double *b, const int64_t *task, const int64_t *winner, int32_t wide,
