@@ -74,11 +74,17 @@ __global__ __launch_bounds__(kBlock, 8) void k_physics(int64_t n, const int32_t 
                 for (int64_t o = 0; o < cnt; ++o) {
                     const double ox = s_obs[3 * o], oy = s_obs[3 * o + 1], r = s_obs[3 * o + 2];
                     const double ex = px - ox, ey = py - oy;
-                    double d = sqrt(ex * ex + ey * ey) - r;
+                    const double s2 = ex * ex + ey * ey;
+                    // far obstacles (most): sqrt(s2) - r >= 5 for certain, so the exact test below could
+                    // not apply the force -- skip its square root (the margin 1e-12 is far above the
+                    // roundings of s2, the square root and the subtraction; NaN falls through)
+                    const double rr = 5.0 + r;
+                    if (s2 > rr * rr * (1.0 + 1e-12)) continue;
+                    double d = sqrt(s2) - r;
                     if (d <= 0.001) d = 0.001;
                     if (d < 5.0) {
                         const double mag = 50.0 * (1.0 / d - 1.0 / 5.0) / (d * d);
-                        const double nrm = sqrt(ex * ex + ey * ey);
+                        const double nrm = sqrt(s2);
                         sing += nrm == 0.0;
                         frx += (ex / nrm) * mag;
                         fry += (ey / nrm) * mag;
