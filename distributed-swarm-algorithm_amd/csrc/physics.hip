@@ -25,7 +25,48 @@ namespace swarm {
 namespace {
 
 constexpr int kObsLds = 1024;  // obstacles staged in LDS per pass (3 doubles each)
-constexpr int kNb = 4;         // neighbour positions gathered in flight per thread (8 waves/SIMD: 4 beats 8 at 4 waves)
+#ifndef SWARM_PHYS_NB
+#define SWARM_PHYS_NB 4
+#endif
+constexpr int kNb = SWARM_PHYS_NB;  // neighbour positions in flight per thread (4 beats 8 at 4 waves, 2: ab_r5t.log)
+
+// Correctly rounded f64 division and square root, written out as LLVM expands them for gfx950 but
+// without their range steps (div_scale / div_fmas scaling / div_fixup; the ldexp pre-scale and class
+// test of sqrt), which are the identity when every operand and result is normal and far from the
+// exponent limits -- in_range() below, checked by the caller, who falls back to '/' and sqrt()
+// otherwise.  Same instructions on the same operands: the same bits.  (Round 5: the separation
+// terms' three divisions and square root were ~60 % of k_physics' fp64 instructions; two divisions
+// by the same norm share its refined reciprocal.)
+#ifndef SWARM_PHYS_LIBM
+#define SWARM_PHYS_LIBM 0  // 1: the library '/' and sqrt() everywhere (A/B builds)
+#endif
+__device__ __forceinline__ bool in_range(double x) {
+    const double a = fabs(x);
+    return a >= 0x1p-500 && a <= 0x1p500;  // (false for 0, denormals, inf, NaN)
+}
+__device__ __forceinline__ double rcp_refined(double den) {  // v_rcp_f64 + two Newton steps
+    double r = __builtin_amdgcn_rcp(den);
+    double e = __builtin_fma(-den, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-den, r, 1.0);
+    return __builtin_fma(r, e, r);
+}
+__device__ __forceinline__ double div_by(double num, double den, double r) {  // num / den, r = rcp_refined(den)
+    const double q = num * r;
+    const double rem = __builtin_fma(-den, q, num);
+    return __builtin_fma(rem, r, q);
+}
+__device__ __forceinline__ double sqrt_core(double x) {  // v_rsq_f64 + Newton steps on (g, h)
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    double d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    return __builtin_fma(d, h, g);
+}
 
 __global__ __launch_bounds__(kBlock, 8) void k_physics(int64_t n, const int32_t *__restrict__ ids,
                                                    const uint8_t *__restrict__ state,
@@ -115,11 +156,26 @@ __global__ __launch_bounds__(kBlock, 8) void k_physics(int64_t n, const int32_t 
             for (int u = 0; u < kNb; ++u) {
                 if (jj[u] < 0) continue;
                 const double ex = px - qq[u].x, ey = py - qq[u].y;
-                double d = sqrt(ex * ex + ey * ey);
+                const double s2 = ex * ex + ey * ey;
+                if (!SWARM_PHYS_LIBM && in_range(ex) && in_range(ey) && in_range(s2)) {
+                    // both offsets nonzero and normal: the norm is in [2^-500, 2^251), d * d in
+                    // [1e-6, 4), every quotient normal -- the range steps are the identity
+                    const double nrm = sqrt_core(s2);
+                    if (nrm < 2.0) {
+                        const double d = nrm <= 0.001 ? 0.001 : nrm;
+                        const double dd = d * d;
+                        const double mag = div_by(20.0, dd, rcp_refined(dd));
+                        const double rn = rcp_refined(nrm);
+                        fsx += div_by(ex, nrm, rn) * mag;
+                        fsy += div_by(ey, nrm, rn) * mag;
+                    }
+                    continue;
+                }
+                double d = sqrt(s2);
                 if (d < 2.0) {
                     if (d <= 0.001) d = 0.001;
                     const double mag = 20.0 / (d * d);
-                    const double nrm = sqrt(ex * ex + ey * ey);
+                    const double nrm = sqrt(s2);
                     sing += nrm == 0.0;
                     fsx += (ex / nrm) * mag;
                     fsy += (ey / nrm) * mag;

@@ -121,3 +121,37 @@ def test_gpu_physics_singular_cases_match_oracle(oracle_mod):
     assert got["singular"] == want["singular"]
     for k in KEYS:
         np.testing.assert_array_equal(got[k], want[k], err_msg=k)
+
+
+@pytest.mark.gpu
+def test_gpu_physics_lattice_and_close_pairs_match_oracle(oracle_mod):
+    """k_physics' separation terms take the written-out division / square root only for nonzero, normal
+    offsets: a lattice (neighbours on the same row or column: an offset exactly 0, the library path),
+    pairs closer than the 0.001 clamp, offsets of 1e-9, and a lattice far from the origin (large
+    coordinates, small differences) give the oracle's bits, as do 1M random agents (~16M terms)."""
+    from swarm_amd import gen
+    side = 40
+    gx, gy = np.meshgrid(np.arange(side) * 0.5, np.arange(side) * 0.5)
+    x, y = gx.ravel().astype(np.float64), gy.ravel().astype(np.float64)
+    n0 = x.size
+    rng = np.random.default_rng(17)
+    pick = rng.choice(n0, 60, replace=False)
+    close = np.concatenate([np.full(20, 3e-4), np.full(20, 1e-9), rng.uniform(1e-6, 1e-3, 20)])
+    x = np.concatenate([x, x[pick] + close])
+    y = np.concatenate([y, y[pick] + close[::-1]])
+    for shift in (0.0, 1.0e6):
+        g = _random_case(len(x), 5, 20.0, m_obs=4)
+        g["x"], g["y"] = x + shift, y + shift
+        g["tx"], g["ty"] = g["x"] + 3.0, g["y"] - 2.0
+        g["obs"][:, :2] += shift
+        g["row_ptr"], g["col"] = gen.rgg_csr(g["x"], g["y"], 1.0)
+        got, _ = _gpu(g)
+        want = _oracle(oracle_mod, g, use_pow=False)
+        for k in KEYS:
+            np.testing.assert_array_equal(got[k], want[k], err_msg=f"{k} shift={shift}")
+    g = _random_case(1_000_000, 23, 250.0, radius=1.0)
+    g["steps"] = np.int64(1)
+    got, _ = _gpu(g)
+    want = _oracle(oracle_mod, g, use_pow=False)
+    for k in KEYS:
+        np.testing.assert_array_equal(got[k], want[k], err_msg=k)
