@@ -26,9 +26,9 @@ namespace {
 
 constexpr int kObsLds = 1024;  // obstacles staged in LDS per pass (3 doubles each)
 #ifndef SWARM_PHYS_NB
-#define SWARM_PHYS_NB 4
+#define SWARM_PHYS_NB 6
 #endif
-constexpr int kNb = SWARM_PHYS_NB;  // neighbour positions in flight per thread (4 beats 8 at 4 waves, 2: ab_r5t.log)
+constexpr int kNb = SWARM_PHYS_NB;  // neighbour positions in flight per thread (6: 0.869-0.879 ms, 4: 0.898, 8: 0.92; r5 physics_nb_ab.log)
 
 // Correctly rounded f64 division and square root, written out as LLVM expands them for gfx950 but
 // without their range steps (div_scale / div_fmas scaling / div_fixup; the ldexp pre-scale and class
