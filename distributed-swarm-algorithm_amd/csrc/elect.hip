@@ -1049,9 +1049,14 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     SW_HIP(hipMemcpyAsync(&e_total, rp + n, sizeof(Off), hipMemcpyDeviceToHost, s));
     SW_HIP(hipStreamSynchronize(s));
     SW_ARG(e_total == 0 || col != nullptr, "col is NULL but the graph has edges");
-    // the int32-CSR kernels address with 32-bit byte offsets (gather_listed's ld4)
-    SW_ARG(sizeof(Off) == 8 || (n < (int64_t(1) << 30) && int64_t(e_total) < (int64_t(1) << 30)),
-           "int32 CSR supports < 2^30 agents and edges: use swarm_elect_i64");
+    // the int32-CSR kernels address with 32-bit byte offsets (gather_listed's ld4 / Col16::at32):
+    // 4-byte columns need < 2^30 edges, 2-byte ones < 2^31 (less a margin for the clamped offsets a
+    // window or a pass computes past its row's end) -- C5's 100M agents (1.6e9 edges) fit with them
+    const bool c16_only = c16 && !hrp && tuning().dense_flat;
+    const int64_t e_cap = c16_only ? (int64_t(1) << 31) - (int64_t(1) << 20) : (int64_t(1) << 30);
+    SW_ARG(sizeof(Off) == 8 || (n < (int64_t(1) << 30) && int64_t(e_total) < e_cap),
+           "int32 CSR supports < 2^30 agents and edges (< 2^31 - 2^20 edges with 16-bit columns): use "
+           "swarm_elect_i64 / swarm_elect_compact_i64");
     if (hrp) {  // directed: the transpose must hold the same edges
         Off h_total = 0;
         SW_HIP(hipMemcpyAsync(&h_total, hrp + n, sizeof(Off), hipMemcpyDeviceToHost, s));

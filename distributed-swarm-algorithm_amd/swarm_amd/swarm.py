@@ -17,12 +17,24 @@ Every compute call goes through the HIP kernels; there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
 import torch
 
 from . import _lib
+
+# swarm_elect_compact's edge cap with 16-bit columns (elect.hip elect_impl: 32-bit byte offsets into
+# the int16 columns, less a margin for the clamped offsets past a row's end)
+_C16_EDGE_CAP = (1 << 31) - (1 << 20)
+
+
+def _c16_rounds() -> bool:
+    """Every round of swarm_elect_compact reads the 16-bit columns (the A/B knobs of elect.hip's
+    tuning(): SWARM_C16 and SWARM_DENSE_FLAT, both on by default)."""
+    return os.environ.get("SWARM_C16", "1") != "0" and os.environ.get("SWARM_DENSE_FLAT", "1") != "0"
+
 
 CAP_VOCAB_DEFAULT = ("extinguisher", "sonar", "camera", "gripper")
 STATUS_NAMES = ("OPEN", "TENTATIVE", "LOCKED", "ASSIGNED")
@@ -225,11 +237,16 @@ class Swarm:
         columns when they fit; swarm_elect_directed when the neighbour lists are not symmetric).
         timed: per-kernel HIP events.  compact=False: the int32-column entry point swarm_elect
         (same results).  wide: int64 row offsets (swarm_elect_i64) -- chosen by itself for
-        graphs of >= 2^30 edges (C5's 100M agents on one GPU: ~1.6e9), True forces it."""
+        graphs of >= 2^30 edges unless their 16-bit columns fit (swarm_elect_compact then takes up
+        to 2^31 - 2^20 edges on 32-bit offsets: C5's 100M agents on one GPU, ~1.6e9), True forces it."""
         if self.row_ptr is None:
             raise RuntimeError("no neighbour graph: call build_graph() or set_graph()")
         if wide is None:
             wide = self.n_edges >= (1 << 30) or self.n >= (1 << 30)
+            if wide and self.n < (1 << 30) and self.n_edges < _C16_EDGE_CAP and compact \
+                    and getattr(self, "_hear", None) is None and _c16_rounds():
+                with torch.cuda.device(self.device):
+                    wide = self.graph_compact() is None
         if wide:
             return self._elect_wide(mode, max_rounds, timed, compact)
         m = {"dense": _lib.ELECT_DENSE, "frontier": _lib.ELECT_FRONTIER}[mode] | (_lib.ELECT_TIMED if timed else 0)
@@ -268,6 +285,7 @@ class Swarm:
         res.gather_ms, res.apply_ms, res.timed_launches = st.gather_ms, st.apply_ms, st.gather_launches
         res.sparse_ms, res.sparse_launches, res.sparse_bytes = st.sparse_ms, st.sparse_launches, st.sparse_bytes
         res.compact = c16 is not None  # the rounds read the 16-bit columns (2 of the 4 column bytes)
+        res.wide = False               # 32-bit row offsets
         return res
 
     def _elect_wide(self, mode: str, max_rounds: int, timed: bool, compact: bool = True) -> ElectResult:
@@ -303,6 +321,7 @@ class Swarm:
         # the int64-offset DENSE rounds read the int32 columns (elect.hip launch_dense_round takes
         # col16 only with 32-bit offsets): only the frontier's sparse rounds read the 16-bit ones
         res.compact = c16 is not None and mode == "frontier"
+        res.wide = True
         return res
 
     # ------------------------------------------------------------------ allocation

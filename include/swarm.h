@@ -139,13 +139,16 @@ int swarm_graph_compact(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const
                         void *stream);
 
 /* swarm_elect reading the graph's compact columns (swarm_graph_compact of the same row_ptr/col;
- * col16 NULL: same as swarm_elect).  Same results, same stats. */
+ * col16 NULL: same as swarm_elect).  Same results, same stats.  With col16 it takes graphs of up to
+ * 2^31 - 2^20 edges (the 16-bit columns' 32-bit byte offsets), so a 1.6e9-edge swarm (C5's 100M agents
+ * on one GPU) runs on 32-bit row offsets; without, < 2^30 edges as swarm_elect. */
 int swarm_elect_compact(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col, const int16_t *col16,
                         const int32_t *ids, int32_t *leader, uint8_t *state, int32_t max_rounds, int32_t mode,
                         int32_t *rounds_exec, int64_t *changes_per_round, swarm_elect_stats *stats, void *stream);
 
 /* Same with int64 row offsets: graphs with >= 2^30 edges or agents (the int32-CSR entry points
- * address with 32-bit byte offsets and reject them with SWARM_ERR_ARG). */
+ * address with 32-bit byte offsets and reject them with SWARM_ERR_ARG; swarm_elect_compact with
+ * 16-bit columns reaches 2^31 - 2^20 edges). */
 int swarm_elect_i64(swarm_ctx *ctx, int64_t n, const int64_t *row_ptr, const int32_t *col,
                     const int32_t *ids, int32_t *leader, uint8_t *state, int32_t max_rounds,
                     int32_t mode, int32_t *rounds_exec, int64_t *changes_per_round,

@@ -103,3 +103,57 @@ def test_elect_int64_offsets(sw, oracle_mod, n, deg):
         assert not r.converged and r.rounds_exec == m
         np.testing.assert_array_equal(r.leader.cpu().numpy(), want[0])
         np.testing.assert_array_equal(r.changes, changes[:m])
+
+
+def test_elect_compact_above_2_30_edges(sw):
+    """swarm_elect_compact on 32-bit row offsets past 2^30 edges (its 16-bit columns' byte offsets
+    reach 2^31; C5's 100M agents on one GPU have 1.6e9 edges): a band graph (agent i hears every j
+    with 0 < |i - j| <= w) of 1.09e9 edges, built on the GPU.  After m rounds agent i holds the
+    maximum ID within m * w slots (agent.py:263-275 applied m times), so leaders, rounds and every
+    per-round change count follow from a sliding maximum on the host; the int64-offset entry point
+    (swarm_elect_compact_i64) must agree with it too."""
+    import torch
+    from scipy.ndimage import maximum_filter1d
+    n, w = 135_000, 4096
+    rng = np.random.default_rng(2030)
+    ids = rng.permutation(4 * n)[:n].astype(np.int32)
+    dev = torch.device("cuda")
+    v = torch.arange(n, dtype=torch.int64, device=dev)
+    lo, hi = (v - w).clamp_min(0), (v + w).clamp_max(n - 1)
+    deg = hi - lo  # the band minus the agent itself
+    rp = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    rp[1:] = torch.cumsum(deg, 0)
+    e = int(rp[-1])
+    assert (1 << 30) < e < sw._C16_EDGE_CAP
+    row = torch.repeat_interleave(v, deg)
+    u = lo[row] + (torch.arange(e, dtype=torch.int64, device=dev) - rp[row])
+    u += (u >= row).to(torch.int64)
+    del row
+    s = sw.Swarm(ids, np.arange(float(n)), np.zeros(n), layout="input", device="cuda")
+    s.row_ptr, s.col, s._hear = rp.to(torch.int32), u.to(torch.int32), None
+    del u, rp
+    torch.cuda.empty_cache()
+    # the sliding-maximum reference: rounds 1.. until nothing changes
+    cur, changes = ids.astype(np.int64), []
+    while True:
+        nxt = maximum_filter1d(cur, size=2 * w + 1, mode="constant", cval=-1)
+        changes.append(int((nxt != cur).sum()))
+        cur = nxt
+        if changes[-1] == 0:
+            break
+    rounds = len(changes)
+    assert rounds > 12  # dense sweeps, then sparse rounds over rows of up to 8 192 edges
+    results = [s.elect(), s.elect(mode="dense"), s.elect(wide=True)]
+    assert [r.wide for r in results] == [False, False, True]
+    assert results[0].compact
+    for r in results:
+        assert r.converged and r.rounds_exec == rounds, (r.wide, r.rounds_exec, rounds)
+        np.testing.assert_array_equal(r.changes, changes)
+        np.testing.assert_array_equal(r.leader.cpu().numpy(), cur.astype(np.int32))
+    m = rounds // 2
+    r = s.elect(max_rounds=m)
+    assert not r.converged and r.rounds_exec == m and not r.wide
+    want = ids.astype(np.int64)
+    for _ in range(m):
+        want = maximum_filter1d(want, size=2 * w + 1, mode="constant", cval=-1)
+    np.testing.assert_array_equal(r.leader.cpu().numpy(), want.astype(np.int32))

@@ -1,8 +1,9 @@
 """C5's swarm size (100M agents, deg 16, 10k tasks) on ONE MI355X: the bench's step (election to
 convergence + one allocation round) timed, with the election checked against the C oracle's
 frontier restatement (leaders, states, rounds, every per-round change count) and the allocation
-against the binned oracle.  The graph has ~1.6e9 edges (>= 2^30), so Swarm.elect takes the
-int64-offset entry point (swarm_elect_i64).  Prints progress every 30 s while the oracle runs (one C call).
+against the binned oracle.  The graph has ~1.6e9 edges (>= 2^30): Swarm.elect takes
+swarm_elect_compact on 32-bit row offsets (its 16-bit columns reach 2^31 - 2^20 edges); the int64-offset
+entry point (swarm_elect_compact_i64, round 2's path) is timed beside it and must agree.  Prints progress every 30 s while the oracle runs (one C call).
 Usage: python tools/c5_one_gpu.py [N] [--no-oracle]"""
 import json
 import sys
@@ -44,10 +45,23 @@ for _ in range(3):
     t3 = time.perf_counter()
     steps.append((t3 - t1, t2 - t1, t3 - t2))
 best = min(steps)
-out = {"agents": s.n, "edges": s.n_edges, "int64_offsets": s.n_edges >= 1 << 30, "rounds": r.rounds_exec,
+wide_ms = []
+for _ in range(3):
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    rw = s.elect(wide=True)
+    torch.cuda.synchronize()
+    wide_ms.append((time.perf_counter() - t1) * 1e3)
+wide_same = bool(rw.rounds_exec == r.rounds_exec and np.array_equal(rw.changes, r.changes))
+lead_w = rw.leader.clone()
+r = s.elect()
+wide_same = wide_same and bool(torch.equal(lead_w, r.leader))
+del lead_w
+out = {"agents": s.n, "edges": s.n_edges, "int64_offsets": bool(r.wide), "rounds": r.rounds_exec,
        "converged": r.converged, "ms_per_step": best[0] * 1e3, "elect_ms": best[1] * 1e3, "alloc_ms": best[2] * 1e3,
        "agent_rounds_per_s": s.n * r.rounds_exec / best[0],
-       "hbm_peak_gib": torch.cuda.max_memory_allocated() / 2**30}
+       "hbm_peak_gib": torch.cuda.max_memory_allocated() / 2**30,
+       "elect_ms_int64_offsets": min(wide_ms), "int64_offsets_same_result": wide_same}
 print(json.dumps(out), flush=True)
 if "--no-oracle" in sys.argv:
     sys.exit(0)
