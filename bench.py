@@ -49,6 +49,10 @@ def parse():
     ap.add_argument("--partition", choices=["strips", "blocks"], default="strips",
                     help="N > 1: strips (strip-major IDs: 2 peers per rank, 16-bit columns) or blocks "
                          "(SURVEY §8e's Morton IDs: Morton-ordered blocks, up to 8 peers per rank)")
+    ap.add_argument("--pieces", type=int, default=1,
+                    help="--partition blocks: cut the Morton IDs into N x PIECES equal ranges dealt round-robin "
+                         "(rank q owns ranges q, q + N, ...: with PIECES = N the q-th Morton piece of every block; "
+                         "dist.block_pieces) -- evens out the election's per-round work across ranks (DESIGN §6)")
     ap.add_argument("--union-gpu", type=int, default=1,
                     help="with --oracle-check: also elect the union swarm on rank 0's GPU (the model's N = 1 time)")
     ap.add_argument("--model", type=int, default=1,
@@ -646,8 +650,12 @@ def sharded(args, rank, world, dev):
 
     from swarm_amd.dist import Rects
     t0 = time.time()
-    d = gen.shard_inputs(args.agents, args.seed, world, rank, deg=args.deg, t=args.tasks, layout=args.partition)
-    region = Rects(d["rects"], rank) if args.partition == "blocks" else d["strip"]
+    if args.partition == "blocks" and args.pieces > 1:
+        from swarm_amd.dist import block_pieces
+        d, region = block_pieces(args.agents, args.seed, world, rank, args.pieces, deg=args.deg, t=args.tasks)
+    else:
+        d = gen.shard_inputs(args.agents, args.seed, world, rank, deg=args.deg, t=args.tasks, layout=args.partition)
+        region = Rects(d["rects"], rank) if args.partition == "blocks" else d["strip"]
     sh = ShardedSwarm(d["ids"], d["x"], d["y"], d["caps"], region, device=dev)
     tx = torch.as_tensor(d["tx"], device=dev)
     ty = torch.as_tensor(d["ty"], device=dev)
@@ -707,7 +715,10 @@ def sharded(args, rank, world, dev):
             "dtype": "int32+f64",
             "data": ("synthetic (seeded RGG, SplitMix64; rank k owns the contiguous ID range [k n, (k+1) n): "
                      + ("its horizontal strip, random order inside it)" if args.partition == "strips" else
-                        "its Morton-ordered block, Morton order inside it)")),
+                        "its Morton-ordered block, Morton order inside it)")
+                     if args.pieces == 1 or args.partition != "blocks" else
+                     "synthetic (seeded RGG, SplitMix64; the Morton-blocks swarm, its IDs cut into %d ranges dealt "
+                     "round-robin: rank k owns the k-th Morton piece of every block)" % (world * args.pieces)),
             "config": {"workload": ("C5: %d agents sharded by ID range over %d GPUs (%d per GPU)"
                                     % (total_agents, world, args.agents) if args.config == "C5" else
                                     "C3 per GPU x %d GPUs (weak scaling): %d agents/GPU" % (world, args.agents))
@@ -715,8 +726,11 @@ def sharded(args, rank, world, dev):
                        "agents_total": total_agents, "tasks_total": args.tasks * world,
                        "partition": ("contiguous ID ranges = horizontal strips (gen.shard_inputs ids='range': strip-major "
                                      "IDs, not a global random permutation)" if args.partition == "strips" else
-                                     "contiguous ID ranges of Morton IDs = Morton-ordered blocks "
-                                     "(gen.shard_inputs layout='blocks')"),
+                                     ("contiguous ID ranges of Morton IDs = Morton-ordered blocks "
+                                      "(gen.shard_inputs layout='blocks')" if args.pieces == 1 else
+                                      "%d ID ranges of Morton IDs per rank, dealt round-robin over the ranks "
+                                      "(dist.block_pieces; layout Cells)" % args.pieces)),
+                       "pieces": args.pieces,
                        "peers_rank0": list(sh.peers), "ghosts_rank0": int(sh.n_glo + sh.n_ghi),
                        "columns_rank0": "int16 deltas" if sh.c16 is not None else "int32",
                        "rounds_exec": r.rounds_exec,

@@ -130,18 +130,30 @@ class Cells:
     tasks, which is all exactness needs."""
     kind = "cells"
 
-    def __init__(self, x, y, who, rank: int, world: int, cell: float, tx=None, ty=None, twho=None):
+    def __init__(self, x, y, who, rank: int, world: int, cell: float, tx=None, ty=None, twho=None, bounds=None):
+        """bounds (x0, y0, x1, y1): the grid's extent, given when the agents arrive in parts (add());
+        every point added must lie inside it.  Otherwise the extent of x, y (and tx, ty)."""
         self.rank, self.world, self.cell = rank, world, float(cell)
         x, y = np.asarray(x, np.float64), np.asarray(y, np.float64)
-        pts = [x, y] + ([np.asarray(tx, np.float64), np.asarray(ty, np.float64)] if tx is not None else [])
-        self.x0 = min(float(v.min()) for v in pts[0::2] if len(v)) if len(x) else 0.0
-        self.y0 = min(float(v.min()) for v in pts[1::2] if len(v)) if len(x) else 0.0
-        x1 = max(float(v.max()) for v in pts[0::2] if len(v)) if len(x) else 0.0
-        y1 = max(float(v.max()) for v in pts[1::2] if len(v)) if len(x) else 0.0
+        if bounds is not None:
+            self.x0, self.y0, x1, y1 = (float(b) for b in bounds)
+        else:
+            pts = [x, y] + ([np.asarray(tx, np.float64), np.asarray(ty, np.float64)] if tx is not None else [])
+            self.x0 = min(float(v.min()) for v in pts[0::2] if len(v)) if len(x) else 0.0
+            self.y0 = min(float(v.min()) for v in pts[1::2] if len(v)) if len(x) else 0.0
+            x1 = max(float(v.max()) for v in pts[0::2] if len(v)) if len(x) else 0.0
+            y1 = max(float(v.max()) for v in pts[1::2] if len(v)) if len(x) else 0.0
         self.shape = (int((y1 - self.y0) // self.cell) + 1, int((x1 - self.x0) // self.cell) + 1)
         self.occ = {"elect": self._occupancy(x, y, who)}
         if tx is not None:
             self.occ["alloc"] = self._occupancy(np.asarray(tx, np.float64), np.asarray(ty, np.float64), twho)
+        self._dil = {}
+
+    def add(self, x, y, who, purpose="elect"):
+        """Mark more points' cells (a swarm that arrives in parts; bounds= at construction)."""
+        occ = self.occ.setdefault(purpose, np.zeros((self.world,) + self.shape, bool))
+        cy, cx = self._cells(np.asarray(x, np.float64), np.asarray(y, np.float64))
+        occ[np.asarray(who, np.int64), cy, cx] = True
         self._dil = {}
 
     def _cells(self, x, y):
@@ -211,6 +223,48 @@ def id_cuts(ids, world: int) -> np.ndarray:
     return np.partition(ids, ks)[ks].astype(np.int64)
 
 
+def piece_owner(ids, cuts, world: int) -> np.ndarray:
+    """Owner of each ID when the IDs are cut into len(cuts) + 1 ranges (id_cuts(ids, world * pieces))
+    dealt round-robin: range j goes to rank j % world.  One range per rank (pieces = 1) is the plain
+    ID-range partition; more pieces spread every rank over the whole square (Morton IDs: each Morton
+    block's j-th piece to rank j), which evens out the per-round work when the election's front crosses
+    the square from one corner."""
+    return np.searchsorted(np.asarray(cuts, np.int64), np.asarray(ids, np.int64), side="right") % world
+
+
+def block_pieces(n_per: int, seed: int, world: int, rank: int, pieces: int, *, deg: float = 16.0, t: int = 0,
+                 cell: float = 1.0):
+    """Rank `rank`'s share of the Morton-blocks swarm (gen.shard_inputs(layout="blocks"), SURVEY §8e's C5
+    shape: IDs 0 .. n_per * world - 1 along the blocks' Morton order) when its IDs are cut into
+    world * pieces equal ranges dealt round-robin (piece_owner): rank q owns the ranges q, q + world, ...
+    -- with pieces = world, the q-th Morton piece of every block.  Every rank generates the whole swarm
+    block by block (same seeds, so the union is the blocks layout's) and keeps its own agents; its
+    tasks are block `rank`'s.  Returns (inputs dict as shard_inputs', Cells layout of every rank's
+    agents and tasks).  The cuts are id_cuts' on the full ID set: (j * total) // (world * pieces)."""
+    from . import gen
+    total = n_per * world
+    cuts = np.array([(j * total) // (world * pieces) for j in range(1, world * pieces)], np.int64)
+    side = gen.side_length(total, deg)
+    layout = Cells(np.zeros(0), np.zeros(0), np.zeros(0, np.int64), rank, world, cell, bounds=(0.0, 0.0, side, side))
+    keep = {k: [] for k in ("x", "y", "ids", "caps")}
+    out = None
+    for b in range(world):
+        d = gen.shard_inputs(n_per, seed, world, b, deg=deg, t=t, layout="blocks")
+        who = piece_owner(d["ids"], cuts, world)
+        layout.add(d["x"], d["y"], who)
+        if t:  # block b's tasks go to rank b
+            layout.add(d["tx"], d["ty"], np.full(len(d["tx"]), b, np.int64), purpose="alloc")
+        m = who == rank
+        for k in keep:
+            keep[k].append(d[k][m])
+        if b == rank:
+            out = d
+        del d, who, m
+    d = dict(out, **{k: np.concatenate(v) for k, v in keep.items()})
+    d.update(n=int(len(d["ids"])), pieces=pieces, id_range=None)
+    return d, layout
+
+
 def _strip_rects(x, y, tx, ty, cuts):
     pts_x = [np.asarray(x, np.float64)] + ([np.asarray(tx, np.float64)] if tx is not None else [])
     pts_y = [np.asarray(y, np.float64)] + ([np.asarray(ty, np.float64)] if ty is not None else [])
@@ -221,7 +275,7 @@ def _strip_rects(x, y, tx, ty, cuts):
 
 
 def partition(x, y, world: int, rank: int, *, ty=None, tx=None, min_height: float = 0.0, by: str = "y",
-              ids=None, cell: float = 1.0) -> Part:
+              ids=None, cell: float = 1.0, pieces: int = 1) -> Part:
     """Split ONE global swarm (every rank passes the same arrays) over `world` ranks; rank `rank`
     owns part.agents and resolves part.tasks.
 
@@ -231,7 +285,8 @@ def partition(x, y, world: int, rank: int, *, ty=None, tx=None, min_height: floa
     `world` contiguous ID ranges of equal agent count, whatever the ID map.  When the ranges are
     horizontal strips (strip-major IDs: gen.strip_ids) the layout is those strips (Rects, tasks by
     strip); otherwise (random IDs, Morton IDs, ...) the layout is Cells and the tasks are dealt in
-    `world` contiguous index ranges.
+    `world` contiguous index ranges.  pieces > 1 (by="id"): world * pieces ID ranges of equal agent
+    count, range j to rank j % world (piece_owner) -- layout Cells.
 
     Why the union of the shards reproduces the single-swarm results: every agent is owned exactly
     once, every task resolved exactly once, and ShardedSwarm's deep halo and claim-radius halo give
@@ -251,8 +306,10 @@ def partition(x, y, world: int, rank: int, *, ty=None, tx=None, min_height: floa
         if ids is None:
             raise ValueError('partition(by="id") needs ids')
         ids = np.asarray(ids, np.int64)
-        icut = id_cuts(ids, world)
-        who = np.searchsorted(icut, ids, side="right")
+        if pieces < 1:
+            raise ValueError("pieces must be >= 1")
+        icut = id_cuts(ids, world * pieces)
+        who = piece_owner(ids, icut, world)
         counts = np.bincount(who, minlength=world)
         if world > 1 and (counts == 0).any():
             raise ValueError(f"ID ranges of equal agent count leave rank(s) {np.nonzero(counts == 0)[0].tolist()} "
@@ -260,8 +317,11 @@ def partition(x, y, world: int, rank: int, *, ty=None, tx=None, min_height: floa
         cuts = np.array([y[who == k].min() for k in range(1, world)], np.float64) if world > 1 else np.zeros(0)
         # strip-major IDs: the ID ranges ARE horizontal strips (every agent of range k below range k+1)
         strips = bool(np.array_equal(np.searchsorted(cuts, y, side="right"), who))
-        edges_id = np.concatenate([[ids.min() if len(ids) else 0], icut, [ids.max() + 1 if len(ids) else 0]])
-        id_range = (int(edges_id[rank]), int(edges_id[rank + 1]))
+        if pieces > 1:
+            strips = False
+        else:
+            edges_id = np.concatenate([[ids.min() if len(ids) else 0], icut, [ids.max() + 1 if len(ids) else 0]])
+            id_range = (int(edges_id[rank]), int(edges_id[rank + 1]))
     else:
         raise ValueError(f"unknown partition key {by!r}")
     agents = np.nonzero(who == rank)[0].astype(np.int64)
@@ -668,7 +728,7 @@ class ShardedSwarm:
 
     @classmethod
     def from_global(cls, ids, x, y, caps=None, *, ty=None, tx=None, radius: float = 1.0, group=None, device=None,
-                    backend=None, halo=None, halo_depth: int | None = None, by: str = "y"):
+                    backend=None, halo=None, halo_depth: int | None = None, by: str = "y", pieces: int = 1):
         """This rank's shard of ONE global swarm (every rank passes the same arrays): strips of
         equal agent count, or (by="id") contiguous ID ranges of any ID map -- partition().
         self.part holds the global indices of the owned agents and of the tasks this rank
@@ -677,7 +737,8 @@ class ShardedSwarm:
             rank, world = halo.rank, halo.world
         else:
             rank, world = dist.get_rank(group), dist.get_world_size(group)
-        part = partition(x, y, world, rank, ty=ty, tx=tx, min_height=radius, by=by, ids=ids, cell=radius)
+        part = partition(x, y, world, rank, ty=ty, tx=tx, min_height=radius, by=by, ids=ids, cell=radius,
+                         pieces=pieces)
         a = part.agents
         caps_a = None if caps is None else np.asarray(caps)[a]
         sh = cls(np.asarray(ids)[a], np.asarray(x)[a], np.asarray(y)[a], caps_a, part.layout, radius=radius,

@@ -4,7 +4,8 @@ bench.py --config C5 with EIGHT ranks sharing one GPU (SWARM_DIST_BACKEND=gloo: 
 sharded loop over the shared-memory transport, 7 peers' worth of ranks), Morton blocks with Morton IDs
 (SURVEY §8e's C5 partition: contiguous ID ranges, up to 8 neighbouring ranks) and strips; the line's
 result_check.union_oracle compares every rank's leaders, rounds_exec and per-round global changes with
-the C oracle over the union swarm.  The full-size run (8 x 12.5M) is the same command without --agents
+the C oracle over the union swarm.  --pieces 8: the same Morton swarm, its IDs cut into 64 ranges dealt
+round-robin (rank q owns the q-th Morton piece of every block: 7 peers each).  The full-size run (8 x 12.5M) is the same command without --agents
 (profiles/)."""
 import json
 import os
@@ -25,13 +26,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("partition,agents", [("blocks", 150_000), ("strips", 100_000)])
-def test_c5_bench_eight_ranks_one_gpu_matches_union_oracle(partition, agents):
+@pytest.mark.parametrize("partition,agents,pieces", [("blocks", 150_000, 1), ("strips", 100_000, 1),
+                                                     ("blocks", 150_000, 8)])
+def test_c5_bench_eight_ranks_one_gpu_matches_union_oracle(partition, agents, pieces):
     env = dict(os.environ, SWARM_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", "8", "--config", "C5", "--agents", str(agents), "--tasks", "200", "--steps", "1",
-           "--warmup", "0", "--cpu-baseline", "0", "--partition", partition]
+           "--warmup", "0", "--cpu-baseline", "0", "--partition", partition, "--pieces", str(pieces)]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     if p.returncode:
         os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
@@ -46,4 +48,5 @@ def test_c5_bench_eight_ranks_one_gpu_matches_union_oracle(partition, agents):
     assert out["n_gpus"] == 8 and out["scaling"] == "strong" and "REHEARSAL" in out["rehearsal"]
     assert "shared-memory" in out["config"]["parallelism"]
     if partition == "blocks":
-        assert len(out["config"]["peers_rank0"]) >= 2
+        assert len(out["config"]["peers_rank0"]) >= (4 if pieces > 1 else 2)
+    assert out["config"]["pieces"] == pieces

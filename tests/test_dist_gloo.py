@@ -159,6 +159,28 @@ def test_partition_by_id_range_is_the_strip_partition(world):
         assert np.array_equal(np.sort(d["ids"][q.agents]), np.arange(lo, hi))
 
 
+@pytest.mark.parametrize("world,pieces", [(4, 4), (8, 8), (2, 3)])
+def test_block_pieces_are_the_round_robin_id_partition(world, pieces):
+    """dist.block_pieces (the C5 rehearsal's --pieces inputs, generated rank by rank): every rank owns
+    exactly what partition(by='id', pieces=) gives on the union of the Morton blocks, n_per agents each,
+    and its Cells layout marks every rank's agents and every block's tasks (block b's tasks: rank b)."""
+    from swarm_amd import gen
+    from swarm_amd.dist import block_pieces, partition
+    n_per, t = 3_000, 40
+    ds = [gen.shard_inputs(n_per, 11, world, b, t=t, layout="blocks") for b in range(world)]
+    x, y = np.concatenate([d["x"] for d in ds]), np.concatenate([d["y"] for d in ds])
+    ids = np.concatenate([d["ids"] for d in ds])
+    for q in range(world):
+        dq, lay = block_pieces(n_per, 11, world, q, pieces, t=t)
+        assert len(dq["ids"]) == n_per
+        pt = partition(x, y, world, q, by="id", ids=ids, pieces=pieces)
+        np.testing.assert_array_equal(np.sort(ids[pt.agents]), np.sort(dq["ids"]))
+        np.testing.assert_array_equal(dq["tx"], ds[q]["tx"])
+        cy, cx = lay._cells(dq["x"], dq["y"])
+        assert lay.occ["elect"][q, cy, cx].all() and lay.occ["alloc"].sum() > 0
+        assert type(pt.layout).__name__ == "Cells"
+
+
 # ----------------------------------------------------------------------------- sharded auction
 A_PER, A_T = 300, 60
 
@@ -225,7 +247,7 @@ def _global_inputs(world, by, ids="strip"):
     return d
 
 
-def _global_worker(rank, world, port, out_q, depth, by="y", ids="strip"):
+def _global_worker(rank, world, port, out_q, depth, by="y", ids="strip", pieces=1):
     import sys
     for p in (PKG, ROOT, os.path.join(ROOT, "tests")):
         sys.path.insert(0, p)
@@ -237,7 +259,7 @@ def _global_worker(rank, world, port, out_q, depth, by="y", ids="strip"):
         from swarm_amd.dist import ShardedSwarm
         d = _global_inputs(world, by, ids)
         sh = ShardedSwarm.from_global(d["ids"], d["x"], d["y"], d["caps"], tx=d["tx"], ty=d["ty"], device="cpu",
-                                      backend=NumpyBackend(), halo_depth=depth, by=by)
+                                      backend=NumpyBackend(), halo_depth=depth, by=by, pieces=pieces)
         r = sh.elect(check_every=5)
         res, won, gst = sh.allocate_global(d["tx"], d["ty"], d["treq"])
         out_q.put(dict(rank=rank, rounds=r.rounds_exec, changes=r.changes, ids=sh.ids.numpy(),
@@ -248,20 +270,21 @@ def _global_worker(rank, world, port, out_q, depth, by="y", ids="strip"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,depth,by,ids", [(2, 4, "y", "strip"), (3, 16, "y", "strip"), (2, 4, "id", "strip"),
-                                               (3, 16, "id", "strip"), (2, 3, "id", "morton"), (3, 5, "id", "morton"),
-                                               (4, 4, "id", "morton"), (2, 2, "id", "random"),
-                                               (3, 1, "id", "random"), (4, 3, "id", "random")])
-def test_partitioned_global_swarm_matches_single_swarm(world, depth, by, ids, oracle_mod):
+@pytest.mark.parametrize("world,depth,by,ids,pieces", [
+    (2, 4, "y", "strip", 1), (3, 16, "y", "strip", 1), (2, 4, "id", "strip", 1), (3, 16, "id", "strip", 1),
+    (2, 3, "id", "morton", 1), (3, 5, "id", "morton", 1), (4, 4, "id", "morton", 1), (2, 2, "id", "random", 1),
+    (3, 1, "id", "random", 1), (4, 3, "id", "random", 1), (2, 3, "id", "morton", 2), (3, 4, "id", "morton", 3)])
+def test_partitioned_global_swarm_matches_single_swarm(world, depth, by, ids, pieces, oracle_mod):
     """ShardedSwarm.from_global: one global input (tasks anywhere) cut on every rank -- by y into strips
     with random IDs, or by contiguous ID range (north_star's ID-range partition) of strip-major IDs
     (strips), of Morton IDs (compact regions with several neighbouring ranks) or of random IDs (every
-    rank a peer of every other); the union of the shards' results equals the single-swarm oracle
-    (leaders, rounds, per-round changes, winners, claim values, conflicts, won counts)."""
+    rank a peer of every other), or world x pieces ID ranges of Morton IDs dealt round-robin (every rank a
+    piece of every region: dist.piece_owner); the union of the shards' results equals the single-swarm
+    oracle (leaders, rounds, per-round changes, winners, claim values, conflicts, won counts)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_global_worker, args=(r, world, port, q, depth, by, ids)) for r in range(world)]
+    procs = [ctx.Process(target=_global_worker, args=(r, world, port, q, depth, by, ids, pieces)) for r in range(world)]
     for p in procs:
         p.start()
     outs = sorted([q.get(timeout=240) for _ in range(world)], key=lambda o: o["rank"])
