@@ -53,6 +53,9 @@ def parse():
                     help="--partition blocks: cut the Morton IDs into N x PIECES equal ranges dealt round-robin "
                          "(rank q owns ranges q, q + N, ...: with PIECES = N the q-th Morton piece of every block; "
                          "dist.block_pieces) -- evens out the election's per-round work across ranks (DESIGN §6)")
+    ap.add_argument("--halo-depth", type=int, default=None,
+                    help="N > 1: rounds between halo exchanges = ghost depth in radio radii (default: "
+                         "SWARM_HALO_DEPTH or 16; C5 blocks with --pieces 16: 4, DESIGN §6)")
     ap.add_argument("--union-gpu", type=int, default=1,
                     help="with --oracle-check: also elect the union swarm on rank 0's GPU (the model's N = 1 time)")
     ap.add_argument("--model", type=int, default=1,
@@ -656,7 +659,7 @@ def sharded(args, rank, world, dev):
     else:
         d = gen.shard_inputs(args.agents, args.seed, world, rank, deg=args.deg, t=args.tasks, layout=args.partition)
         region = Rects(d["rects"], rank) if args.partition == "blocks" else d["strip"]
-    sh = ShardedSwarm(d["ids"], d["x"], d["y"], d["caps"], region, device=dev)
+    sh = ShardedSwarm(d["ids"], d["x"], d["y"], d["caps"], region, device=dev, halo_depth=args.halo_depth)
     tx = torch.as_tensor(d["tx"], device=dev)
     ty = torch.as_tensor(d["ty"], device=dev)
     tq = torch.as_tensor(d["treq"], device=dev)
