@@ -50,9 +50,10 @@ def parse():
                     help="N > 1: strips (strip-major IDs: 2 peers per rank, 16-bit columns) or blocks "
                          "(SURVEY §8e's Morton IDs: Morton-ordered blocks, up to 8 peers per rank)")
     ap.add_argument("--pieces", type=int, default=1,
-                    help="--partition blocks: cut the Morton IDs into N x PIECES equal ranges dealt round-robin "
-                         "(rank q owns ranges q, q + N, ...: with PIECES = N the q-th Morton piece of every block; "
-                         "dist.block_pieces) -- evens out the election's per-round work across ranks (DESIGN §6)")
+                    help="cut the IDs into N x PIECES equal ranges dealt round-robin (rank q owns ranges q, q + N, "
+                         "...) -- evens out the election's per-round work across ranks (DESIGN §6).  blocks: Morton "
+                         "pieces of every block (dist.block_pieces); strips: N x PIECES thin strips, strip-major IDs "
+                         "at that grain (gen.shard_inputs pieces=)")
     ap.add_argument("--halo-depth", type=int, default=None,
                     help="N > 1: rounds between halo exchanges = ghost depth in radio radii (default: "
                          "SWARM_HALO_DEPTH or 16; C5 blocks with --pieces 16: 4, DESIGN §6)")
@@ -657,8 +658,9 @@ def sharded(args, rank, world, dev):
         from swarm_amd.dist import block_pieces
         d, region = block_pieces(args.agents, args.seed, world, rank, args.pieces, deg=args.deg, t=args.tasks)
     else:
-        d = gen.shard_inputs(args.agents, args.seed, world, rank, deg=args.deg, t=args.tasks, layout=args.partition)
-        region = Rects(d["rects"], rank) if args.partition == "blocks" else d["strip"]
+        d = gen.shard_inputs(args.agents, args.seed, world, rank, deg=args.deg, t=args.tasks, layout=args.partition,
+                             pieces=args.pieces)
+        region = Rects(d["rects"], rank) if (args.partition == "blocks" or args.pieces > 1) else d["strip"]
     sh = ShardedSwarm(d["ids"], d["x"], d["y"], d["caps"], region, device=dev, halo_depth=args.halo_depth)
     tx = torch.as_tensor(d["tx"], device=dev)
     ty = torch.as_tensor(d["ty"], device=dev)
@@ -719,16 +721,23 @@ def sharded(args, rank, world, dev):
             "data": ("synthetic (seeded RGG, SplitMix64; rank k owns the contiguous ID range [k n, (k+1) n): "
                      + ("its horizontal strip, random order inside it)" if args.partition == "strips" else
                         "its Morton-ordered block, Morton order inside it)")
-                     if args.pieces == 1 or args.partition != "blocks" else
+                     if args.pieces == 1 else
                      "synthetic (seeded RGG, SplitMix64; the Morton-blocks swarm, its IDs cut into %d ranges dealt "
-                     "round-robin: rank k owns the k-th Morton piece of every block)" % (world * args.pieces)),
+                     "round-robin: rank k owns the k-th Morton pieces of every block)" % (world * args.pieces)
+                     if args.partition == "blocks" else
+                     "synthetic (seeded RGG, SplitMix64; %d thin horizontal strips, thin strip j holding the ID range "
+                     "[j n/%d, (j+1) n/%d) in random order, dealt round-robin: rank k owns thin strips k, k+%d, ...)"
+                     % (world * args.pieces, args.pieces, args.pieces, world)),
             "config": {"workload": ("C5: %d agents sharded by ID range over %d GPUs (%d per GPU)"
                                     % (total_agents, world, args.agents) if args.config == "C5" else
                                     "C3 per GPU x %d GPUs (weak scaling): %d agents/GPU" % (world, args.agents))
                        + ", deg %g, election to convergence + %d tasks/GPU allocation" % (args.deg, args.tasks),
                        "agents_total": total_agents, "tasks_total": args.tasks * world,
-                       "partition": ("contiguous ID ranges = horizontal strips (gen.shard_inputs ids='range': strip-major "
-                                     "IDs, not a global random permutation)" if args.partition == "strips" else
+                       "partition": (("contiguous ID ranges = horizontal strips (gen.shard_inputs ids='range': "
+                                      "strip-major IDs, not a global random permutation)" if args.pieces == 1 else
+                                      "%d ID ranges per rank = thin horizontal strips dealt round-robin (layout Rects, "
+                                      "%d rectangles per rank)" % (args.pieces, args.pieces))
+                                     if args.partition == "strips" else
                                      ("contiguous ID ranges of Morton IDs = Morton-ordered blocks "
                                       "(gen.shard_inputs layout='blocks')" if args.pieces == 1 else
                                       "%d ID ranges of Morton IDs per rank, dealt round-robin over the ranks "
@@ -984,7 +993,8 @@ def union_oracle_check(args, sh, r, rank, world):
     if rank == 0:
         from oracle import oracle as orc
         t0 = time.time()
-        ds = [gen.shard_inputs(args.agents, args.seed, world, q, deg=args.deg, layout=args.partition)
+        ds = [gen.shard_inputs(args.agents, args.seed, world, q, deg=args.deg, layout=args.partition,
+                               pieces=args.pieces if args.partition == "strips" else 1)
               for q in range(world)]
         x = np.concatenate([e["x"] for e in ds])
         y = np.concatenate([e["y"] for e in ds])

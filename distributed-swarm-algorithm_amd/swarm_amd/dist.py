@@ -76,13 +76,16 @@ class StripChain:
 
 
 class Rects:
-    """Every rank's axis-aligned region (world x [x0, x1, y0, y1]; regions may not overlap): rank p needs
-    the agents within `width` (Euclidean) of its rectangle.  Strips cut from one global swarm, Morton
-    blocks (gen.block_rects).  No depth cap: a deep halo reaches as many ranks as it covers."""
+    """Every rank's region as axis-aligned rectangles (world x [x0, x1, y0, y1], or world x k x 4 for k
+    rectangles per rank: thin strips dealt round-robin, gen.shard_inputs(pieces=k); regions may not
+    overlap): rank p needs the agents within `width` (Euclidean) of any of its rectangles.  Strips cut
+    from one global swarm, Morton blocks (gen.block_rects).  No depth cap: a deep halo reaches as many
+    ranks as it covers."""
     kind = "rectangles"
 
     def __init__(self, rects, rank: int):
-        self.rects = np.asarray(rects, np.float64).reshape(-1, 4)
+        r = np.asarray(rects, np.float64)
+        self.rects = r.reshape(-1, 1, 4) if r.ndim <= 2 else r
         self.rank, self.world = rank, len(self.rects)
 
     def depth_cap(self, radius):
@@ -94,16 +97,17 @@ class Rects:
         for p in range(self.world):
             if p == self.rank:
                 continue
-            x0, x1, y0, y1 = self.rects[p]
-            dx = np.maximum(np.maximum(x0 - x, x - x1), 0.0)
-            dy = np.maximum(np.maximum(y0 - y, y - y1), 0.0)
-            m = dx * dx + dy * dy <= w2
+            m = np.zeros(len(x), bool)
+            for x0, x1, y0, y1 in self.rects[p]:
+                dx = np.maximum(np.maximum(x0 - x, x - x1), 0.0)
+                dy = np.maximum(np.maximum(y0 - y, y - y1), 0.0)
+                m |= dx * dx + dy * dy <= w2
             if m.any():
                 out[p] = m
         return out
 
     def min_extent(self):
-        r = self.rects
+        r = self.rects.reshape(-1, 4)
         return float(min((r[:, 1] - r[:, 0]).min(), (r[:, 3] - r[:, 2]).min()))
 
 

@@ -116,7 +116,7 @@ def block_rects(world: int, side: float) -> np.ndarray:
 
 
 def shard_inputs(n_per: int, seed: int, world: int, rank: int, deg: float = 16.0, t: int = 0,
-                 ids: str = "range", layout: str = "strips"):
+                 ids: str = "range", layout: str = "strips", pieces: int = 1):
     """Rank `rank`'s part of a world-wide synthetic swarm of n_per*world agents: uniform
     positions inside the rank's region of the global square, tasks inside the region.
     layout="strips": horizontal strips.  ids="range" (north_star: agents partitioned by ID range): rank k
@@ -144,6 +144,8 @@ def shard_inputs(n_per: int, seed: int, world: int, rank: int, deg: float = 16.0
         return out
     if layout != "strips":
         raise ValueError(f"unknown layout {layout!r}")
+    if pieces > 1:
+        return _strip_pieces(n_per, seed, world, rank, deg, t, pieces, side, sseed)
     x = uniform(sseed, TAG_X, n_per) * side
     y = rank * h + uniform(sseed, TAG_Y, n_per) * h
     if ids == "range":
@@ -159,6 +161,38 @@ def shard_inputs(n_per: int, seed: int, world: int, rank: int, deg: float = 16.0
     if t:
         tx, ty, treq = tasks(t, sseed, side)
         out["tx"], out["ty"], out["treq"] = tx, rank * h + ty / side * h, treq
+    return out
+
+
+def _strip_pieces(n_per, seed, world, rank, deg, t, k, side, sseed):
+    """shard_inputs(layout="strips", pieces=k): the square cut into world * k thin horizontal strips of
+    n_per / k agents each, thin strip j holding the ID range [j n_per / k, (j + 1) n_per / k) in a seeded
+    random order (strip-major IDs at the thin strips' grain), dealt round-robin: rank q owns the thin
+    strips q, q + world, ... -- so every rank has agents at every height, and the election's front, which
+    starts from the top strip's maximum, loads all ranks alike.  Each rank's region is its k
+    thin strips (rects: world x k x 4)."""
+    if n_per % k:
+        raise ValueError("pieces must divide the agents per rank")
+    m, S = n_per // k, world * k
+    hs = side / S
+    xs, ys, idv = [], [], []
+    for i in range(k):
+        j = i * world + rank
+        js = seed * 1000003 + 7_777_777 + j
+        xs.append(uniform(js, TAG_X, m) * side)
+        ys.append(j * hs + uniform(js, TAG_Y, m) * hs)
+        idv.append(feistel_ids(np.arange(m, dtype=np.int64), m, seed * 7919 + 104_729 + j) + np.int64(j) * m)
+    rects = np.array([[[0.0, side, (i * world + q) * hs, (i * world + q + 1) * hs] for i in range(k)]
+                      for q in range(world)], np.float64)
+    out = dict(n=n_per, total=n_per * world, seed=seed, deg=deg, side=side, rects=rects, pieces=k,
+               strip=(float(rects[rank, :, 2].min()), float(rects[rank, :, 3].max())),
+               x=np.concatenate(xs), y=np.concatenate(ys), ids=np.concatenate(idv).astype(np.int32),
+               id_range=None, caps=capabilities(n_per, sseed))
+    if t:
+        tx, ty, treq = tasks(t, sseed, side)
+        f = ty / side * k  # task height -> one of the rank's thin strips, same relative place inside it
+        i = np.minimum(f.astype(np.int64), k - 1)
+        out["tx"], out["ty"], out["treq"] = tx, (i * world + rank + (f - i)) * hs, treq
     return out
 
 

@@ -34,8 +34,9 @@ def _worker(rank, world, port, out_q, n_per, deg, check_every, halo_depth, layou
         from shard_doubles import NumpyBackend
         from swarm_amd import gen
         from swarm_amd.dist import Rects, ShardedSwarm
-        d = gen.shard_inputs(n_per, SEED, world, rank, deg=deg, t=T_PER, layout=layout)
-        region = Rects(d["rects"], rank) if layout == "blocks" else d["strip"]
+        layout, _, pk = layout.partition(":")  # "strips:3": 3 thin strips per rank, dealt round-robin
+        d = gen.shard_inputs(n_per, SEED, world, rank, deg=deg, t=T_PER, layout=layout, pieces=int(pk or 1))
+        region = Rects(d["rects"], rank) if (layout == "blocks" or pk) else d["strip"]
         sh = ShardedSwarm(d["ids"], d["x"], d["y"], d["caps"], region, device="cpu", backend=NumpyBackend(),
                           halo_depth=halo_depth)
         r = sh.elect(check_every=check_every)
@@ -68,17 +69,21 @@ def _run(world, n_per=N_PER, deg=16.0, check_every=7, halo_depth=1, layout="stri
 
 def _union(world, n_per=N_PER, deg=16.0, layout="strips"):
     from swarm_amd import gen
-    ds = [gen.shard_inputs(n_per, SEED, world, r, deg=deg, t=T_PER, layout=layout) for r in range(world)]
+    layout, _, pk = layout.partition(":")
+    ds = [gen.shard_inputs(n_per, SEED, world, r, deg=deg, t=T_PER, layout=layout, pieces=int(pk or 1))
+          for r in range(world)]
     cat = lambda k: np.concatenate([d[k] for d in ds])  # noqa: E731
     return ds, cat
 
 
 @pytest.mark.parametrize("world,depth,layout", [(2, 1, "strips"), (2, 4, "strips"), (3, 16, "strips"),
-                                                (2, 4, "blocks"), (3, 3, "blocks"), (4, 6, "blocks")])
+                                                (2, 4, "blocks"), (3, 3, "blocks"), (4, 6, "blocks"),
+                                                (2, 2, "strips:3"), (3, 4, "strips:2")])
 def test_sharded_election_and_allocation_match_single_graph(world, depth, layout, oracle_mod):
     """depth: halo depth k (ghosts k radii deep, exchanged every k rounds); with strips 16 is capped by
     the strip height (the same cap on every rank).  layout "blocks": Morton-ordered blocks with Morton
-    IDs (SURVEY §8e's C5 partition) -- up to 8 peers per rank, halos deeper than a block reach further."""
+    IDs (SURVEY §8e's C5 partition) -- up to 8 peers per rank, halos deeper than a block reach further.
+    "strips:k": world x k thin strips dealt round-robin (k ID ranges per rank, Rects with k rectangles)."""
     outs = _run(world, halo_depth=depth, layout=layout)
     ds, cat = _union(world, layout=layout)
     x, y, ids, caps = cat("x"), cat("y"), cat("ids"), cat("caps")
@@ -93,7 +98,7 @@ def test_sharded_election_and_allocation_match_single_graph(world, depth, layout
         assert ((o["state"] == 3) == (o["leader"] == o["ids"])).all()
         assert sum(o["n_ghost"]) > 0
         assert o["depth"] == outs[0]["depth"] and 1 <= o["depth"] <= depth
-        if layout == "blocks":
+        if layout != "strips":
             assert o["depth"] == depth  # no cap: the peer set grows instead
     if layout == "blocks" and world == 4:
         assert all(len(o["peers"]) == 3 for o in outs)  # a 2 x 2 grid: every block touches the other three
