@@ -49,11 +49,12 @@ def parse():
     ap.add_argument("--partition", choices=["strips", "blocks"], default="strips",
                     help="N > 1: strips (strip-major IDs: 2 peers per rank, 16-bit columns) or blocks "
                          "(SURVEY §8e's Morton IDs: Morton-ordered blocks, up to 8 peers per rank)")
-    ap.add_argument("--pieces", type=int, default=1,
+    ap.add_argument("--pieces", type=int, default=None,
                     help="cut the IDs into N x PIECES equal ranges dealt round-robin (rank q owns ranges q, q + N, "
                          "...) -- evens out the election's per-round work across ranks (DESIGN §6).  blocks: Morton "
                          "pieces of every block (dist.block_pieces); strips: N x PIECES thin strips, strip-major IDs "
-                         "at that grain (gen.shard_inputs pieces=)")
+                         "at that grain (gen.shard_inputs pieces=)).  Default: 16 for --config C5 --partition "
+                         "blocks (with --halo-depth 4: the model's 6.3x at 8 GPUs), else 1")
     ap.add_argument("--halo-depth", type=int, default=None,
                     help="N > 1: rounds between halo exchanges = ghost depth in radio radii (default: "
                          "SWARM_HALO_DEPTH or 16; C5 blocks with --pieces 16: 4, DESIGN §6)")
@@ -71,6 +72,10 @@ def parse():
         a.agents = 100_000_000 // a.world_hint if a.config == "C5" else 10_000_000
     if a.config == "C5":
         a.rows = 0  # the other §8 rows keep their own (C2 / C3-sized) workloads: not re-run at C5
+    if a.pieces is None:
+        a.pieces = 16 if (a.config == "C5" and a.partition == "blocks") else 1
+        if a.pieces > 1 and a.halo_depth is None and "SWARM_HALO_DEPTH" not in os.environ:
+            a.halo_depth = 4
     if a.oracle_check is None:
         a.oracle_check = 1 if a.config == "C5" else 0
     return a

@@ -2,7 +2,8 @@
 # C5's exact shape on ONE GPU: NPROC ranks (default 8) x 100M / NPROC agents over the
 # host-staged gloo group (libswarm's native loop over the shared-memory transport), checked against the C
 # oracle on the 100M union (result_check.union_oracle), the union also elected on one GPU (the model's
-# N = 1 time), and the election cost model.  PARTITION=blocks (Morton IDs) or strips.
+# N = 1 time), and the election cost model.  PARTITION=blocks (Morton IDs; bench.py defaults to 16
+# pieces per rank and a 4-round halo there) or strips.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
