@@ -672,7 +672,7 @@ def sharded(args, rank, world, dev):
     tq = torch.as_tensor(d["treq"], device=dev)
     torch.cuda.synchronize()
     log(f"[rank {rank}] setup {time.time() - t0:.1f}s: own={sh.n_own} ghosts={sh.n_glo + sh.n_ghi} "
-        f"peers={sh.peers} E_local={sh.col.numel()} col16={sh.c16 is not None}")
+        f"peers={sh.peers} E_local={sh.col.numel()} col16={sh.c16 is not None} escaped={sh.c16_escaped}")
 
     def step():
         r = sh.elect(check_every=128)
@@ -749,7 +749,9 @@ def sharded(args, rank, world, dev):
                                       "(dist.block_pieces; layout Cells)" % args.pieces)),
                        "pieces": args.pieces,
                        "peers_rank0": list(sh.peers), "ghosts_rank0": int(sh.n_glo + sh.n_ghi),
-                       "columns_rank0": "int16 deltas" if sh.c16 is not None else "int32",
+                       "columns_rank0": ("int16 deltas" + (" (%d escaped to int32)" % sh.c16_escaped
+                                                           if sh.c16_escaped else "")) if sh.c16 is not None
+                       else "int32",
                        "rounds_exec": r.rounds_exec,
                        "halo_depth": sh.halo_depth,
                        "parallelism": f"strip-sharded x{world}: {path}; halo exchanged every {sh.halo_depth} "
@@ -1124,16 +1126,19 @@ def shard_roofline(sh, dev):
     rounds = ctypes.c_int32(0)
     st = _lib.ElectStats()
     # the shard's rows are in cell order ([ghosts-lo | owned | ghosts-hi]), so its 16-bit columns
-    # (sh.c16) normally exist and the election reads them, as the sharded run does
+    # (sh.c16) normally exist and the election reads them, as the sharded run does; ESCAPED columns
+    # (swarm_graph_compact_escaped: multi-peer shards) are the frontier stepper's only, so this single-GPU
+    # election of the shard graph reads its int32 columns then
+    c16 = sh.c16 if sh.c16 is not None and not getattr(sh, "c16_escaped", 0) else None
     with torch.cuda.device(dev):
         _lib.check(_lib.lib().swarm_elect_compact(_lib.ctx(), n, _lib.ptr(sh.row_ptr), _lib.ptr(sh.col),
-                                                  _lib.ptr(sh.c16) if sh.c16 is not None else None,
+                                                  _lib.ptr(c16) if c16 is not None else None,
                                                   _lib.ptr(sh.all_ids), _lib.ptr(lead), _lib.ptr(state), 1 << 16,
                                                   _lib.ELECT_FRONTIER | _lib.ELECT_TIMED, ctypes.byref(rounds), None,
                                                   ctypes.byref(st), _lib.stream()))
     torch.cuda.synchronize()
     sb = sparse_round_bytes(st.active_total, st.edges_total, st.dense_rounds, rounds.value, n,
-                            int(sh.row_ptr[-1].item()), max(st.sparse_launches, 1), sh.c16 is not None)
+                            int(sh.row_ptr[-1].item()), max(st.sparse_launches, 1), c16 is not None)
     bpl = sb["bytes_per_launch"]
     ms = st.sparse_ms / max(st.sparse_launches, 1)
     # the committed PMC figure is the N = 1 C3 bench's (10M agents): it stands for shards of about

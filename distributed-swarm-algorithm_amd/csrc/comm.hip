@@ -539,7 +539,9 @@ int swarm_elect_sharded_ex(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *
     }
     int rc = swarm_frontier_begin_range(ctx, sh->own_begin, sh->n_rows, sh->n_all, sh->init, leader0, leader1, stream);
     if (rc) return rc;
-    if ((rc = swarm_frontier_set_compact(ctx, sh->col16))) return rc;
+    if ((rc = sh->col16_escaped ? swarm_frontier_set_compact_escaped(ctx, sh->col16)
+                                : swarm_frontier_set_compact(ctx, sh->col16)))
+        return rc;
     int32_t *sbuf;
     SW_ALLOC(sbuf, ctx, S_TMP0, (nsend + nrecv + 4) * 4);
     int32_t *rbuf = sbuf + nsend;

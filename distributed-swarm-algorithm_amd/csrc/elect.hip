@@ -224,6 +224,30 @@ struct Col16 {
 // Col16 whose base is 16-byte aligned: the dense rounds read it 8 columns per 16-byte load
 struct Col16A : Col16 {};
 
+// Col16 with escapes (swarm_graph_compact_escaped): a neighbour more than 32767 storage slots from its
+// row's base -- in a shard graph, a ghost stored in another peer's block -- is the sentinel kEsc and is
+// read from the int32 columns instead.  The sparse gather checks the wave once per batch of columns, so
+// a batch with no escaped column costs one compare per column.
+constexpr int kEsc = -32768;
+struct Col16E {
+    const int16_t *p;
+    const int32_t *c;  // the int32 columns of the same graph
+    template <typename I>
+    __device__ __forceinline__ int32_t at(I k, int32_t base) const {
+        const int32_t d = p[k];
+        return d == kEsc ? c[k] : base + d;
+    }
+    // the sparse gather's form: base + delta without the escape test; the caller fixes escaped columns
+    // for a whole batch at once (gather_listed: one wave vote per batch, a taken branch only when a
+    // column of the batch is escaped)
+    template <typename I>
+    __device__ __forceinline__ int32_t raw32(I k, int32_t base, bool &esc) const {
+        const int32_t d = *reinterpret_cast<const int16_t *>(reinterpret_cast<const char *>(p) + (uint32_t(k) << 1));
+        esc = d == kEsc;
+        return base + d;
+    }
+};
+
 
 constexpr int kKm = 8;  // marking re-walks: col loads in flight per lane
 
@@ -455,6 +479,7 @@ struct Frontier {
     int64_t c_lo, n_count;   // rows [c_lo, n_count) are owned: only their changes are counted
     StampMap sm, wsm;
     const int16_t *c16;      // Col16 columns of the same graph (swarm_graph_compact), or nullptr
+    bool c16_esc;            // c16 holds escapes (swarm_graph_compact_escaped): read as Col16E
 };
 
 // Max over the G lanes of an agent's group (G = 4: a quad) through DPP quad permutes -- register
@@ -533,8 +558,23 @@ __device__ __forceinline__ void gather_listed(const Off *__restrict__ rp, CT col
         int m = own;
         int c[K];
         for (Off k = b + sub; k < e; k += G * K) {
+            if constexpr (std::is_same_v<CT, Col16E>) {
+                bool esc[K];
+                bool any = false;
 #pragma unroll
-            for (int j = 0; j < K; ++j) c[j] = cols.at32((k + G * j < e) ? k + G * j : e - 1, v & ~63);
+                for (int j = 0; j < K; ++j) {
+                    c[j] = cols.raw32((k + G * j < e) ? k + G * j : e - 1, v & ~63, esc[j]);
+                    any |= esc[j];
+                }
+                if (__builtin_expect(__ballot(any) != 0, 0)) {
+#pragma unroll
+                    for (int j = 0; j < K; ++j)
+                        if (esc[j]) c[j] = ld4(cols.c, (k + G * j < e) ? k + G * j : e - 1);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < K; ++j) c[j] = cols.at32((k + G * j < e) ? k + G * j : e - 1, v & ~63);
+            }
             int val[K];
 #pragma unroll
             for (int j = 0; j < K; ++j) val[j] = ld4(P, Ix(c[j]));
@@ -774,18 +814,26 @@ __global__ __launch_bounds__(kBlock) void k_frontier_ghosts(const Off *__restric
 
 // Col16 copy of an int32 CSR: col16[k] = col[k] - (v & ~63) for every edge k of row v; *bad is set
 // when a delta does not fit 16 bits (the caller then keeps the int32 columns).
+// Deltas fit in [-32767, 32767]: -32768 is kEsc.  ESC: an out-of-range delta is stored as kEsc and
+// counted in *bad (unsigned long long); otherwise *bad (int) is set and the caller keeps the int32 columns.
+template <bool ESC>
 __global__ __launch_bounds__(kBlock) void k_build_col16(const int32_t *__restrict__ rp, const int32_t *__restrict__ col,
-                                                        int64_t n, int16_t *__restrict__ col16, int *__restrict__ bad) {
+                                                        int64_t n, int16_t *__restrict__ col16, void *__restrict__ bad) {
     int out = 0;
     for (int64_t v = int64_t(blockIdx.x) * kBlock + threadIdx.x; v < n; v += int64_t(gridDim.x) * kBlock) {
         const int32_t base = int32_t(v) & ~63;
         for (int32_t k = rp[v]; k < rp[v + 1]; ++k) {
             const int32_t d = col[k] - base;
-            out |= (d < -32768 || d > 32767) ? 1 : 0;
-            col16[k] = int16_t(d);
+            const bool fits = d >= -32767 && d <= 32767;
+            out += fits ? 0 : 1;
+            col16[k] = int16_t(fits ? d : kEsc);
         }
     }
-    if (__ballot(out) && (threadIdx.x & 63) == 0) atomicOr(bad, 1);
+    if constexpr (ESC) {
+        if (out) atomicAdd(static_cast<unsigned long long *>(bad), (unsigned long long)out);
+    } else {
+        if (__ballot(out) && (threadIdx.x & 63) == 0) atomicOr(static_cast<int *>(bad), 1);
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_state(const int32_t *__restrict__ leader,
@@ -932,6 +980,7 @@ int frontier_bind(swarm_ctx *ctx, int32_t *L0, int32_t *L1, Frontier *f) {
     f->n_count = ctx->step_lo + ctx->step_rows;
     f->n_all = ctx->step_all;
     f->c16 = ctx->step_c16;
+    f->c16_esc = ctx->step_c16_esc;
     f->L[0] = L0;
     f->L[1] = L1;
     uint8_t *a = static_cast<uint8_t *>(ctx->slot[S_ACT]);
@@ -957,6 +1006,7 @@ int frontier_alloc(swarm_ctx *ctx, int64_t n_rows, int64_t n_all, int32_t *L0, i
     ctx->step_all = n_all;
     ctx->step_lo = 0;
     ctx->step_c16 = nullptr;
+    ctx->step_c16_esc = false;
     ctx->step_rd_agent = ctx->step_wr_agent = 0;
     int rc = frontier_bind(ctx, L0, L1, f);
     if (rc) return rc;
@@ -987,7 +1037,7 @@ int launch_frontier_round(const Off *rp, const int32_t *col, const Frontier &f, 
         return launch_dense_round<Off>(rp, col, f.L[(t - 1) & 1], f.L[t & 1], f.n_rows, f.c_lo, f.n_count, f.ring,
                                        f.tot,
                                        k == RK_DENSE_MARK ? f.act[(t + 1) & 1] : nullptr, f.wsm, t, guard, s, hrp,
-                                       hcol, f.c16);
+                                       hcol, f.c16_esc ? nullptr : f.c16);  // escapes: dense rounds read int32
     // the buffer this round marks into (parity t+1) was read by round t-1; every 256 rounds, per
     // parity, it is cleared first, so no stamp outlives the 510 rounds after which its value
     // recurs (take_stamps)
@@ -999,6 +1049,12 @@ int launch_frontier_round(const Off *rp, const int32_t *col, const Frontier &f, 
         hipLaunchKernelGGL((k_sparse_block<Off, 2, true>), grid, dim3(kBlock), 0, s, rp, c32, f, t, guard, hrp, hcol);
     else if (hrp)
         hipLaunchKernelGGL((k_sparse_block<Off, kScan, true>), grid, dim3(kBlock), 0, s, rp, c32, f, t, guard, hrp, hcol);
+    else if (f.c16 && f.c16_esc && small)
+        hipLaunchKernelGGL((k_sparse_block<Off, 2, false, Col16E>), grid, dim3(kBlock), 0, s, rp, Col16E{f.c16, col},
+                           f, t, guard, nullptr, nullptr);
+    else if (f.c16 && f.c16_esc)
+        hipLaunchKernelGGL((k_sparse_block<Off, kScan, false, Col16E>), grid, dim3(kBlock), 0, s, rp,
+                           Col16E{f.c16, col}, f, t, guard, nullptr, nullptr);
     else if (f.c16 && small)
         hipLaunchKernelGGL((k_sparse_block<Off, 2, false, Col16>), grid, dim3(kBlock), 0, s, rp, Col16{f.c16}, f, t,
                            guard, nullptr, nullptr);
@@ -1336,7 +1392,8 @@ int swarm_graph_compact(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const
     int *bad;
     SW_ALLOC(bad, ctx, S_TMP1, sizeof(int));
     SW_HIP(hipMemsetAsync(bad, 0, sizeof(int), s));
-    hipLaunchKernelGGL(k_build_col16, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, row_ptr, col, n, col16, bad);
+    hipLaunchKernelGGL(k_build_col16<false>, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, row_ptr, col, n,
+                       col16, static_cast<void *>(bad));
     SW_LAUNCHED();
     int hbad = 0;
     SW_HIP(hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -1345,6 +1402,36 @@ int swarm_graph_compact(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const
         set_error("a neighbour lies more than 32767 storage slots from its row's 64-agent base: keep the int32 columns");
         return SWARM_ERR_RANGE;
     }
+    return SWARM_OK;
+}
+
+int swarm_graph_compact_escaped(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col,
+                                int16_t *col16, int64_t *n_escaped, void *stream) {
+    using namespace swarm;
+    SW_ARG(ctx != nullptr, "ctx is NULL");
+    if (!ctx_on_current_device(ctx)) return SWARM_ERR_ARG;
+    SW_ARG(n_escaped != nullptr, "n_escaped is NULL");
+    *n_escaped = 0;
+    SW_ARG(n >= 0 && n < (int64_t(1) << 30), "n out of range (< 2^30)");
+    if (n == 0) return SWARM_OK;
+    SW_ARG(row_ptr != nullptr, "row_ptr is NULL");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int32_t e_total = 0;
+    SW_HIP(hipMemcpyAsync(&e_total, row_ptr + n, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    SW_HIP(hipStreamSynchronize(s));
+    SW_ARG(e_total >= 0 && e_total < (int64_t(1) << 30), "escaped 16-bit columns: < 2^30 edges (int32 escapes)");
+    if (e_total == 0) return SWARM_OK;
+    SW_ARG(col && col16, "NULL array");
+    unsigned long long *cnt;
+    SW_ALLOC(cnt, ctx, S_TMP1, sizeof(unsigned long long));
+    SW_HIP(hipMemsetAsync(cnt, 0, sizeof(unsigned long long), s));
+    hipLaunchKernelGGL(k_build_col16<true>, dim3(grid_for(n, kBlock, 8192)), dim3(kBlock), 0, s, row_ptr, col, n,
+                       col16, static_cast<void *>(cnt));
+    SW_LAUNCHED();
+    unsigned long long h = 0;
+    SW_HIP(hipMemcpyAsync(&h, cnt, sizeof(h), hipMemcpyDeviceToHost, s));
+    SW_HIP(hipStreamSynchronize(s));
+    *n_escaped = int64_t(h);
     return SWARM_OK;
 }
 
@@ -1414,6 +1501,15 @@ int swarm_frontier_set_compact(swarm_ctx *ctx, const int16_t *col16) {
     using namespace swarm;
     SW_ARG(ctx != nullptr, "ctx is NULL");
     ctx->step_c16 = tuning().use_c16 ? col16 : nullptr;
+    ctx->step_c16_esc = false;
+    return SWARM_OK;
+}
+
+int swarm_frontier_set_compact_escaped(swarm_ctx *ctx, const int16_t *col16) {
+    using namespace swarm;
+    SW_ARG(ctx != nullptr, "ctx is NULL");
+    ctx->step_c16 = tuning().use_c16 ? col16 : nullptr;
+    ctx->step_c16_esc = ctx->step_c16 != nullptr;
     return SWARM_OK;
 }
 

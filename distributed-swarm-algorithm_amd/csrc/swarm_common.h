@@ -92,6 +92,7 @@ struct swarm_ctx {
     int64_t step_all = 0;
     int64_t step_lo = 0;           // frontier stepper: the owned rows are [step_lo, step_lo + step_rows)
     const int16_t *step_c16 = nullptr;  // frontier stepper: 16-bit columns of the shard graph, or NULL
+    bool step_c16_esc = false;          // step_c16 holds escapes (read through the int32 columns)
     int step_rd_agent = 0;         // frontier stepper: the marks the next round reads are in agent order
     int step_wr_agent = 0;         // ... and the next round writes its marks in agent order (the tail)
     hipStream_t side = nullptr;    // a second stream for work that overlaps the caller's (side_stream)

@@ -36,7 +36,8 @@ EXPORTS = ("swarm_last_error", "swarm_version", "swarm_ctx_create", "swarm_ctx_d
            "swarm_allocate_indexed", "swarm_graph_compact", "swarm_elect_compact",
            "swarm_elect_compact_i64", "swarm_frontier_begin_range", "swarm_frontier_set_compact",
            "swarm_comm_unique_id_kind", "swarm_comm_create_kind", "swarm_comm_kind", "swarm_allocate_indexed_ex",
-           "swarm_protocol_run_ex", "swarm_elect_sharded_ex")
+           "swarm_protocol_run_ex", "swarm_elect_sharded_ex", "swarm_graph_compact_escaped",
+           "swarm_frontier_set_compact_escaped")
 
 
 class SwarmError(RuntimeError):
@@ -82,11 +83,11 @@ class Shard(ctypes.Structure):
                 ("col", ctypes.c_void_p), ("init", ctypes.c_void_p), ("own_begin", ctypes.c_int64),
                 ("halo_depth", ctypes.c_int32), ("n_peers", ctypes.c_int32), ("peers", ctypes.c_void_p),
                 ("send_count", ctypes.c_void_p), ("send_rows", ctypes.c_void_p),
-                ("ghost_count", ctypes.c_void_p), ("col16", ctypes.c_void_p)]
+                ("ghost_count", ctypes.c_void_p), ("col16", ctypes.c_void_p), ("col16_escaped", ctypes.c_int32)]
 
 
 def shard_desc(n_rows, n_all, row_ptr, col, init, own_begin, halo_depth, peers=(), send_count=(), send_rows=None,
-               ghost_count=(), col16=None) -> Shard:
+               ghost_count=(), col16=None, col16_escaped=False) -> Shard:
     """A Shard over device tensors (row_ptr, col, init, send_rows, col16) and host peer lists."""
     import numpy as np
     pe = np.ascontiguousarray(peers, np.int32)
@@ -96,7 +97,7 @@ def shard_desc(n_rows, n_all, row_ptr, col, init, own_begin, halo_depth, peers=(
     hp = lambda a: a.ctypes.data_as(ctypes.c_void_p) if a.size else z  # noqa: E731
     dp = lambda t: ptr(t) if t is not None and t.numel() else z  # noqa: E731
     d = Shard(int(n_rows), int(n_all), dp(row_ptr), dp(col), dp(init), int(own_begin), int(halo_depth), len(pe),
-              hp(pe), hp(sc), dp(send_rows), hp(gc), dp(col16))
+              hp(pe), hp(sc), dp(send_rows), hp(gc), dp(col16), int(bool(col16_escaped)))
     d.keep = (pe, sc, gc)
     return d
 
@@ -142,6 +143,8 @@ def load(path: str = LIB_PATH):
         L.swarm_frontier_begin.argtypes = [P, i64, i64, P, P, P, P]
         L.swarm_frontier_begin_range.argtypes = [P, i64, i64, i64, P, P, P, P]
         L.swarm_frontier_set_compact.argtypes = [P, P]
+        L.swarm_frontier_set_compact_escaped.argtypes = [P, P]
+        L.swarm_graph_compact_escaped.argtypes = [P, i64, P, P, P, ctypes.POINTER(i64), P]
         L.swarm_frontier_step.argtypes = [P, i32, P, P, P, P, P]
         L.swarm_frontier_ghosts.argtypes = [P, i32, i64, i64, P, P, P, P, P, P]
         L.swarm_frontier_changes.argtypes = [P, i32, i32, P, P]

@@ -40,6 +40,7 @@ trades k times fewer round trips for stepping k x 10k-20k ghost rows per border 
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from dataclasses import dataclass
 
@@ -475,22 +476,33 @@ class GpuBackend:
         return rp, col
 
     def graph_compact(self, rp, col):
-        """16-bit columns of the shard graph (swarm_graph_compact), or None when a delta does not fit."""
+        """16-bit columns of the shard graph (swarm_graph_compact); when a delta does not fit -- a ghost row
+        stored in another peer's block -- swarm_graph_compact_escaped's, the escaped neighbours read from the
+        int32 columns (self.last_escaped: their count; SWARM_C16_ESC=0: None instead, the int32 columns)."""
+        import os
         L, n = self.L, rp.numel() - 1
+        self.last_escaped = 0
         if n <= 0 or col.numel() == 0:
             return None
         c16 = torch.empty(col.numel(), dtype=torch.int16, device=self.device)
         rc = L.lib().swarm_graph_compact(self.ctx, n, L.ptr(rp), L.ptr(col), L.ptr(c16), L.stream())
-        if rc == L.ERR_RANGE:
+        if rc != L.ERR_RANGE:
+            L.check(rc)
+            return c16
+        if os.environ.get("SWARM_C16_ESC", "1") == "0" or col.numel() >= (1 << 30):
             return None
-        L.check(rc)
+        ne = ctypes.c_int64(0)
+        L.check(L.lib().swarm_graph_compact_escaped(self.ctx, n, L.ptr(rp), L.ptr(col), L.ptr(c16),
+                                                    ctypes.byref(ne), L.stream()))
+        self.last_escaped = int(ne.value)
         return c16
 
-    def begin(self, own_begin, n_own, init, leaders, col16=None):
+    def begin(self, own_begin, n_own, init, leaders, col16=None, escaped=False):
         L = self.L
         L.check(L.lib().swarm_frontier_begin_range(self.ctx, own_begin, n_own, init.numel(), L.ptr(init),
                                                    L.ptr(leaders[0]), L.ptr(leaders[1]), L.stream()))
-        L.check(L.lib().swarm_frontier_set_compact(self.ctx, L.ptr(col16) if col16 is not None else None))
+        setc = L.lib().swarm_frontier_set_compact_escaped if escaped else L.lib().swarm_frontier_set_compact
+        L.check(setc(self.ctx, L.ptr(col16) if col16 is not None else None))
 
     def step(self, t, rp, col, leaders):
         L = self.L
@@ -563,7 +575,8 @@ class GpuBackend:
         desc = L.shard_desc(n_all if alone else sh.n_own, n_all, sh.row_ptr, sh.col, sh.all_ids,
                             0 if alone else sh.own_begin,
                             sh.halo_depth, peers, [sh.send_count[p] for p in peers],
-                            None if alone else sh.send_rows_all, [sh.ghost_count[p] for p in peers], sh.c16)
+                            None if alone else sh.send_rows_all, [sh.ghost_count[p] for p in peers], sh.c16,
+                            col16_escaped=sh.c16_escaped > 0)
         rounds = ctypes.c_int32(0)
         changes = np.zeros(max_rounds, np.int64)
         local = np.zeros((max_rounds, 3), np.int64) if record else None
@@ -702,6 +715,7 @@ class ShardedSwarm:
         self.row_ptr, self.col = self.backend.build_graph(self.all_pos, self.radius)
         self.c16 = self.backend.graph_compact(self.row_ptr, self.col) if hasattr(self.backend, "graph_compact") \
             else None
+        self.c16_escaped = int(getattr(self.backend, "last_escaped", 0)) if self.c16 is not None else 0
         self.leaders = (torch.empty(self.all_ids.numel(), dtype=torch.int32, device=dev),
                         torch.empty(self.all_ids.numel(), dtype=torch.int32, device=dev))
 
@@ -806,7 +820,10 @@ class ShardedSwarm:
         if record:
             raise RuntimeError("elect(record=True) needs the native sharded loop")
         rp, col, lead = self.row_ptr, self.col, self.leaders
-        be.begin(self.own_begin, self.n_own, self.all_ids, lead, self.c16)
+        if self.c16_escaped:
+            be.begin(self.own_begin, self.n_own, self.all_ids, lead, self.c16, escaped=True)
+        else:
+            be.begin(self.own_begin, self.n_own, self.all_ids, lead, self.c16)
         g_lo, g_hi = 0, self.own_begin + self.n_own
         changes = []
         t, found = 1, -1

@@ -138,8 +138,16 @@ int swarm_elect_directed(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, cons
 int swarm_graph_compact(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col, int16_t *col16,
                         void *stream);
 
-/* swarm_elect reading the graph's compact columns (swarm_graph_compact of the same row_ptr/col;
- * col16 NULL: same as swarm_elect).  Same results, same stats.  With col16 it takes graphs of up to
+/* swarm_graph_compact that never refuses: a delta outside [-32767, 32767] is stored as -32768 (an escape)
+ * and the elections read that neighbour from the int32 columns (col must stay alive beside col16).  For
+ * shard graphs, whose ghost rows sit in blocks away from the owned rows: the frontier stepper
+ * takes these columns through swarm_frontier_set_compact_escaped / swarm_shard.col16_escaped.
+ * *n_escaped (host): the escaped edges.  < 2^30 edges. */
+int swarm_graph_compact_escaped(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col,
+                                int16_t *col16, int64_t *n_escaped, void *stream);
+
+/* swarm_elect reading the graph's compact columns (swarm_graph_compact of the same row_ptr/col -- never
+ * swarm_graph_compact_escaped's, which only the frontier stepper reads; col16 NULL: same as swarm_elect).  Same results, same stats.  With col16 it takes graphs of up to
  * 2^31 - 2^20 edges (the 16-bit columns' 32-bit byte offsets), so a 1.6e9-edge swarm (C5's 100M agents
  * on one GPU) runs on 32-bit row offsets; without, < 2^30 edges as swarm_elect. */
 int swarm_elect_compact(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const int32_t *col, const int16_t *col16,
@@ -198,6 +206,8 @@ int swarm_frontier_begin(swarm_ctx *ctx, int64_t n_rows, int64_t n_all, const in
 int swarm_frontier_begin_range(swarm_ctx *ctx, int64_t own_begin, int64_t n_own, int64_t n_all, const int32_t *init,
                                int32_t *leader0, int32_t *leader1, void *stream);
 int swarm_frontier_set_compact(swarm_ctx *ctx, const int16_t *col16);
+/* The same for swarm_graph_compact_escaped's columns (escaped neighbours read from the step's col). */
+int swarm_frontier_set_compact_escaped(swarm_ctx *ctx, const int16_t *col16);
 int swarm_frontier_step(swarm_ctx *ctx, int32_t t, const int32_t *row_ptr, const int32_t *col,
                         int32_t *leader0, int32_t *leader1, void *stream);
 int swarm_frontier_ghosts(swarm_ctx *ctx, int32_t t, int64_t begin, int64_t count,
@@ -242,6 +252,7 @@ typedef struct swarm_shard {
     const int64_t *send_rows;     /* device [sum send_count]: those shard rows, peer after peer */
     const int64_t *ghost_count;   /* host [n_peers]: ghost rows received from each peer */
     const int16_t *col16;         /* swarm_graph_compact of row_ptr / col, or NULL (int32 columns) */
+    int32_t col16_escaped;        /* col16 is swarm_graph_compact_escaped's (escapes read from col) */
 } swarm_shard;
 
 int swarm_comm_available(void);
