@@ -760,9 +760,10 @@ def sharded(args, rank, world, dev):
             "result_check": check,
             "model": model,
             **({"rehearsal": f"REHEARSAL, not a scaling figure: {world} ranks over the host-staged "
-                             f"{dist.get_backend()} group (native loop over the shared-memory transport) on "
+                             f"{dist.get_backend()} group ({path}) on "
                              f"{torch.cuda.device_count()} GPU(s); every exchange goes through host memory"}
                if staged else {}),
+            **({"rccl_double": rccl_double_stats()} if os.environ.get("SWARM_RCCL_PATH") else {}),
             "reference_python": {"value": REF_PYTHON_RATE, "unit": "agent-rounds/s", "cores": 1,
                                  "source": "SURVEY.md §6 (reference election on 1 core of the build container)"},
             "roofline": dict(dom, frac_max_over_ranks=float(fr[0]), frac_min_over_ranks=-float(fr[1]),
@@ -1216,8 +1217,21 @@ def _shard_path(sh):
     if getattr(sh, "_native", None) is not None:
         if getattr(sh.backend, "comm_kind", "rccl") == "shm":
             return "native C loop over the shared-memory transport (host-staged halo + all-reduce per batch)"
-        return "native RCCL loop (swarm_elect_sharded: ncclSend/ncclRecv halo + ncclAllReduce per batch)"
+        dbl = os.environ.get("SWARM_RCCL_PATH", "")
+        return ("native RCCL loop (swarm_elect_sharded: ncclSend/ncclRecv halo + ncclAllReduce per batch)" +
+                (f" through the RCCL test double {os.path.basename(dbl)} (SWARM_RCCL_PATH)" if dbl else ""))
     return f"torch.distributed {dist.get_backend()} halo" + (" (host-staged)" if sh.halo.host_staged else "")
+
+
+def rccl_double_stats():
+    """What the RCCL test double (tests/rccl_double, loaded by libswarm through SWARM_RCCL_PATH) executed in
+    this process: P2P groups, sends, recvs, all-reduces, all-gathers, bytes -- proof that the native loop's
+    RCCL branch ran."""
+    import ctypes
+    L = ctypes.CDLL(os.environ["SWARM_RCCL_PATH"])
+    st = (ctypes.c_longlong * 6)()
+    L.rccl_double_stats(ctypes.cast(st, ctypes.c_void_p))
+    return dict(zip(("groups", "sends", "recvs", "allreduce", "allgather", "bytes"), list(st)))
 
 
 if __name__ == "__main__":

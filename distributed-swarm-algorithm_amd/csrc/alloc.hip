@@ -155,8 +155,11 @@ __global__ __launch_bounds__(kBlock) void k_alloc_init(unsigned long long *__res
 
 // out[0, kNumStats): the shard sums; out[kNumStats] = *dcount (the deferred tasks) when given.  out may
 // be host-mapped memory (the round's stats reach the host without a copy).
+// done / epoch: the host's wait word (mapped host memory) -- written last, after a system-scope fence,
+// so that a host that sees the epoch sees every folded value.
 __global__ void k_fold_stats(const unsigned long long *__restrict__ sh, unsigned long long *__restrict__ out,
-                             const unsigned long long *__restrict__ dcount = nullptr) {
+                             const unsigned long long *__restrict__ dcount = nullptr,
+                             unsigned long long *__restrict__ done = nullptr, unsigned long long epoch = 0) {
     for (int c = 0; c < kNumStats; ++c) {
         unsigned long long v = sh[size_t(threadIdx.x) * kStatStride + c];
 #pragma unroll
@@ -164,6 +167,10 @@ __global__ void k_fold_stats(const unsigned long long *__restrict__ sh, unsigned
         if (threadIdx.x == 0) out[c] = v;
     }
     if (dcount && threadIdx.x == 0) out[kNumStats] = *dcount;
+    if (done && threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(done, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // Per-task epilogue shared by both strategies.
@@ -1136,13 +1143,31 @@ int alloc_impl(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos
     unsigned long long *folded = dstats + size_t(kStatShards) * kStatStride;
     {  // the stats and the deferred count folded straight into host-mapped memory: no copies
         void *fold_dev = nullptr;
-        volatile unsigned long long *hfold = static_cast<unsigned long long *>(mapped(ctx, 16 * 8, &fold_dev));
+        unsigned long long *hfold = static_cast<unsigned long long *>(mapped(ctx, 16 * 8, &fold_dev));
         if (!hfold) return SWARM_ERR_OOM;
+        // The host waits for the fold's epoch word in that memory instead of a stream synchronisation
+        // (the results stay stream-ordered for the caller; only the counters are needed here): a spin
+        // on a host cache line sees the write within ~1 us of the kernel's end, where the synchronise
+        // adds its own wake-up.  hipStreamQuery every 256 spins catches a failed launch.
+        // (the mapped buffer is shared with other calls of this ctx, whose device writes have all been
+        // waited for: the word is cleared here, and the epoch carries a tag no counter reaches)
+        const unsigned long long ep = (0xA110Cull << 40) | (++ctx->fold_epoch & ((1ull << 40) - 1));
+        __atomic_store_n(&hfold[15], 0ull, __ATOMIC_RELEASE);
         hipLaunchKernelGGL(k_fold_stats, dim3(1), dim3(kWave), 0, s, dstats,
-                           static_cast<unsigned long long *>(fold_dev), P.D.count);
+                           static_cast<unsigned long long *>(fold_dev), P.D.count,
+                           static_cast<unsigned long long *>(fold_dev) + 15, ep);
         SW_LAUNCHED();
-        SW_HIP(hipStreamSynchronize(s));
-        for (int c = 0; c <= kNumStats; ++c) hs[c] = hfold[c];
+        for (uint64_t spin = 1; __atomic_load_n(&hfold[15], __ATOMIC_ACQUIRE) != ep; ++spin) {
+            if ((spin & 255) != 0) continue;
+            const hipError_t q = hipStreamQuery(s);
+            if (q == hipErrorNotReady) continue;
+            SW_HIP(q);
+            if (__atomic_load_n(&hfold[15], __ATOMIC_ACQUIRE) != ep) {
+                set_error("allocation: the stream finished without the fold's epoch word");
+                return SWARM_ERR_HIP;
+            }
+        }
+        for (int c = 0; c <= kNumStats; ++c) hs[c] = __atomic_load_n(&hfold[c], __ATOMIC_RELAXED);
     }
     if (hs[7]) {
         set_error("stale cell index: %llu agent(s) outside their cell's range (positions moved since "

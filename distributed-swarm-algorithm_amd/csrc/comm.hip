@@ -364,6 +364,7 @@ int frontier_ghosts_both(swarm_ctx *ctx, int t, const int32_t *rp, const int32_t
                          const int32_t *in_lo, int64_t b_hi, int64_t n_hi, const int32_t *in_hi, int32_t *L0,
                          int32_t *L1, hipStream_t s);
 int frontier_round_totals(swarm_ctx *ctx, int t0, int t1, unsigned long long *dtot, hipStream_t s);
+int frontier_check_compact(swarm_ctx *ctx, const int32_t *rp, const int32_t *col, hipStream_t s);
 int64_t frontier_il_min(int64_t n);
 bool frontier_round_dense(int t);
 }  // namespace swarm
@@ -508,60 +509,96 @@ int swarm_elect_sharded_ex(swarm_ctx *ctx, swarm_comm *comm, const swarm_shard *
     const size_t nsend = size_t(soff[np]), nrecv = size_t(roff[np]);
     constexpr int kMaxBatch = 256;
     constexpr int kC = kElectCounters;
+    const int nr_all = comm->nranks;
+    // agreement row of one rank: [failed, depth, send count to each rank, ghosts from each rank]
+    const size_t aw = 2 + 2 * size_t(nr_all);
     unsigned long long *dtot;
-    SW_ALLOC(dtot, ctx, S_ESTATS, size_t(kC) * 8 * kMaxBatch);
+    SW_ALLOC(dtot, ctx, S_ESTATS, std::max(size_t(kC) * 8 * kMaxBatch, (aw + aw * size_t(nr_all)) * 8));
     // pinned read-back: the batch's global counters, then (local_counts) this rank's own
-    unsigned long long *h = static_cast<unsigned long long *>(pinned(ctx, size_t(kC) * 16 * kMaxBatch));
+    unsigned long long *h = static_cast<unsigned long long *>(
+        pinned(ctx, std::max(size_t(kC) * 16 * kMaxBatch, aw * size_t(nr_all) * 8)));
     if (!h) return SWARM_ERR_OOM;
     unsigned long long *hl = h + size_t(kC) * kMaxBatch;
     const int depth = sh->halo_depth > 1 ? sh->halo_depth : 1;
-    {
-        unsigned long long agree[3] = {why[0] ? 1ull : 0ull, (unsigned long long)depth,
-                                       (unsigned long long)(65536 - depth)};
-        SW_HIP(hipMemcpyAsync(dtot, agree, sizeof(agree), hipMemcpyHostToDevice, s));
-        if (comm->nranks > 1) {
-            if (int rc = comm_allreduce_max_u64(comm, dtot, 3, s)) return rc;
-        }
-        SW_HIP(hipMemcpyAsync(agree, dtot, sizeof(agree), hipMemcpyDeviceToHost, s));
-        SW_HIP(hipStreamSynchronize(s));
-        if (why[0]) {
-            set_error("swarm_elect_sharded: %s", why);
-            return SWARM_ERR_ARG;
-        }
-        if (agree[0]) {
-            set_error("swarm_elect_sharded: a peer rejected its shard (see its error)");
-            return SWARM_ERR_ARG;
-        }
-        if (int(agree[1]) != depth || int(65536 - agree[2]) != depth) {
-            set_error("swarm_elect_sharded: halo_depth differs between ranks (%d here)", depth);
-            return SWARM_ERR_ARG;
-        }
-    }
-    int rc = swarm_frontier_begin_range(ctx, sh->own_begin, sh->n_rows, sh->n_all, sh->init, leader0, leader1, stream);
-    if (rc) return rc;
-    if ((rc = sh->col16_escaped ? swarm_frontier_set_compact_escaped(ctx, sh->col16)
-                                : swarm_frontier_set_compact(ctx, sh->col16)))
-        return rc;
-    int32_t *sbuf;
-    SW_ALLOC(sbuf, ctx, S_TMP0, (nsend + nrecv + 4) * 4);
-    int32_t *rbuf = sbuf + nsend;
-    const int64_t own_end = sh->own_begin + sh->n_rows;
-    // per-round device time of this rank's round launches (round_ms): an event pair per round of a batch
+    // Everything else that one rank alone could fail -- the stepper's scratch, the 16-bit column check,
+    // the loop's buffers and events -- is done before the agreement, so a failure here is agreed on too.
+    int local_rc = SWARM_OK;
+    int32_t *sbuf = nullptr;
+    unsigned long long *lcnt = nullptr;  // this rank's counters of the batch, before the all-reduce
+    // per-round device time of this rank's round launches (round_ms): an event before every round of a
+    // batch and one after its last (round r's time runs from its start to the next round's)
     std::vector<hipEvent_t> ev;
     struct EvFree {
         std::vector<hipEvent_t> &v;
         ~EvFree() { for (auto e : v) (void)hipEventDestroy(e); }
     } ev_free{ev};
-    if (round_ms) {  // one event before every round of a batch and one after its last: round r's time is the
-                     // device time from its start to the next round's (launch gaps included, no second
-                     // event inside the round)
-        ev.resize(kMaxBatch + 1);
-        for (auto &e : ev) SW_HIP(hipEventCreate(&e));
+    if (!why[0]) {
+        int rc = swarm_frontier_begin_range(ctx, sh->own_begin, sh->n_rows, sh->n_all, sh->init, leader0, leader1,
+                                            stream);
+        if (!rc)
+            rc = sh->col16_escaped ? swarm_frontier_set_compact_escaped(ctx, sh->col16)
+                                   : swarm_frontier_set_compact(ctx, sh->col16);
+        if (!rc) rc = frontier_check_compact(ctx, sh->row_ptr, sh->col, s);
+        if (!rc && !(sbuf = static_cast<int32_t *>(scratch(ctx, S_TMP0, (nsend + nrecv + 4) * 4)))) rc = scratch_code();
+        if (!rc && local_counts &&
+            !(lcnt = static_cast<unsigned long long *>(scratch(ctx, S_TMP1, size_t(kC) * 8 * kMaxBatch))))
+            rc = scratch_code();
+        if (!rc && round_ms) {
+            ev.assign(kMaxBatch + 1, nullptr);
+            for (auto &e : ev)
+                if (!rc && hipEventCreate(&e) != hipSuccess) {
+                    set_error("hipEventCreate failed");
+                    rc = SWARM_ERR_HIP;
+                }
+        }
+        if (rc) {
+            local_rc = rc;
+            snprintf(why, sizeof(why), "%s", swarm_last_error());
+        }
     }
-    unsigned long long *lcnt = nullptr;  // this rank's counters of the batch, before the all-reduce
-    if (local_counts) {
-        SW_ALLOC(lcnt, ctx, S_TMP1, size_t(kC) * 8 * kMaxBatch);
+    {
+        // one all-gather of every rank's row: every rank then checks the same matrix and reaches the same
+        // verdict (a count mismatch would otherwise hang an RCCL send/recv pair)
+        std::vector<unsigned long long> row(aw, 0);
+        row[0] = why[0] ? 1ull : 0ull;
+        row[1] = (unsigned long long)depth;
+        for (int j = 0; j < np && !why[0]; ++j) {
+            row[2 + sh->peers[j]] = (unsigned long long)sh->send_count[j];
+            row[2 + nr_all + sh->peers[j]] = (unsigned long long)sh->ghost_count[j];
+        }
+        SW_HIP(hipMemcpyAsync(dtot, row.data(), aw * 8, hipMemcpyHostToDevice, s));
+        if (int rc = comm_allgather_u64(comm, dtot, aw, dtot + aw, s)) return rc;
+        SW_HIP(hipMemcpyAsync(h, dtot + aw, aw * size_t(nr_all) * 8, hipMemcpyDeviceToHost, s));
+        SW_HIP(hipStreamSynchronize(s));
+        if (why[0]) {
+            if (local_rc) return local_rc;  // the error of the failed step is already set
+            set_error("swarm_elect_sharded: %s", why);
+            return SWARM_ERR_ARG;
+        }
+        const auto M = [&](int r, size_t k) { return h[size_t(r) * aw + k]; };
+        for (int r = 0; r < nr_all; ++r) {
+            if (M(r, 0)) {
+                set_error("swarm_elect_sharded: rank %d rejected its shard (see its error)", r);
+                return SWARM_ERR_ARG;
+            }
+            if (int(M(r, 1)) != depth) {
+                set_error("swarm_elect_sharded: halo_depth differs between ranks (%d here, %d on rank %d)", depth,
+                          int(M(r, 1)), r);
+                return SWARM_ERR_ARG;
+            }
+        }
+        for (int a = 0; a < nr_all; ++a)
+            for (int b = 0; b < nr_all; ++b)
+                if (a != b && M(a, 2 + b) != M(b, 2 + nr_all + a)) {
+                    set_error("swarm_elect_sharded: rank %d sends %llu halo rows to rank %d, which expects %llu "
+                              "(send_count / ghost_count / peers disagree)",
+                              a, M(a, 2 + b), b, M(b, 2 + nr_all + a));
+                    return SWARM_ERR_ARG;
+                }
     }
+    int rc = SWARM_OK;
+    int32_t *rbuf = sbuf + nsend;
+    const int64_t own_end = sh->own_begin + sh->n_rows;
     int found = -1, t = 1, batch = 8;
     std::vector<int64_t> hist;
     // the stamp layout: interleaved while rounds are busy, agent order in the tail (as swarm_elect),

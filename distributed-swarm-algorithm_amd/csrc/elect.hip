@@ -836,6 +836,58 @@ __global__ __launch_bounds__(kBlock) void k_build_col16(const int32_t *__restric
     }
 }
 
+// Check of a 16-bit column copy before any election reads it (swarm_elect_compact*, the frontier
+// stepper): every column of row v must name a storage index in [0, n_idx).  A wave takes a task of 64
+// rows -- one delta base (v & ~63) and one contiguous edge slice -- and reads it 8 columns per lane per
+// pass.  ESC = false: the sentinel kEsc is an error (swarm_graph_compact_escaped's columns, which the
+// plain Col16 readers would decode as a delta 32768 below the base); ESC = true: an escaped column's
+// int32 entry is checked instead.  *bad |= 1 (an escape where none may be) or 2 (out of range).
+template <typename Off, bool ESC>
+__global__ __launch_bounds__(kBlock) void k_check_col16(const Off *__restrict__ rp, const int16_t *__restrict__ c16,
+                                                        const int32_t *__restrict__ col, int64_t n_rows, int64_t n_idx,
+                                                        unsigned *__restrict__ bad) {
+    constexpr int kU = 8;
+    const int lane = threadIdx.x & 63;
+    const int64_t ntask = (n_rows + 63) / 64;
+    unsigned out = 0;
+    for (int64_t task = int64_t(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6); task < ntask;
+         task += int64_t(gridDim.x) * kWavesPerBlock) {
+        const int64_t base = task * 64;
+        const Off b = rp[base], e = rp[base + 64 < n_rows ? base + 64 : n_rows];
+        for (Off k0 = b; k0 < e; k0 += 64 * kU) {
+            int32_t d[kU];
+#pragma unroll
+            for (int j = 0; j < kU; ++j) {
+                const Off k = k0 + j * 64 + lane;
+                d[j] = k < e ? int32_t(c16[k]) : 0;
+            }
+#pragma unroll
+            for (int j = 0; j < kU; ++j) {
+                const Off k = k0 + j * 64 + lane;
+                if (k >= e) continue;
+                if (d[j] == kEsc) {
+                    if constexpr (ESC) {
+                        const int32_t c = col[k];
+                        out |= (c < 0 || c >= n_idx) ? 2u : 0u;
+                    } else {
+                        out |= 1u;
+                    }
+                } else {
+                    const int64_t c = base + d[j];
+                    out |= (c < 0 || c >= n_idx) ? 2u : 0u;
+                }
+            }
+        }
+    }
+    // one atomic per wave that found something
+    const unsigned long long any = __ballot(out != 0);
+    if (any) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) out |= __shfl_xor(out, off, 64);
+        if (lane == 0) atomicOr(bad, out);
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_state(const int32_t *__restrict__ leader,
                                                  const int32_t *__restrict__ ids,
                                                  uint8_t *__restrict__ state, int64_t n) {
@@ -1007,6 +1059,7 @@ int frontier_alloc(swarm_ctx *ctx, int64_t n_rows, int64_t n_all, int32_t *L0, i
     ctx->step_lo = 0;
     ctx->step_c16 = nullptr;
     ctx->step_c16_esc = false;
+    ctx->step_c16_checked = false;
     ctx->step_rd_agent = ctx->step_wr_agent = 0;
     int rc = frontier_bind(ctx, L0, L1, f);
     if (rc) return rc;
@@ -1078,6 +1131,46 @@ double round_bytes(bool dense, int64_t n, int64_t e, int64_t active, int64_t edg
     return double(n) + 16.0 * active + 8.0 * edges;
 }
 
+bool esc_registered(const swarm_ctx *ctx, const int16_t *c16) {
+    return std::find(ctx->esc_built.begin(), ctx->esc_built.end(), c16) != ctx->esc_built.end();
+}
+
+// Enqueues the column check of rows [0, n_rows) of (rp, c16) into the ctx's verdict word (zeroed
+// first) and its copy into *hflag; the caller reads *hflag after its next stream synchronisation.
+template <typename Off>
+int enqueue_col16_check(swarm_ctx *ctx, const Off *rp, const int16_t *c16, const int32_t *col, bool esc,
+                        int64_t n_rows, int64_t n_idx, unsigned *hflag, hipStream_t s) {
+    unsigned *d;
+    SW_ALLOC(d, ctx, S_CHECK, sizeof(unsigned));
+    SW_HIP(hipMemsetAsync(d, 0, sizeof(unsigned), s));
+    if (n_rows > 0) {
+        const dim3 grid(grid_for((n_rows + 63) / 64, kWavesPerBlock, 4096));
+        if (esc)
+            hipLaunchKernelGGL((k_check_col16<Off, true>), grid, dim3(kBlock), 0, s, rp, c16, col, n_rows, n_idx, d);
+        else
+            hipLaunchKernelGGL((k_check_col16<Off, false>), grid, dim3(kBlock), 0, s, rp, c16, col, n_rows, n_idx, d);
+        SW_LAUNCHED();
+    }
+    SW_HIP(hipMemcpyAsync(hflag, d, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    return SWARM_OK;
+}
+
+// SWARM_ERR_ARG with the reason for a non-zero check verdict (SWARM_OK for 0).
+int col16_verdict(unsigned hflag, const char *who) {
+    if (hflag & 1u) {
+        set_error("invalid argument: %s: the 16-bit columns hold escapes (swarm_graph_compact_escaped's): "
+                  "pass them through swarm_frontier_set_compact_escaped / swarm_shard.col16_escaped, or build "
+                  "them with swarm_graph_compact", who);
+        return SWARM_ERR_ARG;
+    }
+    if (hflag) {
+        set_error("invalid argument: %s: a 16-bit column names an agent outside the graph (not swarm_graph_compact "
+                  "of this row_ptr / col)", who);
+        return SWARM_ERR_ARG;
+    }
+    return SWARM_OK;
+}
+
 template <typename Off>
 int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, const int32_t *ids,
                int32_t *leader, uint8_t *state, int32_t max_rounds, int32_t mode,
@@ -1101,9 +1194,17 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         if (st) st->rounds_launched = 1;
         return SWARM_OK;
     }
+    // 16-bit columns are checked before any round reads them (one pass over the columns, read back with
+    // the edge count): escaped columns or a foreign buffer are refused, never gathered through
+    SW_ARG(!c16 || !esc_registered(ctx, c16), "col16 holds swarm_graph_compact_escaped's columns (escapes)");
+    unsigned c16_bad = 0;
+    if (c16) {
+        if (int rc = enqueue_col16_check<Off>(ctx, rp, c16, col, false, n, n, &c16_bad, s)) return rc;
+    }
     Off e_total = 0;
     SW_HIP(hipMemcpyAsync(&e_total, rp + n, sizeof(Off), hipMemcpyDeviceToHost, s));
     SW_HIP(hipStreamSynchronize(s));
+    if (int rc = col16_verdict(c16_bad, "swarm_elect_compact")) return rc;
     SW_ARG(e_total == 0 || col != nullptr, "col is NULL but the graph has edges");
     // the int32-CSR kernels address with 32-bit byte offsets (gather_listed's ld4 / Col16::at32):
     // 4-byte columns need < 2^30 edges, 2-byte ones < 2^31 (less a margin for the clamped offsets a
@@ -1316,12 +1417,32 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
 
 // Internal entry points for comm.hip (the RCCL round loop): one stepper round, the ghost update
 // of both borders, and the device per-round totals (kCounters each) of rounds t0..t1.
+// The column check of the stepper's 16-bit columns against the stepped graph (rows and indices
+// [0, n_all)), once per set_compact: comm.hip runs it before its agreement, the public stepper at its
+// first round.
+int frontier_check_compact(swarm_ctx *ctx, const int32_t *rp, const int32_t *col, hipStream_t s) {
+    if (!ctx->step_c16 || ctx->step_c16_checked || ctx->step_all == 0) return SWARM_OK;
+    SW_ARG(rp != nullptr, "row_ptr is NULL");
+    SW_ARG(!ctx->step_c16_esc || col != nullptr, "escaped 16-bit columns need the int32 columns (col is NULL)");
+    unsigned bad = 0;
+    if (int rc = enqueue_col16_check<int32_t>(ctx, rp, ctx->step_c16, col, ctx->step_c16_esc, ctx->step_all,
+                                              ctx->step_all, &bad, s))
+        return rc;
+    SW_HIP(hipStreamSynchronize(s));
+    if (int rc = col16_verdict(bad, ctx->step_c16_esc ? "swarm_frontier_set_compact_escaped"
+                                                      : "swarm_frontier_set_compact"))
+        return rc;
+    ctx->step_c16_checked = true;
+    return SWARM_OK;
+}
+
 int frontier_round_stepper(swarm_ctx *ctx, int t, const int32_t *rp, const int32_t *col, int32_t *L0,
                            int32_t *L1, hipStream_t s) {
     Frontier f{};
     int rc = frontier_bind(ctx, L0, L1, &f);
     if (rc) return rc;
     if (f.n_rows == 0) return SWARM_OK;
+    if ((rc = frontier_check_compact(ctx, rp, col, s))) return rc;
     rc = launch_frontier_round<int32_t>(rp, col, f, t, plan_round(t), /*guard=*/0, s);
     ctx->step_rd_agent = ctx->step_wr_agent;  // the marks this round wrote
     return rc;
@@ -1398,6 +1519,8 @@ int swarm_graph_compact(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const
     int hbad = 0;
     SW_HIP(hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, s));
     SW_HIP(hipStreamSynchronize(s));
+    // the buffer now holds plain deltas (or a refused build): no longer escaped
+    ctx->esc_built.erase(std::remove(ctx->esc_built.begin(), ctx->esc_built.end(), col16), ctx->esc_built.end());
     if (hbad) {
         set_error("a neighbour lies more than 32767 storage slots from its row's 64-agent base: keep the int32 columns");
         return SWARM_ERR_RANGE;
@@ -1432,6 +1555,10 @@ int swarm_graph_compact_escaped(swarm_ctx *ctx, int64_t n, const int32_t *row_pt
     SW_HIP(hipMemcpyAsync(&h, cnt, sizeof(h), hipMemcpyDeviceToHost, s));
     SW_HIP(hipStreamSynchronize(s));
     *n_escaped = int64_t(h);
+    if (h && !esc_registered(ctx, col16))
+        ctx->esc_built.push_back(col16);
+    else if (!h)  // no escape: plain deltas, valid for every reader
+        ctx->esc_built.erase(std::remove(ctx->esc_built.begin(), ctx->esc_built.end(), col16), ctx->esc_built.end());
     return SWARM_OK;
 }
 
@@ -1497,11 +1624,17 @@ int swarm_frontier_begin_range(swarm_ctx *ctx, int64_t own_begin, int64_t n_own,
     return SWARM_OK;
 }
 
+// Both setters leave the columns unchecked: the stepper checks them against its graph before the first
+// round that reads them (frontier_check_compact), and refuses a buffer with escapes here already when
+// this ctx built it with swarm_graph_compact_escaped.
 int swarm_frontier_set_compact(swarm_ctx *ctx, const int16_t *col16) {
     using namespace swarm;
     SW_ARG(ctx != nullptr, "ctx is NULL");
+    SW_ARG(!col16 || !esc_registered(ctx, col16),
+           "col16 holds swarm_graph_compact_escaped's columns: use swarm_frontier_set_compact_escaped");
     ctx->step_c16 = tuning().use_c16 ? col16 : nullptr;
     ctx->step_c16_esc = false;
+    ctx->step_c16_checked = false;
     return SWARM_OK;
 }
 
@@ -1510,6 +1643,7 @@ int swarm_frontier_set_compact_escaped(swarm_ctx *ctx, const int16_t *col16) {
     SW_ARG(ctx != nullptr, "ctx is NULL");
     ctx->step_c16 = tuning().use_c16 ? col16 : nullptr;
     ctx->step_c16_esc = ctx->step_c16 != nullptr;
+    ctx->step_c16_checked = false;
     return SWARM_OK;
 }
 

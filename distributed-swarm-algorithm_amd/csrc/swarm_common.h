@@ -55,6 +55,7 @@ enum Slot {
     S_FPAIRS,         // allocation: the deferred tasks' guard-band pairs (device -> host)
     S_OVR,            // allocation: host libm decisions for those pairs (host -> device)
     S_ENC_FLAGS,      // codec: tile ticket + per-tile look-back words (kept across calls, tagged by epoch)
+    S_CHECK,          // election: the 16-bit column check's verdict word
     S_NUM
 };
 
@@ -93,6 +94,8 @@ struct swarm_ctx {
     int64_t step_lo = 0;           // frontier stepper: the owned rows are [step_lo, step_lo + step_rows)
     const int16_t *step_c16 = nullptr;  // frontier stepper: 16-bit columns of the shard graph, or NULL
     bool step_c16_esc = false;          // step_c16 holds escapes (read through the int32 columns)
+    bool step_c16_checked = false;      // step_c16 passed the column check against the stepped graph
+    std::vector<const int16_t *> esc_built;  // column buffers swarm_graph_compact_escaped last wrote
     int step_rd_agent = 0;         // frontier stepper: the marks the next round reads are in agent order
     int step_wr_agent = 0;         // ... and the next round writes its marks in agent order (the tail)
     hipStream_t side = nullptr;    // a second stream for work that overlaps the caller's (side_stream)
@@ -100,6 +103,7 @@ struct swarm_ctx {
     void *enc_flags = nullptr;     // codec one-pass encode: the S_ENC_FLAGS buffer last zeroed ...
     size_t enc_cap = 0;            // ... and its size
     uint32_t enc_epoch = 0;        // ... the epoch tag of the last call (look-back words carry it)
+    unsigned long long fold_epoch = 0;  // allocation: the last epoch k_fold_stats wrote to mapped memory
 };
 
 namespace swarm {

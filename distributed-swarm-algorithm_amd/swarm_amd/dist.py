@@ -521,8 +521,10 @@ class GpuBackend:
         """A libswarm communicator over the halo's group, or None.  A device (nccl) group gets an RCCL
         communicator; a host-staged (gloo) group whose ranks all run on this host gets the
         shared-memory transport (SWARM_COMM_SHM: the same C loops, every exchange staged through
-        host memory -- how 2-3 processes sharing one GPU run swarm_elect_sharded).  SWARM_NATIVE_HALO=0
-        disables both (the Python stepper then drives the rounds).  Every rank agrees on the outcome
+        host memory -- how 2-3 processes sharing one GPU run swarm_elect_sharded).  SWARM_NATIVE_COMM=rccl
+        takes the RCCL communicator on a gloo group too (with SWARM_RCCL_PATH naming the RCCL test double
+        of tests/rccl_double: the RCCL branch of the native loops with peers that share one GPU, which
+        real RCCL refuses).  SWARM_NATIVE_HALO=0 disables both (the Python stepper then drives the rounds).  Every rank agrees on the outcome
         before anything collective is started, and again after the (collective) create."""
         import ctypes
         import os
@@ -533,6 +535,8 @@ class GpuBackend:
         if os.environ.get("SWARM_NATIVE_HALO", "1") == "0" or halo.world < 2 or not isinstance(halo, Halo):
             return None  # (test doubles that exchange in-process have no torch.distributed group)
         kind = L.COMM_SHM if halo.host_staged else L.COMM_RCCL
+        if os.environ.get("SWARM_NATIVE_COMM", "") == "rccl":
+            kind = L.COMM_RCCL
         dev = "cpu" if halo.host_staged else self.device
         avail = 1 if (kind == L.COMM_SHM or L.lib().swarm_comm_available()) else 0
         host = zlib.crc32(socket.gethostname().encode()) & 0x7FFFFFFF

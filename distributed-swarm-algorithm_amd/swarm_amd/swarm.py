@@ -467,15 +467,19 @@ class Swarm:
                 and c[3][2] is self._id_index):
             return None
         a = c[1]
-        t, dev = a[6], self.device
-        w = torch.empty(t, dtype=torch.int32, device=dev)
-        u = torch.empty(t, dtype=torch.float64, device=dev)
-        won = torch.empty(self.n, dtype=torch.int32, device=dev)
-        nc_nm = torch.empty((2, t), dtype=torch.int64, device=dev)
+        t, n = a[6], self.n
+        # the four outputs carved from ONE allocation (one caching-allocator call instead of four):
+        # util (f64), nclaim + nmsg (i64), winner (i32), won (i32), each 8-byte aligned
+        buf = torch.empty(24 * t + 4 * t + 4 * n + 8, dtype=torch.uint8, device=self.device)
+        b0 = buf.data_ptr()
+        u = buf[:8 * t].view(torch.float64)
+        nc_nm = buf[8 * t:24 * t].view(torch.int64).view(2, t)
+        w = buf[24 * t:28 * t].view(torch.int32)
+        o_won = (28 * t + 7) & ~7
+        won = buf[o_won:o_won + 4 * n].view(torch.int32)
         st = _lib.AllocStats()
-        pn = nc_nm.data_ptr()
-        _lib.check(_lib.lib().swarm_allocate_indexed_ex(_lib.ctx(), *a, w.data_ptr(), u.data_ptr(), won.data_ptr(),
-                                                        *c[2], pn, pn + 8 * t, ctypes.byref(st), _lib.stream()))
+        _lib.check(_lib.lib().swarm_allocate_indexed_ex(_lib.ctx(), *a, b0 + 24 * t, b0, b0 + o_won, *c[2],
+                                                        b0 + 8 * t, b0 + 16 * t, ctypes.byref(st), _lib.stream()))
         return AllocResult(w, u, won, nc_nm[0], nc_nm[1], {k_: getattr(st, k_) for k_, _ in _lib.AllocStats._fields_})
 
     def _task_pos(self, tx, ty) -> torch.Tensor:

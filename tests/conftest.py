@@ -32,6 +32,23 @@ def golden_names(kind_prefix):
     return sorted(k for k in golden_index() if k.startswith(kind_prefix))
 
 
+RCCL_DOUBLE_DIR = os.path.join(ROOT, "tests", "rccl_double")
+RCCL_DOUBLE = os.path.join(RCCL_DOUBLE_DIR, "librccl_double.so")
+
+
+def build_rccl_double():
+    """tests/rccl_double/librccl_double.so (make: rebuilt only when its source changed; g++, host code)."""
+    import subprocess
+    subprocess.run(["make", "-s", "-C", RCCL_DOUBLE_DIR], check=True, capture_output=True)
+    return RCCL_DOUBLE
+
+
+@pytest.fixture(scope="session")
+def rccl_double():
+    """Path of the RCCL test double (SWARM_RCCL_PATH): libswarm's RCCL branch with peers on one GPU."""
+    return build_rccl_double()
+
+
 @pytest.fixture(scope="session")
 def oracle_mod():
     from oracle import oracle

@@ -29,6 +29,28 @@ def c16_np(rp, col):
     return (np.asarray(col, np.int64) - (src & ~63)).astype(np.int16)
 
 
+def far_graph(sw, n=150_000, seed=41):
+    """A swarm graph whose first 4 096 agents are stored at the end: their neighbours' 16-bit deltas
+    do not fit (swarm_graph_compact refuses it; the escaped build marks those columns)."""
+    from swarm_amd import gen
+    d = gen.swarm_inputs(n, seed)
+    s = sw.Swarm(d["ids"], d["x"], d["y"], device="cuda").build_graph(1.0)
+    n = s.n
+    perm = np.concatenate([np.arange(4096, n), np.arange(4096)])
+    inv = np.empty(n, np.int64)
+    inv[perm] = np.arange(n)
+    rp = s.row_ptr.cpu().numpy().astype(np.int64)
+    col = s.col.cpu().numpy().astype(np.int64)
+    deg = np.diff(rp)[perm]
+    rp2 = np.concatenate([[0], np.cumsum(deg)])
+    flat = np.repeat(rp[:-1][perm] - rp2[:-1], deg) + np.arange(rp2[-1])
+    col2 = inv[col[flat]]
+    ids2 = s.ids.cpu().numpy()[perm]
+    rp_t = torch.as_tensor(rp2.astype(np.int32), device="cuda")
+    col_t = torch.as_tensor(col2.astype(np.int32), device="cuda")
+    return n, deg, rp_t, col_t, ids2, col2
+
+
 def test_graph_compact_layout(sw):
     from swarm_amd import gen
     d = gen.swarm_inputs(200000, 31)
@@ -145,23 +167,8 @@ def test_graph_compact_escaped_layout_and_sharded_election(sw):
     """swarm_graph_compact_escaped: deltas outside [-32767, 32767] become -32768 (escapes, read from the
     int32 columns), counted; then the frontier stepper over those columns (swarm_frontier_set_compact_escaped)
     returns the int32-column stepper's leaders and per-round counts exactly."""
-    from swarm_amd import _lib, gen
-    d = gen.swarm_inputs(150_000, 41)
-    s = sw.Swarm(d["ids"], d["x"], d["y"], device="cuda").build_graph(1.0)
-    n = s.n
-    # move the storage of the first 4 096 agents to the end: their neighbours' deltas no longer fit
-    perm = np.concatenate([np.arange(4096, n), np.arange(4096)])
-    inv = np.empty(n, np.int64)
-    inv[perm] = np.arange(n)
-    rp = s.row_ptr.cpu().numpy().astype(np.int64)
-    col = s.col.cpu().numpy().astype(np.int64)
-    deg = np.diff(rp)[perm]
-    rp2 = np.concatenate([[0], np.cumsum(deg)])
-    flat = np.repeat(rp[:-1][perm] - rp2[:-1], deg) + np.arange(rp2[-1])
-    col2 = inv[col[flat]]
-    ids2 = s.ids.cpu().numpy()[perm]
-    rp_t = torch.as_tensor(rp2.astype(np.int32), device="cuda")
-    col_t = torch.as_tensor(col2.astype(np.int32), device="cuda")
+    from swarm_amd import _lib
+    n, deg, rp_t, col_t, ids2, col2 = far_graph(sw)
     c16 = torch.empty(col_t.numel(), dtype=torch.int16, device="cuda")
     L = _lib.lib()
     assert L.swarm_graph_compact(_lib.ctx(), n, _lib.ptr(rp_t), _lib.ptr(col_t), _lib.ptr(c16), _lib.stream()) \
@@ -193,3 +200,68 @@ def test_graph_compact_escaped_layout_and_sharded_election(sw):
         res.append((ch, lead[len(ch) & 1].cpu().numpy()))
     assert res[0][0] == res[1][0] and res[0][0][-1] == 0
     np.testing.assert_array_equal(res[0][1], res[1][1])
+
+
+def test_escaped_columns_refused_by_plain_readers(sw, oracle_mod):
+    """swarm_graph_compact_escaped's columns hold -32768 sentinels that the plain 16-bit readers would
+    decode as a delta 32 768 below the row base (round 5: an illegal address in k_sparse_block).  Every
+    entry point that reads plain 16-bit columns refuses them with SWARM_ERR_ARG before any round runs:
+    the buffer this ctx built (remembered), a copy of it (the device column check), the int64-offset
+    election, the stepper (at set time, or at its first step for the copy), the sharded loop on its own,
+    and a buffer of out-of-range deltas.  The ctx then still elects exactly (agent.py:263-275)."""
+    import ctypes
+    from swarm_amd import _lib
+    n, deg, rp_t, col_t, ids2, col2 = far_graph(sw)
+    L, cx, st = _lib.lib(), _lib.ctx(), _lib.stream()
+    c16 = torch.empty(col_t.numel(), dtype=torch.int16, device="cuda")
+    ne = ctypes.c_int64(0)
+    _lib.check(L.swarm_graph_compact_escaped(cx, n, _lib.ptr(rp_t), _lib.ptr(col_t), _lib.ptr(c16),
+                                             ctypes.byref(ne), st))
+    assert ne.value > 0
+    copy = c16.clone()
+    garbage = torch.full_like(c16, 32767)  # every row base + 32767: past the end for the last rows
+    ids_t = torch.as_tensor(ids2.astype(np.int32), device="cuda")
+    rp64 = rp_t.to(torch.int64)
+    lead = torch.empty(n, dtype=torch.int32, device="cuda")
+    state = torch.empty(n, dtype=torch.uint8, device="cuda")
+    rx = ctypes.c_int32(0)
+    for buf in (c16, copy, garbage):
+        for fn, rp in ((L.swarm_elect_compact, rp_t), (L.swarm_elect_compact_i64, rp64)):
+            for mode in (_lib.ELECT_FRONTIER, _lib.ELECT_DENSE):
+                rc = fn(cx, n, _lib.ptr(rp), _lib.ptr(col_t), _lib.ptr(buf), _lib.ptr(ids_t), _lib.ptr(lead),
+                        _lib.ptr(state), 1 << 16, mode, ctypes.byref(rx), None, None, st)
+                assert rc == _lib.ERR_ARG, (fn, rc, _lib.last_error())
+    # the stepper: the remembered buffer at set time, the copy and the garbage at the first step
+    L0, L1 = torch.empty_like(ids_t), torch.empty_like(ids_t)
+    _lib.check(L.swarm_frontier_begin(cx, n, n, _lib.ptr(ids_t), _lib.ptr(L0), _lib.ptr(L1), st))
+    assert L.swarm_frontier_set_compact(cx, _lib.ptr(c16)) == _lib.ERR_ARG
+    assert "escaped" in _lib.last_error()
+    for buf in (copy, garbage):
+        _lib.check(L.swarm_frontier_begin(cx, n, n, _lib.ptr(ids_t), _lib.ptr(L0), _lib.ptr(L1), st))
+        _lib.check(L.swarm_frontier_set_compact(cx, _lib.ptr(buf)))
+        assert L.swarm_frontier_step(cx, 1, _lib.ptr(rp_t), _lib.ptr(col_t), _lib.ptr(L0), _lib.ptr(L1), st) \
+            == _lib.ERR_ARG
+    # escaped reading of an out-of-range buffer is refused too
+    _lib.check(L.swarm_frontier_begin(cx, n, n, _lib.ptr(ids_t), _lib.ptr(L0), _lib.ptr(L1), st))
+    _lib.check(L.swarm_frontier_set_compact_escaped(cx, _lib.ptr(garbage)))
+    assert L.swarm_frontier_step(cx, 1, _lib.ptr(rp_t), _lib.ptr(col_t), _lib.ptr(L0), _lib.ptr(L1), st) \
+        == _lib.ERR_ARG
+    # the sharded loop (one rank, no communicator) with the escaped columns declared plain
+    for buf in (c16, copy):
+        sh = _lib.shard_desc(n, n, rp_t, col_t, ids_t, 0, 1, col16=buf, col16_escaped=False)
+        rc = L.swarm_elect_sharded(cx, None, ctypes.byref(sh), _lib.ptr(L0), _lib.ptr(L1), 1 << 16,
+                                   ctypes.byref(rx), None, st)
+        assert rc == _lib.ERR_ARG, _lib.last_error()
+    # the same ctx, the same columns declared escaped: exact against the oracle
+    o_lead, o_state, o_rounds, o_changes = oracle_mod.elect(rp_t.cpu().numpy(), col2.astype(np.int32), ids2)
+    sh = _lib.shard_desc(n, n, rp_t, col_t, ids_t, 0, 1, col16=c16, col16_escaped=True)
+    _lib.check(L.swarm_elect_sharded(cx, None, ctypes.byref(sh), _lib.ptr(L0), _lib.ptr(L1), 1 << 16,
+                                     ctypes.byref(rx), None, st))
+    assert rx.value == o_rounds
+    np.testing.assert_array_equal((L0 if o_rounds % 2 == 0 else L1).cpu().numpy(), o_lead)
+    _lib.check(L.swarm_elect(cx, n, _lib.ptr(rp_t), _lib.ptr(col_t), _lib.ptr(ids_t), _lib.ptr(lead),
+                             _lib.ptr(state), 1 << 16, _lib.ELECT_FRONTIER, ctypes.byref(rx), None, None, st))
+    torch.cuda.synchronize()
+    assert rx.value == o_rounds
+    np.testing.assert_array_equal(lead.cpu().numpy(), o_lead)
+    np.testing.assert_array_equal(state.cpu().numpy(), o_state)

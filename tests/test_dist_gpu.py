@@ -9,6 +9,10 @@ one device, so the ranks talk through host memory, in two ways:
                       code that runs over RCCL on a multi-GPU node;
   transport "shm-agent"  the same, with the tail's agent-order stamp layout forced from the second
                       batch of rounds on (SWARM_IL_MIN_CHANGES): the layout switch of the native loop;
+  transport "rccl-double"  the native loops' RCCL branch (SWARM_NATIVE_COMM=rccl) over the RCCL test
+                      double (tests/rccl_double via SWARM_RCCL_PATH): the ncclSend/ncclRecv groups, the
+                      per-peer counts and datatypes, the ncclSum counter all-reduce and the auction's
+                      MAX all-reduce / all-gather, with real peers on one GPU;
   transport "python"  SWARM_NATIVE_HALO=0: ShardedSwarm's Python stepper, halo over gloo.
 Every rank's leaders, rounds and per-round global change counts, the sharded allocation (winners,
 claim values, conflicts, won counts) and -- native -- the sharded auction (owners, prices, per-round
@@ -54,12 +58,14 @@ def _auction_tasks(kind, world):
     return d["tx"], d["ty"], d["treq"]
 
 
-def _worker(rank, world, port, out_q, kind, depth, transport):
+def _worker(rank, world, port, out_q, kind, depth, transport, dbl):
     import sys
     for p in (PKG, ROOT, os.path.join(ROOT, "tests")):
         sys.path.insert(0, p)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                       SWARM_NATIVE_HALO="0" if transport == "python" else "1")
+    if transport == "rccl-double":
+        os.environ.update(SWARM_NATIVE_COMM="rccl", SWARM_RCCL_PATH=dbl, RCCL_DOUBLE_TIMEOUT_S="60")
     if transport == "shm-agent":  # the tail's agent-order stamp layout from the second batch on
         os.environ["SWARM_IL_MIN_CHANGES"] = str(1 << 40)
     import torch
@@ -85,7 +91,8 @@ def _worker(rank, world, port, out_q, kind, depth, transport):
         assert isinstance(sh.backend, GpuBackend) and sh.halo.host_staged
         r = sh.elect(check_every=16)
         native = getattr(sh, "_native", None) is not None
-        assert native == (transport != "python") and (not native or sh.backend.comm_kind == "shm")
+        want_kind = {"rccl-double": "rccl", "python": None}.get(transport, "shm")
+        assert native == (transport != "python") and (not native or sh.backend.comm_kind == want_kind)
         sh._check_ghosts(sh.leaders[r.rounds_exec & 1])
         res, won, gst = sh.allocate(tx, ty, tq)
         auc = None
@@ -94,7 +101,14 @@ def _worker(rank, world, port, out_q, kind, depth, transport):
             auc = dict(owner=a.owner_id.cpu().numpy(), price=a.price.cpu().numpy(), bidders=a.bidders,
                        rounds=a.rounds_exec, ids=sh.ids.cpu().numpy(), assigned=a.assigned.cpu().numpy())
         torch.cuda.synchronize()
-        out_q.put(dict(rank=rank, rounds=r.rounds_exec, changes=r.changes, ids=sh.ids.cpu().numpy(),
+        dstats = None
+        if transport == "rccl-double":  # what the double executed in this process (the RCCL branch ran)
+            import ctypes
+            D = ctypes.CDLL(dbl)
+            st = (ctypes.c_longlong * 6)()
+            D.rccl_double_stats(ctypes.cast(st, ctypes.c_void_p))
+            dstats = list(st)
+        out_q.put(dict(rank=rank, dstats=dstats, rounds=r.rounds_exec, changes=r.changes, ids=sh.ids.cpu().numpy(),
                        leader=r.leader.cpu().numpy(), state=r.state.cpu().numpy(), winner=res.winner.cpu().numpy(),
                        util=res.util.cpu().numpy(), nmsg=res.nmsg.cpu().numpy(), won=won.cpu().numpy(),
                        gstats=gst, tasks=tasks, converged=r.converged, ghosts=sh.n_glo + sh.n_ghi, native=native,
@@ -111,12 +125,18 @@ def _worker(rank, world, port, out_q, kind, depth, transport):
                                                          (3, "blocks", 5, "shm"), (2, "blocks", 8, "python"),
                                                          (3, "global-morton", 6, "shm"), (4, "global-morton", 16, "shm"),
                                                          (2, "global-random", 2, "shm"), (4, "global-random", 3, "shm"),
-                                                         (3, "global-random", 2, "python")])
-def test_hip_sharded_processes_match_union_oracle(world, kind, depth, transport, oracle_mod):
+                                                         (3, "global-random", 2, "python"),
+                                                         (2, "shards", 16, "rccl-double"),
+                                                         (3, "global", 1, "rccl-double"),
+                                                         (4, "blocks", 16, "rccl-double"),
+                                                         (3, "global-morton", 6, "rccl-double"),
+                                                         (4, "global-random", 3, "rccl-double")])
+def test_hip_sharded_processes_match_union_oracle(world, kind, depth, transport, oracle_mod, rccl_double):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, kind, depth, transport)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, kind, depth, transport, rccl_double))
+             for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -136,6 +156,10 @@ def test_hip_sharded_processes_match_union_oracle(world, kind, depth, transport,
     rp, col = oracle_mod.rgg_csr(x, y, 1.0)
     lead, _, rounds, changes = oracle_mod.elect(rp, col, ids)
     want = dict(zip(ids.tolist(), lead.tolist()))
+    if transport == "rccl-double":  # groups, sends, recvs, all-reduces, all-gathers, bytes
+        for o in outs:
+            g, sd, rv, ar, ag, _ = o["dstats"]
+            assert g > 0 and ar > 0 and ag > 0 and (sd > 0 and rv > 0) == bool(o["peers"]), o["dstats"]
     for o in outs:
         assert o["native"] == (transport != "python")
         assert o["converged"] and o["rounds"] == rounds and o["ghosts"] > 0
