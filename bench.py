@@ -755,7 +755,9 @@ def sharded(args, rank, world, dev):
                        "rounds_exec": r.rounds_exec,
                        "halo_depth": sh.halo_depth,
                        "parallelism": f"strip-sharded x{world}: {path}; halo exchanged every {sh.halo_depth} "
-                                      "rounds (ghosts that deep, stepped locally)"},
+                                      "rounds (ghosts that deep, stepped locally)",
+                       # the cost model's transport constants (out["model"]): assumed, never measured
+                       "transport_model_assumed": transport_assumed()},
             "alloc_stats": a[2],
             "result_check": check,
             "model": model,
@@ -819,6 +821,12 @@ ALPHA_AR_US = 20.0
 LINK_GBS = 100.0
 STAMP_US_PER_MB = 0.23  # the sparse round's stamp scan: 10 MB in ~2.3 us (per-workgroup clocks)
 EXCH_LAUNCH_US = 4.0    # the pack and ghost-apply kernels of an exchange
+
+
+def transport_assumed():
+    """The model's three transport constants, ASSUMED (no multi-GPU box in the pool: never measured)."""
+    return {"alpha_p2p_us": ALPHA_P2P_US, "alpha_allreduce_us": ALPHA_AR_US, "link_GBps": LINK_GBS,
+            "status": "assumed, not measured (one-GPU boxes only)"}
 
 
 def batch_schedule(changes, max_batch=256):
@@ -901,6 +909,23 @@ def election_model(per_rank, shard_rows, shard_edges, send_bytes, changes, depth
             "imbalance": float(compute / max(t.sum(0).sum() / k, 1e-9))}
 
 
+# The 100M-agent C5 swarm with RANDOM IDs elected on one GPU (DESIGN §7, round 5, 32-bit offsets with
+# 16-bit columns): the comparison C5's Morton-ID model rates are stated against.
+C5_RANDOM_IDS_1GPU = {"agent_rounds_per_s": 1.54e12, "ms": 328.0, "agents": 100_000_000,
+                      "source": "profiles/r5 (DESIGN §7): swarm_elect_compact at 100M agents, random IDs"}
+
+
+def annotate_model(table, agents_total, rounds):
+    """Every model row gets its absolute predicted rate (agent-rounds/s of the whole job: agents_total x
+    rounds over the predicted election time) and its speedup over the model's own N = 1 row, so that no
+    ratio is printed without the rate it comes from."""
+    t1 = next((e["ms"] for e in table if e["n_gpus"] == 1), None)
+    for e in table:
+        e["agent_rounds_per_s"] = agents_total * rounds / (e["ms"] * 1e-3)
+        e["speedup_vs_model_n1"] = (t1 / e["ms"]) if t1 else None
+    return table
+
+
 def sharded_model(args, sh, rank, world, check):
     """DESIGN §6's election cost model for this run: one more (untimed, identical) sharded election records
     every rank's per-round work; rank 0 then elects its shard graph alone (the other ranks wait, the GPU is
@@ -933,21 +958,28 @@ def sharded_model(args, sh, rank, world, check):
             if world % m == 0:
                 table.append(election_model(per_rank, rows, edges, send, rec.changes, sh.halo_depth, cal, merge=m))
             m *= 2
+        annotate_model(table, args.agents * world, int(rec.rounds_exec))
         by_n = {e["n_gpus"]: e for e in table}
         out = {"calibration": dict(cal, rounds=int(ra), wall_ms=wall, shard_rows=info["rows"]),
-               "assumed": {"alpha_p2p_us": ALPHA_P2P_US, "alpha_allreduce_us": ALPHA_AR_US, "link_GBps": LINK_GBS,
-                           "stamp_us_per_MB": STAMP_US_PER_MB, "exchange_launch_us": EXCH_LAUNCH_US},
+               "assumed": dict(transport_assumed(), stamp_us_per_MB=STAMP_US_PER_MB,
+                               exchange_launch_us=EXCH_LAUNCH_US),
                "table": table,
                "note": "per-round work = this run's per-rank counts (exact, timing-free); N/2 ... 1 merge adjacent "
                        "ranks; the election only (the allocation is ~0.2 ms)"}
         t1 = (check.get("union_oracle") or {}).get("t1_gpu_ms")
+        out["model_agent_rounds_per_s"] = {str(e["n_gpus"]): e["agent_rounds_per_s"] for e in table}
         if args.config == "C5":  # strong scaling: the union's election on one GPU against the model at N
             if t1:
                 out["t1_measured_ms"] = t1
+                out["t1_measured_agent_rounds_per_s"] = args.agents * world * int(rec.rounds_exec) / (t1 * 1e-3)
                 out["model_vs_measured_n1"] = by_n[1]["ms"] / t1
             out["model_speedup"] = (t1 or by_n[1]["ms"]) / by_n[world]["ms"]
             out["model_speedup_basis"] = ("the union elected on one GPU (measured)" if t1 else
                                           "the model's own N = 1") + " / the model at N"
+            out["comparison"] = dict(C5_RANDOM_IDS_1GPU, note=(
+                "the same 100M-agent swarm with random IDs elected on ONE GPU (measured, DESIGN §7): Morton IDs "
+                "make C5's election dense-like (about half the agents change every round for ~7.4k rounds), so "
+                "every predicted Morton rate above is set against this 1-GPU figure"))
         else:  # weak scaling: agent-rounds/s at N (model) against one GPU electing one rank's shard (measured)
             v1 = info["rows"] * int(ra) / (wall * 1e-3)
             vn = args.agents * world * int(rec.rounds_exec) / (by_n[world]["ms"] * 1e-3)

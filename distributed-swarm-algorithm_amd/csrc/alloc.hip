@@ -1146,9 +1146,8 @@ int alloc_impl(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos
         unsigned long long *hfold = static_cast<unsigned long long *>(mapped(ctx, 16 * 8, &fold_dev));
         if (!hfold) return SWARM_ERR_OOM;
         // The host waits for the fold's epoch word in that memory instead of a stream synchronisation
-        // (the results stay stream-ordered for the caller; only the counters are needed here): a spin
-        // on a host cache line sees the write within ~1 us of the kernel's end, where the synchronise
-        // adds its own wake-up.  hipStreamQuery every 256 spins catches a failed launch.
+        // (the results stay stream-ordered for the caller; only the counters are needed here):
+        // wait_mapped_word spins on it.
         // (the mapped buffer is shared with other calls of this ctx, whose device writes have all been
         // waited for: the word is cleared here, and the epoch carries a tag no counter reaches)
         const unsigned long long ep = (0xA110Cull << 40) | (++ctx->fold_epoch & ((1ull << 40) - 1));
@@ -1157,16 +1156,7 @@ int alloc_impl(swarm_ctx *ctx, int64_t n, const int32_t *ids, const double *apos
                            static_cast<unsigned long long *>(fold_dev), P.D.count,
                            static_cast<unsigned long long *>(fold_dev) + 15, ep);
         SW_LAUNCHED();
-        for (uint64_t spin = 1; __atomic_load_n(&hfold[15], __ATOMIC_ACQUIRE) != ep; ++spin) {
-            if ((spin & 255) != 0) continue;
-            const hipError_t q = hipStreamQuery(s);
-            if (q == hipErrorNotReady) continue;
-            SW_HIP(q);
-            if (__atomic_load_n(&hfold[15], __ATOMIC_ACQUIRE) != ep) {
-                set_error("allocation: the stream finished without the fold's epoch word");
-                return SWARM_ERR_HIP;
-            }
-        }
+        SW_TRY(wait_mapped_word(&hfold[15], ep, s, "allocation"));
         for (int c = 0; c <= kNumStats; ++c) hs[c] = __atomic_load_n(&hfold[c], __ATOMIC_RELAXED);
     }
     if (hs[7]) {

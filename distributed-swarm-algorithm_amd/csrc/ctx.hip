@@ -111,6 +111,20 @@ void *mapped(swarm_ctx *ctx, size_t bytes, void **dev) {
     return ctx->host_mapped;
 }
 
+int wait_mapped_word(const unsigned long long *w, unsigned long long v, hipStream_t s, const char *what) {
+    for (uint64_t spin = 1; __atomic_load_n(w, __ATOMIC_ACQUIRE) != v; ++spin) {
+        if ((spin & 255) != 0) continue;
+        const hipError_t q = hipStreamQuery(s);
+        if (q == hipErrorNotReady) continue;
+        SW_HIP(q);
+        if (__atomic_load_n(w, __ATOMIC_ACQUIRE) != v) {
+            set_error("%s: the stream finished without writing its read-back word", what);
+            return SWARM_ERR_HIP;
+        }
+    }
+    return SWARM_OK;
+}
+
 }  // namespace swarm
 
 extern "C" {

@@ -812,6 +812,213 @@ __global__ __launch_bounds__(kBlock) void k_frontier_ghosts(const Off *__restric
         atomicAdd(slot(f.ring, t, C_GHOST, blockIdx.x & (kShards - 1)), (unsigned long long)rises);
 }
 
+// ------------------------------------------------------------------ one-workgroup tail (opt-in)
+// SWARM_TAIL_WG=cap (a bounded experiment): once the marked set of the next round fits
+// `cap`, ONE 1 024-thread workgroup runs the remaining rounds in one launch, the marked list and the
+// next round's dedupe in LDS, rounds separated by __syncthreads only (one CU: no grid barrier, no
+// cross-XCD hand-off).  Round t as k_sparse_block's: the listed agents gather their rows from
+// L[(t-1)&1] and write L[t&1] (4 lanes per agent), risers are listed; the next round's list is the
+// risers and their neighbours, deduplicated by an LDS hash set.  It exits at the first zero-change
+// round, at t_end, or when the next list outgrows LDS: then the risers' neighbourhoods are written as
+// stamps for round t+1 (agent-order layout f.wsm) and the frontier rounds take over.  Per-round
+// counters go to the counter ring as the sparse rounds' (C_CHG / C_ACT / C_EDGE, tot[], recycling).
+constexpr int kTailThreads = 1024;
+constexpr int kTailCap = 2048;   // list capacity (agents per round)
+constexpr int kTailHash = 8192;  // LDS hash-set slots
+constexpr int kTailProbe = 64;   // linear probes before the set counts as full
+enum TailReason : unsigned long long { TAIL_DONE = 1, TAIL_HANDBACK = 2, TAIL_NOT_STARTED = 3 };
+
+// Stamp marks of the round after `t` for risers ris[0, nr) and their neighbours (hand-back).
+template <typename CT>
+__device__ void tail_handback(const int32_t *__restrict__ rp, CT cols, const Frontier &f, const int *ris, int nr,
+                              int t) {
+    uint8_t *aw = f.act[(t + 1) & 1];
+    const uint8_t sw = stamp_of(t + 1);
+    for (int r = threadIdx.x; r < nr; r += kTailThreads) {
+        const int32_t v = ris[r];
+        aw[stamp_slot(f.wsm, v)] = sw;
+        for (int32_t k = rp[v]; k < rp[v + 1]; ++k) aw[stamp_slot(f.wsm, cols.at(k, v & ~63))] = sw;
+    }
+}
+
+// The marked agents of round t0 (stamps act[t0 & 1] in layout f.sm) into glist[0, cap) and *gcount
+// (the count keeps counting past cap: the tail then does not start).
+__global__ __launch_bounds__(kBlock) void k_tail_collect(Frontier f, int t0, int32_t *__restrict__ glist,
+                                                         unsigned *__restrict__ gcount, int cap) {
+    const uint8_t *ar = f.act[t0 & 1];
+    const unsigned stamp4 = unsigned(stamp_of(t0)) * 0x01010101u;
+    const int64_t nchunks = f.sm.M;
+    for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+        const int j0 = threadIdx.x * kScan;
+        const uint2 w = *reinterpret_cast<const uint2 *>(ar + chunk * kChunk + uint32_t(threadIdx.x * sizeof(uint2)));
+        unsigned mask = take_stamps<kScan>(stamp_agent(f.sm, chunk, j0), f.n_rows, w, stamp4);
+        const int cnt = __popc(mask);
+        int wtot;
+        const int ex = wave_excl_scan<4>(cnt, wtot);
+        unsigned base = 0;
+        if ((threadIdx.x & 63) == 0 && wtot) base = atomicAdd(gcount, unsigned(wtot));
+        base = __shfl(base, 0, 64);
+        int pos = int(base) + ex;
+        while (mask) {
+            const int bit = __ffs(mask) - 1;
+            mask &= mask - 1;
+            if (pos < cap) glist[pos] = int32_t(stamp_agent(f.sm, chunk, j0)) + bit;
+            ++pos;
+        }
+    }
+}
+
+// Both stamp buffers zeroed when the tail will start (*gcount <= cap): it writes fresh marks at its exit.
+__global__ __launch_bounds__(kBlock) void k_tail_clear(uint4 *__restrict__ a, int64_t n16,
+                                                       const unsigned *__restrict__ gcount, int cap) {
+    if (*gcount > unsigned(cap)) return;
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n16; i += int64_t(gridDim.x) * kBlock)
+        a[i] = make_uint4(0, 0, 0, 0);
+}
+
+// out[0] last round run, out[1] reason, out[2] rounds run, out[3] done flag (the host's wait word);
+// clk (optional, debug): per round the wall clock at its start and its marked count.
+template <typename CT>
+__global__ __launch_bounds__(kTailThreads) void k_tail_wg(const int32_t *__restrict__ rp, CT cols, Frontier f,
+                                                          const int32_t *__restrict__ glist,
+                                                          const unsigned *__restrict__ gcount, int t0, int t_end,
+                                                          int cap, unsigned long long *out,
+                                                          unsigned long long ep, unsigned long long *clk) {
+    constexpr int G = 4, K = 4;
+    __shared__ int s_list[2][kTailCap];
+    __shared__ int s_ris[kTailCap];
+    __shared__ int s_hash[kTailHash];
+    __shared__ int s_n[2], s_nris, s_over;
+    __shared__ unsigned long long s_edges;
+    const int tid = threadIdx.x, sub = tid & (G - 1);
+    const unsigned m0 = *gcount;
+    auto finish = [&](unsigned long long last, unsigned long long why, unsigned long long runs) {
+        if (tid == 0) {
+            out[0] = last;
+            out[1] = why;
+            out[2] = runs;
+            __threadfence_system();
+            __hip_atomic_store(&out[3], ep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    };
+    if (m0 == 0 || m0 > unsigned(cap) || cap > kTailCap) {
+        finish(t0 - 1, TAIL_NOT_STARTED, 0);
+        return;
+    }
+    for (int q = tid; q < int(m0); q += kTailThreads) s_list[0][q] = glist[q];
+    for (int q = tid; q < kTailHash; q += kTailThreads) s_hash[q] = -1;
+    if (tid < kWave && t0 > 1) {  // round t0's bookkeeping: publish round t0-1's total (the sparse guard's)
+        unsigned long long v = *slot(f.ring, t0 - 1, C_CHG, tid);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        if (tid == 0) f.tot[(t0 - 1) % kRing] = v;
+    }
+    if (tid == 0) {
+        s_n[0] = int(m0);
+        s_n[1] = 0;
+        s_nris = 0;
+        s_over = 0;
+        s_edges = 0;
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int t = t0;; ++t) {
+        const int m = s_n[cur];
+        if (clk && tid == 0) {
+            clk[2 * (t - t0)] = wall_clock64();
+            clk[2 * (t - t0) + 1] = unsigned(m);
+        }
+        const int32_t *__restrict__ P = f.L[(t - 1) & 1];
+        int32_t *__restrict__ Q = f.L[t & 1];
+        unsigned my_edges = 0;
+        // gather: 4 lanes per listed agent, K columns in flight per lane
+        for (int base = 0; base < m; base += kTailThreads / G) {
+            const int i = base + tid / G;
+            const bool valid = i < m;
+            const int32_t v = s_list[cur][valid ? i : m - 1];
+            const int32_t b = rp[v], e = rp[v + 1];
+            const int own = P[v];
+            int mx = own;
+            for (int32_t k = b + sub; k < e; k += G * K) {
+                int c[K];
+#pragma unroll
+                for (int j = 0; j < K; ++j) c[j] = cols.at((k + G * j < e) ? k + G * j : e - 1, v & ~63);
+                int val[K];
+#pragma unroll
+                for (int j = 0; j < K; ++j) val[j] = P[c[j]];
+#pragma unroll
+                for (int j = 0; j < K; ++j) mx = max(mx, val[j]);
+            }
+            mx = group_max<G>(mx);
+            if (valid && sub == 0) {
+                Q[v] = mx;
+                my_edges += unsigned(e - b);
+                if (mx > own) s_ris[atomicAdd(&s_nris, 1)] = v;
+            }
+        }
+        const int wsum = wave_sum(int(my_edges));
+        if ((tid & 63) == 0 && wsum) atomicAdd(&s_edges, (unsigned long long)wsum);
+        __syncthreads();
+        const int nr = s_nris;
+        if (tid == 0) {  // the round's counters, as a sparse round leaves them (shard 0 of each)
+            *slot(f.ring, t, C_CHG, 0) = (unsigned long long)nr;
+            *slot(f.ring, t, C_ACT, 0) = (unsigned long long)m;
+            *slot(f.ring, t, C_EDGE, 0) = s_edges;
+            f.tot[t % kRing] = (unsigned long long)nr;
+        }
+        for (int q = tid; q < kCounters * kShards; q += kTailThreads)  // recycle round t + kRing/2's slots
+            *slot(f.ring, t + kRing / 2, q / kShards, q % kShards) = 0;
+        if (nr == 0) {
+            finish(t, TAIL_DONE, t - t0 + 1);
+            return;
+        }
+        if (t >= t_end) {
+            tail_handback(rp, cols, f, s_ris, nr, t);
+            finish(t, TAIL_HANDBACK, t - t0 + 1);
+            return;
+        }
+        // the next list: the risers and their neighbours, each once (LDS hash set)
+        const int nxt = cur ^ 1;
+        auto insert = [&](int32_t key) {
+            uint32_t h = (uint32_t(key) * 2654435761u) & (kTailHash - 1);
+            for (int p = 0; p < kTailProbe; ++p) {
+                const int old = atomicCAS(&s_hash[h], -1, key);
+                if (old == -1) {
+                    const int idx = atomicAdd(&s_n[nxt], 1);
+                    if (idx < cap)
+                        s_list[nxt][idx] = key;
+                    else
+                        s_over = 1;
+                    return;
+                }
+                if (old == key) return;
+                h = (h + 1) & (kTailHash - 1);
+            }
+            s_over = 1;
+        };
+        for (int r = tid / G; r < nr; r += kTailThreads / G) {
+            const int32_t v = s_ris[r];
+            if (sub == 0) insert(v);
+            for (int32_t k = rp[v] + sub; k < rp[v + 1]; k += G) insert(cols.at(k, v & ~63));
+        }
+        __syncthreads();
+        if (s_over) {
+            tail_handback(rp, cols, f, s_ris, nr, t);
+            finish(t, TAIL_HANDBACK, t - t0 + 1);
+            return;
+        }
+        // reset for the next round (8 slots of the set per thread)
+        for (int q = tid; q < kTailHash; q += kTailThreads) s_hash[q] = -1;
+        if (tid == 0) {
+            s_n[cur] = 0;
+            s_nris = 0;
+            s_edges = 0;
+        }
+        cur = nxt;
+        __syncthreads();
+    }
+}
+
 // Col16 copy of an int32 CSR: col16[k] = col[k] - (v & ~63) for every edge k of row v; *bad is set
 // when a delta does not fit 16 bits (the caller then keeps the int32 columns).
 // Deltas fit in [-32767, 32767]: -32768 is kEsc.  ESC: an out-of-range delta is stored as kEsc and
@@ -904,6 +1111,13 @@ __global__ void k_sum_shards(unsigned long long *ring, int t, unsigned long long
     if (threadIdx.x == 0) *out += v;
 }
 
+// *w = v in mapped host memory, after a system-scope fence: the host's wait word for everything the stream
+// wrote there before this kernel (k_batch_totals' per-round totals).
+__global__ void k_signal(unsigned long long *w, unsigned long long v) {
+    __threadfence_system();
+    __hip_atomic_store(w, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // totals[(r - t0) * kCounters + c] = sum over shards of counter c of round r, one wave per round.
 __global__ void k_batch_totals(unsigned long long *ring, int t0, unsigned long long *totals) {
     const int r = t0 + blockIdx.x;
@@ -932,7 +1146,12 @@ struct Tuning {
     int use_c16 = 1;          // swarm_elect_compact reads the 16-bit columns (0: its int32 ones; A/B aid)
     int il_min_changes = -1;   // interleaved stamp layout while the last read round changed >= this
                                // (-1: 8e-4 x agents, measured best at 100k, 1M and 10M agents)
+    int tail_wg = 0;           // > 0: the one-workgroup tail (k_tail_wg) once a round's marks fit this many
+    int tail_log = 0;          // SWARM_TAIL_LOG=1: per-round clocks of the tail to stderr (experiment aid)
     Tuning() {
+        tail_wg = env_int("SWARM_TAIL_WG", 0);
+        if (tail_wg > kTailCap) tail_wg = kTailCap;
+        tail_log = env_int("SWARM_TAIL_LOG", 0);
         il_min_changes = env_int("SWARM_IL_MIN_CHANGES", -1);
         use_c16 = env_int("SWARM_C16", 1);
         dense_flat = env_int("SWARM_DENSE_FLAT", 1);
@@ -1238,12 +1457,19 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         ctx->step_rows = ctx->step_all = 0;  // the stepper state is gone
     }
     constexpr int kMaxBatch = 256;
-    // the per-round totals land in mapped host memory, written by k_batch_totals itself
+    // the per-round totals land in mapped host memory, written by k_batch_totals itself, then the batch's
+    // epoch word after them (k_signal), which the host spins on
     void *dmap = nullptr;
     unsigned long long *hbuf =
-        static_cast<unsigned long long *>(mapped(ctx, size_t(kCounters) * 8 * kMaxBatch, &dmap));
+        static_cast<unsigned long long *>(mapped(ctx, size_t(kCounters) * 8 * kMaxBatch + 128, &dmap));
     if (!hbuf) return SWARM_ERR_OOM;
     unsigned long long *dtot = static_cast<unsigned long long *>(dmap);
+    unsigned long long *h_epoch = hbuf + size_t(kCounters) * kMaxBatch;
+    unsigned long long *d_epoch = dtot + size_t(kCounters) * kMaxBatch;
+    // a tag no counter value reaches, then the batch number (the word is shared with other calls)
+    const unsigned long long ep_tag = 0xE1EC7ull << 40;
+    unsigned long long ep = 0;
+    __atomic_store_n(h_epoch, 0ull, __ATOMIC_RELEASE);
 
     int found = -1, t = 1, batch = 8, launched = 0;
     std::vector<int64_t> hist;  // per-round change counts read so far (batch sizing, layout)
@@ -1278,12 +1504,6 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     // and enqueues it (no idle gap at a batch boundary).  Rounds launched past convergence are
     // guarded no-ops.  Per-round timing and the round log keep the plain read-at-the-end batches.
     const int kLook = (timed || rlog) ? 0 : 8;
-    hipEvent_t ev_read;
-    SW_HIP(hipEventCreateWithFlags(&ev_read, hipEventDisableTiming));
-    struct EvReadFree {
-        hipEvent_t e;
-        ~EvReadFree() { (void)hipEventDestroy(e); }
-    } ev_read_free{ev_read};
     int read_upto = 0;  // rounds whose counters the host has read
     // the per-round counters of rounds (read_upto, tread], read back into hbuf: hist, stats, found
     auto consume = [&](int tread) {
@@ -1313,17 +1533,89 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         }
         read_upto = tread;
     };
+    // the counters of rounds (read_upto, upto] read back and consumed (every launched round drained)
+    auto read_rounds = [&](int upto) -> int {
+        if (upto <= read_upto) return SWARM_OK;
+        hipLaunchKernelGGL(k_batch_totals, dim3(upto - read_upto), dim3(kWave), 0, s, ring, read_upto + 1, dtot);
+        SW_LAUNCHED();
+        hipLaunchKernelGGL(k_signal, dim3(1), dim3(1), 0, s, d_epoch, ep_tag | ++ep);
+        SW_LAUNCHED();
+        if (int rc2 = wait_mapped_word(h_epoch, ep_tag | ep, s, "election read-back")) return rc2;
+        consume(upto);
+        return SWARM_OK;
+    };
+    int64_t tail_retry_below = INT64_MAX;  // the tail did not start: retry once the changes halve
+    // One-workgroup tail from round launched + 1: drain, collect the marked agents, run k_tail_wg, read its
+    // rounds' counters.  Leaves launched / rd_map where the frontier rounds go on.
+    auto tail_rounds = [&](int cap) -> int {
+        if (int rc2 = read_rounds(launched)) return rc2;
+        if (found > 0 || launched >= max_rounds) return SWARM_OK;
+        const int t0 = launched + 1;
+        const int t_end = std::min(max_rounds, t0 + 199);  // <= 200 rounds: one counter read-back
+        char *tb;
+        const size_t clk_words = tuning().tail_log ? 2 * 201 : 0;
+        SW_ALLOC(tb, ctx, S_LIST, 64 + size_t(kTailCap) * 4 + clk_words * 8);
+        unsigned *gcount = reinterpret_cast<unsigned *>(tb);
+        int32_t *glist = reinterpret_cast<int32_t *>(tb + 64);
+        unsigned long long *clk = clk_words ? reinterpret_cast<unsigned long long *>(tb + 64 + size_t(kTailCap) * 4)
+                                            : nullptr;
+        SW_HIP(hipMemsetAsync(gcount, 0, 4, s));
+        f.sm = rd_map;
+        hipLaunchKernelGGL(k_tail_collect, dim3(grid_for(f.sm.M, 1, unsigned(tuning().sparse_blocks))), dim3(kBlock),
+                           0, s, f, t0, glist, gcount, cap);
+        SW_LAUNCHED();
+        const int64_t n16 = int64_t(2 * act_bytes(n)) / 16;
+        hipLaunchKernelGGL(k_tail_clear, dim3(grid_for(n16, kBlock, 2048)), dim3(kBlock), 0, s,
+                           reinterpret_cast<uint4 *>(f.act[0]), n16, gcount, cap);
+        SW_LAUNCHED();
+        f.wsm = ag_map;  // hand-back marks in agent order
+        // out[0..3] in mapped memory after the batch totals' epoch word
+        unsigned long long *h_out = h_epoch + 1, *d_out = d_epoch + 1;
+        const unsigned long long tep = (0x7A11ull << 40) | ++ep;
+        __atomic_store_n(&h_out[3], 0ull, __ATOMIC_RELEASE);
+        if (c16)
+            hipLaunchKernelGGL((k_tail_wg<Col16>), dim3(1), dim3(kTailThreads), 0, s,
+                               reinterpret_cast<const int32_t *>(rp), Col16{c16}, f, glist, gcount, t0, t_end, cap,
+                               d_out, tep, clk);
+        else
+            hipLaunchKernelGGL((k_tail_wg<Col32>), dim3(1), dim3(kTailThreads), 0, s,
+                               reinterpret_cast<const int32_t *>(rp), Col32{col}, f, glist, gcount, t0, t_end, cap,
+                               d_out, tep, clk);
+        SW_LAUNCHED();
+        if (int rc2 = wait_mapped_word(&h_out[3], tep, s, "one-workgroup tail")) return rc2;
+        const unsigned long long why = __atomic_load_n(&h_out[1], __ATOMIC_ACQUIRE);
+        const int last = int(__atomic_load_n(&h_out[0], __ATOMIC_ACQUIRE));
+        if (why == TAIL_NOT_STARTED) {
+            tail_retry_below = std::max<int64_t>(1, hist.back() / 2);
+            return SWARM_OK;
+        }
+        if (clk) {  // experiment aid: per-round microseconds (100 MHz wall clock) and marked agents
+            SW_HIP(hipStreamSynchronize(s));
+            std::vector<unsigned long long> hc(clk_words);
+            SW_HIP(hipMemcpy(hc.data(), clk, clk_words * 8, hipMemcpyDeviceToHost));
+            for (int r = t0; r < last; ++r)
+                fprintf(stderr, "[tail] round %d marked %llu us %.2f\n", r, hc[2 * (r - t0) + 1],
+                        double(hc[2 * (r - t0 + 1)] - hc[2 * (r - t0)]) / 100.0);
+        }
+        launched = last;
+        if (int rc2 = read_rounds(last)) return rc2;
+        rd_map = ag_map;  // the hand-back marks (if the run goes on)
+        batch = 8;
+        return SWARM_OK;
+    };
     while (read_upto < max_rounds && found < 0) {
         t = launched + 1;  // first round launched in this batch (> tend when only a read is left)
         const int tend = std::min(max_rounds, launched + batch);
         // read rounds (read_upto, tread]: at least one (the first batches are shorter than kLook)
         const int tread = tend == max_rounds ? tend : std::max(read_upto + 1, tend - kLook);
         int rc = 0;
-        // per-round totals of rounds (read_upto, tread], reduced on device into mapped host memory, an event
+        // per-round totals of rounds (read_upto, tread], reduced on device into mapped host memory, then
+        // the batch's epoch word
         auto enqueue_read = [&]() -> int {
             hipLaunchKernelGGL(k_batch_totals, dim3(tread - read_upto), dim3(kWave), 0, s, ring, read_upto + 1, dtot);
             SW_LAUNCHED();
-            SW_HIP(hipEventRecord(ev_read, s));
+            hipLaunchKernelGGL(k_signal, dim3(1), dim3(1), 0, s, d_epoch, ep_tag | ++ep);
+            SW_LAUNCHED();
             return SWARM_OK;
         };
         if (tread <= launched && (rc = enqueue_read())) return rc;
@@ -1357,7 +1649,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         }
         if (seg_n) SW_HIP(hipEventRecord(ev[2 * kMaxBatch + 1], s));
         launched = std::max(launched, tend);
-        SW_HIP(hipEventSynchronize(ev_read));
+        if ((rc = wait_mapped_word(h_epoch, ep_tag | ep, s, "election read-back"))) return rc;
         if (timed) {  // kLook == 0: this batch's rounds are exactly the rounds read
             SW_HIP(hipStreamSynchronize(s));
             for (int r = t; r <= tend; ++r) {  // every launched round's kernel time (rocprof's view)
@@ -1385,6 +1677,13 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         // a batch spans at most kRing/2 rounds of counter slots, look-ahead included (bookkeeping
         // recycles the slot of round t - kRing/2 in round t)
         batch = next_round_batch(hist.data(), hist.size(), batch, kMaxBatch - kLook);
+        // the one-workgroup tail (opt-in experiment): once the last read round's risers x 8 fit its list
+        const int cap = tuning().tail_wg;
+        if (cap > 0 && found < 0 && mode == SWARM_ELECT_FRONTIER && !hrp && !timed && !rlog && sizeof(Off) == 4 &&
+            !hist.empty() && hist.back() > 0 && hist.back() * 8 <= cap && hist.back() < tail_retry_below &&
+            launched < max_rounds && plan_round(launched + 1) == RK_SPARSE) {
+            if ((rc = tail_rounds(cap))) return rc;
+        }
     }
     const int last = found > 0 ? found : max_rounds;
     if (found < 0 && (last & 1)) {

@@ -124,6 +124,11 @@ void *pinned(swarm_ctx *ctx, size_t bytes);
 // wait for join on the caller's stream.
 int side_stream(swarm_ctx *ctx, hipStream_t *side, hipEvent_t *fork, hipEvent_t *join);
 void *mapped(swarm_ctx *ctx, size_t bytes, void **dev);
+// Host wait for a device-written word of mapped memory to equal v (a spin: a waiting host thread stays
+// on its core, where a stream / event synchronisation may yield it -- and the next call's launches then
+// start from a cold core); hipStreamQuery every 256 spins reports a failed stream, and a stream that
+// finished without the write is an error.
+int wait_mapped_word(const unsigned long long *w, unsigned long long v, hipStream_t s, const char *what);
 
 }  // namespace swarm
 

@@ -53,3 +53,25 @@ def test_batch_schedule_grows_then_caps():
     n = bench.batch_schedule(flat)
     # 8, 16, ..., 256 then 256 per batch
     assert n == 6 + int(np.ceil((5000 - (8 + 16 + 32 + 64 + 128 + 256)) / 256))
+
+
+def test_model_rows_carry_absolute_rates_and_assumed_constants():
+    """Every model row prints its predicted agent-rounds/s beside its speedup, and the line carries the
+    transport constants marked assumed (VERDICT r5 #5)."""
+    world, R = 8, 600
+    per = _counts(world, R, seed=5)
+    changes = np.maximum(1, np.linspace(10_000, 1, R)).astype(np.int64)
+    changes[-1] = 0
+    cal = {"a_us": 7.0, "b_us_per_row": 0.002, "c_us_per_edge": 0.0, "dense_us_per_row_or_edge": 0.001,
+           "calib_rows": 1_000_000, "calib_edges": 16_000_000}
+    rows, edges, send = [1_000_000] * world, [16_000_000] * world, [400_000] * world
+    table = [bench.election_model(per, rows, edges, send, changes, 16, cal, merge=m) for m in (1, 2, 4, 8)]
+    bench.annotate_model(table, 8 * 1_000_000, R)
+    by_n = {e["n_gpus"]: e for e in table}
+    assert set(by_n) == {1, 2, 4, 8}
+    for k, e in by_n.items():
+        assert e["agent_rounds_per_s"] == 8e6 * R / (e["ms"] * 1e-3)
+        assert abs(e["speedup_vs_model_n1"] - by_n[1]["ms"] / e["ms"]) < 1e-12
+    a = bench.transport_assumed()
+    assert {"alpha_p2p_us", "alpha_allreduce_us", "link_GBps"} <= set(a) and "assumed" in a["status"]
+    assert bench.C5_RANDOM_IDS_1GPU["agent_rounds_per_s"] == 1.54e12
