@@ -841,17 +841,21 @@ __device__ void tail_handback(const int32_t *__restrict__ rp, CT cols, const Fro
     }
 }
 
-// The marked agents of round t0 (stamps act[t0 & 1] in layout f.sm) into glist[0, cap) and *gcount
-// (the count keeps counting past cap: the tail then does not start).
+// The marked agents of round t0 (stamps act[t0 & 1] in layout f.sm: S stamps per thread, 256 S-stamp
+// chunks -- k_sparse_block's reading) into glist[0, cap) and *gcount (the count keeps counting past cap:
+// the tail then does not start).
+template <int S>
 __global__ __launch_bounds__(kBlock) void k_tail_collect(Frontier f, int t0, int32_t *__restrict__ glist,
                                                          unsigned *__restrict__ gcount, int cap) {
+    using W = typename StampWord<S>::T;
+    constexpr int kC = kBlock * S;
     const uint8_t *ar = f.act[t0 & 1];
     const unsigned stamp4 = unsigned(stamp_of(t0)) * 0x01010101u;
     const int64_t nchunks = f.sm.M;
+    const int j0 = threadIdx.x * S;
     for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
-        const int j0 = threadIdx.x * kScan;
-        const uint2 w = *reinterpret_cast<const uint2 *>(ar + chunk * kChunk + uint32_t(threadIdx.x * sizeof(uint2)));
-        unsigned mask = take_stamps<kScan>(stamp_agent(f.sm, chunk, j0), f.n_rows, w, stamp4);
+        const W w = *reinterpret_cast<const W *>(ar + chunk * kC + uint32_t(threadIdx.x * sizeof(W)));
+        unsigned mask = take_stamps<S>(stamp_agent(f.sm, chunk, j0), f.n_rows, w, stamp4);
         const int cnt = __popc(mask);
         int wtot;
         const int ex = wave_excl_scan<4>(cnt, wtot);
@@ -934,8 +938,9 @@ __global__ __launch_bounds__(kTailThreads) void k_tail_wg(const int32_t *__restr
         // gather: 4 lanes per listed agent, K columns in flight per lane
         for (int base = 0; base < m; base += kTailThreads / G) {
             const int i = base + tid / G;
-            const bool valid = i < m;
-            const int32_t v = s_list[cur][valid ? i : m - 1];
+            const int32_t v0 = s_list[cur][i < m ? i : m - 1];
+            const bool valid = i < m && v0 >= 0 && v0 < f.n_rows;  // (a bad entry is never gathered)
+            const int32_t v = valid ? v0 : 0;
             const int32_t b = rp[v], e = rp[v + 1];
             const int own = P[v];
             int mx = own;
@@ -1561,8 +1566,11 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
                                             : nullptr;
         SW_HIP(hipMemsetAsync(gcount, 0, 4, s));
         f.sm = rd_map;
-        hipLaunchKernelGGL(k_tail_collect, dim3(grid_for(f.sm.M, 1, unsigned(tuning().sparse_blocks))), dim3(kBlock),
-                           0, s, f, t0, glist, gcount, cap);
+        const dim3 cgrid(grid_for(f.sm.M, 1, unsigned(tuning().sparse_blocks)));
+        if (f.sm.cshift == 9)  // small swarm: 512-stamp chunks (2 per thread)
+            hipLaunchKernelGGL((k_tail_collect<2>), cgrid, dim3(kBlock), 0, s, f, t0, glist, gcount, cap);
+        else
+            hipLaunchKernelGGL((k_tail_collect<kScan>), cgrid, dim3(kBlock), 0, s, f, t0, glist, gcount, cap);
         SW_LAUNCHED();
         const int64_t n16 = int64_t(2 * act_bytes(n)) / 16;
         hipLaunchKernelGGL(k_tail_clear, dim3(grid_for(n16, kBlock, 2048)), dim3(kBlock), 0, s,
@@ -1677,10 +1685,14 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
         // a batch spans at most kRing/2 rounds of counter slots, look-ahead included (bookkeeping
         // recycles the slot of round t - kRing/2 in round t)
         batch = next_round_batch(hist.data(), hist.size(), batch, kMaxBatch - kLook);
-        // the one-workgroup tail (opt-in experiment): once the last read round's risers x 8 fit its list
+        // the one-workgroup tail (opt-in experiment): once the last read round's risers x 4 fit its list (the
+        // marked agents of a tail round are ~3x the previous round's risers at 100k-10M agents; a list that
+        // does not fit is caught by the collect), with short batches once that is near, so that the switch
+        // is not a long batch late
         const int cap = tuning().tail_wg;
+        if (cap > 0 && !hist.empty() && hist.back() * 4 <= 8 * int64_t(cap)) batch = std::min(batch, 8);
         if (cap > 0 && found < 0 && mode == SWARM_ELECT_FRONTIER && !hrp && !timed && !rlog && sizeof(Off) == 4 &&
-            !hist.empty() && hist.back() > 0 && hist.back() * 8 <= cap && hist.back() < tail_retry_below &&
+            !hist.empty() && hist.back() > 0 && hist.back() * 4 <= cap && hist.back() < tail_retry_below &&
             launched < max_rounds && plan_round(launched + 1) == RK_SPARSE) {
             if ((rc = tail_rounds(cap))) return rc;
         }
