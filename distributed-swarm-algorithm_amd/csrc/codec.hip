@@ -774,6 +774,8 @@ int swarm_codec_encode(swarm_ctx *ctx, int64_t m, const int64_t *type, const int
         }
         const uint32_t epoch = ++ctx->enc_epoch;
         SW_ARG(ntiles < (int64_t(1) << 31), "m out of range");
+        if (const char *e = getenv("SWARM_ENC_TEST_POISON"); e && e[0] == '1')  // test aid: a ticket left over
+            SW_HIP(hipMemsetAsync(lb, 0x40, 4, s));                             // by a failed call
         const auto al16 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
         const bool pair = enc_pair() && al16(type) && al16(sender) && al16(tick) && al16(a) && al16(b) &&
                           al16(task) && al16(winner) && al16(offsets) && (reinterpret_cast<uintptr_t>(status) & 1) == 0;
@@ -784,6 +786,8 @@ int swarm_codec_encode(swarm_ctx *ctx, int64_t m, const int64_t *type, const int
         SW_HIP(hipStreamSynchronize(s));
         *total_bytes = host[0];
         if (const unsigned fl = reinterpret_cast<volatile const unsigned *>(host + 2)[0]) {
+            // the ticket and the look-back words are in an unknown state: the next call zeroes them first
+            ctx->enc_flags = nullptr;
             set_error("encode: tile offsets lost (%s); concurrent encode calls on one ctx are not supported",
                       fl & 2u ? "a tile ticket out of range" : "a look-back walk gave up");
             return SWARM_ERR_HIP;

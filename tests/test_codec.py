@@ -269,3 +269,26 @@ def test_gpu_encode_large_matches_oracle_on_a_sample(oracle_mod, wide):
     np.testing.assert_array_equal(st[idx], ost)
     for k, i in enumerate(idx):
         assert bytes(buf[off[i]:off[i + 1]]) == opk[k], int(i)
+
+
+@pytest.mark.gpu
+def test_gpu_encode_recovers_after_a_failed_call(oracle_mod, monkeypatch):
+    """A one-pass encode that fails (here: a tile ticket left over, as a failed or overlapping call would
+    leave it -- SWARM_ENC_TEST_POISON) reports SWARM_ERR_HIP, and the NEXT call on the same ctx zeroes the
+    ticket and the look-back words again and encodes exactly (the ctx no longer trusts a
+    buffer a failure left behind)."""
+    from swarm_amd import _lib, codec
+    m = 200_000
+    f = _random_msgs(m, 77)
+    good = codec.encode(*f, device="cuda")
+    monkeypatch.setenv("SWARM_ENC_TEST_POISON", "1")
+    with pytest.raises(_lib.SwarmError) as ei:
+        codec.encode(*f, device="cuda")
+    assert ei.value.code == _lib.ERR_HIP and "ticket" in str(ei.value)
+    monkeypatch.delenv("SWARM_ENC_TEST_POISON")
+    for _ in range(2):
+        e = codec.encode(*f, device="cuda")
+        assert e.total_bytes == good.total_bytes
+        np.testing.assert_array_equal(e.offsets.cpu().numpy(), good.offsets.cpu().numpy())
+        np.testing.assert_array_equal(e.buf.cpu().numpy(), good.buf.cpu().numpy())
+        np.testing.assert_array_equal(e.status.cpu().numpy(), good.status.cpu().numpy())
