@@ -27,7 +27,8 @@
 //            buf(t+1) and clears buf(t+2).
 // (Rounds 2-3 ran k_compact + k_receive + k_sweep + k_mail, round 4 first k_tick + k_mail: the
 // boundaries and the list round trips per tick.)
-// A quiet agent costs ~15 B (alive, state, outbox byte, tick phase, its 8-byte timer) plus its mail
+// A quiet agent costs ~13 B (its flag word -- state, alive, leader-position flag, tick phase --, outbox
+// byte and 8-byte timer) plus its mail
 // bit; only receivers pay for their rows.  Storm ticks: when a workgroup's senders exceed pull_frac x the
 // agents of its share (a timeout wave: thousands of ACCLAIMs at once), it skips the mail atomics
 // and the next tick pulls instead -- every alive agent walks its own row, as pull mode does.  Same results: an agent
@@ -61,18 +62,54 @@ __device__ __forceinline__ double jitter_u(uint64_t seed, int32_t id, int64_t t)
     return double(x >> 11) * (1.0 / 9007199254740992.0);
 }
 
+// An agent's small per-tick fields packed in one 32-bit word for the run (the C-ABI's separate state /
+// alive / has_leader_pos bytes and int32 tick_off are packed at the start and unpacked at the end): a
+// receiver touches one line for them instead of four, and the sweep streams 4 B instead of 7.
+//   byte 0 state, byte 1 alive, byte 2 has_leader_pos, byte 3 tick phase = tick_off mod 10 in [0, 9]
+// ((t + tick_off) % 10 == 0 iff (t + phase) % 10 == 0 for every tick t >= 0).
+__host__ __device__ __forceinline__ uint8_t fw_state(uint32_t w) { return uint8_t(w); }
+__host__ __device__ __forceinline__ uint8_t fw_alive(uint32_t w) { return uint8_t(w >> 8); }
+__host__ __device__ __forceinline__ uint8_t fw_hl(uint32_t w) { return uint8_t(w >> 16); }
+__host__ __device__ __forceinline__ int32_t fw_phase(uint32_t w) { return int32_t(w >> 24); }
+__host__ __device__ __forceinline__ uint32_t fw_make(uint8_t st, uint8_t al, uint8_t hl, int32_t ph) {
+    return uint32_t(st) | (uint32_t(al) << 8) | (uint32_t(hl) << 16) | (uint32_t(ph) << 24);
+}
+
 struct Fsm {
-    uint8_t *state;
+    uint32_t *flags;  // fw_* fields
     int32_t *leader;
     double *last_hb, *wait_start, *delay;
     float2 *lpos;
-    uint8_t *has_lpos, *alive;
 };
 
-__global__ __launch_bounds__(kBlock) void k_kill_leaders(int64_t n, const uint8_t *__restrict__ state,
-                                                        uint8_t *__restrict__ alive) {
-    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock)
-        if (alive[i] && state[i] == ST_L) alive[i] = 0;
+__global__ __launch_bounds__(kBlock) void k_kill_leaders(int64_t n, uint32_t *__restrict__ flags) {
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+        const uint32_t w = flags[i];
+        if (fw_alive(w) && fw_state(w) == ST_L) flags[i] = w & ~0xFF00u;
+    }
+}
+
+// The C-ABI's fields -> flag words, and back (once per run each).
+__global__ __launch_bounds__(kBlock) void k_pack_flags(int64_t n, const uint8_t *__restrict__ state,
+                                                      const uint8_t *__restrict__ alive,
+                                                      const uint8_t *__restrict__ hl,
+                                                      const int32_t *__restrict__ tick_off,
+                                                      uint32_t *__restrict__ flags) {
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+        const int32_t ph = ((tick_off[i] % 10) + 10) % 10;
+        flags[i] = fw_make(state[i], alive[i], hl[i], ph);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_unpack_flags(int64_t n, const uint32_t *__restrict__ flags,
+                                                        uint8_t *__restrict__ state, uint8_t *__restrict__ alive,
+                                                        uint8_t *__restrict__ hl) {
+    for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
+        const uint32_t w = flags[i];
+        state[i] = fw_state(w);
+        alive[i] = fw_alive(w);
+        hl[i] = fw_hl(w);
+    }
 }
 
 // Handlers for everything agent (me) hears in CSR row [b, e) (see the header).  The row in
@@ -134,14 +171,15 @@ __device__ __forceinline__ void receive_row(int32_t b, int32_t e, const int32_t 
     }
 }
 
-// Write back the liveness proof and the heartbeat's leader position (state / leader: caller).
+// Write back the liveness proof and the heartbeat's leader position (state / leader / the position flag
+// hl: caller).
 __device__ __forceinline__ void apply_heard(int64_t i, const Heard &h, double now, const double2 *__restrict__ pos,
-                                            const Fsm &f) {
+                                            const Fsm &f, uint8_t &hl) {
     if (h.live) f.last_hb[i] = now;
     if (h.hb_from >= 0) {
         const double2 q = pos[h.hb_from];
         f.lpos[i] = make_float2(float(q.x), float(q.y));
-        f.has_lpos[i] = 1;
+        hl = 1;
     }
 }
 
@@ -149,8 +187,8 @@ __device__ __forceinline__ void apply_heard(int64_t i, const Heard &h, double no
 // st; `heard`: it got a liveness proof this tick (its last_hb is now).  Returns the sends.
 __device__ __forceinline__ uint8_t timers(int64_t i, uint8_t &st, bool heard, int32_t &lead, bool &lead_set,
                                           int64_t t, double now, double timeout, double jitter, uint64_t seed,
-                                          const int32_t *__restrict__ ids, int32_t toff, double last_hb,
-                                          const Fsm &f) {
+                                          const int32_t *__restrict__ ids, int32_t phase, double last_hb,
+                                          const Fsm &f, uint8_t &hl) {
     uint8_t ob = 0;
     if (st == ST_F && !heard && now - last_hb > timeout) {
         st = ST_W;
@@ -158,7 +196,7 @@ __device__ __forceinline__ uint8_t timers(int64_t i, uint8_t &st, bool heard, in
         f.delay[i] = 0.0 + jitter * jitter_u(seed, ids[i], t);
         lead = -1;
         lead_set = true;
-        f.has_lpos[i] = 0;
+        hl = 0;
         f.lpos[i] = make_float2(0.f, 0.f);
     }
     if (st == ST_W && now - f.wait_start[i] > f.delay[i]) {
@@ -167,7 +205,7 @@ __device__ __forceinline__ uint8_t timers(int64_t i, uint8_t &st, bool heard, in
         lead_set = true;
         ob |= kAcclaim;
     }
-    if (st == ST_L && ((t + toff) % 10) == 0) ob |= kHeartbeat;
+    if (st == ST_L && ((t + phase) % 10) == 0) ob |= kHeartbeat;
     return ob;
 }
 
@@ -219,8 +257,7 @@ __global__ __launch_bounds__(kBlock) void k_sum_counts(int64_t ticks, const unsi
 // ---------------------------------------------------------------- pull mode: one fused launch
 __global__ __launch_bounds__(kBlock) void k_tick_pull(int64_t n, int64_t t, const int32_t *__restrict__ ids,
                                                      const double2 *__restrict__ pos, const int32_t *__restrict__ rp,
-                                                     const int32_t *__restrict__ col,
-                                                     const int32_t *__restrict__ tick_off, Fsm f,
+                                                     const int32_t *__restrict__ col, Fsm f,
                                                      const uint8_t *__restrict__ ob_in, uint8_t *__restrict__ ob_out,
                                                      double dt, double timeout, double jitter, uint64_t seed,
                                                      unsigned long long *__restrict__ counts) {
@@ -230,17 +267,21 @@ __global__ __launch_bounds__(kBlock) void k_tick_pull(int64_t n, int64_t t, cons
     const double now = double(t) * dt;
     unsigned c_lead = 0, c_wait = 0, c_acc = 0, c_hb = 0;
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
-        if (!f.alive[i]) {
+        const uint32_t fw = f.flags[i];
+        if (!fw_alive(fw)) {
             ob_out[i] = 0;
             continue;
         }
-        const uint8_t st0 = f.state[i];
+        const uint8_t st0 = fw_state(fw);
+        const int32_t ph = fw_phase(fw);
+        uint8_t hl = fw_hl(fw);
         Heard h{st0, 0, false, false, 0, -1};
-        receive_row<kRecv>(rp[i], rp[i + 1], col, ob_in, ids, ids[i], ((t + tick_off[i]) % 10) == 0, h);
-        apply_heard(i, h, now, pos, f);
+        receive_row<kRecv>(rp[i], rp[i + 1], col, ob_in, ids, ids[i], ((t + ph) % 10) == 0, h);
+        apply_heard(i, h, now, pos, f, hl);
         const uint8_t ob = h.ob | timers(i, h.st, h.live, h.lead, h.lead_set, t, now, timeout, jitter, seed, ids,
-                                         tick_off[i], f.last_hb[i], f);
-        if (h.st != st0) f.state[i] = h.st;
+                                         ph, f.last_hb[i], f, hl);
+        const uint32_t fw1 = fw_make(h.st, 1, hl, ph);
+        if (fw1 != fw) f.flags[i] = fw1;
         if (h.lead_set) f.leader[i] = h.lead;
         ob_out[i] = ob;
         c_lead += h.st == ST_L;
@@ -338,7 +379,7 @@ __global__ __launch_bounds__(kBlock) void k_mail_from_outbox(int64_t n, const ui
 // it.  (A single role -- each sweep wave serving its own receivers -- held every wave for its
 // receivers' chains: 0.170 vs 0.152 ms per tick with separate kernels.)
 //   sweep    (workgroups g_recv ..): kSweepV consecutive agents per thread, their byte fields
-//            (alive, outbox, state) as one 32-bit word each, their timers (last_hb, tick_off) and
+//            (outbox) as one 32-bit word, their flag words as one 16-byte load, their timers (last_hb) and
 //            their 64-agent mail word loaded up front; agents with a mail bit are left to the
 //            receive role, the others tick their timers.
 //   receive  (workgroups 0 .. g_recv - 1; all of them on a pulled tick): chunks of 4 096 agents;
@@ -409,14 +450,16 @@ struct NextMail {
 };
 
 // Timers and writes of alive agent i after what it heard (h), its sends listed.
-__device__ __forceinline__ void finish_agent(int64_t i, Heard &h, uint8_t st0, uint8_t prev, int64_t t, double now,
-                                             double timeout, double jitter, uint64_t seed,
-                                             const int32_t *__restrict__ ids, int32_t toff, double lhb, const Fsm &f,
+__device__ __forceinline__ void finish_agent(int64_t i, Heard &h, uint32_t fw0, uint8_t hl, uint8_t prev, int64_t t,
+                                             double now, double timeout, double jitter, uint64_t seed,
+                                             const int32_t *__restrict__ ids, double lhb, const Fsm &f,
                                              uint8_t *__restrict__ ob_out, int32_t *seg, int *s_ns, TickCounts &c) {
     uint8_t st = h.st;
+    const int32_t ph = fw_phase(fw0);
     const uint8_t ob = uint8_t(h.ob | timers(i, st, h.live, h.lead, h.lead_set, t, now, timeout, jitter, seed, ids,
-                                             toff, lhb, f));
-    if (st != st0) f.state[i] = st;
+                                             ph, lhb, f, hl));
+    const uint32_t fw1 = fw_make(st, 1, hl, ph);
+    if (fw1 != fw0) f.flags[i] = fw1;
     if (h.lead_set) f.leader[i] = h.lead;
     if (ob != prev) ob_out[i] = ob;
     if (ob) seg[atomicAdd(s_ns, 1)] = int32_t(i);  // this workgroup's sender segment (LDS counter)
@@ -428,7 +471,7 @@ __device__ __forceinline__ void finish_agent(int64_t i, Heard &h, uint8_t st0, u
 
 __global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int32_t *__restrict__ ids,
                                                 const double2 *__restrict__ pos, const int32_t *__restrict__ rp,
-                                                const int32_t *__restrict__ col, const int32_t *__restrict__ tick_off,
+                                                const int32_t *__restrict__ col,
                                                 Fsm f, Mail mail, const uint8_t *__restrict__ ob_in,
                                                 uint8_t *__restrict__ ob_out, const unsigned *__restrict__ pull,
                                                 Segs segs, double dt, double timeout,
@@ -506,22 +549,24 @@ __global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int
                 const bool multi = (entry & 0x80000000u) != 0;
                 // the receiver's fields and its single sender, all loads at once (no load behind the
                 // alive test), then the sender's outbox, ID and position at once
-                const uint8_t prev = ob_out[i], al = f.alive[i], st0 = f.state[i];
-                const int32_t toff = tick_off[i], me = ids[i];
+                const uint8_t prev = ob_out[i];
+                const uint32_t fw = f.flags[i];
+                const int32_t me = ids[i];
                 const double lhb = f.last_hb[i];
                 const int32_t j = multi ? 0 : mail.from[i];
-                if (!al) {
+                if (!fw_alive(fw)) {
                     if (prev) ob_out[i] = 0;
                     continue;
                 }
-                Heard h{st0, 0, false, false, 0, -1};
-                const bool hb_tick = ((t + toff) % 10) == 0;
+                Heard h{fw_state(fw), 0, false, false, 0, -1};
+                uint8_t hl = fw_hl(fw);
+                const bool hb_tick = ((t + fw_phase(fw)) % 10) == 0;
                 if (multi) {  // several senders (or a pull): the row, in CSR order
                     const int32_t b = rp[i], e = rp[i + 1];
                     receive_row<kRecvTick>(b, e, col, ob_in, ids, me, hb_tick, h);
                     ++c.multi;
                     c.edges += unsigned(e - b);
-                    apply_heard(i, h, now, pos, f);
+                    apply_heard(i, h, now, pos, f, hl);
                 } else {  // exactly one sender: no row walk
                     const uint8_t o = ob_in[j] & (kAcclaim | kHeartbeat);
                     const int32_t sid = ids[j];
@@ -531,10 +576,10 @@ __global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int
                     if (h.live) f.last_hb[i] = now;
                     if (h.hb_from >= 0) {
                         f.lpos[i] = make_float2(float(sp.x), float(sp.y));
-                        f.has_lpos[i] = 1;
+                        hl = 1;
                     }
                 }
-                finish_agent(i, h, st0, prev, t, now, timeout, jitter, seed, ids, toff, lhb, f, ob_out, seg, &s_ns, c);
+                finish_agent(i, h, fw, hl, prev, t, now, timeout, jitter, seed, ids, lhb, f, ob_out, seg, &s_ns, c);
             }
             __syncthreads();  // the list is reused
         }
@@ -549,33 +594,25 @@ __global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int
         for (int64_t gi = int64_t(rank) * kBlock + threadIdx.x; gi < ngroups; gi += stride) {
             const int64_t i0 = gi * kSweepV;
             const bool full = vec && i0 + kSweepV <= n;
-            uint8_t al[kSweepV], pv[kSweepV], sv[kSweepV];
-            int32_t to[kSweepV];
+            uint32_t fw[kSweepV];
+            uint8_t pv[kSweepV];
             double lh[kSweepV];
             const unsigned mine = unsigned(mail.bits[i0 >> 6] >> (i0 & 63)) & ((1u << kSweepV) - 1u);
             if (full) {  // vec: the host checked the alignments; i0 is a multiple of 4
-                const uint32_t wa = *reinterpret_cast<const uint32_t *>(f.alive + i0);
+                const uint4 wv = *reinterpret_cast<const uint4 *>(f.flags + i0);
                 const uint32_t wp = *reinterpret_cast<const uint32_t *>(ob_out + i0);
-                const uint32_t ws = *reinterpret_cast<const uint32_t *>(f.state + i0);
-                const int4 tv = *reinterpret_cast<const int4 *>(tick_off + i0);
                 const double2 l0 = *reinterpret_cast<const double2 *>(f.last_hb + i0);
                 const double2 l1 = *reinterpret_cast<const double2 *>(f.last_hb + i0 + 2);
+                fw[0] = wv.x; fw[1] = wv.y; fw[2] = wv.z; fw[3] = wv.w;
 #pragma unroll
-                for (int v = 0; v < kSweepV; ++v) {
-                    al[v] = uint8_t(wa >> (8 * v));
-                    pv[v] = uint8_t(wp >> (8 * v));
-                    sv[v] = uint8_t(ws >> (8 * v));
-                }
-                to[0] = tv.x; to[1] = tv.y; to[2] = tv.z; to[3] = tv.w;
+                for (int v = 0; v < kSweepV; ++v) pv[v] = uint8_t(wp >> (8 * v));
                 lh[0] = l0.x; lh[1] = l0.y; lh[2] = l1.x; lh[3] = l1.y;
             } else {
 #pragma unroll
                 for (int v = 0; v < kSweepV; ++v) {
                     const int64_t i = i0 + v < n ? i0 + v : n - 1;
-                    al[v] = i0 + v < n ? f.alive[i] : 0;
+                    fw[v] = i0 + v < n ? f.flags[i] : 0u;  // past n: not alive
                     pv[v] = ob_out[i];
-                    sv[v] = f.state[i];
-                    to[v] = tick_off[i];
                     lh[v] = f.last_hb[i];
                 }
             }
@@ -584,13 +621,13 @@ __global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int
                 const int64_t i = i0 + v;
                 if ((mine >> v) & 1u) continue;  // a receiver: the receive role's
                 const uint8_t prev = pv[v];      // this slot's byte from tick t-2
-                if (!al[v]) {
+                if (!fw_alive(fw[v])) {
                     if (i < n && prev) ob_out[i] = 0;
                     continue;
                 }
-                Heard h{sv[v], 0, false, false, 0, -1};
-                finish_agent(i, h, sv[v], prev, t, now, timeout, jitter, seed, ids, to[v], lh[v], f, ob_out, seg,
-                             &s_ns, c);
+                Heard h{fw_state(fw[v]), 0, false, false, 0, -1};
+                finish_agent(i, h, fw[v], fw_hl(fw[v]), prev, t, now, timeout, jitter, seed, ids, lh[v], f, ob_out,
+                             seg, &s_ns, c);
             }
         }
     }
@@ -676,8 +713,12 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
     unsigned long long *d_sum = d_cnt + size_t(ticks) * kShards * 4;
     unsigned long long *d_tr = traffic ? d_sum + size_t(ticks) * 4 : nullptr;
     if (d_tr) SW_HIP(hipMemsetAsync(d_tr, 0, tr_bytes, s));
-    const Fsm f{fsm->state, fsm->leader, fsm->last_hb, fsm->wait_start, fsm->delay,
-                reinterpret_cast<float2 *>(fsm->leader_pos), fsm->has_leader_pos, fsm->alive};
+    // the run's flag words: state, alive, leader-position flag and tick phase of every agent (unpacked into
+    // the caller's arrays at the end of the run)
+    uint32_t *flags;
+    SW_ALLOC(flags, ctx, S_FSM_FLAGS, size_t(n) * 4);
+    const Fsm f{flags, fsm->leader, fsm->last_hb, fsm->wait_start, fsm->delay,
+                reinterpret_cast<float2 *>(fsm->leader_pos)};
     // the sweep role's grid: 2 560 workgroups at most, with half as many in the receive role (10M
     // agents, one-launch ticks, two boxes: 0.1208-0.1212 ms per tick against 0.1232-0.1234 for
     // 2 048 + 1 280, 0.122 for 1 536 + 1 280, 2 560 + 1 536 and 3 072 + 1 280; the two-launch form
@@ -688,8 +729,11 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
     }();
     const unsigned grid = grid_for(n, kBlock, sweep_env > 0 ? unsigned(sweep_env) : 2560u);
     auto a16 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-    // k_sweep's word loads: byte arrays 4-byte aligned (the tick's outbox half too), timers 16-byte
-    const int vec = a16(fsm->alive) && a16(fsm->outbox) && a16(fsm->state) && a16(tick_off) && a16(fsm->last_hb);
+    // k_sweep's word loads: the outbox 4-byte aligned (the tick's half too), timers 16-byte (flag words: scratch)
+    const int vec = a16(fsm->outbox) && a16(fsm->last_hb) && a16(flags);
+    hipLaunchKernelGGL(k_pack_flags, dim3(grid), dim3(kBlock), 0, s, n, fsm->state, fsm->alive, fsm->has_leader_pos,
+                       tick_off, flags);
+    SW_LAUNCHED();
     const bool push = hear_row_ptr != nullptr;
     const int64_t n_words = (n + 63) / 64;
     Mail mail{};
@@ -764,7 +808,7 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
         bool kill = false;
         for (int32_t k = 0; k < n_kill; ++k) kill |= kill_ticks[k] == t;
         if (kill) {
-            hipLaunchKernelGGL(k_kill_leaders, dim3(grid), dim3(kBlock), 0, s, n, fsm->state, fsm->alive);
+            hipLaunchKernelGGL(k_kill_leaders, dim3(grid), dim3(kBlock), 0, s, n, flags);
             SW_LAUNCHED();
         }
         const uint8_t *ob_in = fsm->outbox + size_t((t - 1) & 1) * size_t(n);
@@ -781,16 +825,19 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
             im.trp = hear_row_ptr;
             im.tcol = hear_col;
             hipLaunchKernelGGL(k_tick, dim3(tgrid), dim3(kBlock), 0, s, n, t, ids,
-                               reinterpret_cast<const double2 *>(pos), row_ptr, col, tick_off, f, mail_of(t), ob_in,
+                               reinterpret_cast<const double2 *>(pos), row_ptr, col, f, mail_of(t), ob_in,
                                ob_out, pullf + t % nbuf, segs, dt, timeout, jitter, seed, cnt,
                                int(vec && (reinterpret_cast<uintptr_t>(ob_out) & 3) == 0), d_tr, im, xg);
         } else {
             hipLaunchKernelGGL(k_tick_pull, dim3(grid), dim3(kBlock), 0, s, n, t, ids,
-                               reinterpret_cast<const double2 *>(pos), row_ptr, col, tick_off, f, ob_in, ob_out, dt,
+                               reinterpret_cast<const double2 *>(pos), row_ptr, col, f, ob_in, ob_out, dt,
                                timeout, jitter, seed, cnt);
         }
         SW_LAUNCHED();
     }
+    hipLaunchKernelGGL(k_unpack_flags, dim3(grid), dim3(kBlock), 0, s, n, flags, fsm->state, fsm->alive,
+                       fsm->has_leader_pos);
+    SW_LAUNCHED();
     if (d_tr) {  // pull-mode runs: every tick walks every row (the receivers are all agents)
         unsigned long long *hs = static_cast<unsigned long long *>(pinned(ctx, kTraffic * 8));
         if (!hs) return SWARM_ERR_OOM;
