@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU session: selected test files (-k filter), then optionally the default bench line.
 # Stops at the first crash-like exit (fault / abort / timeout).
-#   TESTS="tests/a.py tests/b.py" K="expr" TAG=x BENCH=1 bash tools/gpu_r6.sh
+#   TESTS="tests/a.py tests/b.py" K="expr" TAG=x BENCH=1 bash tools/gpu_session.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
