@@ -52,10 +52,6 @@ constexpr int kRecv = 8;  // CSR entries loaded per receive chunk (pull mode, he
 #define SWARM_RECV_TICK 8
 #endif
 constexpr int kRecvTick = SWARM_RECV_TICK;
-// several-sender receivers served 4 lanes per receiver (k_tick's receive role; 0: one thread each, A/B aid)
-#ifndef SWARM_COOP_RECV
-#define SWARM_COOP_RECV 1
-#endif
 constexpr uint8_t ST_F = SWARM_FOLLOWER, ST_W = SWARM_ELECTION_WAIT, ST_L = SWARM_LEADER;
 
 __device__ __forceinline__ double jitter_u(uint64_t seed, int32_t id, int64_t t) {
@@ -539,25 +535,6 @@ __global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int
                     if (b16) m16 = unsigned(mail.multi[w] >> sh) & b16;
                 }
             }
-#if SWARM_COOP_RECV
-            // singles listed from the front, several-sender receivers (every agent on a pulled tick) from
-            // the back: the first are served one per thread, the second 4 lanes per receiver
-            unsigned s16 = b16 & ~m16;
-            int total, total_m;
-            int pos_ = block_excl_scan<5>(__popc(s16), total, s_wave);
-            int pos_m = block_excl_scan<5>(__popc(m16), total_m, s_wave);
-            while (s16 | m16) {
-                const int q = __ffs(s16 | m16) - 1;
-                const bool mq = (m16 >> q) & 1u;
-                if (mq)
-                    s_list[kRecvChunk - 1 - pos_m++] = uint32_t(a0 + q);
-                else
-                    s_list[pos_++] = uint32_t(a0 + q);
-                b16 &= ~(1u << q);
-                m16 &= ~(1u << q);
-                s16 &= ~(1u << q);
-            }
-#else
             int total;
             int pos_ = block_excl_scan<5>(__popc(b16), total, s_wave);
             while (b16) {
@@ -565,12 +542,11 @@ __global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int
                 b16 &= b16 - 1;
                 s_list[pos_++] = uint32_t(a0 + q) | (((m16 >> q) & 1u) ? 0x80000000u : 0u);
             }
-#endif
             __syncthreads();
             for (int q = threadIdx.x; q < total; q += kBlock) {
                 const uint32_t entry = s_list[q];
                 const int64_t i = int32_t(entry & 0x7FFFFFFFu);
-                const bool multi = !SWARM_COOP_RECV && (entry & 0x80000000u) != 0;  // (coop: singles only here)
+                const bool multi = (entry & 0x80000000u) != 0;
                 // the receiver's fields and its single sender, all loads at once (no load behind the
                 // alive test), then the sender's outbox, ID and position at once
                 const uint8_t prev = ob_out[i];
@@ -605,69 +581,6 @@ __global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int
                 }
                 finish_agent(i, h, fw, hl, prev, t, now, timeout, jitter, seed, ids, lhb, f, ob_out, seg, &s_ns, c);
             }
-#if SWARM_COOP_RECV
-            // several-sender receivers, 4 lanes each: lane `sub` loads edges b + sub + 4u of every 16-edge batch
-            // (columns, then outbox bytes, then the senders' IDs, each step all in flight), and every lane of the
-            // group replays the batch's senders in CSR order -- fetched from their lanes by bpermute -- on its own
-            // copy of the receiver's state, so all four hold the same result; lane 0 writes it
-            for (int mb = 0; mb < total_m; mb += kBlock / 4) {
-                const int sub = threadIdx.x & 3, gsrc = threadIdx.x & 60;  // gsrc: the group's first lane
-                const int idx = mb + int(threadIdx.x >> 2);
-                const bool act = idx < total_m;
-                const int64_t i = int32_t(s_list[kRecvChunk - 1 - (act ? idx : 0)]);
-                const uint8_t prev = ob_out[i];
-                const uint32_t fw = f.flags[i];
-                const int32_t me = ids[i];
-                const double lhb = f.last_hb[i];
-                const int32_t b = rp[i], e = rp[i + 1];
-                if (!act) continue;              // group-uniform
-                if (!fw_alive(fw)) {              // group-uniform
-                    if (sub == 0 && prev) ob_out[i] = 0;
-                    continue;
-                }
-                Heard h{fw_state(fw), 0, false, false, 0, -1};
-                uint8_t hl = fw_hl(fw);
-                const bool hb_tick = ((t + fw_phase(fw)) % 10) == 0;
-                for (int32_t k0 = b; k0 < e; k0 += 16) {  // group-uniform trip count
-                    int32_t jj[4], ss[4];
-                    uint8_t oo[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int32_t k = k0 + sub + 4 * u;
-                        jj[u] = k < e ? col[k] : -1;
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) oo[u] = jj[u] >= 0 ? uint8_t(ob_in[jj[u]] & (kAcclaim | kHeartbeat)) : 0;
-                    unsigned mine = 0;
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        ss[u] = oo[u] ? ids[jj[u]] : 0;
-                        mine |= oo[u] ? (1u << (4 * u + sub)) : 0u;
-                    }
-                    // the group's senders of this batch, bit k - k0 (quad OR by DPP)
-                    unsigned gm = mine | unsigned(__builtin_amdgcn_update_dpp(0, int(mine), 0xB1, 0xF, 0xF, false));
-                    gm |= unsigned(__builtin_amdgcn_update_dpp(0, int(gm), 0x4E, 0xF, 0xF, false));
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {  // bit 4u + lane: CSR order is u, then the lane
-                        unsigned gu = (gm >> (4 * u)) & 0xFu;
-                        while (gu) {  // group-uniform
-                            const int src = gsrc + __ffs(gu) - 1;
-                            gu &= gu - 1;
-                            const uint8_t o = uint8_t(__shfl(int(oo[u]), src, 64));
-                            const int32_t sid = __shfl(ss[u], src, 64), jv = __shfl(jj[u], src, 64);
-                            hear(h, o, sid, jv, me, hb_tick);
-                        }
-                    }
-                }
-                if (sub == 0) {
-                    ++c.multi;
-                    c.edges += unsigned(e - b);
-                    apply_heard(i, h, now, pos, f, hl);
-                    finish_agent(i, h, fw, hl, prev, t, now, timeout, jitter, seed, ids, lhb, f, ob_out, seg, &s_ns,
-                                 c);
-                }
-            }
-#endif
             __syncthreads();  // the list is reused
         }
     } else {
