@@ -1237,7 +1237,7 @@ def sharded_auction_row(args, rank, world, dev):
            "path": _shard_path(sh)}
     if dist.get_backend() != "nccl":
         out["rehearsal"] = ("REHEARSAL, not a scaling figure: the ranks exchange every round through host memory "
-                            "(gloo group, shared-memory transport); C4's rounds are latency-bound and do not shard "
+                            f"(gloo group; {_shard_path(sh)}); C4's rounds are latency-bound and do not shard "
                             "(DESIGN §4b)")
     return out
 
