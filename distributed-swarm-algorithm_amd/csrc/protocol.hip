@@ -27,10 +27,9 @@
 //            buf(t+1) and clears buf(t+2).
 // (Rounds 2-3 ran k_compact + k_receive + k_sweep + k_mail, round 4 first k_tick + k_mail: the
 // boundaries and the list round trips per tick.)
-// A quiet agent costs ~13 B (its flag word -- state, alive, leader-position flag, tick phase --, outbox
-// byte and 8-byte timer) plus its mail
-// bit; only receivers pay for their rows.  Storm ticks: when a workgroup's senders exceed pull_frac x the
-// agents of its share (a timeout wave: thousands of ACCLAIMs at once), it skips the mail atomics
+// A quiet agent costs ~9 B (its 8-byte record -- state, alive, leader-position flag, tick phase and its
+// timer as a tick of the run -- and its outbox byte) plus its mail bit; only receivers pay for their
+// rows.  Storm ticks: when a workgroup's senders exceed pull_frac x the agents of its share (a timeout wave: thousands of ACCLAIMs at once), it skips the mail atomics
 // and the next tick pulls instead -- every alive agent walks its own row, as pull mode does.  Same results: an agent
 // without a sender in its row hears nothing either way.  Pull mode (no hearers CSR): one fused
 // launch in which every agent walks its row -- the cross-check.  Both are latency-bound gathers, no
@@ -62,53 +61,124 @@ __device__ __forceinline__ double jitter_u(uint64_t seed, int32_t id, int64_t t)
     return double(x >> 11) * (1.0 / 9007199254740992.0);
 }
 
-// An agent's small per-tick fields packed in one 32-bit word for the run (the C-ABI's separate state /
-// alive / has_leader_pos bytes and int32 tick_off are packed at the start and unpacked at the end): a
-// receiver touches one line for them instead of four, and the sweep streams 4 B instead of 7.
-//   byte 0 state, byte 1 alive, byte 2 has_leader_pos, byte 3 tick phase = tick_off mod 10 in [0, 9]
-// ((t + tick_off) % 10 == 0 iff (t + phase) % 10 == 0 for every tick t >= 0).
+// An agent's per-tick fields for the run, in one 8-byte record (the C-ABI's separate arrays are packed at
+// the start of a run and unpacked at its end): a receiver touches one line for them instead of four, and
+// the sweep streams 8 B per agent instead of 15.
+//   x: the flag word -- byte 0 state, byte 1 alive, byte 2 bits (kHL: has_leader_pos, kH64, kDirty),
+//      byte 3 tick phase = tick_off mod 10 in [0, 9] ((t + tick_off) % 10 == 0 iff (t + phase) % 10 == 0
+//      for every tick t >= 0);
+//   y: the agent's timer as a tick of the run (relative to t0), exact because the reference's clock is
+//      t * dt: FOLLOWER -- the tick its last_heartbeat_time was set at (last_hb == double(t0 + y) * dt,
+//      the timeout test evaluated on that value, as _check_election_timeout does, agent.py:223);
+//      ELECTION_WAIT -- the first tick t at which now - election_wait_start > election_delay holds
+//      (agent.py:234; found once, when the wait starts: the test is monotone in t for dt > 0), 0 = never.
+//   kH64: the timer is in the caller's f64 arrays instead (a value no tick of the run represents, or
+//      dt <= 0): the test reads them, as before.  kDirty: last_hb changed in the run; the unpack writes
+//      double(t0 + y) * dt (a FOLLOWER entering ELECTION_WAIT writes it at once).
+// Leader and leader position are write-only during a run: one 16-byte record per agent (LRec), one line
+// per heartbeat receiver instead of two.
+constexpr uint32_t kHL = 1, kH64 = 2, kDirty = 4;
 __host__ __device__ __forceinline__ uint8_t fw_state(uint32_t w) { return uint8_t(w); }
 __host__ __device__ __forceinline__ uint8_t fw_alive(uint32_t w) { return uint8_t(w >> 8); }
-__host__ __device__ __forceinline__ uint8_t fw_hl(uint32_t w) { return uint8_t(w >> 16); }
+__host__ __device__ __forceinline__ uint32_t fw_bits(uint32_t w) { return (w >> 16) & 0xFFu; }
 __host__ __device__ __forceinline__ int32_t fw_phase(uint32_t w) { return int32_t(w >> 24); }
-__host__ __device__ __forceinline__ uint32_t fw_make(uint8_t st, uint8_t al, uint8_t hl, int32_t ph) {
-    return uint32_t(st) | (uint32_t(al) << 8) | (uint32_t(hl) << 16) | (uint32_t(ph) << 24);
+__host__ __device__ __forceinline__ uint32_t fw_make(uint8_t st, uint8_t al, uint32_t bits, int32_t ph) {
+    return uint32_t(st) | (uint32_t(al) << 8) | (bits << 16) | (uint32_t(ph) << 24);
 }
 
-struct Fsm {
-    uint32_t *flags;  // fw_* fields
-    int32_t *leader;
-    double *last_hb, *wait_start, *delay;
-    float2 *lpos;
+struct alignas(16) LRec {
+    float x, y;      // leader_pos
+    int32_t leader;  // leader
+    int32_t pad;
 };
 
-__global__ __launch_bounds__(kBlock) void k_kill_leaders(int64_t n, uint32_t *__restrict__ flags) {
+struct Fsm {
+    uint2 *rec;  // (flag word, timer tick)
+    LRec *lrec;
+    double *last_hb, *wait_start, *delay;  // the caller's (kH64 timers; written when a wait starts)
+    int64_t t0, t_end;                     // the run's ticks: t0 + 1 .. t_end
+    double dt;
+};
+
+__device__ __forceinline__ void set_lpos(const Fsm &f, int64_t i, float x, float y) {
+    *reinterpret_cast<float2 *>(&f.lrec[i].x) = make_float2(x, y);
+}
+
+// The first tick t in [lo, f.t_end] with double(t) * dt - ws > d, relative to t0; 0 when there is none
+// (dt > 0: the test is monotone in t).  A guess from d / dt, then bisection if it was off.
+__host__ __device__ __forceinline__ int32_t wait_exit(int64_t lo, int64_t t_end, int64_t t0, double dt, double ws,
+                                                      double d) {
+    auto go = [&](int64_t t) { return double(t) * dt - ws > d; };
+    if (lo > t_end || !go(t_end)) return 0;
+    int64_t hi = t_end;  // go(hi)
+    const double g = std::floor((ws + d) / dt);
+    if (g == g && g >= double(lo) && g < double(t_end)) {  // near the answer: one step either side
+        const int64_t gi = int64_t(g);
+        if (go(gi + 1)) {
+            if (!go(gi)) return int32_t(gi + 1 - t0);
+            hi = gi;
+        } else {
+            lo = gi + 2;
+        }
+    }
+    while (lo < hi) {
+        const int64_t mid = lo + (hi - lo) / 2;
+        if (go(mid)) hi = mid;
+        else lo = mid + 1;
+    }
+    return int32_t(lo - t0);
+}
+
+__global__ __launch_bounds__(kBlock) void k_kill_leaders(int64_t n, uint2 *__restrict__ rec) {
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
-        const uint32_t w = flags[i];
-        if (fw_alive(w) && fw_state(w) == ST_L) flags[i] = w & ~0xFF00u;
+        const uint32_t w = rec[i].x;
+        if (fw_alive(w) && fw_state(w) == ST_L) rec[i].x = w & ~0xFF00u;
     }
 }
 
-// The C-ABI's fields -> flag words, and back (once per run each).
-__global__ __launch_bounds__(kBlock) void k_pack_flags(int64_t n, const uint8_t *__restrict__ state,
-                                                      const uint8_t *__restrict__ alive,
-                                                      const uint8_t *__restrict__ hl,
-                                                      const int32_t *__restrict__ tick_off,
-                                                      uint32_t *__restrict__ flags) {
+// The C-ABI's fields -> records (once per run).
+__global__ __launch_bounds__(kBlock) void k_pack_fsm(int64_t n, const uint8_t *__restrict__ state,
+                                                    const uint8_t *__restrict__ alive,
+                                                    const uint8_t *__restrict__ hl,
+                                                    const int32_t *__restrict__ tick_off,
+                                                    const int32_t *__restrict__ leader,
+                                                    const float2 *__restrict__ lpos, Fsm f) {
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
         const int32_t ph = ((tick_off[i] % 10) + 10) % 10;
-        flags[i] = fw_make(state[i], alive[i], hl[i], ph);
+        const uint8_t st = state[i];
+        uint32_t bits = hl[i] ? kHL : 0u;
+        int32_t y = 0;
+        if (st == ST_F) {  // last_hb as a tick of the run, if one represents it exactly
+            const double lhb = f.last_hb[i];
+            const double k = f.dt != 0.0 ? std::nearbyint(lhb / f.dt) : 0.0;
+            const bool ok = f.dt != 0.0 && std::fabs(k) < 9.0e15 && k * f.dt == lhb &&
+                            k - double(f.t0) > -2147483647.0 && k - double(f.t0) < 2147483647.0;
+            if (ok) y = int32_t(int64_t(k) - f.t0);
+            else bits |= kH64;
+        } else if (st == ST_W) {
+            if (f.dt > 0.0) y = wait_exit(f.t0 + 1, f.t_end, f.t0, f.dt, f.wait_start[i], f.delay[i]);
+            else bits |= kH64;
+        }
+        f.rec[i] = make_uint2(fw_make(st, alive[i], bits, ph), uint32_t(y));
+        const float2 q = lpos[i];
+        f.lrec[i] = LRec{q.x, q.y, leader[i], 0};
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_unpack_flags(int64_t n, const uint32_t *__restrict__ flags,
-                                                        uint8_t *__restrict__ state, uint8_t *__restrict__ alive,
-                                                        uint8_t *__restrict__ hl) {
+// Records -> the C-ABI's fields (once per run).
+__global__ __launch_bounds__(kBlock) void k_unpack_fsm(int64_t n, uint8_t *__restrict__ state,
+                                                      uint8_t *__restrict__ alive, uint8_t *__restrict__ hl,
+                                                      int32_t *__restrict__ leader, float2 *__restrict__ lpos,
+                                                      Fsm f) {
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
-        const uint32_t w = flags[i];
-        state[i] = fw_state(w);
-        alive[i] = fw_alive(w);
-        hl[i] = fw_hl(w);
+        const uint2 r = f.rec[i];
+        state[i] = fw_state(r.x);
+        alive[i] = fw_alive(r.x);
+        hl[i] = (fw_bits(r.x) & kHL) ? 1 : 0;
+        if (fw_bits(r.x) & kDirty) f.last_hb[i] = double(f.t0 + int32_t(r.y)) * f.dt;
+        const LRec q = f.lrec[i];
+        leader[i] = q.leader;
+        lpos[i] = make_float2(q.x, q.y);
     }
 }
 
@@ -171,39 +241,56 @@ __device__ __forceinline__ void receive_row(int32_t b, int32_t e, const int32_t 
     }
 }
 
-// Write back the liveness proof and the heartbeat's leader position (state / leader / the position flag
-// hl: caller).
-__device__ __forceinline__ void apply_heard(int64_t i, const Heard &h, double now, const double2 *__restrict__ pos,
-                                            const Fsm &f, uint8_t &hl) {
-    if (h.live) f.last_hb[i] = now;
+// A liveness proof sets last_hb = now: the timer becomes this tick; the heartbeat's leader position (state
+// / leader: caller).
+__device__ __forceinline__ void apply_heard(int64_t i, const Heard &h, int64_t t, const double2 *__restrict__ pos,
+                                            const Fsm &f, uint32_t &bits, int32_t &y) {
+    if (h.live) {
+        y = int32_t(t - f.t0);
+        bits = (bits & ~kH64) | kDirty;
+    }
     if (h.hb_from >= 0) {
         const double2 q = pos[h.hb_from];
-        f.lpos[i] = make_float2(float(q.x), float(q.y));
-        hl = 1;
+        set_lpos(f, i, float(q.x), float(q.y));
+        bits |= kHL;
     }
 }
 
 // _check_election_timeout (217-241) and the leader's heartbeat (283-289) for agent i in state
-// st; `heard`: it got a liveness proof this tick (its last_hb is now).  Returns the sends.
+// st; `heard`: it got a liveness proof this tick (its timer is now).  Returns the sends.
 __device__ __forceinline__ uint8_t timers(int64_t i, uint8_t &st, bool heard, int32_t &lead, bool &lead_set,
                                           int64_t t, double now, double timeout, double jitter, uint64_t seed,
-                                          const int32_t *__restrict__ ids, int32_t phase, double last_hb,
-                                          const Fsm &f, uint8_t &hl) {
+                                          const int32_t *__restrict__ ids, int32_t phase, const Fsm &f,
+                                          uint32_t &bits, int32_t &y) {
     uint8_t ob = 0;
-    if (st == ST_F && !heard && now - last_hb > timeout) {
-        st = ST_W;
-        f.wait_start[i] = now;
-        f.delay[i] = 0.0 + jitter * jitter_u(seed, ids[i], t);
-        lead = -1;
-        lead_set = true;
-        hl = 0;
-        f.lpos[i] = make_float2(0.f, 0.f);
+    if (st == ST_F && !heard) {
+        const double last_hb = (bits & kH64) ? f.last_hb[i] : double(f.t0 + y) * f.dt;
+        if (now - last_hb > timeout) {
+            if (bits & kDirty) f.last_hb[i] = last_hb;
+            st = ST_W;
+            const double d = 0.0 + jitter * jitter_u(seed, ids[i], t);
+            f.wait_start[i] = now;
+            f.delay[i] = d;
+            lead = -1;
+            lead_set = true;
+            bits &= ~(kHL | kDirty);
+            set_lpos(f, i, 0.f, 0.f);
+            if (f.dt > 0.0) {
+                y = wait_exit(t + 1, f.t_end, f.t0, f.dt, now, d);
+                bits &= ~kH64;
+            } else {
+                bits |= kH64;
+            }
+        }
     }
-    if (st == ST_W && now - f.wait_start[i] > f.delay[i]) {
-        st = ST_L;
-        lead = ids[i];
-        lead_set = true;
-        ob |= kAcclaim;
+    if (st == ST_W) {
+        const bool done = (bits & kH64) ? now - f.wait_start[i] > f.delay[i] : (y != 0 && t - f.t0 >= int64_t(y));
+        if (done) {
+            st = ST_L;
+            lead = ids[i];
+            lead_set = true;
+            ob |= kAcclaim;
+        }
     }
     if (st == ST_L && ((t + phase) % 10) == 0) ob |= kHeartbeat;
     return ob;
@@ -267,22 +354,24 @@ __global__ __launch_bounds__(kBlock) void k_tick_pull(int64_t n, int64_t t, cons
     const double now = double(t) * dt;
     unsigned c_lead = 0, c_wait = 0, c_acc = 0, c_hb = 0;
     for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += int64_t(gridDim.x) * kBlock) {
-        const uint32_t fw = f.flags[i];
+        const uint2 r = f.rec[i];
+        const uint32_t fw = r.x;
         if (!fw_alive(fw)) {
             ob_out[i] = 0;
             continue;
         }
         const uint8_t st0 = fw_state(fw);
         const int32_t ph = fw_phase(fw);
-        uint8_t hl = fw_hl(fw);
+        uint32_t bits = fw_bits(fw);
+        int32_t y = int32_t(r.y);
         Heard h{st0, 0, false, false, 0, -1};
         receive_row<kRecv>(rp[i], rp[i + 1], col, ob_in, ids, ids[i], ((t + ph) % 10) == 0, h);
-        apply_heard(i, h, now, pos, f, hl);
+        apply_heard(i, h, t, pos, f, bits, y);
         const uint8_t ob = h.ob | timers(i, h.st, h.live, h.lead, h.lead_set, t, now, timeout, jitter, seed, ids,
-                                         ph, f.last_hb[i], f, hl);
-        const uint32_t fw1 = fw_make(h.st, 1, hl, ph);
-        if (fw1 != fw) f.flags[i] = fw1;
-        if (h.lead_set) f.leader[i] = h.lead;
+                                         ph, f, bits, y);
+        const uint32_t fw1 = fw_make(h.st, 1, bits, ph);
+        if (fw1 != fw || uint32_t(y) != r.y) f.rec[i] = make_uint2(fw1, uint32_t(y));
+        if (h.lead_set) f.lrec[i].leader = h.lead;
         ob_out[i] = ob;
         c_lead += h.st == ST_L;
         c_wait += h.st == ST_W;
@@ -449,18 +538,19 @@ struct NextMail {
     const int32_t *trp, *tcol;       // who hears each agent
 };
 
-// Timers and writes of alive agent i after what it heard (h), its sends listed.
-__device__ __forceinline__ void finish_agent(int64_t i, Heard &h, uint32_t fw0, uint8_t hl, uint8_t prev, int64_t t,
-                                             double now, double timeout, double jitter, uint64_t seed,
-                                             const int32_t *__restrict__ ids, double lhb, const Fsm &f,
+// Timers and writes of alive agent i after what it heard (h; r0: its record at the start of the tick,
+// bits / y: after the receive), its sends listed.
+__device__ __forceinline__ void finish_agent(int64_t i, Heard &h, uint2 r0, uint32_t bits, int32_t y, uint8_t prev,
+                                             int64_t t, double now, double timeout, double jitter, uint64_t seed,
+                                             const int32_t *__restrict__ ids, const Fsm &f,
                                              uint8_t *__restrict__ ob_out, int32_t *seg, int *s_ns, TickCounts &c) {
     uint8_t st = h.st;
-    const int32_t ph = fw_phase(fw0);
+    const int32_t ph = fw_phase(r0.x);
     const uint8_t ob = uint8_t(h.ob | timers(i, st, h.live, h.lead, h.lead_set, t, now, timeout, jitter, seed, ids,
-                                             ph, lhb, f, hl));
-    const uint32_t fw1 = fw_make(st, 1, hl, ph);
-    if (fw1 != fw0) f.flags[i] = fw1;
-    if (h.lead_set) f.leader[i] = h.lead;
+                                             ph, f, bits, y));
+    const uint32_t fw1 = fw_make(st, 1, bits, ph);
+    if (fw1 != r0.x || uint32_t(y) != r0.y) f.rec[i] = make_uint2(fw1, uint32_t(y));
+    if (h.lead_set) f.lrec[i].leader = h.lead;
     if (ob != prev) ob_out[i] = ob;
     if (ob) seg[atomicAdd(s_ns, 1)] = int32_t(i);  // this workgroup's sender segment (LDS counter)
     c.lead += st == ST_L;
@@ -469,7 +559,19 @@ __device__ __forceinline__ void finish_agent(int64_t i, Heard &h, uint32_t fw0, 
     c.hb += (ob & kHeartbeat) != 0;
 }
 
-__global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int32_t *__restrict__ ids,
+// k_tick at >= 7 waves per SIMD (72 VGPRs, a few spilled): 0.1111 ms per tick against 0.1142 at 6 (79 VGPRs)
+// and 0.1194 at the compiler's 5 (82), 0.129 at 8 (64 VGPRs, 26 spilled); 6 row entries per chunk at 7
+// waves 0.1110-0.1116, 4 entries 0.1181 at 7 / 0.1156 at 8 (same box; SWARM_TICK_WAVES=0: the compiler's
+// choice, A/B aid)
+#ifndef SWARM_TICK_WAVES
+#define SWARM_TICK_WAVES 7
+#endif
+#if SWARM_TICK_WAVES
+#define SWARM_TICK_BOUNDS __launch_bounds__(kBlock, SWARM_TICK_WAVES)
+#else
+#define SWARM_TICK_BOUNDS __launch_bounds__(kBlock)
+#endif
+__global__ SWARM_TICK_BOUNDS void k_tick(int64_t n, int64_t t, const int32_t *__restrict__ ids,
                                                 const double2 *__restrict__ pos, const int32_t *__restrict__ rp,
                                                 const int32_t *__restrict__ col,
                                                 Fsm f, Mail mail, const uint8_t *__restrict__ ob_in,
@@ -550,36 +652,39 @@ __global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int
                 // the receiver's fields and its single sender, all loads at once (no load behind the
                 // alive test), then the sender's outbox, ID and position at once
                 const uint8_t prev = ob_out[i];
-                const uint32_t fw = f.flags[i];
+                const uint2 r = f.rec[i];
                 const int32_t me = ids[i];
-                const double lhb = f.last_hb[i];
                 const int32_t j = multi ? 0 : mail.from[i];
-                if (!fw_alive(fw)) {
+                if (!fw_alive(r.x)) {
                     if (prev) ob_out[i] = 0;
                     continue;
                 }
-                Heard h{fw_state(fw), 0, false, false, 0, -1};
-                uint8_t hl = fw_hl(fw);
-                const bool hb_tick = ((t + fw_phase(fw)) % 10) == 0;
+                Heard h{fw_state(r.x), 0, false, false, 0, -1};
+                uint32_t bits = fw_bits(r.x);
+                int32_t y = int32_t(r.y);
+                const bool hb_tick = ((t + fw_phase(r.x)) % 10) == 0;
                 if (multi) {  // several senders (or a pull): the row, in CSR order
                     const int32_t b = rp[i], e = rp[i + 1];
                     receive_row<kRecvTick>(b, e, col, ob_in, ids, me, hb_tick, h);
                     ++c.multi;
                     c.edges += unsigned(e - b);
-                    apply_heard(i, h, now, pos, f, hl);
+                    apply_heard(i, h, t, pos, f, bits, y);
                 } else {  // exactly one sender: no row walk
                     const uint8_t o = ob_in[j] & (kAcclaim | kHeartbeat);
                     const int32_t sid = ids[j];
                     const double2 sp = pos[j];  // used when its heartbeat is accepted (hb_from = j)
                     if (o) hear(h, o, sid, j, me, hb_tick);
                     ++c.single;
-                    if (h.live) f.last_hb[i] = now;
+                    if (h.live) {
+                        y = int32_t(t - f.t0);
+                        bits = (bits & ~kH64) | kDirty;
+                    }
                     if (h.hb_from >= 0) {
-                        f.lpos[i] = make_float2(float(sp.x), float(sp.y));
-                        hl = 1;
+                        set_lpos(f, i, float(sp.x), float(sp.y));
+                        bits |= kHL;
                     }
                 }
-                finish_agent(i, h, fw, hl, prev, t, now, timeout, jitter, seed, ids, lhb, f, ob_out, seg, &s_ns, c);
+                finish_agent(i, h, r, bits, y, prev, t, now, timeout, jitter, seed, ids, f, ob_out, seg, &s_ns, c);
             }
             __syncthreads();  // the list is reused
         }
@@ -594,26 +699,23 @@ __global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int
         for (int64_t gi = int64_t(rank) * kBlock + threadIdx.x; gi < ngroups; gi += stride) {
             const int64_t i0 = gi * kSweepV;
             const bool full = vec && i0 + kSweepV <= n;
-            uint32_t fw[kSweepV];
+            uint2 rv[kSweepV];
             uint8_t pv[kSweepV];
-            double lh[kSweepV];
             const unsigned mine = unsigned(mail.bits[i0 >> 6] >> (i0 & 63)) & ((1u << kSweepV) - 1u);
-            if (full) {  // vec: the host checked the alignments; i0 is a multiple of 4
-                const uint4 wv = *reinterpret_cast<const uint4 *>(f.flags + i0);
+            if (full) {  // vec: the host checked the outbox's alignment; i0 is a multiple of 4 (records: scratch)
+                const uint4 r01 = *reinterpret_cast<const uint4 *>(f.rec + i0);
+                const uint4 r23 = *reinterpret_cast<const uint4 *>(f.rec + i0 + 2);
                 const uint32_t wp = *reinterpret_cast<const uint32_t *>(ob_out + i0);
-                const double2 l0 = *reinterpret_cast<const double2 *>(f.last_hb + i0);
-                const double2 l1 = *reinterpret_cast<const double2 *>(f.last_hb + i0 + 2);
-                fw[0] = wv.x; fw[1] = wv.y; fw[2] = wv.z; fw[3] = wv.w;
+                rv[0] = make_uint2(r01.x, r01.y); rv[1] = make_uint2(r01.z, r01.w);
+                rv[2] = make_uint2(r23.x, r23.y); rv[3] = make_uint2(r23.z, r23.w);
 #pragma unroll
                 for (int v = 0; v < kSweepV; ++v) pv[v] = uint8_t(wp >> (8 * v));
-                lh[0] = l0.x; lh[1] = l0.y; lh[2] = l1.x; lh[3] = l1.y;
             } else {
 #pragma unroll
                 for (int v = 0; v < kSweepV; ++v) {
                     const int64_t i = i0 + v < n ? i0 + v : n - 1;
-                    fw[v] = i0 + v < n ? f.flags[i] : 0u;  // past n: not alive
+                    rv[v] = i0 + v < n ? f.rec[i] : make_uint2(0u, 0u);  // past n: not alive
                     pv[v] = ob_out[i];
-                    lh[v] = f.last_hb[i];
                 }
             }
 #pragma unroll
@@ -621,13 +723,13 @@ __global__ __launch_bounds__(kBlock) void k_tick(int64_t n, int64_t t, const int
                 const int64_t i = i0 + v;
                 if ((mine >> v) & 1u) continue;  // a receiver: the receive role's
                 const uint8_t prev = pv[v];      // this slot's byte from tick t-2
-                if (!fw_alive(fw[v])) {
+                if (!fw_alive(rv[v].x)) {
                     if (i < n && prev) ob_out[i] = 0;
                     continue;
                 }
-                Heard h{fw_state(fw[v]), 0, false, false, 0, -1};
-                finish_agent(i, h, fw[v], fw_hl(fw[v]), prev, t, now, timeout, jitter, seed, ids, lh[v], f, ob_out,
-                             seg, &s_ns, c);
+                Heard h{fw_state(rv[v].x), 0, false, false, 0, -1};
+                finish_agent(i, h, rv[v], fw_bits(rv[v].x), int32_t(rv[v].y), prev, t, now, timeout, jitter, seed,
+                             ids, f, ob_out, seg, &s_ns, c);
             }
         }
     }
@@ -713,12 +815,12 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
     unsigned long long *d_sum = d_cnt + size_t(ticks) * kShards * 4;
     unsigned long long *d_tr = traffic ? d_sum + size_t(ticks) * 4 : nullptr;
     if (d_tr) SW_HIP(hipMemsetAsync(d_tr, 0, tr_bytes, s));
-    // the run's flag words: state, alive, leader-position flag and tick phase of every agent (unpacked into
-    // the caller's arrays at the end of the run)
-    uint32_t *flags;
-    SW_ALLOC(flags, ctx, S_FSM_FLAGS, size_t(n) * 4);
-    const Fsm f{flags, fsm->leader, fsm->last_hb, fsm->wait_start, fsm->delay,
-                reinterpret_cast<float2 *>(fsm->leader_pos)};
+    // the run's records (flag word + timer tick, leader + leader position; unpacked into the caller's arrays
+    // at the end of the run)
+    uint8_t *recs;
+    SW_ALLOC(recs, ctx, S_FSM_FLAGS, size_t(n) * 24);
+    const Fsm f{reinterpret_cast<uint2 *>(recs), reinterpret_cast<LRec *>(recs + size_t(n) * 8), fsm->last_hb,
+                fsm->wait_start, fsm->delay, t0, t0 + ticks, dt};
     // the sweep role's grid: 2 560 workgroups at most, with half as many in the receive role (10M
     // agents, one-launch ticks, two boxes: 0.1208-0.1212 ms per tick against 0.1232-0.1234 for
     // 2 048 + 1 280, 0.122 for 1 536 + 1 280, 2 560 + 1 536 and 3 072 + 1 280; the two-launch form
@@ -729,10 +831,11 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
     }();
     const unsigned grid = grid_for(n, kBlock, sweep_env > 0 ? unsigned(sweep_env) : 2560u);
     auto a16 = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-    // k_sweep's word loads: the outbox 4-byte aligned (the tick's half too), timers 16-byte (flag words: scratch)
-    const int vec = a16(fsm->outbox) && a16(fsm->last_hb) && a16(flags);
-    hipLaunchKernelGGL(k_pack_flags, dim3(grid), dim3(kBlock), 0, s, n, fsm->state, fsm->alive, fsm->has_leader_pos,
-                       tick_off, flags);
+    // the sweep's word loads: the outbox 4-byte aligned (the tick's half too; records: scratch)
+    const int vec = a16(fsm->outbox) && a16(recs);
+    SW_ARG((reinterpret_cast<uintptr_t>(fsm->leader_pos) & 7) == 0, "leader_pos is not 8-byte aligned");
+    hipLaunchKernelGGL(k_pack_fsm, dim3(grid), dim3(kBlock), 0, s, n, fsm->state, fsm->alive, fsm->has_leader_pos,
+                       tick_off, fsm->leader, reinterpret_cast<const float2 *>(fsm->leader_pos), f);
     SW_LAUNCHED();
     const bool push = hear_row_ptr != nullptr;
     const int64_t n_words = (n + 63) / 64;
@@ -808,7 +911,7 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
         bool kill = false;
         for (int32_t k = 0; k < n_kill; ++k) kill |= kill_ticks[k] == t;
         if (kill) {
-            hipLaunchKernelGGL(k_kill_leaders, dim3(grid), dim3(kBlock), 0, s, n, flags);
+            hipLaunchKernelGGL(k_kill_leaders, dim3(grid), dim3(kBlock), 0, s, n, f.rec);
             SW_LAUNCHED();
         }
         const uint8_t *ob_in = fsm->outbox + size_t((t - 1) & 1) * size_t(n);
@@ -835,8 +938,8 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
         }
         SW_LAUNCHED();
     }
-    hipLaunchKernelGGL(k_unpack_flags, dim3(grid), dim3(kBlock), 0, s, n, flags, fsm->state, fsm->alive,
-                       fsm->has_leader_pos);
+    hipLaunchKernelGGL(k_unpack_fsm, dim3(grid), dim3(kBlock), 0, s, n, fsm->state, fsm->alive, fsm->has_leader_pos,
+                       fsm->leader, reinterpret_cast<float2 *>(fsm->leader_pos), f);
     SW_LAUNCHED();
     if (d_tr) {  // pull-mode runs: every tick walks every row (the receivers are all agents)
         unsigned long long *hs = static_cast<unsigned long long *>(pinned(ctx, kTraffic * 8));

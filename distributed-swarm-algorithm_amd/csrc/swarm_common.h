@@ -56,7 +56,7 @@ enum Slot {
     S_OVR,            // allocation: host libm decisions for those pairs (host -> device)
     S_ENC_FLAGS,      // codec: tile ticket + per-tile look-back words (kept across calls, tagged by epoch)
     S_CHECK,          // election: the 16-bit column check's verdict word
-    S_FSM_FLAGS,      // protocol: per-agent flag words of a run (state, alive, leader-position flag, tick phase)
+    S_FSM_FLAGS,      // protocol: per-agent records of a run (flag word + timer tick; leader + leader position)
     S_NUM
 };
 

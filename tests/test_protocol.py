@@ -163,6 +163,51 @@ def test_gpu_matches_oracle_random(oracle_mod, n, seed, side, mode, directed):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dt,t0", [(0.1, 0), (0.07, 1234), (-0.05, 3)])
+def test_gpu_timer_encodings_match_oracle(oracle_mod, dt, t0):
+    """A run keeps a FOLLOWER's last_heartbeat_time as a tick of the run and an ELECTION_WAIT's end as the
+    first tick its test holds (protocol.hip, the per-agent record); values no tick represents, and waits
+    when dt <= 0, stay in the f64 arrays.  Mixed initial states -- FOLLOWERs with tick-exact and arbitrary
+    last_hb, ELECTION_WAITs with arbitrary wait_start / delay, LEADERs, dead agents, leader positions --
+    at other dt and a nonzero start tick, in two chunks: every state, timer, leader position and count
+    equals the oracle's (agent.py:217-241)."""
+    import torch
+    from swarm_amd.swarm import Swarm
+    n = 20000
+    g = _random_case(n, 11, 50.0)
+    rng = np.random.default_rng(7)
+    st = rng.choice([F, W, L], n, p=[0.6, 0.3, 0.1]).astype(np.uint8)
+    lhb = np.where(rng.uniform(size=n) < 0.5, (t0 - rng.integers(0, 40, n)).astype(np.float64) * dt,
+                   t0 * dt - rng.uniform(0, 4, n))
+    ws, dl = t0 * dt - rng.uniform(0, 0.3, n), rng.uniform(0, 0.2, n)
+    leader = np.where(st == L, g["ids"], rng.choice(g["ids"], n)).astype(np.int32)
+    alive = (rng.uniform(size=n) > 0.02).astype(np.uint8)
+    lpos = rng.uniform(-5, 5, (n, 2)).astype(np.float32)
+    has = (rng.uniform(size=n) < 0.5).astype(np.uint8)
+    kills = np.array([t0 + 50, t0 + 100], np.int64)
+    want = oracle_mod.protocol(g["ids"], g["x"], g["y"], g["row_ptr"], g["col"], g["tick_off"], 130, state=st,
+                               leader=leader, last_hb=lhb, wait_start=ws, delay=dl, lpos=lpos, has_lpos=has,
+                               alive=alive, t0=t0, dt=dt, seed=11, kill_ticks=kills)
+    s = Swarm(g["ids"], g["x"], g["y"], device="cuda")
+    s.set_graph(g["row_ptr"], g["col"])
+    s.protocol_reset(tick_off=g["tick_off"], last_hb=lhb)
+    s.state.copy_(s._storage(st, torch.uint8))
+    s.leader.copy_(s._storage(leader, torch.int32))
+    s.fsm["wait_start"], s.fsm["delay"] = s._storage(ws, torch.float64), s._storage(dl, torch.float64)
+    s.fsm["alive"], s.fsm["has_leader_pos"] = s._storage(alive, torch.uint8), s._storage(has, torch.uint8)
+    s.fsm["leader_pos"] = torch.as_tensor(lpos, device="cuda")[s.perm.long()].contiguous()
+    s.fsm_tick = t0
+    c1 = s.protocol_run(60, kill_ticks=kills, dt=dt, seed=11)
+    c2 = s.protocol_run(70, kill_ticks=kills, dt=dt, seed=11)
+    got = _gpu_state(s)
+    for k in OUT:
+        np.testing.assert_array_equal(got[k], want[k], err_msg=k)
+    np.testing.assert_array_equal(np.concatenate([c1, c2]), want["counts"])
+    if dt > 0:
+        assert want["counts"][:, 1].sum() > 0 and want["counts"][:, 0].max() > 0
+
+
+@pytest.mark.gpu
 def test_gpu_empty_and_isolated():
     from swarm_amd.swarm import Swarm
     s = Swarm(np.zeros(0, np.int32), [], [], device="cuda")

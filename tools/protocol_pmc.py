@@ -13,7 +13,11 @@ import torch
 
 sys.path.insert(0, "distributed-swarm-algorithm_amd")
 sys.path.insert(0, ".")
-from swarm_amd import gen  # noqa: E402
+import os  # noqa: E402
+
+from swarm_amd import _lib, gen  # noqa: E402
+if os.environ.get("PROTO_LIB"):  # A/B builds under swarm_amd/
+    _lib.load(os.path.join(_lib.HERE, os.environ["PROTO_LIB"]))
 from swarm_amd.swarm import Swarm  # noqa: E402
 
 tag = sys.argv[1] if len(sys.argv) > 1 else "p"
