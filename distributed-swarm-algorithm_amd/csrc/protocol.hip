@@ -477,7 +477,11 @@ __global__ __launch_bounds__(kBlock) void k_mail_from_outbox(int64_t n, const ui
 //            order when it has several (multi bit) or the tick is pulled -- then its timers run on
 //            the result.
 // Senders of both roles are listed in the workgroup's own segment, then mailed by it.
-constexpr int kSweepV = 4;
+#ifndef SWARM_SWEEP_V  // A/B aid: agents per sweep thread (4 or 8)
+#define SWARM_SWEEP_V 4
+#endif
+constexpr int kSweepV = SWARM_SWEEP_V;
+static_assert(kSweepV == 4 || kSweepV == 8, "sweep: 4 or 8 agents per thread");
 constexpr int kRecvChunk = 4096;  // agents per receive-role pass (64 mail words, 16 agents per thread;
                                   // 2 048: 0.144 vs 0.138 ms per tick)
 
@@ -703,13 +707,18 @@ __global__ SWARM_TICK_BOUNDS void k_tick(int64_t n, int64_t t, const int32_t *__
             uint8_t pv[kSweepV];
             const unsigned mine = unsigned(mail.bits[i0 >> 6] >> (i0 & 63)) & ((1u << kSweepV) - 1u);
             if (full) {  // vec: the host checked the outbox's alignment; i0 is a multiple of 4 (records: scratch)
-                const uint4 r01 = *reinterpret_cast<const uint4 *>(f.rec + i0);
-                const uint4 r23 = *reinterpret_cast<const uint4 *>(f.rec + i0 + 2);
-                const uint32_t wp = *reinterpret_cast<const uint32_t *>(ob_out + i0);
-                rv[0] = make_uint2(r01.x, r01.y); rv[1] = make_uint2(r01.z, r01.w);
-                rv[2] = make_uint2(r23.x, r23.y); rv[3] = make_uint2(r23.z, r23.w);
 #pragma unroll
-                for (int v = 0; v < kSweepV; ++v) pv[v] = uint8_t(wp >> (8 * v));
+                for (int q = 0; q < kSweepV / 2; ++q) {
+                    const uint4 r2 = *reinterpret_cast<const uint4 *>(f.rec + i0 + 2 * q);
+                    rv[2 * q] = make_uint2(r2.x, r2.y);
+                    rv[2 * q + 1] = make_uint2(r2.z, r2.w);
+                }
+#pragma unroll
+                for (int q = 0; q < kSweepV / 4; ++q) {
+                    const uint32_t wp = *reinterpret_cast<const uint32_t *>(ob_out + i0 + 4 * q);
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) pv[4 * q + v] = uint8_t(wp >> (8 * v));
+                }
             } else {
 #pragma unroll
                 for (int v = 0; v < kSweepV; ++v) {
