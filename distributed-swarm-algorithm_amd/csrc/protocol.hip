@@ -104,21 +104,22 @@ __device__ __forceinline__ void set_lpos(const Fsm &f, int64_t i, float x, float
     *reinterpret_cast<float2 *>(&f.lrec[i].x) = make_float2(x, y);
 }
 
-// The first tick t in [lo, f.t_end] with double(t) * dt - ws > d, relative to t0; 0 when there is none
-// (dt > 0: the test is monotone in t).  A guess from d / dt, then bisection if it was off.
+// The first tick t in [lo, t_end] with double(t) * dt - ws > d, relative to t0; 0 when there is none
+// (dt > 0: the test is monotone in t).  Tried first at the estimate floor((ws + d) / dt) + 1, clamped to
+// [lo, t_end] (right but for rounding: then one test each side), bisection only when that is off.
 __host__ __device__ __forceinline__ int32_t wait_exit(int64_t lo, int64_t t_end, int64_t t0, double dt, double ws,
                                                       double d) {
     auto go = [&](int64_t t) { return double(t) * dt - ws > d; };
     if (lo > t_end || !go(t_end)) return 0;
     int64_t hi = t_end;  // go(hi)
-    const double g = std::floor((ws + d) / dt);
-    if (g == g && g >= double(lo) && g < double(t_end)) {  // near the answer: one step either side
-        const int64_t gi = int64_t(g);
-        if (go(gi + 1)) {
-            if (!go(gi)) return int32_t(gi + 1 - t0);
-            hi = gi;
+    const double g = std::floor((ws + d) / dt) + 1.0;
+    if (g == g) {
+        const int64_t c = g <= double(lo) ? lo : g >= double(t_end) ? t_end : int64_t(g);
+        if (go(c)) {
+            if (c == lo || !go(c - 1)) return int32_t(c - t0);
+            hi = c - 1;
         } else {
-            lo = gi + 2;
+            lo = c + 1;  // c < t_end: go(t_end) holds
         }
     }
     while (lo < hi) {
