@@ -1235,11 +1235,68 @@ def sharded_auction_row(args, rank, world, dev):
     out = {"ms": float(ms[0]), "agents": n_tot, "tasks": len(tx), "gpus": world, "rounds": r.rounds_exec,
            "bids": int(r.bidders.sum()), "converged": r.converged,
            "path": _shard_path(sh)}
+    if args.oracle_check:
+        out["union_oracle"] = auction_union_check(sh, r, ds, tx, ty, tq, rank, world)
     if dist.get_backend() != "nccl":
         out["rehearsal"] = ("REHEARSAL, not a scaling figure: the ranks exchange every round through host memory "
                             f"(gloo group; {_shard_path(sh)}); C4's rounds are latency-bound and do not shard "
                             "(DESIGN §4b)")
     return out
+
+
+def _gather_rows(t, rank, world, dev):
+    """Every rank's 1-D int64 tensor (any lengths) -> the list on rank 0 (None elsewhere); host-staged
+    groups gather host tensors, nccl groups device ones."""
+    import torch
+    import torch.distributed as dist
+    staged = dist.get_backend() != "nccl"
+    on = (lambda v: v) if staged else (lambda v: v.to(dev))  # noqa: E731
+    n_t = torch.tensor([t.numel()], dtype=torch.int64)
+    counts = [on(torch.zeros(1, dtype=torch.int64)) for _ in range(world)]
+    dist.all_gather(counts, on(n_t))
+    counts = [int(c) for c in counts]
+    mx = max(counts)
+    padded = on(torch.cat([t.cpu().to(torch.int64), torch.full((mx - t.numel(),), -1, dtype=torch.int64)]))
+    if staged:
+        g = [torch.empty(mx, dtype=torch.int64) for _ in range(world)] if rank == 0 else None
+        dist.gather(padded, g, dst=0)
+    else:
+        g = [torch.empty(mx, dtype=torch.int64, device=dev) for _ in range(world)]
+        dist.all_gather(g, padded)
+    return [g[q][:counts[q]].cpu() for q in range(world)] if rank == 0 else None
+
+
+def auction_union_check(sh, r, ds, tx, ty, tq, rank, world):
+    """The sharded auction against the C oracle's auction over the UNION (rank 0's host): rounds, bidders
+    per round, every task's owner (by agent ID) and price bits, every agent's assigned task.  The oracle
+    is the checker here, never the measured path."""
+    ids_l = _gather_rows(sh.ids, rank, world, sh.device)
+    asg_l = _gather_rows(r.assigned, rank, world, sh.device)
+    if rank != 0:
+        return None
+    from oracle import oracle as orc
+    t0 = time.time()
+    orc.set_threads(_threads())
+    ids = np.concatenate([e["ids"] for e in ds]).astype(np.int32)
+    w = orc.auction(ids, np.concatenate([e["x"] for e in ds]), np.concatenate([e["y"] for e in ds]),
+                    np.concatenate([e["caps"] for e in ds]), tx, ty, tq)
+    own_w = np.where(w["owner"] >= 0, ids[np.maximum(w["owner"], 0)], -1)
+    by_id = dict(zip(ids.tolist(), w["assigned"].tolist()))
+    got_ids = torch_cat_np(ids_l)
+    got_asg = torch_cat_np(asg_l)
+    rounds = int(w["rounds"])
+    ok = {"rounds": r.rounds_exec == rounds,
+          "bidders": r.rounds_exec == rounds and bool(np.array_equal(r.bidders, w["bidders"][:rounds])),
+          "owner": bool(np.array_equal(r.owner_id.cpu().numpy(), own_w)),
+          "price_bits": bool(np.array_equal(r.price.cpu().numpy().view(np.uint32),
+                                            np.asarray(w["price"], np.float32).view(np.uint32))),
+          "assigned": len(got_ids) == len(ids) and all(by_id[int(i)] == int(a) for i, a in zip(got_ids, got_asg))}
+    return {"equal": all(ok.values()), **ok, "oracle_rounds": rounds, "oracle_s": time.time() - t0,
+            "oracle": "C oracle orc_auction over the union (checker only)"}
+
+
+def torch_cat_np(ts):
+    return np.concatenate([t.numpy() for t in ts]) if ts else np.zeros(0, np.int64)
 
 
 def _shard_path(sh):

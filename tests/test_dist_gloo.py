@@ -345,3 +345,46 @@ def test_partition_by_id_empty_range_is_a_clear_error():
     y = np.array([0.0, 0.1, 0.2, 0.3, 5.0, 5.1])
     with pytest.raises(ValueError, match="without agents"):
         partition(np.zeros_like(y), y, 3, 0, by="id", ids=ids)
+
+
+def _auction_check_worker(rank, world, port, out_q):
+    import sys
+    for p in (PKG, ROOT, os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        from shard_doubles import NumpyBackend
+        from swarm_amd import gen
+        from swarm_amd.dist import ShardedSwarm
+        ds = [gen.shard_inputs(A_PER, SEED + 2, world, r, t=A_T) for r in range(world)]
+        d = ds[rank]
+        tx, ty, tq = (np.concatenate([e[k] for e in ds]) for k in ("tx", "ty", "treq"))
+        sh = ShardedSwarm(d["ids"], d["x"], d["y"], d["caps"], d["strip"], device="cpu", backend=NumpyBackend())
+        r = sh.auction(tx, ty, tq)
+        good = bench.auction_union_check(sh, r, ds, tx, ty, tq, rank, world)
+        r.assigned[0] = -2 if r.assigned.numel() else 0  # one agent's assignment spoiled on every rank
+        bad = bench.auction_union_check(sh, r, ds, tx, ty, tq, rank, world)
+        out_q.put(dict(rank=rank, good=good, bad=bad))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_auction_union_check():
+    """bench.py's union-oracle check of the sharded auction (the N > 1 line's rows.C4_auction_sharded):
+    equal on a correct run, and it notices one wrong assignment."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_auction_check_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=300) for _ in range(2)], key=lambda o: o["rank"])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g, b = outs[0]["good"], outs[0]["bad"]
+    assert g["equal"] and g["rounds"] and g["owner"] and g["price_bits"] and g["assigned"]
+    assert not b["equal"] and not b["assigned"]
+    assert outs[1]["good"] is None
