@@ -1234,12 +1234,12 @@ def sharded_auction_row(args, rank, world, dev):
     dist.all_reduce(ms, op=dist.ReduceOp.MAX)
     out = {"ms": float(ms[0]), "agents": n_tot, "tasks": len(tx), "gpus": world, "rounds": r.rounds_exec,
            "bids": int(r.bidders.sum()), "converged": r.converged,
-           "path": _shard_path(sh)}
+           "path": _shard_path(sh, "auction")}
     if args.oracle_check:
         out["union_oracle"] = auction_union_check(sh, r, ds, tx, ty, tq, rank, world)
     if dist.get_backend() != "nccl":
         out["rehearsal"] = ("REHEARSAL, not a scaling figure: the ranks exchange every round through host memory "
-                            f"(gloo group; {_shard_path(sh)}); C4's rounds are latency-bound and do not shard "
+                            f"(gloo group; {_shard_path(sh, 'auction')}); C4's rounds are latency-bound and do not shard "
                             "(DESIGN §4b)")
     return out
 
@@ -1299,15 +1299,20 @@ def torch_cat_np(ts):
     return np.concatenate([t.numpy() for t in ts]) if ts else np.zeros(0, np.int64)
 
 
-def _shard_path(sh):
+def _shard_path(sh, what="elect"):
     """Which halo path the sharded run took: libswarm's native C loop over RCCL or over the shared-memory
-    transport (gloo rehearsal: processes of one host), or the Python stepper over torch.distributed."""
+    transport (gloo rehearsal: processes of one host), or the Python stepper over torch.distributed.
+    what: "elect" (swarm_elect_sharded) or "auction" (swarm_auction_sharded)."""
     import torch.distributed as dist
     if getattr(sh, "_native", None) is not None:
         if getattr(sh.backend, "comm_kind", "rccl") == "shm":
-            return "native C loop over the shared-memory transport (host-staged halo + all-reduce per batch)"
+            return ("native C loop over the shared-memory transport (" +
+                    ("host-staged halo + all-reduce per batch)" if what == "elect" else
+                     "host-staged all-gather of each round's bids)"))
         dbl = os.environ.get("SWARM_RCCL_PATH", "")
-        return ("native RCCL loop (swarm_elect_sharded: ncclSend/ncclRecv halo + ncclAllReduce per batch)" +
+        return (("native RCCL loop (swarm_elect_sharded: ncclSend/ncclRecv halo + ncclAllReduce per batch)"
+                 if what == "elect" else
+                 "native RCCL loop (swarm_auction_sharded: ncclAllGather of each round's bids + ncclAllReduce)") +
                 (f" through the RCCL test double {os.path.basename(dbl)} (SWARM_RCCL_PATH)" if dbl else ""))
     return f"torch.distributed {dist.get_backend()} halo" + (" (host-staged)" if sh.halo.host_staged else "")
 
