@@ -541,6 +541,7 @@ struct NextMail {
     unsigned *pull_next, *pull_clear;
     double frac;                     // < 0: never a storm
     const int32_t *trp, *tcol;       // who hears each agent
+    int64_t clk_t0;                  // SWARM_TICK_CLOCKS: the run's first tick
 };
 
 // Timers and writes of alive agent i after what it heard (h; r0: its record at the start of the tick,
@@ -571,6 +572,24 @@ __device__ __forceinline__ void finish_agent(int64_t i, Heard &h, uint2 r0, uint
 #ifndef SWARM_TICK_WAVES
 #define SWARM_TICK_WAVES 7
 #endif
+// Experiment aid (A/B builds with -DSWARM_TICK_CLOCKS=1): per tick and workgroup, the 100 MHz wall clock
+// at its start, after its role's work (all threads: add_counts' barrier), after its storm decision and at
+// its end, plus its sender count; written to SWARM_TICK_CLOCKS_FILE after the run.
+#ifndef SWARM_TICK_CLOCKS
+#define SWARM_TICK_CLOCKS 0
+#endif
+#if SWARM_TICK_CLOCKS
+__device__ unsigned long long *g_tick_clk;
+#define TICK_CLK(slot, v)                                                                        \
+    do {                                                                                          \
+        if (threadIdx.x == 0 && g_tick_clk)                                                       \
+            g_tick_clk[((t - 1 - clk_t0) * int64_t(gridDim.x) + blockIdx.x) * 5 + (slot)] = (v);  \
+    } while (0)
+#else
+#define TICK_CLK(slot, v) \
+    do {                  \
+    } while (0)
+#endif
 #if SWARM_TICK_WAVES
 #define SWARM_TICK_BOUNDS __launch_bounds__(kBlock, SWARM_TICK_WAVES)
 #else
@@ -591,6 +610,10 @@ __global__ SWARM_TICK_BOUNDS void k_tick(int64_t n, int64_t t, const int32_t *__
     static_assert(kRecvChunk % kBlock == 0 && kRecvChunk / kBlock <= 16, "receive slice: <= 16 bits of a word");
     if (threadIdx.x < 4) s_cnt[threadIdx.x] = 0;
     if (threadIdx.x == 0) s_ns = 0;
+#if SWARM_TICK_CLOCKS
+    const int64_t clk_t0 = im.clk_t0;
+#endif
+    TICK_CLK(0, wall_clock64());
     __syncthreads();
     int32_t *seg = segs.of(blockIdx.x);
     const int g_recv = segs.g_recv;
@@ -750,12 +773,16 @@ __global__ SWARM_TICK_BOUNDS void k_tick(int64_t n, int64_t t, const int32_t *__
         if (pulled && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&tr[7], 1ull);  // pulled ticks
     }
     add_counts(c.lead, c.wait, c.acc, c.hb, s_cnt, counts);  // (ends with a barrier: s_ns is final)
+    TICK_CLK(1, wall_clock64());
     for (int64_t q = int64_t(blockIdx.x) * kBlock + threadIdx.x; q < im.n_clear; q += int64_t(gridDim.x) * kBlock)
         if (im.clear[q]) im.clear[q] = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) *im.pull_clear = 0;
     const int ns = s_ns;
+    TICK_CLK(4, (unsigned long long)ns | ((unsigned long long)recv_role << 40) | ((unsigned long long)pulled << 41));
+    TICK_CLK(2, wall_clock64());
     if (im.frac >= 0.0 && double(ns) > im.frac * double(span)) {
         if (threadIdx.x == 0) *im.pull_next = 1u;
+        TICK_CLK(3, wall_clock64());
         return;
     }
     // the segment was written by this workgroup's threads before add_counts' barrier
@@ -770,6 +797,10 @@ __global__ SWARM_TICK_BOUNDS void k_tick(int64_t n, int64_t t, const int32_t *__
         add_traffic(tr, 3, threadIdx.x < unsigned(ns) ? uint64_t((ns - int(threadIdx.x) + kBlock - 1) / kBlock) : 0ull);
         add_traffic(tr, 4, c_edges);
     }
+#if SWARM_TICK_CLOCKS
+    __syncthreads();
+#endif
+    TICK_CLK(3, wall_clock64());
 }
 
 // traffic shards -> out[kTraffic]
@@ -917,6 +948,15 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
                            fsm->outbox + size_t(t0 & 1) * size_t(n), hear_row_ptr, hear_col, mail_of(t0 + 1));
         SW_LAUNCHED();
     }
+#if SWARM_TICK_CLOCKS
+    unsigned long long *clk_buf = nullptr;
+    const char *clk_file = getenv("SWARM_TICK_CLOCKS_FILE");
+    if (push && clk_file) {
+        SW_HIP(hipMalloc(&clk_buf, size_t(ticks) * tgrid * 5 * 8));
+        SW_HIP(hipMemsetAsync(clk_buf, 0, size_t(ticks) * tgrid * 5 * 8, s));
+    }
+    SW_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_tick_clk), &clk_buf, sizeof(clk_buf), 0, hipMemcpyHostToDevice, s));
+#endif
     for (int64_t t = t0 + 1; t <= t0 + ticks; ++t) {
         bool kill = false;
         for (int32_t k = 0; k < n_kill; ++k) kill |= kill_ticks[k] == t;
@@ -937,6 +977,7 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
             im.frac = pull_frac < 0.0 ? -1.0 : pull_frac;
             im.trp = hear_row_ptr;
             im.tcol = hear_col;
+            im.clk_t0 = t0;
             hipLaunchKernelGGL(k_tick, dim3(tgrid), dim3(kBlock), 0, s, n, t, ids,
                                reinterpret_cast<const double2 *>(pos), row_ptr, col, f, mail_of(t), ob_in,
                                ob_out, pullf + t % nbuf, segs, dt, timeout, jitter, seed, cnt,
@@ -948,6 +989,20 @@ int swarm_protocol_run_ex(swarm_ctx *ctx, int64_t n, const int32_t *ids, const d
         }
         SW_LAUNCHED();
     }
+#if SWARM_TICK_CLOCKS
+    if (clk_buf) {  // experiment aid: header (ticks, workgroups, receive-role workgroups) + the records
+        std::vector<unsigned long long> hc(size_t(ticks) * tgrid * 5);
+        SW_HIP(hipMemcpyAsync(hc.data(), clk_buf, hc.size() * 8, hipMemcpyDeviceToHost, s));
+        SW_HIP(hipStreamSynchronize(s));
+        SW_HIP(hipFree(clk_buf));
+        if (FILE *fp = fopen(clk_file, "wb")) {
+            const long long hdr[3] = {ticks, (long long)tgrid, g_recv};
+            fwrite(hdr, 8, 3, fp);
+            fwrite(hc.data(), 8, hc.size(), fp);
+            fclose(fp);
+        }
+    }
+#endif
     hipLaunchKernelGGL(k_unpack_fsm, dim3(grid), dim3(kBlock), 0, s, n, fsm->state, fsm->alive, fsm->has_leader_pos,
                        fsm->leader, reinterpret_cast<float2 *>(fsm->leader_pos), f);
     SW_LAUNCHED();
