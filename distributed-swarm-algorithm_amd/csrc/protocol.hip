@@ -615,12 +615,20 @@ __global__ SWARM_TICK_BOUNDS void k_tick(int64_t n, int64_t t, const int32_t *__
 #endif
     TICK_CLK(0, wall_clock64());
     __syncthreads();
-    int32_t *seg = segs.of(blockIdx.x);
+#ifndef SWARM_SWEEP_FIRST  // A/B aid: the sweep role's workgroups dispatched before the receive role's
+#define SWARM_SWEEP_FIRST 0
+#endif
+    // the workgroup's place in the role order (receive role first)
+    const int lb = SWARM_SWEEP_FIRST ? (int(blockIdx.x) < int(gridDim.x) - segs.g_recv
+                                            ? int(blockIdx.x) + segs.g_recv
+                                            : int(blockIdx.x) - (int(gridDim.x) - segs.g_recv))
+                                     : int(blockIdx.x);
+    int32_t *seg = segs.of(lb);
     const int g_recv = segs.g_recv;
     // receive-role workgroups first: dispatched first, all their chains in flight at once (every
     // R-th workgroup instead, the roles side by side: 0.151 vs 0.138 ms per tick)
-    const bool recv_role = int(blockIdx.x) < g_recv;
-    const int rank = recv_role ? int(blockIdx.x) : int(blockIdx.x) - g_recv;
+    const bool recv_role = lb < g_recv;
+    const int rank = recv_role ? lb : lb - g_recv;
     const double now = double(t) * dt;
     const bool pulled = *pull != 0;
     TickCounts c;
@@ -636,7 +644,7 @@ __global__ SWARM_TICK_BOUNDS void k_tick(int64_t n, int64_t t, const int32_t *__
         // xg > 0: groups of xg chunks (4 xg units on a pulled tick) dealt round robin to the 8 XCDs
         // (workgroup r runs on XCD r % 8 under round-robin dispatch), so a receiver's neighbours -- in the
         // chunks around its own -- are mostly fetched into the L2 of the XCD that serves it
-        const int64_t me = pulled ? int64_t(blockIdx.x) : int64_t(rank);
+        const int64_t me = pulled ? int64_t(lb) : int64_t(rank);
         const int64_t gsz = pulled ? 4 * int64_t(xg) : int64_t(xg);
         const int64_t nl = nrole / 8, xcd = me % 8, l = me / 8;
         for (int64_t q = xg ? l : me;; q += xg ? nl : nrole) {
