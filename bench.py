@@ -81,6 +81,14 @@ def parse():
     return a
 
 
+def _spin_until_idle():
+    """Wait for torch's current stream (libswarm launches on it) by polling, the thread kept awake."""
+    import torch
+    st = torch.cuda.current_stream()
+    while not st.query():
+        pass
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -207,8 +215,11 @@ def main():
         ev[0].record()
         r = sw.elect(mode=args.elect_mode, max_rounds=1 << 16)
         # elect() returns with its last kernels queued and then builds its result on the host:
-        # wait, so that host tail counts as election time, not as the allocation's
-        torch.cuda.synchronize()
+        # wait, so that host tail counts as election time, not as the allocation's.  Spin on the stream
+        # rather than block in a synchronize: in the timed step the allocation is launched by a thread
+        # that never slept (libswarm's own waits spin), and a woken thread's first launches are slower
+        # by up to ~0.1 ms on some boxes -- host wake-up, not allocation time
+        _spin_until_idle()
         ev[1].record()
         a = sw.allocate(tpos_x, tpos_y, treq)
         ev[2].record()
