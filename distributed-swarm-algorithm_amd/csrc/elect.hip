@@ -1359,6 +1359,19 @@ bool esc_registered(const swarm_ctx *ctx, const int16_t *c16) {
     return std::find(ctx->esc_built.begin(), ctx->esc_built.end(), c16) != ctx->esc_built.end();
 }
 
+// swarm_graph_compact's records of the buffers it wrote (SWARM_ELECT_TRUST_C16)
+void c16_forget(swarm_ctx *ctx, const int16_t *c16) {
+    auto &v = ctx->c16_built;
+    v.erase(std::remove_if(v.begin(), v.end(), [&](const swarm_ctx::C16Built &b) { return b.c16 == c16; }), v.end());
+}
+
+const swarm_ctx::C16Built *c16_record(swarm_ctx *ctx, const int16_t *c16, const void *rp, const int32_t *col,
+                                      int64_t n) {
+    for (const auto &b : ctx->c16_built)
+        if (b.c16 == c16 && b.rp == rp && b.col == col && b.n == n) return &b;
+    return nullptr;
+}
+
 // Enqueues the column check of rows [0, n_rows) of (rp, c16) into the ctx's verdict word (zeroed
 // first) and its copy into *hflag; the caller reads *hflag after its next stream synchronisation.
 template <typename Off>
@@ -1406,7 +1419,8 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     SW_ARG(n < (int64_t(1) << 31), "n must be < 2^31");
     SW_ARG(max_rounds >= 1, "max_rounds < 1");
     const bool timed = (mode & SWARM_ELECT_TIMED) != 0;
-    mode &= ~SWARM_ELECT_TIMED;
+    const bool trust_c16 = (mode & SWARM_ELECT_TRUST_C16) != 0;
+    mode &= ~(SWARM_ELECT_TIMED | SWARM_ELECT_TRUST_C16);
     SW_ARG(mode == SWARM_ELECT_DENSE || mode == SWARM_ELECT_FRONTIER, "unknown mode");
     SW_ARG(rounds_exec != nullptr, "rounds_exec is NULL");
     SW_ARG(n == 0 || (rp && ids && leader && state), "NULL array (col may be NULL only without edges)");
@@ -1421,14 +1435,20 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     // 16-bit columns are checked before any round reads them (one pass over the columns, read back with
     // the edge count): escaped columns or a foreign buffer are refused, never gathered through
     SW_ARG(!c16 || !esc_registered(ctx, c16), "col16 holds swarm_graph_compact_escaped's columns (escapes)");
-    unsigned c16_bad = 0;
-    if (c16) {
-        if (int rc = enqueue_col16_check<Off>(ctx, rp, c16, col, false, n, n, &c16_bad, s)) return rc;
-    }
+    // SWARM_ELECT_TRUST_C16 with this ctx's record of the buffer: its columns and the edge count are known
+    const swarm_ctx::C16Built *rec = (trust_c16 && c16 && !hrp) ? c16_record(ctx, c16, rp, col, n) : nullptr;
     Off e_total = 0;
-    SW_HIP(hipMemcpyAsync(&e_total, rp + n, sizeof(Off), hipMemcpyDeviceToHost, s));
-    SW_HIP(hipStreamSynchronize(s));
-    if (int rc = col16_verdict(c16_bad, "swarm_elect_compact")) return rc;
+    if (rec) {
+        e_total = Off(rec->e_total);
+    } else {
+        unsigned c16_bad = 0;
+        if (c16) {
+            if (int rc = enqueue_col16_check<Off>(ctx, rp, c16, col, false, n, n, &c16_bad, s)) return rc;
+        }
+        SW_HIP(hipMemcpyAsync(&e_total, rp + n, sizeof(Off), hipMemcpyDeviceToHost, s));
+        SW_HIP(hipStreamSynchronize(s));
+        if (int rc = col16_verdict(c16_bad, "swarm_elect_compact")) return rc;
+    }
     SW_ARG(e_total == 0 || col != nullptr, "col is NULL but the graph has edges");
     // the int32-CSR kernels address with 32-bit byte offsets (gather_listed's ld4 / Col16::at32):
     // 4-byte columns need < 2^30 edges, 2-byte ones < 2^31 (less a margin for the clamped offsets a
@@ -1832,6 +1852,8 @@ int swarm_graph_compact(swarm_ctx *ctx, int64_t n, const int32_t *row_ptr, const
     SW_HIP(hipStreamSynchronize(s));
     // the buffer now holds plain deltas (or a refused build): no longer escaped
     ctx->esc_built.erase(std::remove(ctx->esc_built.begin(), ctx->esc_built.end(), col16), ctx->esc_built.end());
+    c16_forget(ctx, col16);
+    if (!hbad) ctx->c16_built.push_back({col16, row_ptr, col, n, e_total});
     if (hbad) {
         set_error("a neighbour lies more than 32767 storage slots from its row's 64-agent base: keep the int32 columns");
         return SWARM_ERR_RANGE;
@@ -1866,6 +1888,7 @@ int swarm_graph_compact_escaped(swarm_ctx *ctx, int64_t n, const int32_t *row_pt
     SW_HIP(hipMemcpyAsync(&h, cnt, sizeof(h), hipMemcpyDeviceToHost, s));
     SW_HIP(hipStreamSynchronize(s));
     *n_escaped = int64_t(h);
+    c16_forget(ctx, col16);
     if (h && !esc_registered(ctx, col16))
         ctx->esc_built.push_back(col16);
     else if (!h)  // no escape: plain deltas, valid for every reader

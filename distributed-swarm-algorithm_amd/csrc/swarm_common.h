@@ -97,6 +97,13 @@ struct swarm_ctx {
     bool step_c16_esc = false;          // step_c16 holds escapes (read through the int32 columns)
     bool step_c16_checked = false;      // step_c16 passed the column check against the stepped graph
     std::vector<const int16_t *> esc_built;  // column buffers swarm_graph_compact_escaped last wrote
+    struct C16Built {                        // column buffers swarm_graph_compact last wrote (all deltas fit)
+        const int16_t *c16;
+        const void *rp;
+        const int32_t *col;
+        int64_t n, e_total;
+    };
+    std::vector<C16Built> c16_built;
     int step_rd_agent = 0;         // frontier stepper: the marks the next round reads are in agent order
     int step_wr_agent = 0;         // ... and the next round writes its marks in agent order (the tail)
     hipStream_t side = nullptr;    // a second stream for work that overlaps the caller's (side_stream)

@@ -19,7 +19,7 @@ LIB_PATH = os.path.join(HERE, "libswarm.so")
 OK, NOT_CONVERGED = 0, 1
 ERR_ARG, ERR_HIP, ERR_OOM, ERR_RANGE, ERR_STALE = -1, -2, -3, -4, -5
 FOLLOWER, ELECTION_WAIT, LEADER = 1, 2, 3
-ELECT_DENSE, ELECT_FRONTIER, ELECT_TIMED = 0, 1, 0x100
+ELECT_DENSE, ELECT_FRONTIER, ELECT_TIMED, ELECT_TRUST_C16 = 0, 1, 0x100, 0x200
 COMM_RCCL, COMM_SHM = 0, 1  # swarm_comm_create_kind transports
 ALLOC_TRUST_INDEX, ALLOC_FRESH_CLAIMS = 1, 2  # swarm_allocate_indexed_ex flags
 ALLOC_AUTO, ALLOC_BINNED, ALLOC_DENSE = 0, 1, 2

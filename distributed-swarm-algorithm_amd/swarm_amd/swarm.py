@@ -61,6 +61,10 @@ def _to(a, dtype, device):
     return torch.as_tensor(a, dtype=dtype, device=device)
 
 
+# SWARM_TRUST_C16=0 (A/B aid): every election re-checks the 16-bit columns on the device
+_TRUST_C16 = _lib.ELECT_TRUST_C16 if os.environ.get("SWARM_TRUST_C16", "1") != "0" else 0
+
+
 @dataclass
 class ElectResult:
     rounds_exec: int
@@ -259,10 +263,12 @@ class Swarm:
         with torch.cuda.device(self.device):
             c16 = self.graph_compact() if (compact and hear is None) else None
             if c16 is not None:  # symmetric graph, 16-bit columns
+                # graph_compact built them on this ctx from the current row_ptr / col (its cache key holds
+                # their versions): the library skips its column check and edge-count read-back
                 rc = _lib.check(_lib.lib().swarm_elect_compact(
                     _lib.ctx(), n, _lib.ptr(self.row_ptr, torch.int32), _lib.ptr(self.col, torch.int32),
                     _lib.ptr(c16), _lib.ptr(self.ids, torch.int32), _lib.ptr(self.leader, torch.int32),
-                    _lib.ptr(self.state, torch.uint8), cap, m, ctypes.byref(rounds),
+                    _lib.ptr(self.state, torch.uint8), cap, m | _TRUST_C16, ctypes.byref(rounds),
                     changes.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st), _lib.stream()))
             elif hear is None:  # symmetric graph: risers mark through their own rows
                 rc = _lib.check(_lib.lib().swarm_elect(

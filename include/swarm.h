@@ -50,6 +50,12 @@ extern "C" {
 #define SWARM_ELECT_FRONTIER 1 /* dense sweeps while many agents change, then only the agents
                                   marked by last round's risers gather (sparse rounds) */
 #define SWARM_ELECT_TIMED 0x100 /* OR into mode: time every kernel with HIP events (stats) */
+#define SWARM_ELECT_TRUST_C16 0x200 /* OR into mode (swarm_elect_compact*): the caller vouches that col16 was
+                                       written by swarm_graph_compact on this ctx from the same row_ptr / col
+                                       and n, and that none of the three changed since; the 16-bit column
+                                       check and the edge-count read-back are then skipped (no host wait
+                                       before the first round).  Without such a record on the ctx the call
+                                       checks the columns as usual. */
 
 /* Allocation execution strategies (all exact). */
 #define SWARM_ALLOC_AUTO 0

@@ -227,7 +227,8 @@ def test_escaped_columns_refused_by_plain_readers(sw, oracle_mod):
     rx = ctypes.c_int32(0)
     for buf in (c16, copy, garbage):
         for fn, rp in ((L.swarm_elect_compact, rp_t), (L.swarm_elect_compact_i64, rp64)):
-            for mode in (_lib.ELECT_FRONTIER, _lib.ELECT_DENSE):
+            # (SWARM_ELECT_TRUST_C16 vouches only for buffers swarm_graph_compact wrote: none of these)
+            for mode in (_lib.ELECT_FRONTIER, _lib.ELECT_DENSE, _lib.ELECT_FRONTIER | _lib.ELECT_TRUST_C16):
                 rc = fn(cx, n, _lib.ptr(rp), _lib.ptr(col_t), _lib.ptr(buf), _lib.ptr(ids_t), _lib.ptr(lead),
                         _lib.ptr(state), 1 << 16, mode, ctypes.byref(rx), None, None, st)
                 assert rc == _lib.ERR_ARG, (fn, rc, _lib.last_error())
@@ -265,3 +266,36 @@ def test_escaped_columns_refused_by_plain_readers(sw, oracle_mod):
     assert rx.value == o_rounds
     np.testing.assert_array_equal(lead.cpu().numpy(), o_lead)
     np.testing.assert_array_equal(state.cpu().numpy(), o_state)
+
+
+def test_trusted_columns_need_the_ctx_record(sw, oracle_mod):
+    """SWARM_ELECT_TRUST_C16 (Swarm.elect passes it for the columns its graph_compact built) skips the
+    column check only for a buffer this ctx's swarm_graph_compact wrote from the same row_ptr / col / n:
+    exact there; a call with another row_ptr is checked as usual; and once swarm_graph_compact_escaped
+    rewrites the buffer its record is gone (refused).  Reference semantics agent.py:263-275."""
+    from swarm_amd import _lib, gen
+    L, cx, st = _lib.lib(), _lib.ctx(), _lib.stream()
+    n, deg, rp_t, col_t, ids2, col2 = far_graph(sw)
+    d = gen.swarm_inputs(30_000, 5, deg=12.0)
+    s2 = sw.Swarm(d["ids"], d["x"], d["y"], device="cuda").build_graph(1.0)
+    buf = torch.empty(max(s2.n_edges, col_t.numel()), dtype=torch.int16, device="cuda")
+    _lib.check(L.swarm_graph_compact(cx, s2.n, _lib.ptr(s2.row_ptr), _lib.ptr(s2.col), _lib.ptr(buf), st))
+    m = _lib.ELECT_FRONTIER | _lib.ELECT_TRUST_C16
+    lead2, st2 = torch.empty_like(s2.leader), torch.empty_like(s2.state)
+    rx = ctypes.c_int32(0)
+    ch = np.zeros(1 << 12, np.int64)
+    want = oracle_mod.elect(s2.row_ptr.cpu().numpy(), s2.col.cpu().numpy(), s2.ids.cpu().numpy())
+    for rp in (s2.row_ptr, s2.row_ptr.clone()):  # the recorded row_ptr (trusted), a copy (checked)
+        _lib.check(L.swarm_elect_compact(cx, s2.n, _lib.ptr(rp), _lib.ptr(s2.col), _lib.ptr(buf), _lib.ptr(s2.ids),
+                                         _lib.ptr(lead2), _lib.ptr(st2), 1 << 12, m, ctypes.byref(rx),
+                                         ch.ctypes.data_as(ctypes.c_void_p), None, st))
+        assert rx.value == want[2]
+        np.testing.assert_array_equal(ch[:rx.value], want[3])
+        np.testing.assert_array_equal(lead2.cpu().numpy(), want[0])
+    ne = ctypes.c_int64(0)
+    _lib.check(L.swarm_graph_compact_escaped(cx, n, _lib.ptr(rp_t), _lib.ptr(col_t), _lib.ptr(buf), ctypes.byref(ne),
+                                             st))
+    assert ne.value > 0
+    rc = L.swarm_elect_compact(cx, s2.n, _lib.ptr(s2.row_ptr), _lib.ptr(s2.col), _lib.ptr(buf), _lib.ptr(s2.ids),
+                               _lib.ptr(lead2), _lib.ptr(st2), 1 << 12, m, ctypes.byref(rx), None, None, st)
+    assert rc == _lib.ERR_ARG
