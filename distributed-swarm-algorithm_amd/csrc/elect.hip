@@ -1153,7 +1153,11 @@ struct Tuning {
                                // (-1: 8e-4 x agents, measured best at 100k, 1M and 10M agents)
     int tail_wg = 0;           // > 0: the one-workgroup tail (k_tail_wg) once a round's marks fit this many
     int tail_log = 0;          // SWARM_TAIL_LOG=1: per-round clocks of the tail to stderr (experiment aid)
+    int look = 8;              // SWARM_LOOKAHEAD: rounds between a batch's read-back point and its end
     Tuning() {
+        look = env_int("SWARM_LOOKAHEAD", 8);
+        if (look < 1) look = 1;
+        if (look > 64) look = 64;
         tail_wg = env_int("SWARM_TAIL_WG", 0);
         if (tail_wg > kTailCap) tail_wg = kTailCap;
         tail_log = env_int("SWARM_TAIL_LOG", 0);
@@ -1528,7 +1532,7 @@ int elect_impl(swarm_ctx *ctx, int64_t n, const Off *rp, const int32_t *col, con
     // the GPU is still running the batch's last rounds while the host reads, decides the next batch
     // and enqueues it (no idle gap at a batch boundary).  Rounds launched past convergence are
     // guarded no-ops.  Per-round timing and the round log keep the plain read-at-the-end batches.
-    const int kLook = (timed || rlog) ? 0 : 8;
+    const int kLook = (timed || rlog) ? 0 : tuning().look;
     int read_upto = 0;  // rounds whose counters the host has read
     // the per-round counters of rounds (read_upto, tread], read back into hbuf: hist, stats, found
     auto consume = [&](int tread) {
