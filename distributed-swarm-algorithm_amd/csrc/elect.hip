@@ -1141,7 +1141,8 @@ int env_int(const char *name, int dflt) {
 }
 
 struct Tuning {
-    int dense_blocks = 2048;  // grid cap of the dense round kernel
+    int dense_blocks = 8192;  // grid cap of the dense round kernel (C3 election, same box, 3 runs each:
+                              // 8192 23.96-24.07 ms, 2048 24.05-24.16, 4096 24.00-24.13, 16384 23.99-24.12)
     int dense_rounds = 9;     // frontier: rounds 1..dense_rounds run dense (the last one marks)
     int sparse_blocks = 2048; // grid cap of k_sparse_block (8 resident workgroups per CU)
     int small_chunks = 512;   // fewer 2048-agent chunks than this: 512-agent chunks instead
@@ -1166,7 +1167,7 @@ struct Tuning {
         dense_flat = env_int("SWARM_DENSE_FLAT", 1);
         dense_vec = env_int("SWARM_DENSE_VEC", 1);
         stamp_bshift = env_int("SWARM_STAMP_BSHIFT", 5);
-        dense_blocks = env_int("SWARM_DENSE_BLOCKS", 2048);
+        dense_blocks = env_int("SWARM_DENSE_BLOCKS", 8192);
         dense_rounds = env_int("SWARM_DENSE_ROUNDS", 9);
         sparse_blocks = env_int("SWARM_SPARSE_BLOCKS", 2048);
         small_chunks = env_int("SWARM_SMALL_CHUNKS", 512);
