@@ -242,7 +242,9 @@ class Swarm:
         timed: per-kernel HIP events.  compact=False: the int32-column entry point swarm_elect
         (same results).  wide: int64 row offsets (swarm_elect_i64) -- chosen by itself for
         graphs of >= 2^30 edges unless their 16-bit columns fit (swarm_elect_compact then takes up
-        to 2^31 - 2^20 edges on 32-bit offsets: C5's 100M agents on one GPU, ~1.6e9), True forces it."""
+        to 2^31 - 2^20 edges on 32-bit offsets: C5's 100M agents on one GPU, ~1.6e9), True forces it.
+        The 16-bit columns are graph_compact's, rebuilt whenever row_ptr / col change: the call passes
+        SWARM_ELECT_TRUST_C16, so the library skips its device check of them (include/swarm.h)."""
         if self.row_ptr is None:
             raise RuntimeError("no neighbour graph: call build_graph() or set_graph()")
         if wide is None:
